@@ -1,0 +1,257 @@
+"""ctypes bindings of libacestep_mi355x.so.
+
+`GGMLCAPIBridge` keeps the reference bridge's surface
+(scripts/run_non_ggml_real_case.py:135-354: constructor args, `load_dit`,
+`dit_forward_tfirst`, `close`, RuntimeError "<where> failed: <last_error>
+(status=N)") so reference callers switch by pointing `lib_path` at this
+library.  The MI355X extensions (`dit_forward_batched_device`,
+`dit_sample_device`) take raw device pointers (e.g. torch ROCm
+`tensor.data_ptr()`) and keep everything on the GPU.
+"""
+from __future__ import annotations
+
+import atexit
+import ctypes
+import os
+from pathlib import Path
+from typing import List, Optional, Tuple
+
+import numpy as np
+
+from . import LIB_PATH
+
+ACE_GGML_OK = 0
+ACE_GGML_ERR = 1
+ACE_GGML_ERR_INVALID_ARG = 2
+ACE_GGML_ERR_IO = 3
+ACE_GGML_ERR_UNSUPPORTED = 4
+
+# Every symbol declared in include/acestep_ggml.h and include/acestep_mi355x.h.
+EXPORTED_SYMBOLS = (
+    "ace_ggml_create", "ace_ggml_destroy", "ace_ggml_last_error", "ace_ggml_load_dit", "ace_ggml_dit_forward",
+    "ace_mi_create_on_device", "ace_mi_dit_get_info", "ace_mi_dit_forward_batched", "ace_mi_dit_sample",
+    "ace_mi_profile_enable", "ace_mi_profile_reset", "ace_mi_profile_get", "ace_mi_probe_gemm",
+    "ace_mi_synchronize", "ace_mi_kernel_gemm", "ace_mi_kernel_attention",
+)
+
+
+class AceInitParams(ctypes.Structure):
+    _fields_ = [
+        ("n_threads", ctypes.c_int32),
+        ("use_metal", ctypes.c_int32),
+        ("compute_buffer_bytes", ctypes.c_size_t),
+    ]
+
+
+class AceMiDitInfo(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "hidden_size", "intermediate_size", "num_layers", "num_heads", "num_kv_heads", "head_dim",
+        "patch_size", "in_channels", "audio_dim", "sliding_window", "act_type", "device")] + [
+        ("weight_bytes", ctypes.c_int64)]
+
+
+_LIB = None
+
+
+def load_library(path: Optional[str] = None) -> ctypes.CDLL:
+    """Load and bind the shared library (raises if it was not built: there is no fallback)."""
+    global _LIB
+    p = path or os.environ.get("ACE_MI_LIB") or LIB_PATH
+    if _LIB is not None and path is None:
+        return _LIB
+    if not os.path.exists(p):
+        raise RuntimeError(f"libacestep_mi355x.so not found at {p}: run __graft_entry__.build() / make -C "
+                           "ace-step-1.5-ggml_amd/csrc")
+    lib = ctypes.CDLL(p)
+    vp, i32, f32, sz = ctypes.c_void_p, ctypes.c_int32, ctypes.c_float, ctypes.c_size_t
+    fp = ctypes.POINTER(ctypes.c_float)
+    ip = ctypes.POINTER(ctypes.c_int32)
+    lib.ace_ggml_create.argtypes = [ctypes.POINTER(AceInitParams), ctypes.POINTER(vp)]
+    lib.ace_ggml_create.restype = ctypes.c_int
+    lib.ace_mi_create_on_device.argtypes = [ctypes.POINTER(AceInitParams), i32, ctypes.POINTER(vp)]
+    lib.ace_mi_create_on_device.restype = ctypes.c_int
+    lib.ace_ggml_destroy.argtypes = [vp]
+    lib.ace_ggml_destroy.restype = None
+    lib.ace_ggml_last_error.argtypes = [vp]
+    lib.ace_ggml_last_error.restype = ctypes.c_char_p
+    lib.ace_ggml_load_dit.argtypes = [vp, ctypes.c_char_p]
+    lib.ace_ggml_load_dit.restype = ctypes.c_int
+    lib.ace_ggml_dit_forward.argtypes = [vp, fp, fp, fp, ip, ip, i32, i32, f32, f32, fp, sz]
+    lib.ace_ggml_dit_forward.restype = ctypes.c_int
+    lib.ace_mi_dit_get_info.argtypes = [vp, ctypes.POINTER(AceMiDitInfo)]
+    lib.ace_mi_dit_get_info.restype = ctypes.c_int
+    lib.ace_mi_dit_forward_batched.argtypes = [vp, i32, vp, vp, vp, vp, vp, i32, i32, vp, vp, vp, vp]
+    lib.ace_mi_dit_forward_batched.restype = ctypes.c_int
+    lib.ace_mi_dit_sample.argtypes = [vp, i32, vp, vp, vp, vp, vp, i32, i32, fp, i32, vp]
+    lib.ace_mi_dit_sample.restype = ctypes.c_int
+    lib.ace_mi_profile_enable.argtypes = [vp, i32]
+    lib.ace_mi_profile_enable.restype = ctypes.c_int
+    lib.ace_mi_profile_reset.argtypes = [vp]
+    lib.ace_mi_profile_reset.restype = ctypes.c_int
+    lib.ace_mi_profile_get.argtypes = [vp, ctypes.c_char_p, sz, ctypes.POINTER(ctypes.c_double), ip, i32, ip]
+    lib.ace_mi_profile_get.restype = ctypes.c_int
+    lib.ace_mi_probe_gemm.argtypes = [vp, i32, i32, i32]
+    lib.ace_mi_probe_gemm.restype = ctypes.c_int
+    lib.ace_mi_synchronize.argtypes = [vp]
+    lib.ace_mi_synchronize.restype = ctypes.c_int
+    u16p = ctypes.POINTER(ctypes.c_uint16)
+    lib.ace_mi_kernel_gemm.argtypes = [i32, i32, i32, i32, i32, u16p, u16p, fp, fp, u16p]
+    lib.ace_mi_kernel_gemm.restype = ctypes.c_int
+    lib.ace_mi_kernel_attention.argtypes = [i32, i32, i32, i32, i32, i32, f32, fp, fp, ip, fp]
+    lib.ace_mi_kernel_attention.restype = ctypes.c_int
+    if path is None:
+        _LIB = lib
+    return lib
+
+
+def _fptr(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+def _iptr(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+
+
+class GGMLCAPIBridge:
+    """Drop-in for the reference GGMLCAPIBridge (DiT part) backed by the MI355X library."""
+
+    ACE_GGML_OK = ACE_GGML_OK
+
+    def __init__(self, lib_path: Optional[Path] = None, n_threads: int = 0, compute_buffer_mb: int = 0,
+                 use_metal: bool = False, device: Optional[int] = None):
+        self.lib_path = str(lib_path) if lib_path else LIB_PATH
+        self.lib = load_library(None if lib_path is None else str(lib_path))
+        self.ctx = ctypes.c_void_p()
+        self.closed = False
+        self.use_metal = bool(use_metal)
+        params = AceInitParams(n_threads=int(n_threads), use_metal=1 if use_metal else 0,
+                               compute_buffer_bytes=int(compute_buffer_mb) * 1024 * 1024)
+        if device is None:
+            st = self.lib.ace_ggml_create(ctypes.byref(params), ctypes.byref(self.ctx))
+        else:
+            st = self.lib.ace_mi_create_on_device(ctypes.byref(params), int(device), ctypes.byref(self.ctx))
+        self._ensure_ok(st, "ace_ggml_create")
+        atexit.register(self.close)
+        self.info: Optional[AceMiDitInfo] = None
+
+    # -- reference surface -------------------------------------------------
+    def _last_error(self) -> str:
+        msg = self.lib.ace_ggml_last_error(self.ctx)
+        return msg.decode("utf-8", errors="replace") if msg else "unknown error"
+
+    def _ensure_ok(self, status: int, where: str) -> None:
+        if status != self.ACE_GGML_OK:
+            raise RuntimeError(f"{where} failed: {self._last_error()} (status={status})")
+
+    def close(self) -> None:
+        if not self.closed and self.ctx:
+            self.lib.ace_ggml_destroy(self.ctx)
+            self.closed = True
+
+    def load_dit(self, model_dir) -> None:
+        st = self.lib.ace_ggml_load_dit(self.ctx, str(model_dir).encode("utf-8"))
+        self._ensure_ok(st, "ace_ggml_load_dit")
+        info = AceMiDitInfo()
+        self._ensure_ok(self.lib.ace_mi_dit_get_info(self.ctx, ctypes.byref(info)), "ace_mi_dit_get_info")
+        self.info = info
+
+    def dit_forward_tfirst(self, hidden_states_tfirst, context_latents_tfirst, encoder_hidden_states_tfirst,
+                           attention_mask, encoder_attention_mask, timestep: float, timestep_r: float) -> np.ndarray:
+        """[T, D], [T, Ctx], [L, H], [T] int32, [L] int32 -> vt [T, D] float32 (host buffers)."""
+        hs = np.ascontiguousarray(hidden_states_tfirst, dtype=np.float32)
+        ctx = np.ascontiguousarray(context_latents_tfirst, dtype=np.float32)
+        enc = np.ascontiguousarray(encoder_hidden_states_tfirst, dtype=np.float32)
+        am = None if attention_mask is None else np.ascontiguousarray(attention_mask, dtype=np.int32)
+        eam = None if encoder_attention_mask is None else np.ascontiguousarray(encoder_attention_mask, dtype=np.int32)
+        if hs.ndim != 2 or ctx.ndim != 2 or enc.ndim != 2:
+            raise ValueError("dit inputs must be 2D arrays [T,D]/[T,Ctx]/[L,H]")
+        seq_len = int(hs.shape[0])
+        enc_len = int(enc.shape[0])
+        out = np.empty_like(hs, dtype=np.float32)
+        st = self.lib.ace_ggml_dit_forward(self.ctx, _fptr(hs), _fptr(ctx), _fptr(enc), _iptr(am), _iptr(eam),
+                                           seq_len, enc_len, float(timestep), float(timestep_r), _fptr(out),
+                                           out.nbytes)
+        self._ensure_ok(st, "ace_ggml_dit_forward")
+        return out
+
+    # -- MI355X extensions ---------------------------------------------------
+    def dit_forward_batched_device(self, batch: int, seq_len: int, enc_len: int, d_hidden: int, d_context: int,
+                                   d_enc: int, d_mask: int, d_enc_mask: int, d_t: int, d_r: int, d_out: int,
+                                   stream: int = 0) -> None:
+        st = self.lib.ace_mi_dit_forward_batched(self.ctx, int(batch), d_hidden or None, d_context or None,
+                                                 d_enc or None, d_mask or None, d_enc_mask or None, int(seq_len),
+                                                 int(enc_len), d_t, d_r, d_out, stream or None)
+        self._ensure_ok(st, "ace_mi_dit_forward_batched")
+
+    def dit_sample_device(self, batch: int, seq_len: int, enc_len: int, d_xt: int, d_context: int, d_enc: int,
+                          d_mask: int, d_enc_mask: int, schedule: List[float], stream: int = 0) -> None:
+        sched = np.ascontiguousarray(schedule, dtype=np.float32)
+        st = self.lib.ace_mi_dit_sample(self.ctx, int(batch), d_xt, d_context or None, d_enc or None,
+                                        d_mask or None, d_enc_mask or None, int(seq_len), int(enc_len),
+                                        _fptr(sched), int(sched.shape[0]), stream or None)
+        self._ensure_ok(st, "ace_mi_dit_sample")
+
+    def synchronize(self) -> None:
+        self._ensure_ok(self.lib.ace_mi_synchronize(self.ctx), "ace_mi_synchronize")
+
+    def profile_enable(self, on: bool) -> None:
+        self._ensure_ok(self.lib.ace_mi_profile_enable(self.ctx, 1 if on else 0), "ace_mi_profile_enable")
+
+    def profile_reset(self) -> None:
+        self._ensure_ok(self.lib.ace_mi_profile_reset(self.ctx), "ace_mi_profile_reset")
+
+    def profile_get(self) -> List[Tuple[str, float, int]]:
+        cap = 64
+        names = ctypes.create_string_buffer(8192)
+        ms = (ctypes.c_double * cap)()
+        counts = (ctypes.c_int32 * cap)()
+        n = ctypes.c_int32(0)
+        self._ensure_ok(self.lib.ace_mi_profile_get(self.ctx, names, 8192, ms, counts, cap, ctypes.byref(n)),
+                        "ace_mi_profile_get")
+        raw = names.raw.split(b"\0")
+        return [(raw[i].decode(), float(ms[i]), int(counts[i])) for i in range(min(n.value, cap))]
+
+    def probe_gemm(self, which: int, m_rows: int, iters: int) -> None:
+        self._ensure_ok(self.lib.ace_mi_probe_gemm(self.ctx, int(which), int(m_rows), int(iters)),
+                        "ace_mi_probe_gemm")
+
+
+# ---- kernel self-test wrappers (GPU parity tests) ----------------------------
+def kernel_gemm(a_bits: np.ndarray, w_bits: np.ndarray, act_type: int = 0, epi: int = 0,
+                bias: Optional[np.ndarray] = None) -> np.ndarray:
+    """a_bits [M][K], w_bits [N][K] uint16 words; epi 0 -> f32 [M][N], epi 4 -> uint16 [M][N/2]."""
+    lib = load_library()
+    a = np.ascontiguousarray(a_bits, dtype=np.uint16)
+    w = np.ascontiguousarray(w_bits, dtype=np.uint16)
+    M, K = a.shape
+    N = w.shape[0]
+    u16p = ctypes.POINTER(ctypes.c_uint16)
+    b = None if bias is None else np.ascontiguousarray(bias, dtype=np.float32)
+    if epi == 0:
+        out = np.empty((M, N), dtype=np.float32)
+        st = lib.ace_mi_kernel_gemm(act_type, epi, M, N, K, a.ctypes.data_as(u16p), w.ctypes.data_as(u16p),
+                                    _fptr(b), _fptr(out), None)
+    else:
+        out = np.empty((M, N // 2), dtype=np.uint16)
+        st = lib.ace_mi_kernel_gemm(act_type, epi, M, N, K, a.ctypes.data_as(u16p), w.ctypes.data_as(u16p),
+                                    _fptr(b), None, out.ctypes.data_as(u16p))
+    if st != ACE_GGML_OK:
+        raise RuntimeError(f"ace_mi_kernel_gemm failed (status={st})")
+    return out
+
+
+def kernel_attention(q: np.ndarray, kv: np.ndarray, hq: int, hkv: int, window: int = 0,
+                     kmask: Optional[np.ndarray] = None, scale: Optional[float] = None) -> np.ndarray:
+    """q [B][nq][hq*128] f32, kv [B][nk][2*hkv*128] f32 -> out [B][nq][hq*128] f32 (bf16-rounded)."""
+    lib = load_library()
+    q = np.ascontiguousarray(q, dtype=np.float32)
+    kv = np.ascontiguousarray(kv, dtype=np.float32)
+    B, nq, _ = q.shape
+    nk = kv.shape[1]
+    km = None if kmask is None else np.ascontiguousarray(kmask, dtype=np.int32)
+    out = np.empty_like(q)
+    sc = float(scale) if scale is not None else 1.0 / np.sqrt(128.0)
+    st = lib.ace_mi_kernel_attention(B, hq, hkv, nq, nk, int(window), sc, _fptr(q), _fptr(kv), _iptr(km), _fptr(out))
+    if st != ACE_GGML_OK:
+        raise RuntimeError(f"ace_mi_kernel_attention failed (status={st})")
+    return out

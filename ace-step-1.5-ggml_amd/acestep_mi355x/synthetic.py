@@ -1,0 +1,133 @@
+"""Synthetic DiT checkpoints with the real ACE-Step 1.5 tensor names and shapes.
+
+No checkpoints are available offline, so tests and benchmarks use random
+weights written in the reference's on-disk format: `config.json` with the keys
+read by acestep_dit_config.cpp:58-87 and `model.safetensors` with the
+`decoder.*` names loaded by acestep_dit_model.cpp:870-1082.  2-D weights and
+biases ~ N(0, 0.02); norm weights ~ 1 + N(0, 0.02); AdaLN tables ~ N(0, 0.02).
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import struct
+import tempfile
+from typing import Dict, Iterator, Tuple
+
+import numpy as np
+
+FULL_CONFIG = dict(
+    hidden_size=2048, intermediate_size=6144, num_hidden_layers=24, num_attention_heads=16,
+    num_key_value_heads=8, head_dim=128, max_position_embeddings=32768, rms_norm_eps=1e-6,
+    rope_theta=1000000.0, patch_size=2, in_channels=192, audio_acoustic_hidden_dim=64,
+    use_sliding_window=True, sliding_window=128, attention_bias=False,
+)
+
+
+def make_config(**overrides) -> dict:
+    cfg = dict(FULL_CONFIG)
+    cfg.update(overrides)
+    n = cfg["num_hidden_layers"]
+    # acestep/mlx_dit/model.py:447-451 default: even layers sliding, odd layers full
+    cfg.setdefault("layer_types", ["sliding_attention" if (i + 1) % 2 else "full_attention" for i in range(n)])
+    if len(cfg["layer_types"]) != n:
+        cfg["layer_types"] = ["sliding_attention" if (i + 1) % 2 else "full_attention" for i in range(n)]
+    return cfg
+
+
+TINY_CONFIG = make_config(hidden_size=256, intermediate_size=512, num_hidden_layers=2, num_attention_heads=4,
+                          num_key_value_heads=2, head_dim=128, sliding_window=16)
+
+
+def tensor_specs(cfg: dict) -> Iterator[Tuple[str, Tuple[int, ...], str]]:
+    """(name, shape, kind) for every DiT decoder tensor; kind in {w, b, norm, table}."""
+    H, I, D = cfg["hidden_size"], cfg["intermediate_size"], cfg["head_dim"]
+    hq, hkv = cfg["num_attention_heads"], cfg["num_key_value_heads"]
+    cin, audio, P = cfg["in_channels"], cfg["audio_acoustic_hidden_dim"], cfg["patch_size"]
+    yield "decoder.proj_in.1.weight", (H, cin, P), "w"
+    yield "decoder.proj_in.1.bias", (H,), "b"
+    yield "decoder.proj_out.1.weight", (H, audio, P), "w"
+    yield "decoder.proj_out.1.bias", (audio,), "b"
+    yield "decoder.condition_embedder.weight", (H, H), "w"
+    yield "decoder.condition_embedder.bias", (H,), "b"
+    yield "decoder.norm_out.weight", (H,), "norm"
+    yield "decoder.scale_shift_table", (1, 2, H), "table"
+    for tag in ("time_embed", "time_embed_r"):
+        p = f"decoder.{tag}."
+        yield p + "linear_1.weight", (H, 256), "w"
+        yield p + "linear_1.bias", (H,), "b"
+        yield p + "linear_2.weight", (H, H), "w"
+        yield p + "linear_2.bias", (H,), "b"
+        yield p + "time_proj.weight", (6 * H, H), "w"
+        yield p + "time_proj.bias", (6 * H,), "b"
+    for i in range(cfg["num_hidden_layers"]):
+        p = f"decoder.layers.{i}."
+        yield p + "self_attn_norm.weight", (H,), "norm"
+        for a in ("self_attn", "cross_attn"):
+            yield p + f"{a}.q_proj.weight", (hq * D, H), "w"
+            yield p + f"{a}.k_proj.weight", (hkv * D, H), "w"
+            yield p + f"{a}.v_proj.weight", (hkv * D, H), "w"
+            yield p + f"{a}.o_proj.weight", (H, hq * D), "w"
+            yield p + f"{a}.q_norm.weight", (D,), "norm"
+            yield p + f"{a}.k_norm.weight", (D,), "norm"
+        yield p + "cross_attn_norm.weight", (H,), "norm"
+        yield p + "mlp_norm.weight", (H,), "norm"
+        yield p + "mlp.gate_proj.weight", (I, H), "w"
+        yield p + "mlp.up_proj.weight", (I, H), "w"
+        yield p + "mlp.down_proj.weight", (H, I), "w"
+        yield p + "scale_shift_table", (1, 6, H), "table"
+
+
+def _bf16_bits(x: np.ndarray) -> np.ndarray:
+    u = np.ascontiguousarray(x, dtype=np.float32).view(np.uint32)
+    return ((u + (np.uint32(0x7FFF) + ((u >> np.uint32(16)) & np.uint32(1)))) >> np.uint32(16)).astype("<u2")
+
+
+def _encode(values: np.ndarray, dtype: str) -> bytes:
+    if dtype == "BF16":
+        return _bf16_bits(values).tobytes()
+    if dtype == "F16":
+        return values.astype("<f2").tobytes()
+    if dtype == "F32":
+        return values.astype("<f4").tobytes()
+    raise ValueError(dtype)
+
+
+def write_checkpoint(out_dir: str, cfg: dict, seed: int = 0, dtype: str = "BF16", std: float = 0.02) -> str:
+    """Write config.json + model.safetensors into out_dir; returns out_dir."""
+    os.makedirs(out_dir, exist_ok=True)
+    with open(os.path.join(out_dir, "config.json"), "w", encoding="utf-8") as f:
+        json.dump(cfg, f, indent=1)
+    specs = list(tensor_specs(cfg))
+    esz = {"BF16": 2, "F16": 2, "F32": 4}[dtype]
+    header: Dict[str, dict] = {}
+    off = 0
+    for name, shape, _ in specs:
+        n = int(np.prod(shape)) * esz
+        header[name] = {"dtype": dtype, "shape": list(shape), "data_offsets": [off, off + n]}
+        off += n
+    hjson = json.dumps(header, separators=(",", ":")).encode("utf-8")
+    hjson += b" " * ((8 - len(hjson) % 8) % 8)
+    rng = np.random.default_rng(seed)
+    tmp = os.path.join(out_dir, "model.safetensors.tmp")
+    with open(tmp, "wb") as f:
+        f.write(struct.pack("<Q", len(hjson)))
+        f.write(hjson)
+        for name, shape, kind in specs:
+            v = rng.standard_normal(size=shape, dtype=np.float32) * np.float32(std)
+            if kind == "norm":
+                v = v + np.float32(1.0)
+            f.write(_encode(v, dtype))
+    os.replace(tmp, os.path.join(out_dir, "model.safetensors"))
+    return out_dir
+
+
+def cached_checkpoint(cfg: dict, seed: int = 0, dtype: str = "BF16", root: str | None = None) -> str:
+    """Write the checkpoint once per (cfg, seed, dtype) under a cache dir and reuse it."""
+    key = hashlib.sha1(json.dumps([cfg, seed, dtype], sort_keys=True).encode()).hexdigest()[:16]
+    root = root or os.environ.get("ACE_MI_SYNTH_DIR") or os.path.join(tempfile.gettempdir(), "acestep_mi355x_synth")
+    d = os.path.join(root, key)
+    if not os.path.exists(os.path.join(d, "model.safetensors")):
+        write_checkpoint(d, cfg, seed=seed, dtype=dtype)
+    return d

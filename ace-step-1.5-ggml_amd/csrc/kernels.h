@@ -1,0 +1,104 @@
+// Host-side launch wrappers for the gfx950 kernels (all stream-ordered, no
+// allocation, no synchronisation: safe to capture into a hipGraph).
+#pragma once
+
+#include "common.h"
+
+namespace acemi {
+
+// ---------------------------------------------------------------- GEMM
+// C[M][N] = A[M][K] . W[N][K]^T   (A, W: 16-bit act type, f32 accumulate)
+// followed by a fused epilogue.  N % 128 == 0, K % 64 == 0, M >= 1.
+enum GemmEpiKind : int {
+    EPI_STORE_F32 = 0,      // c_f32[m*ldc+n] = acc (+ bias[n])
+    EPI_STORE_ACT = 1,      // c_act[m*ldc+n] = act(acc (+ bias[n]))
+    EPI_RESID_GATED = 2,    // c_f32[m*ldc+n] += acc * gate[(m / rows_per_item)*gate_stride + n]
+    EPI_RESID = 3,          // c_f32[m*ldc+n] += acc
+    EPI_SWIGLU = 4,         // columns interleaved [g0..15,u0..15,g16..]: c_act[m*ldc + n'] = act(silu(g)*u)
+    EPI_PROJ_OUT = 5,       // c_f32[b][2p+k][c] = acc[m=(b,p)][n = c + k*out_ch] + bias[c], cropped to T
+};
+
+struct GemmEpilogue {
+    int kind = EPI_STORE_F32;
+    const float* bias = nullptr;
+    float* c_f32 = nullptr;
+    uint16_t* c_act = nullptr;
+    int ldc = 0;
+    const float* gate = nullptr;
+    int64_t gate_stride = 0;
+    int rows_per_item = 1;
+    int out_T = 0;        // EPI_PROJ_OUT: frames per item
+    int out_ch = 0;       // EPI_PROJ_OUT: channels (64)
+    int patch = 2;        // EPI_PROJ_OUT
+};
+
+void launch_gemm(ActType t, const uint16_t* A, int lda, const uint16_t* W, int ldw, int M, int N, int K,
+                 const GemmEpilogue& epi, hipStream_t s);
+
+// ------------------------------------------------------------ attention
+// Flash-style fp16 attention, f32 softmax/accumulate.  D = 128.
+// Qh [B][Hq][nq_pad][128] f16, Kh [B][Hkv][nk_pad][128] f16,
+// Vt [B][Hkv][128][nk_pad] f16 (keys permuted within groups of 16, see ops.hip),
+// kbias [B][nk_pad] f32 additive (0 / -inf) or null, out act [B*nq][Hq*128].
+struct AttnArgs {
+    const uint16_t* q;
+    const uint16_t* k;
+    const uint16_t* vt;
+    const float* kbias;
+    uint16_t* out;
+    int B, Hq, Hkv;
+    int nq, nq_pad, nk, nk_pad;
+    int window;  // >0: bidirectional sliding window |q-k| <= window
+    float scale;
+};
+void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s);
+
+// ------------------------------------------------------------ elementwise
+// Pack [context | hidden] frames into patches: out act [B*Np][P*Cin].
+void launch_pack_input(ActType t, const float* hidden, const float* context, int B, int T, int Np, int P,
+                       int audio_dim, int ctx_dim, uint16_t* out, hipStream_t s);
+// f32 -> act conversion (row-major copy), optionally act(silu(x)).
+void launch_to_act(ActType t, const float* in, int64_t n, bool silu, uint16_t* out, hipStream_t s);
+// y = act( RMSNorm(x) * w * (1 + scale) + shift ); scale/shift optional, per item
+// (item = row / rows_per_item, stride mod_stride floats).
+void launch_rmsnorm_mod(ActType t, const float* x, int M, int H, const float* w, const float* scale,
+                        const float* shift, int64_t mod_stride, int rows_per_item, float eps, uint16_t* out,
+                        hipStream_t s);
+// Per-head RMSNorm (+ NEOX RoPE) of the q/k sections and f16 re-layout for attention.
+struct PrepArgs {
+    const float* src;
+    int ld;
+    int q_col, k_col, v_col;  // -1: section absent
+    int hq, hkv;
+    int n_tok, n_pad, B;
+    const float* q_norm;
+    const float* k_norm;
+    const float* rope_cos;  // [n_tok][64] or null
+    const float* rope_sin;
+    float eps;
+    uint16_t* qh;
+    uint16_t* kh;
+    uint16_t* vt;
+};
+void launch_attn_prep(const PrepArgs& a, hipStream_t s);
+// kbias[b][k] = (k < nk && pooled mask) ? 0 : -inf ; mask [B][nk*patch-ish frames] or null.
+void launch_key_bias(const int32_t* mask, int B, int frames, int patch, int nk, int nk_pad, float* kbias,
+                     hipStream_t s);
+// Sinusoidal timestep features f[b][256] of t[b] - (r ? r[b] : 0) (acestep_dit_model.cpp:1261-1284).
+// log_max = logf(10000) evaluated on the host exactly as the reference does.
+void launch_timestep_freq(const float* t, const float* r, int B, int dim, float scale, float log_max, float* f,
+                          hipStream_t s);
+// Small-M GEMV (timestep MLPs): v = sum_k x_act[m][k] W[n][k] + bias[n]; v = silu(v) if silu_out;
+// y[m][n] = accumulate ? y[m][n] + v : v.  M <= 8, K % 512 == 0.
+void launch_gemv(ActType t, const uint16_t* x_act, int M, const uint16_t* W, int N, int K, const float* bias,
+                 bool silu_out, bool accumulate, float* y, hipStream_t s);
+// mod[l][b][j][c] = table[l][j][c] + proj[b][j*H + c]  (j < 6)
+void launch_layer_mods(const float* tables, const float* proj, int n_layers, int B, int H, float* mod,
+                       hipStream_t s);
+// outmod[b][j][c] = out_table[j][c] + (temb_t[b][c] + temb_r[b][c]) (j < 2)
+void launch_out_mods(const float* out_table, const float* temb_t, const float* temb_r, int B, int H,
+                     float* outmod, hipStream_t s);
+// xt -= v * dt
+void launch_euler(float* xt, const float* v, int64_t n, float dt, hipStream_t s);
+
+}  // namespace acemi

@@ -1,0 +1,412 @@
+// Memory-bound kernels around the DiT GEMMs and attention (gfx950).
+// Each kernel cites the ggml graph nodes of ace_dit::forward_dit it fuses.
+#include "../kernels.h"
+
+namespace acemi {
+namespace {
+
+__device__ __forceinline__ uint16_t f32_to_bf16_rne(float f) {
+    uint32_t u = __float_as_uint(f);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 64u);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+__device__ __forceinline__ uint16_t f32_to_f16(float f) {
+    _Float16 h = (_Float16)f;
+    return __builtin_bit_cast(uint16_t, h);
+}
+__device__ __forceinline__ uint16_t to_act(bool f16, float f) { return f16 ? f32_to_f16(f) : f32_to_bf16_rne(f); }
+__device__ __forceinline__ float act_to_f32(bool f16, uint16_t v) {
+    if (f16) return (float)__builtin_bit_cast(_Float16, v);
+    return __uint_as_float((uint32_t)v << 16);
+}
+__device__ __forceinline__ float silu_f(float x) { return x / (1.0f + expf(-x)); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// ---------------------------------------------------------------- pack
+// input pack + patchify (acestep_dit_model.cpp:1350-1380): x0[t] = concat(context[t], hidden[t]),
+// zero padded to a multiple of the patch, viewed as [Np][P*Cin] (index k*Cin + c).
+__global__ void pack_input_kernel(bool f16, const float* __restrict__ hidden, const float* __restrict__ context,
+                                  int B, int T, int Np, int P, int audio, int cdim, uint16_t* __restrict__ out) {
+    const int cin = audio + cdim;
+    const int64_t total = (int64_t)B * Np * P * cin;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(i % cin);
+        int64_t r = i / cin;
+        const int k = (int)(r % P);
+        r /= P;
+        const int p = (int)(r % Np);
+        const int b = (int)(r / Np);
+        const int t = p * P + k;
+        float v = 0.f;
+        if (t < T) {
+            if (c < cdim) {
+                if (context) v = context[((int64_t)b * T + t) * cdim + c];
+            } else {
+                if (hidden) v = hidden[((int64_t)b * T + t) * audio + (c - cdim)];
+            }
+        }
+        out[i] = to_act(f16, v);
+    }
+}
+
+__global__ void to_act_kernel(bool f16, const float* __restrict__ in, int64_t n, bool silu, uint16_t* __restrict__ out) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        float v = in[i];
+        if (silu) v = silu_f(v);
+        out[i] = to_act(f16, v);
+    }
+}
+
+// ------------------------------------------------------------ rmsnorm
+// rms_norm (:1097-1106) + AdaLN modulate (:1477-1481, :1522-1526, :1545-1549):
+// y = ((x * 1/sqrt(mean(x^2)+eps)) * w) * (1 + scale) + shift, written in the act type that the
+// following mul_mat converts it to.
+template <bool F16>
+__global__ void __launch_bounds__(256) rmsnorm_mod_kernel(const float* __restrict__ x, int H, const float* __restrict__ w,
+                                                          const float* __restrict__ scale, const float* __restrict__ shift,
+                                                          int64_t mod_stride, int rows_per_item, float eps,
+                                                          uint16_t* __restrict__ out) {
+    const int m = blockIdx.x;
+    const float* xr = x + (int64_t)m * H;
+    __shared__ float red[4];
+    float ss = 0.f;
+    for (int i = threadIdx.x * 4; i < H; i += 1024) {
+        const float4 v = *(const float4*)(xr + i);
+        ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+    }
+    ss = wave_sum(ss);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+    __syncthreads();
+    const float tot = red[0] + red[1] + red[2] + red[3];
+    const float mean = tot / (float)H;
+    const float sc = 1.0f / sqrtf(mean + eps);
+    const int item = m / rows_per_item;
+    const float* scp = scale ? scale + (int64_t)item * mod_stride : nullptr;
+    const float* shp = shift ? shift + (int64_t)item * mod_stride : nullptr;
+    uint16_t* orow = out + (int64_t)m * H;
+    for (int i = threadIdx.x * 4; i < H; i += 1024) {
+        const float4 v = *(const float4*)(xr + i);
+        float y[4] = {v.x, v.y, v.z, v.w};
+        uint16_t o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float t = __fmul_rn(y[j], sc);
+            t = __fmul_rn(t, w[i + j]);
+            if (scp) t = __fadd_rn(__fmul_rn(t, __fadd_rn(scp[i + j], 1.0f)), shp[i + j]);
+            o[j] = F16 ? f32_to_f16(t) : f32_to_bf16_rne(t);
+        }
+        uint2 pk;
+        pk.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
+        pk.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
+        *(uint2*)(orow + i) = pk;
+    }
+}
+
+// ------------------------------------------------------------ attention prep
+// QK-RMSNorm over head_dim (:1202-1203), NEOX RoPE (:1205-1210), the permute/cont copies
+// (:1212-1231) and the V transpose for the P.V MFMA: writes
+//   qh [B][hq][n_pad][128], kh [B][hkv][n_pad][128]  (f16, rows >= n_tok zero)
+//   vt [B][hkv][128][n_pad] (f16, key position permuted inside each 16-group: positions
+//      4..7 <-> 8..11, the k order of the attention kernel's P^T operand)
+__device__ __forceinline__ int vperm(int k) {
+    const int w = k & 15;
+    const int g = w >> 2;
+    const int gp = (g == 1) ? 2 : (g == 2 ? 1 : g);
+    return (k & ~15) | (gp << 2) | (w & 3);
+}
+
+__global__ void __launch_bounds__(256) attn_prep_kernel(PrepArgs a) {
+    __shared__ float vs[64][129];
+    const int b = blockIdx.y;
+    const int n0 = blockIdx.x * 64;
+    const int lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
+    const int nq = a.q_col >= 0 ? a.hq : 0;
+    const int nk = a.k_col >= 0 ? a.hkv : 0;
+    const int nh = nq + nk;
+    for (int idx = wid; idx < 64 * nh; idx += 4) {
+        const int tok = idx / nh;
+        const int hh = idx % nh;
+        const int n = n0 + tok;
+        const bool isq = hh < nq;
+        const int head = isq ? hh : hh - nq;
+        float r0 = 0.f, r1 = 0.f;
+        if (n < a.n_tok) {
+            const float* row = a.src + ((int64_t)b * a.n_tok + n) * a.ld + (isq ? a.q_col : a.k_col) + head * 128;
+            const float x0 = row[lane];
+            const float x1 = row[lane + 64];
+            const float* w = isq ? a.q_norm : a.k_norm;
+            float y0 = x0, y1 = x1;
+            if (w) {  // null weight: plain copy (kernel self-test entry)
+                const float ss = wave_sum(x0 * x0 + x1 * x1);
+                const float sc = 1.0f / sqrtf(ss / 128.0f + a.eps);
+                y0 = __fmul_rn(__fmul_rn(x0, sc), w[lane]);
+                y1 = __fmul_rn(__fmul_rn(x1, sc), w[lane + 64]);
+            }
+            if (a.rope_cos) {
+                const float c = a.rope_cos[(int64_t)n * 64 + lane];
+                const float s = a.rope_sin[(int64_t)n * 64 + lane];
+                r0 = __fsub_rn(__fmul_rn(y0, c), __fmul_rn(y1, s));
+                r1 = __fadd_rn(__fmul_rn(y0, s), __fmul_rn(y1, c));
+            } else {
+                r0 = y0;
+                r1 = y1;
+            }
+        }
+        uint16_t* dst = isq ? a.qh + (((int64_t)b * a.hq + head) * a.n_pad + n) * 128
+                            : a.kh + (((int64_t)b * a.hkv + head) * a.n_pad + n) * 128;
+        dst[lane] = f32_to_f16(r0);
+        dst[lane + 64] = f32_to_f16(r1);
+    }
+    if (a.v_col < 0) return;
+    for (int hk = 0; hk < a.hkv; ++hk) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < 64 * 128; i += 256) {
+            const int tok = i >> 7;
+            const int d = i & 127;
+            const int n = n0 + tok;
+            float v = 0.f;
+            if (n < a.n_tok) v = a.src[((int64_t)b * a.n_tok + n) * a.ld + a.v_col + hk * 128 + d];
+            vs[tok][d] = v;
+        }
+        __syncthreads();
+        const int d = threadIdx.x >> 1;
+        const int half = threadIdx.x & 1;
+        uint16_t* dst = a.vt + (((int64_t)b * a.hkv + hk) * 128 + d) * a.n_pad + n0 + half * 32;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            uint32_t wv[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int p0 = half * 32 + c * 8 + 2 * j;
+                const float v0 = vs[vperm(p0)][d];
+                const float v1 = vs[vperm(p0 + 1)][d];
+                wv[j] = (uint32_t)f32_to_f16(v0) | ((uint32_t)f32_to_f16(v1) << 16);
+            }
+            *(uint4*)(dst + c * 8) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+        }
+    }
+}
+
+// ------------------------------------------------------------ masks
+// patch-pooled key mask (:1433-1449) / encoder key mask, as an additive bias.
+__global__ void key_bias_kernel(const int32_t* __restrict__ mask, int B, int frames, int patch, int nk, int nk_pad,
+                                float* __restrict__ kbias) {
+    const int64_t total = (int64_t)B * nk_pad;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int b = (int)(i / nk_pad);
+        const int k = (int)(i % nk_pad);
+        bool ok = k < nk;
+        if (ok && mask) {
+            bool any = false;
+            for (int j = 0; j < patch; ++j) {
+                const int f = k * patch + j;
+                if (f < frames && mask[(int64_t)b * frames + f] != 0) any = true;
+            }
+            ok = any;
+        }
+        kbias[i] = ok ? 0.f : -INFINITY;
+    }
+}
+
+// ------------------------------------------------------------ timestep
+// build_timestep_freq (:1261-1284) for t[b] - r[b] (r optional; the second embedder
+// takes timestep - timestep_r, :1421).
+__global__ void timestep_freq_kernel(const float* __restrict__ t, const float* __restrict__ r, int B, int dim,
+                                     float scale, float log_max, float* __restrict__ f) {
+    const int b = blockIdx.x;
+    const int half = dim / 2;
+    float tv = t[b];
+    if (r) tv = __fsub_rn(tv, r[b]);
+    const float ts = __fmul_rn(tv, scale);
+    for (int i = threadIdx.x; i < half; i += blockDim.x) {
+        const float expo = __fdiv_rn(__fmul_rn(-log_max, (float)i), (float)half);
+        const float fr = expf(expo);
+        const float arg = __fmul_rn(ts, fr);
+        f[(int64_t)b * dim + i] = cosf(arg);
+        f[(int64_t)b * dim + i + half] = sinf(arg);
+    }
+    if ((dim & 1) && threadIdx.x == 0) f[(int64_t)b * dim + dim - 1] = 0.f;
+}
+
+// small-M GEMV: one wave computes 4 output columns for all M rows.
+template <bool F16>
+__global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ x, int M, const uint16_t* __restrict__ W,
+                                                   int N, int K, const float* __restrict__ bias, bool silu_out,
+                                                   bool accumulate, float* __restrict__ y) {
+    const int lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
+    const int n0 = (blockIdx.x * 4 + wid) * 4;
+    if (n0 >= N) return;
+    float acc[8][4];
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[m][c] = 0.f;
+    for (int k = lane * 8; k < K; k += 512) {
+        float wf[4][8];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint4 wv = *(const uint4*)(W + (int64_t)(n0 + c) * K + k);
+            const uint16_t* ws = (const uint16_t*)&wv;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) wf[c][j] = act_to_f32(F16, ws[j]);
+        }
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            if (m < M) {
+                const uint4 xv = *(const uint4*)(x + (int64_t)m * K + k);
+                const uint16_t* xs = (const uint16_t*)&xv;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float xf = act_to_f32(F16, xs[j]);
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) acc[m][c] = fmaf(xf, wf[c][j], acc[m][c]);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+        if (m < M) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                float v = wave_sum(acc[m][c]);
+                if (lane == 0) {
+                    if (bias) v = __fadd_rn(v, bias[n0 + c]);
+                    if (silu_out) v = silu_f(v);
+                    float* yp = y + (int64_t)m * N + n0 + c;
+                    *yp = accumulate ? __fadd_rn(*yp, v) : v;
+                }
+            }
+        }
+    }
+}
+
+// AdaLN tables (:1469-1475): mod = scale_shift_table + timestep proj.
+__global__ void layer_mods_kernel(const float* __restrict__ tables, const float* __restrict__ proj, int L, int B, int H,
+                                  float* __restrict__ mod) {
+    const int64_t total = (int64_t)L * B * 6 * H;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(i % H);
+        int64_t r = i / H;
+        const int j = (int)(r % 6);
+        r /= 6;
+        const int b = (int)(r % B);
+        const int l = (int)(r / B);
+        mod[i] = __fadd_rn(tables[((int64_t)l * 6 + j) * H + c], proj[((int64_t)b * 6 + j) * H + c]);
+    }
+}
+
+// output AdaLN (:1537-1543): (shift, scale) = out_table + (temb_t + temb_r).
+__global__ void out_mods_kernel(const float* __restrict__ table, const float* __restrict__ tt, const float* __restrict__ tr,
+                                int B, int H, float* __restrict__ om) {
+    const int64_t total = (int64_t)B * 2 * H;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(i % H);
+        const int j = (int)((i / H) % 2);
+        const int b = (int)(i / (2 * H));
+        const float temb = __fadd_rn(tt[(int64_t)b * H + c], tr[(int64_t)b * H + c]);
+        om[i] = __fadd_rn(table[(int64_t)j * H + c], temb);
+    }
+}
+
+__global__ void euler_kernel(float* __restrict__ xt, const float* __restrict__ v, int64_t n, float dt) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        xt[i] = __fsub_rn(xt[i], __fmul_rn(v[i], dt));
+}
+
+inline dim3 grid_for(int64_t n, int block = 256) {
+    int64_t g = (n + block - 1) / block;
+    if (g > 8192) g = 8192;
+    if (g < 1) g = 1;
+    return dim3((unsigned)g);
+}
+
+}  // namespace
+
+void launch_pack_input(ActType t, const float* hidden, const float* context, int B, int T, int Np, int P,
+                       int audio_dim, int ctx_dim, uint16_t* out, hipStream_t s) {
+    const int64_t n = (int64_t)B * Np * P * (audio_dim + ctx_dim);
+    hipLaunchKernelGGL(pack_input_kernel, grid_for(n), dim3(256), 0, s, t == ActType::F16, hidden, context, B, T, Np,
+                       P, audio_dim, ctx_dim, out);
+    ACEMI_HIP(hipGetLastError());
+}
+
+void launch_to_act(ActType t, const float* in, int64_t n, bool silu, uint16_t* out, hipStream_t s) {
+    hipLaunchKernelGGL(to_act_kernel, grid_for(n), dim3(256), 0, s, t == ActType::F16, in, n, silu, out);
+    ACEMI_HIP(hipGetLastError());
+}
+
+void launch_rmsnorm_mod(ActType t, const float* x, int M, int H, const float* w, const float* scale,
+                        const float* shift, int64_t mod_stride, int rows_per_item, float eps, uint16_t* out,
+                        hipStream_t s) {
+    ACEMI_CHECK(H % 4 == 0, "rmsnorm: H % 4");
+    if (t == ActType::F16)
+        hipLaunchKernelGGL(rmsnorm_mod_kernel<true>, dim3(M), dim3(256), 0, s, x, H, w, scale, shift, mod_stride,
+                           rows_per_item, eps, out);
+    else
+        hipLaunchKernelGGL(rmsnorm_mod_kernel<false>, dim3(M), dim3(256), 0, s, x, H, w, scale, shift, mod_stride,
+                           rows_per_item, eps, out);
+    ACEMI_HIP(hipGetLastError());
+}
+
+void launch_attn_prep(const PrepArgs& a, hipStream_t s) {
+    ACEMI_CHECK(a.n_pad % 64 == 0, "attn_prep: n_pad % 64");
+    hipLaunchKernelGGL(attn_prep_kernel, dim3(a.n_pad / 64, a.B), dim3(256), 0, s, a);
+    ACEMI_HIP(hipGetLastError());
+}
+
+void launch_key_bias(const int32_t* mask, int B, int frames, int patch, int nk, int nk_pad, float* kbias,
+                     hipStream_t s) {
+    const int64_t n = (int64_t)B * nk_pad;
+    hipLaunchKernelGGL(key_bias_kernel, grid_for(n), dim3(256), 0, s, mask, B, frames, patch, nk, nk_pad, kbias);
+    ACEMI_HIP(hipGetLastError());
+}
+
+void launch_timestep_freq(const float* t, const float* r, int B, int dim, float scale, float log_max, float* f,
+                          hipStream_t s) {
+    hipLaunchKernelGGL(timestep_freq_kernel, dim3(B), dim3(128), 0, s, t, r, B, dim, scale, log_max, f);
+    ACEMI_HIP(hipGetLastError());
+}
+
+void launch_gemv(ActType t, const uint16_t* x_act, int M, const uint16_t* W, int N, int K, const float* bias,
+                 bool silu_out, bool accumulate, float* y, hipStream_t s) {
+    ACEMI_CHECK(M >= 1 && M <= 8, "gemv: M must be 1..8");
+    ACEMI_CHECK(N % 16 == 0 && K % 8 == 0, "gemv: N % 16, K % 8");
+    const dim3 grid(N / 16);
+    if (t == ActType::F16)
+        hipLaunchKernelGGL(gemv_kernel<true>, grid, dim3(256), 0, s, x_act, M, W, N, K, bias, silu_out, accumulate,
+                           y);
+    else
+        hipLaunchKernelGGL(gemv_kernel<false>, grid, dim3(256), 0, s, x_act, M, W, N, K, bias, silu_out, accumulate,
+                           y);
+    ACEMI_HIP(hipGetLastError());
+}
+
+void launch_layer_mods(const float* tables, const float* proj, int n_layers, int B, int H, float* mod,
+                       hipStream_t s) {
+    const int64_t n = (int64_t)n_layers * B * 6 * H;
+    hipLaunchKernelGGL(layer_mods_kernel, grid_for(n), dim3(256), 0, s, tables, proj, n_layers, B, H, mod);
+    ACEMI_HIP(hipGetLastError());
+}
+
+void launch_out_mods(const float* out_table, const float* temb_t, const float* temb_r, int B, int H,
+                     float* outmod, hipStream_t s) {
+    const int64_t n = (int64_t)B * 2 * H;
+    hipLaunchKernelGGL(out_mods_kernel, grid_for(n), dim3(256), 0, s, out_table, temb_t, temb_r, B, H, outmod);
+    ACEMI_HIP(hipGetLastError());
+}
+
+void launch_euler(float* xt, const float* v, int64_t n, float dt, hipStream_t s) {
+    hipLaunchKernelGGL(euler_kernel, grid_for(n), dim3(256), 0, s, xt, v, n, dt);
+    ACEMI_HIP(hipGetLastError());
+}
+
+}  // namespace acemi

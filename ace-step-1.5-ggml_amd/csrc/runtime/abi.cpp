@@ -1,0 +1,392 @@
+// extern "C" entry points of libacestep_mi355x.so (include/acestep_ggml.h, include/acestep_mi355x.h).
+//
+// Status/error behaviour follows the reference implementation
+// (acestep_ggml/cpp/acestep_ggml.cpp:65-70 ace_set_error, :108-194 create,
+// :230-236 last_error, :260-357 load_dit, :1304-1482 dit_forward).
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../../include/acestep_mi355x.h"
+#include "engine.h"
+
+struct ace_ggml_context {
+    int32_t n_threads = 0;
+    bool use_metal = false;
+    size_t compute_buffer_bytes = 0;
+    std::string last_error;
+    int device = -1;
+    hipStream_t stream = nullptr;
+    std::unique_ptr<acemi::DitEngine> dit;
+    // host-ABI staging (device)
+    void* d_in = nullptr;
+    size_t d_in_bytes = 0;
+    // sampler scratch
+    float* d_v = nullptr;
+    size_t d_v_bytes = 0;
+    float* d_sched = nullptr;
+    size_t d_sched_bytes = 0;
+};
+
+namespace {
+
+ace_ggml_status set_error(ace_ggml_context* ctx, ace_ggml_status code, const std::string& msg) {
+    if (ctx) ctx->last_error = msg;
+    return code;
+}
+
+bool env_enabled(const char* key) {
+    const char* v = std::getenv(key);
+    return v && v[0] && std::strcmp(v, "0") != 0;
+}
+
+int env_int(const char* key, int fallback) {
+    const char* v = std::getenv(key);
+    if (!v || !v[0]) return fallback;
+    char* end = nullptr;
+    const long long x = std::strtoll(v, &end, 10);
+    return (end && end != v) ? static_cast<int>(x) : fallback;
+}
+
+// ACE_GGML_DIT_MAX_LAYERS (acestep_dit_model.cpp:1457-1464)
+int max_layers_env() {
+    const int v = env_int("ACE_GGML_DIT_MAX_LAYERS", -1);
+    return v > 0 ? v : -1;
+}
+
+void bind_device(ace_ggml_context* ctx) {
+    if (ctx->device < 0) {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) throw std::runtime_error("no HIP device available");
+        ctx->device = env_int("ACE_MI_DEVICE", 0);
+        if (ctx->device >= n) throw std::runtime_error("ACE_MI_DEVICE out of range");
+    }
+    ACEMI_HIP(hipSetDevice(ctx->device));
+    if (!ctx->stream) ACEMI_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+}
+
+void ensure_dev(void*& p, size_t& have, size_t need) {
+    if (have >= need) return;
+    if (p) ACEMI_HIP(hipFree(p));
+    p = nullptr;
+    have = 0;
+    ACEMI_HIP(hipMalloc(&p, need));
+    have = need;
+}
+
+}  // namespace
+
+extern "C" {
+
+ace_ggml_status ace_ggml_create(const ace_ggml_init_params* params, ace_ggml_context** out_ctx) {
+    if (!out_ctx) return ACE_GGML_ERR_INVALID_ARG;
+    ace_ggml_context* ctx = new (std::nothrow) ace_ggml_context();
+    if (!ctx) return ACE_GGML_ERR;
+    if (params) {
+        ctx->n_threads = params->n_threads;
+        ctx->use_metal = params->use_metal != 0;
+        ctx->compute_buffer_bytes = params->compute_buffer_bytes;
+    }
+    if (ctx->compute_buffer_bytes == 0) ctx->compute_buffer_bytes = 512ULL * 1024ULL * 1024ULL;
+    *out_ctx = ctx;
+    return ACE_GGML_OK;
+}
+
+ace_ggml_status ace_mi_create_on_device(const ace_ggml_init_params* params, int32_t device,
+                                        ace_ggml_context** out_ctx) {
+    ace_ggml_status st = ace_ggml_create(params, out_ctx);
+    if (st != ACE_GGML_OK) return st;
+    if (device < 0) {
+        ace_ggml_destroy(*out_ctx);
+        *out_ctx = nullptr;
+        return ACE_GGML_ERR_INVALID_ARG;
+    }
+    (*out_ctx)->device = device;
+    return ACE_GGML_OK;
+}
+
+void ace_ggml_destroy(ace_ggml_context* ctx) {
+    if (!ctx) return;
+    if (ctx->device >= 0) (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    ctx->dit.reset();
+    if (ctx->d_in) (void)hipFree(ctx->d_in);
+    if (ctx->d_v) (void)hipFree(ctx->d_v);
+    if (ctx->d_sched) (void)hipFree(ctx->d_sched);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char* ace_ggml_last_error(const ace_ggml_context* ctx) {
+    if (!ctx) return "ace_ggml_last_error: null context";
+    return ctx->last_error.c_str();
+}
+
+ace_ggml_status ace_ggml_load_dit(ace_ggml_context* ctx, const char* model_dir) {
+    if (!ctx || !model_dir) return ACE_GGML_ERR_INVALID_ARG;
+    int hint = 3;
+    try {
+        bind_device(ctx);
+        ACEMI_HIP(hipStreamSynchronize(ctx->stream));
+        ctx->dit.reset();
+        auto eng = std::make_unique<acemi::DitEngine>(ctx->device);
+        acemi::load_dit_model(model_dir, eng->model(), hint);
+        ctx->dit = std::move(eng);
+    } catch (const acemi::HipError& e) {
+        ctx->dit.reset();
+        return set_error(ctx, ACE_GGML_ERR, e.what());
+    } catch (const std::exception& e) {
+        ctx->dit.reset();
+        return set_error(ctx, hint == 4 ? ACE_GGML_ERR_UNSUPPORTED : (hint == 1 ? ACE_GGML_ERR : ACE_GGML_ERR_IO),
+                         e.what());
+    }
+    return ACE_GGML_OK;
+}
+
+ace_ggml_status ace_ggml_dit_forward(ace_ggml_context* ctx, const float* hidden_states, const float* context_latents,
+                                     const float* encoder_hidden_states, const int32_t* attention_mask,
+                                     const int32_t* encoder_attention_mask, int32_t seq_len, int32_t enc_len,
+                                     float timestep, float timestep_r, float* out, size_t out_size) {
+    if (!ctx || !out || seq_len <= 0) return ACE_GGML_ERR_INVALID_ARG;
+    if (!ctx->dit) return set_error(ctx, ACE_GGML_ERR, "dit not loaded");
+    const acemi::DitConfig& c = ctx->dit->model().cfg;
+    const int audio = c.audio_dim, cdim = c.ctx_dim(), H = c.hidden;
+    const size_t needed = (size_t)audio * (size_t)seq_len * sizeof(float);
+    if (out_size < needed) return set_error(ctx, ACE_GGML_ERR_INVALID_ARG, "output buffer too small");
+    const int L = enc_len > 0 ? enc_len : 0;
+    if (L > 0 && !encoder_hidden_states) return set_error(ctx, ACE_GGML_ERR, "dit forward failed");
+    const bool profile = env_enabled("ACE_GGML_DIT_PROFILE");
+    try {
+        const auto t0 = std::chrono::steady_clock::now();
+        bind_device(ctx);
+        hipStream_t s = ctx->stream;
+        // device staging layout: hidden | context | enc | mask | enc_mask | t | r | out
+        const size_t n_h = (size_t)seq_len * audio, n_c = (size_t)seq_len * cdim, n_e = (size_t)L * H;
+        auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+        const size_t o_h = 0, o_c = o_h + al(n_h * 4), o_e = o_c + al(n_c * 4), o_m = o_e + al(n_e * 4),
+                     o_em = o_m + al((size_t)seq_len * 4), o_t = o_em + al((size_t)L * 4 + 4), o_out = o_t + 256,
+                     total = o_out + al(n_h * 4);
+        ensure_dev(ctx->d_in, ctx->d_in_bytes, total);
+        char* base = static_cast<char*>(ctx->d_in);
+        acemi::ForwardIO io;
+        io.B = 1;
+        io.T = seq_len;
+        io.L = L;
+        if (hidden_states) {
+            ACEMI_HIP(hipMemcpyAsync(base + o_h, hidden_states, n_h * 4, hipMemcpyHostToDevice, s));
+            io.hidden = reinterpret_cast<const float*>(base + o_h);
+        }
+        if (context_latents) {
+            ACEMI_HIP(hipMemcpyAsync(base + o_c, context_latents, n_c * 4, hipMemcpyHostToDevice, s));
+            io.context = reinterpret_cast<const float*>(base + o_c);
+        }
+        if (L > 0) {
+            ACEMI_HIP(hipMemcpyAsync(base + o_e, encoder_hidden_states, n_e * 4, hipMemcpyHostToDevice, s));
+            io.enc = reinterpret_cast<const float*>(base + o_e);
+        }
+        if (attention_mask) {
+            ACEMI_HIP(hipMemcpyAsync(base + o_m, attention_mask, (size_t)seq_len * 4, hipMemcpyHostToDevice, s));
+            io.mask = reinterpret_cast<const int32_t*>(base + o_m);
+        }
+        if (encoder_attention_mask && L > 0) {
+            ACEMI_HIP(hipMemcpyAsync(base + o_em, encoder_attention_mask, (size_t)L * 4, hipMemcpyHostToDevice, s));
+            io.enc_mask = reinterpret_cast<const int32_t*>(base + o_em);
+        }
+        const float tr[2] = {timestep, timestep_r};
+        ACEMI_HIP(hipMemcpyAsync(base + o_t, tr, 8, hipMemcpyHostToDevice, s));
+        io.t = reinterpret_cast<const float*>(base + o_t);
+        io.r = reinterpret_cast<const float*>(base + o_t + 4);
+        io.out = reinterpret_cast<float*>(base + o_out);
+        io.max_layers = max_layers_env();
+        ACEMI_HIP(hipStreamSynchronize(s));
+        const auto t1 = std::chrono::steady_clock::now();
+        ctx->dit->forward(io, s);
+        ACEMI_HIP(hipStreamSynchronize(s));
+        const auto t2 = std::chrono::steady_clock::now();
+        ACEMI_HIP(hipMemcpyAsync(out, io.out, needed, hipMemcpyDeviceToHost, s));
+        ACEMI_HIP(hipStreamSynchronize(s));
+        const auto t3 = std::chrono::steady_clock::now();
+        if (profile) {
+            using ms = std::chrono::duration<double, std::milli>;
+            std::fprintf(stderr,
+                         "ace_ggml_dit_forward profile: backend=mi355x seq=%d enc=%d device=%d upload_ms=%.3f "
+                         "compute_ms=%.3f copy_ms=%.3f total_ms=%.3f\n",
+                         seq_len, L, ctx->device, ms(t1 - t0).count(), ms(t2 - t1).count(), ms(t3 - t2).count(),
+                         ms(t3 - t0).count());
+        }
+    } catch (const std::exception& e) {
+        return set_error(ctx, ACE_GGML_ERR, std::string("dit forward failed: ") + e.what());
+    }
+    return ACE_GGML_OK;
+}
+
+ace_ggml_status ace_mi_dit_get_info(ace_ggml_context* ctx, ace_mi_dit_info* out) {
+    if (!ctx || !out) return ACE_GGML_ERR_INVALID_ARG;
+    if (!ctx->dit) return set_error(ctx, ACE_GGML_ERR, "dit not loaded");
+    const auto& m = ctx->dit->model();
+    const auto& c = m.cfg;
+    out->hidden_size = c.hidden;
+    out->intermediate_size = c.intermediate;
+    out->num_layers = c.layers;
+    out->num_heads = c.hq;
+    out->num_kv_heads = c.hkv;
+    out->head_dim = c.head_dim;
+    out->patch_size = c.patch;
+    out->in_channels = c.in_channels;
+    out->audio_dim = c.audio_dim;
+    out->sliding_window = c.sliding_window;
+    out->act_type = static_cast<int32_t>(m.act);
+    out->device = ctx->device;
+    out->weight_bytes = static_cast<int64_t>(m.weight_bytes);
+    return ACE_GGML_OK;
+}
+
+ace_ggml_status ace_mi_dit_forward_batched(ace_ggml_context* ctx, int32_t batch, const float* d_hidden,
+                                           const float* d_context, const float* d_enc, const int32_t* d_mask,
+                                           const int32_t* d_enc_mask, int32_t seq_len, int32_t enc_len,
+                                           const float* d_timestep, const float* d_timestep_r, float* d_out,
+                                           void* stream) {
+    if (!ctx || !d_out || seq_len <= 0 || batch <= 0 || !d_timestep || !d_timestep_r)
+        return ACE_GGML_ERR_INVALID_ARG;
+    if (!ctx->dit) return set_error(ctx, ACE_GGML_ERR, "dit not loaded");
+    if (enc_len > 0 && !d_enc) return set_error(ctx, ACE_GGML_ERR_INVALID_ARG, "encoder_hidden_states is null");
+    try {
+        bind_device(ctx);
+        hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+        acemi::ForwardIO io;
+        io.B = batch;
+        io.T = seq_len;
+        io.L = enc_len > 0 ? enc_len : 0;
+        io.hidden = d_hidden;
+        io.context = d_context;
+        io.enc = d_enc;
+        io.mask = d_mask;
+        io.enc_mask = d_enc_mask;
+        io.t = d_timestep;
+        io.r = d_timestep_r;
+        io.out = d_out;
+        io.max_layers = max_layers_env();
+        ctx->dit->forward(io, s);
+    } catch (const std::exception& e) {
+        return set_error(ctx, ACE_GGML_ERR, std::string("dit forward failed: ") + e.what());
+    }
+    return ACE_GGML_OK;
+}
+
+ace_ggml_status ace_mi_dit_sample(ace_ggml_context* ctx, int32_t batch, float* d_xt, const float* d_context,
+                                  const float* d_enc, const int32_t* d_mask, const int32_t* d_enc_mask,
+                                  int32_t seq_len, int32_t enc_len, const float* schedule, int32_t n_steps,
+                                  void* stream) {
+    if (!ctx || !d_xt || seq_len <= 0 || batch <= 0 || !schedule || n_steps <= 0) return ACE_GGML_ERR_INVALID_ARG;
+    if (!ctx->dit) return set_error(ctx, ACE_GGML_ERR, "dit not loaded");
+    if (enc_len > 0 && !d_enc) return set_error(ctx, ACE_GGML_ERR_INVALID_ARG, "encoder_hidden_states is null");
+    try {
+        bind_device(ctx);
+        hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+        const auto& c = ctx->dit->model().cfg;
+        const size_t n = (size_t)batch * seq_len * c.audio_dim;
+        void* vp = ctx->d_v;
+        ensure_dev(vp, ctx->d_v_bytes, n * 4);
+        ctx->d_v = static_cast<float*>(vp);
+        std::vector<float> tt((size_t)n_steps * batch);
+        for (int i = 0; i < n_steps; ++i)
+            for (int b = 0; b < batch; ++b) tt[(size_t)i * batch + b] = schedule[i];
+        void* sp = ctx->d_sched;
+        ensure_dev(sp, ctx->d_sched_bytes, tt.size() * 4);
+        ctx->d_sched = static_cast<float*>(sp);
+        ACEMI_HIP(hipMemcpyAsync(ctx->d_sched, tt.data(), tt.size() * 4, hipMemcpyHostToDevice, s));
+        ACEMI_HIP(hipStreamSynchronize(s));
+        acemi::ForwardIO io;
+        io.B = batch;
+        io.T = seq_len;
+        io.L = enc_len > 0 ? enc_len : 0;
+        io.hidden = d_xt;
+        io.context = d_context;
+        io.enc = d_enc;
+        io.mask = d_mask;
+        io.enc_mask = d_enc_mask;
+        io.out = ctx->d_v;
+        io.max_layers = max_layers_env();
+        for (int i = 0; i < n_steps; ++i) {
+            io.t = ctx->d_sched + (size_t)i * batch;
+            io.r = io.t;
+            ctx->dit->forward(io, s);
+            const float dt = (i + 1 == n_steps) ? schedule[i] : schedule[i] - schedule[i + 1];
+            acemi::launch_euler(d_xt, ctx->d_v, (int64_t)n, dt, s);
+        }
+    } catch (const std::exception& e) {
+        return set_error(ctx, ACE_GGML_ERR, std::string("dit sample failed: ") + e.what());
+    }
+    return ACE_GGML_OK;
+}
+
+ace_ggml_status ace_mi_profile_enable(ace_ggml_context* ctx, int32_t on) {
+    if (!ctx) return ACE_GGML_ERR_INVALID_ARG;
+    if (!ctx->dit) return set_error(ctx, ACE_GGML_ERR, "dit not loaded");
+    try {
+        bind_device(ctx);
+        ctx->dit->set_profiling(on != 0);
+    } catch (const std::exception& e) {
+        return set_error(ctx, ACE_GGML_ERR, e.what());
+    }
+    return ACE_GGML_OK;
+}
+
+ace_ggml_status ace_mi_profile_reset(ace_ggml_context* ctx) {
+    if (!ctx) return ACE_GGML_ERR_INVALID_ARG;
+    if (!ctx->dit) return set_error(ctx, ACE_GGML_ERR, "dit not loaded");
+    ctx->dit->reset_times();
+    return ACE_GGML_OK;
+}
+
+ace_ggml_status ace_mi_profile_get(ace_ggml_context* ctx, char* names, size_t names_cap, double* ms, int32_t* counts,
+                                   int32_t cap, int32_t* n_out) {
+    if (!ctx || !n_out) return ACE_GGML_ERR_INVALID_ARG;
+    if (!ctx->dit) return set_error(ctx, ACE_GGML_ERR, "dit not loaded");
+    const auto& t = ctx->dit->times();
+    *n_out = static_cast<int32_t>(t.names.size());
+    size_t pos = 0;
+    for (int i = 0; i < cap && i < (int)t.names.size(); ++i) {
+        if (ms) ms[i] = t.ms[i];
+        if (counts) counts[i] = t.count[i];
+        if (names) {
+            const std::string& nm = t.names[i];
+            if (pos + nm.size() + 1 <= names_cap) {
+                std::memcpy(names + pos, nm.c_str(), nm.size() + 1);
+                pos += nm.size() + 1;
+            }
+        }
+    }
+    return ACE_GGML_OK;
+}
+
+ace_ggml_status ace_mi_probe_gemm(ace_ggml_context* ctx, int32_t which, int32_t m_rows, int32_t iters) {
+    if (!ctx || m_rows <= 0 || iters <= 0 || which < 0 || which > 1) return ACE_GGML_ERR_INVALID_ARG;
+    if (!ctx->dit) return set_error(ctx, ACE_GGML_ERR, "dit not loaded");
+    try {
+        bind_device(ctx);
+        ctx->dit->probe_gemm(which, m_rows, iters, ctx->stream);
+    } catch (const std::exception& e) {
+        return set_error(ctx, ACE_GGML_ERR, e.what());
+    }
+    return ACE_GGML_OK;
+}
+
+ace_ggml_status ace_mi_synchronize(ace_ggml_context* ctx) {
+    if (!ctx) return ACE_GGML_ERR_INVALID_ARG;
+    try {
+        if (ctx->stream) {
+            ACEMI_HIP(hipSetDevice(ctx->device));
+            ACEMI_HIP(hipStreamSynchronize(ctx->stream));
+        }
+    } catch (const std::exception& e) {
+        return set_error(ctx, ACE_GGML_ERR, e.what());
+    }
+    return ACE_GGML_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,473 @@
+// DiT forward orchestration: the ggml graph of ace_dit::forward_dit
+// (acestep_dit_model.cpp:1316-1560) as a fixed sequence of fused gfx950 kernels.
+#include "engine.h"
+
+#include <cmath>
+#include <cstring>
+#include <map>
+
+namespace acemi {
+
+DitEngine::~DitEngine() {
+    for (Buf* b : {&a0_, &x_, &act_, &attn_, &act2_, &qkv_, &qh_, &kh_, &vt_, &kbias_, &enc_act_, &encp_, &ckv_, &kc_,
+                   &vc_, &kbias_c_, &freq_, &freq_act_, &th_, &th_act_, &temb_t_, &temb_r_, &temb_act_, &proj_,
+                   &mods_, &outmod_, &cos_, &sin_}) {
+        if (b->p) (void)hipFree(b->p);
+    }
+    if (ev0_) (void)hipEventDestroy(ev0_);
+    if (ev1_) (void)hipEventDestroy(ev1_);
+}
+
+void DitEngine::ensure(Buf& b, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (b.bytes >= bytes) return;
+    if (b.p) {
+        ACEMI_HIP(hipDeviceSynchronize());
+        ACEMI_HIP(hipFree(b.p));
+        b.p = nullptr;
+        b.bytes = 0;
+    }
+    const size_t alloc = (bytes + 255) & ~size_t(255);
+    ACEMI_HIP(hipMalloc(&b.p, alloc));
+    ACEMI_HIP(hipMemset(b.p, 0, alloc));
+    b.bytes = alloc;
+}
+
+void DitEngine::set_profiling(bool on) {
+    profiling_ = on;
+    if (on && !ev0_) {
+        ACEMI_HIP(hipEventCreate(&ev0_));
+        ACEMI_HIP(hipEventCreate(&ev1_));
+    }
+}
+
+void DitEngine::reset_times() { times_ = KernelTimes{}; }
+
+void DitEngine::tic(hipStream_t s) {
+    if (profiling_) ACEMI_HIP(hipEventRecord(ev0_, s));
+}
+
+void DitEngine::toc(const char* name, hipStream_t s) {
+    if (!profiling_) return;
+    ACEMI_HIP(hipEventRecord(ev1_, s));
+    ACEMI_HIP(hipEventSynchronize(ev1_));
+    float ms = 0.f;
+    ACEMI_HIP(hipEventElapsedTime(&ms, ev0_, ev1_));
+    for (size_t i = 0; i < times_.names.size(); ++i) {
+        if (times_.names[i] == name) {
+            times_.ms[i] += ms;
+            times_.count[i] += 1;
+            return;
+        }
+    }
+    times_.names.emplace_back(name);
+    times_.ms.push_back(ms);
+    times_.count.push_back(1);
+}
+
+void DitEngine::prepare_shape(int B, int Np, int L) {
+    const DitConfig& c = model_.cfg;
+    const int H = c.hidden, I = c.intermediate, D = c.head_dim;
+    const int64_t M = (int64_t)B * Np;
+    const int64_t Npad = round_up(Np, 128);
+    const int qd = c.hq * D, kd = c.hkv * D;
+    const size_t act = 2;
+    ensure(a0_, M * c.patch * c.in_channels * act);
+    ensure(x_, M * H * 4);
+    ensure(act_, M * std::max(H, qd) * act);
+    ensure(attn_, M * qd * act);
+    ensure(act2_, M * I * act);
+    ensure(qkv_, M * (qd + 2 * kd) * 4);
+    ensure(qh_, (size_t)B * c.hq * Npad * D * 2);
+    ensure(kh_, (size_t)B * c.hkv * Npad * D * 2);
+    ensure(vt_, (size_t)B * c.hkv * D * Npad * 2);
+    ensure(kbias_, (size_t)B * Npad * 4);
+    if (L > 0) {
+        const int64_t Lpad = round_up(L, 64);
+        const int64_t Me = (int64_t)B * L;
+        ensure(enc_act_, Me * H * act);
+        ensure(encp_, Me * H * act);
+        ensure(ckv_, Me * 2 * kd * 4);
+        ensure(kc_, (size_t)c.layers * B * c.hkv * Lpad * D * 2);
+        ensure(vc_, (size_t)c.layers * B * c.hkv * D * Lpad * 2);
+        ensure(kbias_c_, (size_t)B * Lpad * 4);
+    }
+    ensure(freq_, (size_t)B * 256 * 4);
+    ensure(freq_act_, (size_t)B * 256 * act);
+    ensure(th_, (size_t)B * H * 4);
+    ensure(th_act_, (size_t)B * H * act);
+    ensure(temb_t_, (size_t)B * H * 4);
+    ensure(temb_r_, (size_t)B * H * 4);
+    ensure(temb_act_, (size_t)B * H * act);
+    ensure(proj_, (size_t)B * 6 * H * 4);
+    ensure(mods_, (size_t)c.layers * B * 6 * H * 4);
+    ensure(outmod_, (size_t)B * 2 * H * 4);
+}
+
+// NEOX RoPE table with the reference's own float arithmetic: ggml_rope_cache_init runs
+// theta = p; theta *= theta_scale per pair, theta_scale = powf(base, -2/n_dims), cos/sinf on the CPU
+// (acestep_dit_model.cpp:1205-1210).  Computed once per sequence length on the host.
+void DitEngine::rope_for(int Np) {
+    if (rope_np_ == Np) return;
+    const DitConfig& c = model_.cfg;
+    const int half = c.head_dim / 2;
+    const float theta_scale = powf(c.rope_theta, -2.0f / (float)c.head_dim);
+    std::vector<float> cs((size_t)Np * half), sn((size_t)Np * half);
+    for (int p = 0; p < Np; ++p) {
+        float theta = (float)p;
+        for (int i = 0; i < half; ++i) {
+            cs[(size_t)p * half + i] = cosf(theta);
+            sn[(size_t)p * half + i] = sinf(theta);
+            theta *= theta_scale;
+        }
+    }
+    ensure(cos_, cs.size() * 4);
+    ensure(sin_, sn.size() * 4);
+    ACEMI_HIP(hipMemcpy(cos_.p, cs.data(), cs.size() * 4, hipMemcpyHostToDevice));
+    ACEMI_HIP(hipMemcpy(sin_.p, sn.data(), sn.size() * 4, hipMemcpyHostToDevice));
+    rope_np_ = Np;
+}
+
+void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
+    const DitModel& m = model_;
+    const DitConfig& c = m.cfg;
+    const ActType at = m.act;
+    const int B = io.B, T = io.T, L = io.L > 0 ? io.L : 0;
+    const int P = c.patch, H = c.hidden, I = c.intermediate, D = c.head_dim;
+    const int Np = (T + P - 1) / P;
+    const int64_t M = (int64_t)B * Np;
+    const int Npad = (int)round_up(Np, 128);
+    const int Lpad = (int)round_up(std::max(L, 1), 64);
+    const int qd = c.hq * D, kd = c.hkv * D;
+    ACEMI_CHECK(B >= 1 && B <= 8, "batch must be 1..8 per GPU");
+    ACEMI_CHECK(T >= 1, "seq_len must be > 0");
+    ACEMI_CHECK(L == 0 || io.enc != nullptr, "encoder_hidden_states required when enc_len > 0");
+    prepare_shape(B, Np, L);
+    rope_for(Np);
+
+    int n_layers = c.layers;
+    if (io.max_layers > 0) n_layers = std::min(n_layers, io.max_layers);
+
+    uint16_t* a0 = get<uint16_t>(a0_);
+    float* x = get<float>(x_);
+    uint16_t* act = get<uint16_t>(act_);
+    uint16_t* attn = get<uint16_t>(attn_);
+    uint16_t* act2 = get<uint16_t>(act2_);
+    float* qkv = get<float>(qkv_);
+
+    // ---- input pack + proj_in (:1343-1382)
+    tic(s);
+    launch_pack_input(at, io.hidden, io.context, B, T, Np, P, c.audio_dim, c.ctx_dim(), a0, s);
+    toc("pack_input", s);
+    {
+        GemmEpilogue e;
+        e.kind = EPI_STORE_F32;
+        e.bias = m.proj_in_b;
+        e.c_f32 = x;
+        e.ldc = H;
+        tic(s);
+        launch_gemm(at, a0, P * c.in_channels, m.proj_in_w, P * c.in_channels, (int)M, H, P * c.in_channels, e, s);
+        toc("gemm_proj_in", s);
+    }
+
+    // ---- timestep embeddings (:1416-1424, timestep_forward :1286-1308)
+    {
+        const float log_max = std::log(10000.0f);
+        float* freq = get<float>(freq_);
+        uint16_t* freq_act = get<uint16_t>(freq_act_);
+        float* th = get<float>(th_);
+        uint16_t* th_act = get<uint16_t>(th_act_);
+        uint16_t* temb_act = get<uint16_t>(temb_act_);
+        float* proj = get<float>(proj_);
+        tic(s);
+        for (int e = 0; e < 2; ++e) {
+            float* temb = get<float>(e == 0 ? temb_t_ : temb_r_);
+            launch_timestep_freq(io.t, e == 0 ? nullptr : io.r, B, 256, 1000.0f, log_max, freq, s);
+            launch_to_act(at, freq, (int64_t)B * 256, false, freq_act, s);
+            launch_gemv(at, freq_act, B, m.te[e].w1, H, 256, m.te[e].b1, true, false, th, s);
+            launch_to_act(at, th, (int64_t)B * H, false, th_act, s);
+            launch_gemv(at, th_act, B, m.te[e].w2, H, H, m.te[e].b2, false, false, temb, s);
+            launch_to_act(at, temb, (int64_t)B * H, true, temb_act, s);
+            launch_gemv(at, temb_act, B, m.te[e].wp, 6 * H, H, m.te[e].bp, false, e == 1, proj, s);
+        }
+        launch_layer_mods(m.tables, proj, n_layers, B, H, get<float>(mods_), s);
+        launch_out_mods(m.out_table, get<float>(temb_t_), get<float>(temb_r_), B, H, get<float>(outmod_), s);
+        toc("timestep", s);
+    }
+
+    // ---- key masks
+    tic(s);
+    launch_key_bias(io.mask, B, T, P, Np, Npad, get<float>(kbias_), s);
+    if (L > 0) launch_key_bias(io.enc_mask, B, L, 1, L, Lpad, get<float>(kbias_c_), s);
+    toc("key_bias", s);
+
+    // ---- condition embedder (:1384-1414) + per-layer cross K/V (constant over the layer loop)
+    if (L > 0) {
+        const int64_t Me = (int64_t)B * L;
+        uint16_t* enc_act = get<uint16_t>(enc_act_);
+        uint16_t* encp = get<uint16_t>(encp_);
+        tic(s);
+        launch_to_act(at, io.enc, Me * H, false, enc_act, s);
+        GemmEpilogue e;
+        e.kind = EPI_STORE_ACT;
+        e.bias = m.cond_b;
+        e.c_act = encp;
+        e.ldc = H;
+        launch_gemm(at, enc_act, H, m.cond_w, H, (int)Me, H, H, e, s);
+        toc("gemm_condition", s);
+        for (int li = 0; li < n_layers; ++li) {
+            const DevLayer& ly = m.layers[li];
+            GemmEpilogue ek;
+            ek.kind = EPI_STORE_F32;
+            ek.c_f32 = get<float>(ckv_);
+            ek.ldc = 2 * kd;
+            tic(s);
+            launch_gemm(at, encp, H, ly.w_ckv, H, (int)Me, 2 * kd, H, ek, s);
+            toc("gemm_cross_kv", s);
+            PrepArgs pa{};
+            pa.src = get<float>(ckv_);
+            pa.ld = 2 * kd;
+            pa.q_col = -1;
+            pa.k_col = 0;
+            pa.v_col = kd;
+            pa.hq = c.hq;
+            pa.hkv = c.hkv;
+            pa.n_tok = L;
+            pa.n_pad = Lpad;
+            pa.B = B;
+            pa.k_norm = ly.ck_norm;
+            pa.eps = c.eps;
+            pa.kh = get<uint16_t>(kc_) + (size_t)li * B * c.hkv * Lpad * D;
+            pa.vt = get<uint16_t>(vc_) + (size_t)li * B * c.hkv * D * Lpad;
+            tic(s);
+            launch_attn_prep(pa, s);
+            toc("attn_prep", s);
+        }
+    }
+
+    const float* mods = get<float>(mods_);
+    const int64_t mstride = 6LL * H;  // per item within a layer
+    const float scale = 1.0f / std::sqrt((float)D);
+
+    for (int li = 0; li < n_layers; ++li) {  // :1466-1535
+        const DevLayer& ly = m.layers[li];
+        const float* lm = mods + (size_t)li * B * 6 * H;
+        const float* shift_msa = lm + 0 * H;
+        const float* scale_msa = lm + 1 * H;
+        const float* gate_msa = lm + 2 * H;
+        const float* c_shift = lm + 3 * H;
+        const float* c_scale = lm + 4 * H;
+        const float* c_gate = lm + 5 * H;
+
+        // self-attention block
+        tic(s);
+        launch_rmsnorm_mod(at, x, (int)M, H, ly.self_norm, scale_msa, shift_msa, mstride, Np, c.eps, act, s);
+        toc("rmsnorm_mod", s);
+        {
+            GemmEpilogue e;
+            e.kind = EPI_STORE_F32;
+            e.c_f32 = qkv;
+            e.ldc = qd + 2 * kd;
+            tic(s);
+            launch_gemm(at, act, H, ly.w_qkv, H, (int)M, qd + 2 * kd, H, e, s);
+            toc("gemm_qkv", s);
+        }
+        {
+            PrepArgs pa{};
+            pa.src = qkv;
+            pa.ld = qd + 2 * kd;
+            pa.q_col = 0;
+            pa.k_col = qd;
+            pa.v_col = qd + kd;
+            pa.hq = c.hq;
+            pa.hkv = c.hkv;
+            pa.n_tok = Np;
+            pa.n_pad = Npad;
+            pa.B = B;
+            pa.q_norm = ly.sq_norm;
+            pa.k_norm = ly.sk_norm;
+            pa.rope_cos = get<float>(cos_);
+            pa.rope_sin = get<float>(sin_);
+            pa.eps = c.eps;
+            pa.qh = get<uint16_t>(qh_);
+            pa.kh = get<uint16_t>(kh_);
+            pa.vt = get<uint16_t>(vt_);
+            tic(s);
+            launch_attn_prep(pa, s);
+            toc("attn_prep", s);
+        }
+        {
+            AttnArgs aa{};
+            aa.q = get<uint16_t>(qh_);
+            aa.k = get<uint16_t>(kh_);
+            aa.vt = get<uint16_t>(vt_);
+            aa.kbias = get<float>(kbias_);
+            aa.out = attn;
+            aa.B = B;
+            aa.Hq = c.hq;
+            aa.Hkv = c.hkv;
+            aa.nq = Np;
+            aa.nq_pad = Npad;
+            aa.nk = Np;
+            aa.nk_pad = Npad;
+            aa.window = ly.sliding ? std::max(c.sliding_window, 0) : 0;
+            if (ly.sliding && c.sliding_window <= 0) aa.window = 0;
+            aa.scale = scale;
+            tic(s);
+            launch_attention(at, aa, s);
+            toc(ly.sliding ? "attn_self_sliding" : "attn_self_full", s);
+        }
+        {
+            GemmEpilogue e;
+            e.kind = EPI_RESID_GATED;
+            e.c_f32 = x;
+            e.ldc = H;
+            e.gate = gate_msa;
+            e.gate_stride = mstride;
+            e.rows_per_item = Np;
+            tic(s);
+            launch_gemm(at, attn, qd, ly.w_o, qd, (int)M, H, qd, e, s);
+            toc("gemm_o", s);
+        }
+
+        // cross-attention block (:1502-1520): no AdaLN, no gate, no RoPE
+        if (ly.cross && L > 0) {
+            tic(s);
+            launch_rmsnorm_mod(at, x, (int)M, H, ly.cross_norm, nullptr, nullptr, 0, Np, c.eps, act, s);
+            toc("rmsnorm_mod", s);
+            {
+                GemmEpilogue e;
+                e.kind = EPI_STORE_F32;
+                e.c_f32 = qkv;
+                e.ldc = qd;
+                tic(s);
+                launch_gemm(at, act, H, ly.w_cq, H, (int)M, qd, H, e, s);
+                toc("gemm_cross_q", s);
+            }
+            {
+                PrepArgs pa{};
+                pa.src = qkv;
+                pa.ld = qd;
+                pa.q_col = 0;
+                pa.k_col = -1;
+                pa.v_col = -1;
+                pa.hq = c.hq;
+                pa.hkv = c.hkv;
+                pa.n_tok = Np;
+                pa.n_pad = Npad;
+                pa.B = B;
+                pa.q_norm = ly.cq_norm;
+                pa.eps = c.eps;
+                pa.qh = get<uint16_t>(qh_);
+                tic(s);
+                launch_attn_prep(pa, s);
+                toc("attn_prep", s);
+            }
+            {
+                AttnArgs aa{};
+                aa.q = get<uint16_t>(qh_);
+                aa.k = get<uint16_t>(kc_) + (size_t)li * B * c.hkv * Lpad * D;
+                aa.vt = get<uint16_t>(vc_) + (size_t)li * B * c.hkv * D * Lpad;
+                aa.kbias = get<float>(kbias_c_);
+                aa.out = attn;
+                aa.B = B;
+                aa.Hq = c.hq;
+                aa.Hkv = c.hkv;
+                aa.nq = Np;
+                aa.nq_pad = Npad;
+                aa.nk = L;
+                aa.nk_pad = Lpad;
+                aa.window = 0;
+                aa.scale = scale;
+                tic(s);
+                launch_attention(at, aa, s);
+                toc("attn_cross", s);
+            }
+            {
+                GemmEpilogue e;
+                e.kind = EPI_RESID;
+                e.c_f32 = x;
+                e.ldc = H;
+                tic(s);
+                launch_gemm(at, attn, qd, ly.w_co, qd, (int)M, H, qd, e, s);
+                toc("gemm_cross_o", s);
+            }
+        }
+
+        // MLP block (:1522-1534)
+        tic(s);
+        launch_rmsnorm_mod(at, x, (int)M, H, ly.mlp_norm, c_scale, c_shift, mstride, Np, c.eps, act, s);
+        toc("rmsnorm_mod", s);
+        {
+            GemmEpilogue e;
+            e.kind = EPI_SWIGLU;
+            e.c_act = act2;
+            e.ldc = I;
+            tic(s);
+            launch_gemm(at, act, H, ly.w_gu, H, (int)M, 2 * I, H, e, s);
+            toc("gemm_gate_up", s);
+        }
+        {
+            GemmEpilogue e;
+            e.kind = EPI_RESID_GATED;
+            e.c_f32 = x;
+            e.ldc = H;
+            e.gate = c_gate;
+            e.gate_stride = mstride;
+            e.rows_per_item = Np;
+            tic(s);
+            launch_gemm(at, act2, I, ly.w_down, I, (int)M, H, I, e, s);
+            toc("gemm_down", s);
+        }
+    }
+
+    // ---- output head (:1537-1559)
+    {
+        const float* om = get<float>(outmod_);
+        tic(s);
+        launch_rmsnorm_mod(at, x, (int)M, H, m.norm_out, om + H, om, 2LL * H, Np, c.eps, act, s);
+        toc("rmsnorm_mod", s);
+        GemmEpilogue e;
+        e.kind = EPI_PROJ_OUT;
+        e.bias = m.proj_out_b;
+        e.c_f32 = io.out;
+        e.rows_per_item = Np;
+        e.out_T = T;
+        e.out_ch = c.audio_dim;
+        e.patch = P;
+        tic(s);
+        launch_gemm(at, act, H, m.proj_out_w, H, (int)M, P * c.audio_dim, H, e, s);
+        toc("gemm_proj_out", s);
+    }
+}
+
+void DitEngine::probe_gemm(int which, int M, int iters, hipStream_t s) {
+    const DitModel& m = model_;
+    const DitConfig& c = m.cfg;
+    const int H = c.hidden, I = c.intermediate;
+    prepare_shape(1, M, 0);
+    const DevLayer& ly = m.layers[0];
+    for (int it = 0; it < iters; ++it) {
+        GemmEpilogue e;
+        if (which == 0) {
+            e.kind = EPI_SWIGLU;
+            e.c_act = get<uint16_t>(act2_);
+            e.ldc = I;
+            tic(s);
+            launch_gemm(m.act, get<uint16_t>(act_), H, ly.w_gu, H, M, 2 * I, H, e, s);
+            toc("probe_gemm_gate_up", s);
+        } else {
+            e.kind = EPI_RESID_GATED;
+            e.c_f32 = get<float>(x_);
+            e.ldc = H;
+            e.gate = get<float>(mods_);
+            e.gate_stride = 0;
+            e.rows_per_item = M;
+            tic(s);
+            launch_gemm(m.act, get<uint16_t>(act2_), I, ly.w_down, I, M, H, I, e, s);
+            toc("probe_gemm_down", s);
+        }
+    }
+}
+
+}  // namespace acemi

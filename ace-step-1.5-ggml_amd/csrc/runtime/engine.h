@@ -1,0 +1,78 @@
+// Batched DiT forward on one MI355X (stream-ordered, device pointers).
+//
+// One call = one denoising step for B samples that share (T, L): the token
+// dimension of every linear becomes M = B * ceil(T / patch), so the GEMMs stay
+// MFMA-bound even at batch 1 for long audio.  Functionally equal to B calls
+// of ace_ggml_dit_forward (acestep_ggml.cpp:1304-1482), which the reference
+// issues serially per item (scripts/run_non_ggml_real_case.py:518-527).
+#pragma once
+
+#include <memory>
+#include <vector>
+
+#include "../kernels.h"
+#include "model.h"
+
+namespace acemi {
+
+struct ForwardIO {
+    int B = 1, T = 0, L = 0;
+    const float* hidden = nullptr;    // [B][T][audio] or null (zeros)
+    const float* context = nullptr;   // [B][T][ctx]   or null (zeros)
+    const float* enc = nullptr;       // [B][L][H]     (L > 0)
+    const int32_t* mask = nullptr;    // [B][T] or null
+    const int32_t* enc_mask = nullptr;// [B][L] or null
+    const float* t = nullptr;         // [B]
+    const float* r = nullptr;         // [B]
+    float* out = nullptr;             // [B][T][audio]
+    int max_layers = -1;              // ACE_GGML_DIT_MAX_LAYERS
+};
+
+// Per-kernel-class timing, filled when profiling is enabled (hipEvents on the launch stream).
+struct KernelTimes {
+    std::vector<std::string> names;
+    std::vector<double> ms;
+    std::vector<int> count;
+};
+
+class DitEngine {
+   public:
+    explicit DitEngine(int device) : device_(device) {}
+    ~DitEngine();
+    DitModel& model() { return model_; }
+    void forward(const ForwardIO& io, hipStream_t s);
+    // enable per-kernel-class event timing for subsequent forwards
+    void set_profiling(bool on);
+    const KernelTimes& times() const { return times_; }
+    void reset_times();
+    // launch only the MLP gate/up GEMM of layer 0 for a given M (bench / roofline probe)
+    void probe_gemm(int which, int M, int iters, hipStream_t s);
+
+   private:
+    struct Buf {
+        void* p = nullptr;
+        size_t bytes = 0;
+    };
+    void ensure(Buf& b, size_t bytes);
+    template <typename T>
+    T* get(Buf& b) {
+        return static_cast<T*>(b.p);
+    }
+    void prepare_shape(int B, int Np, int L);
+    void rope_for(int Np);
+    void tic(hipStream_t s);
+    void toc(const char* name, hipStream_t s);
+
+    int device_;
+    DitModel model_;
+    // workspace
+    Buf a0_, x_, act_, attn_, act2_, qkv_, qh_, kh_, vt_, kbias_, enc_act_, encp_, ckv_, kc_, vc_, kbias_c_;
+    Buf freq_, freq_act_, th_, th_act_, temb_t_, temb_r_, temb_act_, proj_, mods_, outmod_, cos_, sin_;
+    int rope_np_ = -1;
+    // profiling
+    bool profiling_ = false;
+    hipEvent_t ev0_ = nullptr, ev1_ = nullptr;
+    KernelTimes times_;
+};
+
+}  // namespace acemi

@@ -1,0 +1,384 @@
+// Weight ingestion: config.json + model.safetensors -> HBM (see model.h).
+#include "model.h"
+
+#include <algorithm>
+#include <cctype>
+#include <cstdlib>
+#include <cstring>
+#include <filesystem>
+#include <fstream>
+#include <map>
+#include <sstream>
+
+#include "json.h"
+
+namespace acemi {
+namespace {
+
+struct IoError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+struct Unsupported : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
+std::string read_file(const std::string& path) {
+    std::ifstream in(path, std::ios::binary);
+    if (!in) throw IoError("failed to read " + path);
+    std::ostringstream ss;
+    ss << in.rdbuf();
+    return ss.str();
+}
+
+// ------------------------------------------------------------ safetensors
+// Format: u64 little-endian header length, JSON header {name: {dtype, shape, data_offsets}}, data.
+// Same contract as ace_safetensors::File (acestep_ggml/cpp/safetensors.cpp:46-171).
+struct StTensor {
+    std::string dtype;
+    std::vector<int64_t> shape;
+    uint64_t begin = 0, end = 0;
+    int64_t numel() const {
+        int64_t n = 1;
+        for (auto d : shape) n *= d;
+        return n;
+    }
+};
+
+struct StFile {
+    std::string path;
+    uint64_t data_offset = 0;
+    std::map<std::string, StTensor> tensors;
+
+    void open(const std::string& p) {
+        path = p;
+        std::ifstream in(p, std::ios::binary);
+        if (!in) throw IoError("failed to open " + p);
+        uint64_t hlen = 0;
+        unsigned char b8[8];
+        if (!in.read(reinterpret_cast<char*>(b8), 8)) throw IoError("failed to read header size");
+        for (int i = 7; i >= 0; --i) hlen = (hlen << 8) | b8[i];
+        if (hlen > (1ull << 31)) throw IoError("invalid safetensors header size");
+        std::string header(hlen, '\0');
+        if (!in.read(header.data(), static_cast<std::streamsize>(hlen))) throw IoError("failed to read header");
+        data_offset = 8 + hlen;
+        Json root;
+        try {
+            root = Json::parse(header);
+        } catch (const std::exception& e) {
+            throw IoError(std::string("invalid safetensors header: ") + e.what());
+        }
+        if (root.kind != Json::Object) throw IoError("invalid safetensors header");
+        for (const auto& kv : root.obj) {
+            if (kv.first == "__metadata__") continue;
+            StTensor t;
+            t.dtype = kv.second.at("dtype").as_str();
+            for (const auto& d : kv.second.at("shape").arr) t.shape.push_back(d.as_int());
+            const auto& off = kv.second.at("data_offsets").arr;
+            if (off.size() != 2) throw IoError("data_offsets invalid");
+            t.begin = static_cast<uint64_t>(off[0].as_int());
+            t.end = static_cast<uint64_t>(off[1].as_int());
+            tensors[kv.first] = t;
+        }
+    }
+    bool has(const std::string& n) const { return tensors.count(n) != 0; }
+    const StTensor& get(const std::string& n) const {
+        auto it = tensors.find(n);
+        if (it == tensors.end()) throw IoError("missing tensor: " + n);
+        return it->second;
+    }
+    std::vector<uint8_t> read(const StTensor& t) const {
+        std::vector<uint8_t> buf(t.end - t.begin);
+        std::ifstream in(path, std::ios::binary);
+        in.seekg(static_cast<std::streamoff>(data_offset + t.begin));
+        if (!in || !in.read(reinterpret_cast<char*>(buf.data()), static_cast<std::streamsize>(buf.size())))
+            throw IoError("read failed");
+        return buf;
+    }
+};
+
+float half_to_f32(uint16_t h) {
+    const uint32_t s = (h >> 15) & 1u, e = (h >> 10) & 31u, f = h & 1023u;
+    uint32_t out;
+    if (e == 0) {
+        if (f == 0) {
+            out = s << 31;
+        } else {  // subnormal
+            int ee = -1;
+            uint32_t ff = f;
+            do {
+                ++ee;
+                ff <<= 1;
+            } while ((ff & 1024u) == 0);
+            out = (s << 31) | ((127 - 15 - ee) << 23) | ((ff & 1023u) << 13);
+        }
+    } else if (e == 31) {
+        out = (s << 31) | 0x7f800000u | (f << 13);
+    } else {
+        out = (s << 31) | ((e - 15 + 127) << 23) | (f << 13);
+    }
+    float r;
+    std::memcpy(&r, &out, 4);
+    return r;
+}
+
+std::vector<float> to_f32(const StTensor& t, const std::vector<uint8_t>& raw) {
+    const int64_t n = t.numel();
+    std::vector<float> out(static_cast<size_t>(n));
+    if (t.dtype == "F32") {
+        std::memcpy(out.data(), raw.data(), static_cast<size_t>(n) * 4);
+    } else if (t.dtype == "BF16") {
+        const uint16_t* s = reinterpret_cast<const uint16_t*>(raw.data());
+        for (int64_t i = 0; i < n; ++i) {
+            uint32_t u = static_cast<uint32_t>(s[i]) << 16;
+            std::memcpy(&out[static_cast<size_t>(i)], &u, 4);
+        }
+    } else if (t.dtype == "F16") {
+        const uint16_t* s = reinterpret_cast<const uint16_t*>(raw.data());
+        for (int64_t i = 0; i < n; ++i) out[static_cast<size_t>(i)] = half_to_f32(s[i]);
+    } else {
+        throw Unsupported("unsupported dtype: " + t.dtype);
+    }
+    return out;
+}
+
+std::string upper(const char* v) {
+    std::string s(v ? v : "");
+    std::transform(s.begin(), s.end(), s.begin(), [](unsigned char c) { return static_cast<char>(std::toupper(c)); });
+    return s;
+}
+
+struct Loader {
+    DitModel& m;
+    StFile st;
+    std::string wdtype;  // dtype of the 2-D weights (BF16 or F16)
+    explicit Loader(DitModel& mm) : m(mm) {}
+
+    template <typename T>
+    T* upload(const void* host, size_t bytes) {
+        void* d = nullptr;
+        ACEMI_HIP(hipMalloc(&d, bytes));
+        m.allocs.push_back(d);
+        ACEMI_HIP(hipMemcpy(d, host, bytes, hipMemcpyHostToDevice));
+        m.weight_bytes += bytes;
+        return static_cast<T*>(d);
+    }
+    float* vec_f32(const std::string& name, int64_t expect) {
+        const auto& t = st.get(name);
+        if (expect >= 0 && t.numel() != expect) throw IoError("invalid tensor shape for " + name);
+        auto v = to_f32(t, st.read(t));
+        return upload<float>(v.data(), v.size() * 4);
+    }
+    // raw 16-bit matrix [rows][cols]
+    std::vector<uint16_t> mat16(const std::string& name, int64_t rows, int64_t cols) {
+        const auto& t = st.get(name);
+        int64_t r = 1, c = 1;
+        if (t.shape.size() == 2) {
+            r = t.shape[0];
+            c = t.shape[1];
+        } else if (t.shape.size() == 3) {
+            r = t.shape[0];
+            c = t.shape[1] * t.shape[2];
+        } else {
+            throw IoError("invalid tensor shape for " + name);
+        }
+        if (r != rows || c != cols) throw IoError("invalid tensor shape for " + name);
+        if (t.dtype != "BF16" && t.dtype != "F16")
+            throw Unsupported("DiT 2-D weight " + name + " has dtype " + t.dtype + " (BF16/F16 supported)");
+        if (wdtype.empty()) wdtype = t.dtype;
+        if (t.dtype != wdtype) throw Unsupported("mixed 2-D weight dtypes are not supported (" + name + ")");
+        auto raw = st.read(t);
+        std::vector<uint16_t> out(static_cast<size_t>(rows * cols));
+        std::memcpy(out.data(), raw.data(), out.size() * 2);
+        return out;
+    }
+    uint16_t* up16(const std::vector<uint16_t>& v) { return upload<uint16_t>(v.data(), v.size() * 2); }
+};
+
+}  // namespace
+
+DitModel::~DitModel() {
+    for (void* p : allocs) (void)hipFree(p);
+}
+
+void load_config(const std::string& path, DitConfig& c) {
+    // acestep_dit_config.cpp:19-93 (required keys + optional ones)
+    std::string text;
+    try {
+        text = read_file(path);
+    } catch (const std::exception&) {
+        throw IoError("failed to read config");
+    }
+    Json o;
+    try {
+        o = Json::parse(text);
+    } catch (const std::exception& e) {
+        throw IoError(e.what());
+    }
+    if (o.kind != Json::Object) throw IoError("config is not object");
+    try {
+        c.hidden = (int)o.at("hidden_size").as_int();
+        c.intermediate = (int)o.at("intermediate_size").as_int();
+        c.layers = (int)o.at("num_hidden_layers").as_int();
+        c.hq = (int)o.at("num_attention_heads").as_int();
+        c.hkv = (int)o.at("num_key_value_heads").as_int();
+        c.head_dim = (int)o.at("head_dim").as_int();
+        c.max_pos = (int)o.at("max_position_embeddings").as_int();
+        c.eps = (float)o.at("rms_norm_eps").as_num();
+        c.patch = (int)o.at("patch_size").as_int();
+        c.in_channels = (int)o.at("in_channels").as_int();
+        c.audio_dim = (int)o.at("audio_acoustic_hidden_dim").as_int();
+        if (o.has("use_sliding_window")) c.use_sliding_window = o.at("use_sliding_window").as_bool();
+        if (o.has("sliding_window") && o.at("sliding_window").kind == Json::Number)
+            c.sliding_window = (int)o.at("sliding_window").as_int();
+        if (o.has("rope_theta")) c.rope_theta = (float)o.at("rope_theta").as_num();
+        const auto& lt = o.at("layer_types");
+        if (lt.kind != Json::Array) throw IoError("missing layer_types");
+        c.layer_types.clear();
+        for (const auto& v : lt.arr) c.layer_types.push_back(v.as_str());
+    } catch (const IoError&) {
+        throw;
+    } catch (const std::exception& e) {
+        throw IoError(std::string("config: ") + e.what());
+    }
+}
+
+void load_dit_model(const std::string& dir, DitModel& m, int& status_hint) {
+    status_hint = 3;
+    try {
+        namespace fs = std::filesystem;
+        const fs::path p(dir);
+        const fs::path root = p.extension() == ".gguf" ? p.parent_path() : p;
+        // GGUF resolution order of resolve_gguf_path (acestep_dit_model.cpp:47-70)
+        for (const char* key : {"ACE_GGML_DIT_GGUF", "ACE_GGML_DIT_GGUF_PATH"}) {
+            const char* v = std::getenv(key);
+            if (v && v[0] && fs::exists(v)) throw Unsupported("GGUF DiT weights are not supported by the MI355X engine yet");
+        }
+        if ((p.extension() == ".gguf" && fs::exists(p)) || (fs::is_directory(p) && fs::exists(p / "model.gguf")))
+            throw Unsupported("GGUF DiT weights are not supported by the MI355X engine yet");
+        // online quantization request (acestep_dit_model.cpp:27-45)
+        std::string q = upper(std::getenv("ACE_GGML_DIT_WEIGHT_QTYPE"));
+        if (q.empty()) q = upper(std::getenv("ACE_GGML_WEIGHT_QTYPE"));
+        if (q == "Q8" || q == "Q8_0" || q == "Q6" || q == "Q6_K" || q == "Q4" || q == "Q4_K" || q == "Q4_K_M")
+            throw Unsupported("quantized DiT weights (" + q + ") are not supported by the MI355X engine yet");
+
+        DitConfig& c = m.cfg;
+        load_config((root / "config.json").string(), c);
+        if (c.head_dim != 128) throw Unsupported("head_dim must be 128");
+        if (c.hidden % 128 != 0 || c.intermediate % 128 != 0) throw Unsupported("hidden/intermediate must be multiples of 128");
+        if (c.hkv <= 0 || c.hq % c.hkv != 0) throw Unsupported("num_attention_heads must be a multiple of num_key_value_heads");
+        const int rep = c.hq / c.hkv;
+        if (rep != 1 && rep != 2 && rep != 4) throw Unsupported("GQA ratio must be 1, 2 or 4");
+        if ((c.patch * c.in_channels) % 64 != 0) throw Unsupported("patch*in_channels must be a multiple of 64");
+        if ((c.patch * c.audio_dim) % 128 != 0) throw Unsupported("patch*audio_dim must be a multiple of 128");
+
+        Loader L(m);
+        L.st.open((root / "model.safetensors").string());
+        const int H = c.hidden, I = c.intermediate, D = c.head_dim, P = c.patch, Cin = c.in_channels, A = c.audio_dim;
+        const int qd = c.hq * D, kd = c.hkv * D;
+
+        // proj_in: conv1d [H][Cin][P] -> [H][P*Cin] (load_conv1d_weight_as_linear :334-411)
+        {
+            auto w = L.mat16("decoder.proj_in.1.weight", H, (int64_t)Cin * P);
+            std::vector<uint16_t> r(w.size());
+            for (int o = 0; o < H; ++o)
+                for (int ci = 0; ci < Cin; ++ci)
+                    for (int k = 0; k < P; ++k) r[(size_t)o * P * Cin + k * Cin + ci] = w[((size_t)o * Cin + ci) * P + k];
+            m.proj_in_w = L.up16(r);
+            m.proj_in_b = L.vec_f32("decoder.proj_in.1.bias", H);
+        }
+        // proj_out: convtranspose1d [H][A][P] -> [(o + k*A)][H] (load_convtranspose1d_weight_as_linear :413-490)
+        {
+            auto w = L.mat16("decoder.proj_out.1.weight", H, (int64_t)A * P);
+            std::vector<uint16_t> r(w.size());
+            for (int i = 0; i < H; ++i)
+                for (int o = 0; o < A; ++o)
+                    for (int k = 0; k < P; ++k) r[(size_t)(o + k * A) * H + i] = w[((size_t)i * A + o) * P + k];
+            m.proj_out_w = L.up16(r);
+            m.proj_out_b = L.vec_f32("decoder.proj_out.1.bias", A);
+        }
+        m.cond_w = L.up16(L.mat16("decoder.condition_embedder.weight", H, H));
+        m.cond_b = L.vec_f32("decoder.condition_embedder.bias", H);
+        m.norm_out = L.vec_f32("decoder.norm_out.weight", H);
+        m.out_table = L.vec_f32("decoder.scale_shift_table", 2 * H);
+        const char* tags[2] = {"decoder.time_embed.", "decoder.time_embed_r."};
+        for (int e = 0; e < 2; ++e) {
+            const std::string p2 = tags[e];
+            const auto& t1 = L.st.get(p2 + "linear_1.weight");
+            if (t1.shape.size() != 2 || t1.shape[0] != H) throw IoError("invalid tensor shape for " + p2 + "linear_1.weight");
+            const int64_t fin = t1.shape[1];
+            if (fin != 256) throw Unsupported("timestep embedding input dim must be 256");
+            m.te[e].w1 = L.up16(L.mat16(p2 + "linear_1.weight", H, fin));
+            m.te[e].b1 = L.vec_f32(p2 + "linear_1.bias", H);
+            m.te[e].w2 = L.up16(L.mat16(p2 + "linear_2.weight", H, H));
+            m.te[e].b2 = L.vec_f32(p2 + "linear_2.bias", H);
+            m.te[e].wp = L.up16(L.mat16(p2 + "time_proj.weight", 6LL * H, H));
+            m.te[e].bp = L.vec_f32(p2 + "time_proj.bias", 6LL * H);
+        }
+        std::vector<float> tables((size_t)c.layers * 6 * H);
+        m.layers.resize(c.layers);
+        for (int i = 0; i < c.layers; ++i) {
+            const std::string p2 = "decoder.layers." + std::to_string(i) + ".";
+            DevLayer& ly = m.layers[i];
+            ly.self_norm = L.vec_f32(p2 + "self_attn_norm.weight", H);
+            ly.cross_norm = L.vec_f32(p2 + "cross_attn_norm.weight", H);
+            ly.mlp_norm = L.vec_f32(p2 + "mlp_norm.weight", H);
+            ly.sq_norm = L.vec_f32(p2 + "self_attn.q_norm.weight", D);
+            ly.sk_norm = L.vec_f32(p2 + "self_attn.k_norm.weight", D);
+            ly.cq_norm = L.vec_f32(p2 + "cross_attn.q_norm.weight", D);
+            ly.ck_norm = L.vec_f32(p2 + "cross_attn.k_norm.weight", D);
+            {
+                auto wq = L.mat16(p2 + "self_attn.q_proj.weight", qd, H);
+                auto wk = L.mat16(p2 + "self_attn.k_proj.weight", kd, H);
+                auto wv = L.mat16(p2 + "self_attn.v_proj.weight", kd, H);
+                std::vector<uint16_t> cat;
+                cat.reserve(wq.size() + wk.size() + wv.size());
+                cat.insert(cat.end(), wq.begin(), wq.end());
+                cat.insert(cat.end(), wk.begin(), wk.end());
+                cat.insert(cat.end(), wv.begin(), wv.end());
+                ly.w_qkv = L.up16(cat);
+            }
+            ly.w_o = L.up16(L.mat16(p2 + "self_attn.o_proj.weight", H, qd));
+            ly.w_cq = L.up16(L.mat16(p2 + "cross_attn.q_proj.weight", qd, H));
+            {
+                auto wk = L.mat16(p2 + "cross_attn.k_proj.weight", kd, H);
+                auto wv = L.mat16(p2 + "cross_attn.v_proj.weight", kd, H);
+                std::vector<uint16_t> cat;
+                cat.reserve(wk.size() + wv.size());
+                cat.insert(cat.end(), wk.begin(), wk.end());
+                cat.insert(cat.end(), wv.begin(), wv.end());
+                ly.w_ckv = L.up16(cat);
+            }
+            ly.w_co = L.up16(L.mat16(p2 + "cross_attn.o_proj.weight", H, qd));
+            {
+                auto wg = L.mat16(p2 + "mlp.gate_proj.weight", I, H);
+                auto wu = L.mat16(p2 + "mlp.up_proj.weight", I, H);
+                std::vector<uint16_t> gu((size_t)2 * I * H);
+                for (int r = 0; r < 2 * I; ++r) {
+                    const int grp = r / 32, w = r % 32;
+                    const auto& src = (w < 16) ? wg : wu;
+                    const int srow = grp * 16 + (w % 16);
+                    std::memcpy(&gu[(size_t)r * H], &src[(size_t)srow * H], (size_t)H * 2);
+                }
+                ly.w_gu = L.up16(gu);
+            }
+            ly.w_down = L.up16(L.mat16(p2 + "mlp.down_proj.weight", H, I));
+            {
+                const auto& t = L.st.get(p2 + "scale_shift_table");
+                if (t.numel() != 6LL * H) throw IoError("invalid tensor shape for " + p2 + "scale_shift_table");
+                auto v = to_f32(t, L.st.read(t));
+                std::memcpy(&tables[(size_t)i * 6 * H], v.data(), v.size() * 4);
+            }
+            ly.sliding = i < (int)c.layer_types.size() && c.layer_types[i] == "sliding_attention";
+        }
+        m.tables = L.upload<float>(tables.data(), tables.size() * 4);
+        m.act = (L.wdtype == "F16") ? ActType::F16 : ActType::BF16;
+    } catch (const Unsupported& e) {
+        status_hint = 4;
+        throw std::runtime_error(e.what());
+    } catch (const HipError&) {
+        status_hint = 1;
+        throw;
+    }
+}
+
+}  // namespace acemi

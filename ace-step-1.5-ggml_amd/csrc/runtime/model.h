@@ -1,0 +1,83 @@
+// DiT weights resident in HBM, laid out for the gfx950 kernels.
+//
+// Mirrors ace_dit::Model / Layer / AttnWeights / MLPWeights / TimestepWeights
+// (acestep_ggml/cpp/acestep_dit_model.h:15-91) and ace_dit::Config
+// (acestep_dit_config.h:10-32), loaded like ace_dit::load_model_from_dir
+// (acestep_dit_model.cpp:753-1088) but fused for the MI355X kernels:
+//   * q|k|v rows concatenated into one [ (Hq+2Hkv)*D ][H] matrix (one GEMM),
+//   * cross k|v concatenated, gate|up interleaved in 16-row groups so the
+//     GEMM epilogue sees matching gate/up columns in one wave,
+//   * norms, biases and AdaLN tables widened to f32 once (ggml cast_f32).
+#pragma once
+
+#include <string>
+#include <vector>
+
+#include "../common.h"
+
+namespace acemi {
+
+struct DitConfig {
+    int hidden = 0, intermediate = 0, layers = 0, hq = 0, hkv = 0, head_dim = 0;
+    int max_pos = 0, patch = 0, in_channels = 0, audio_dim = 0;
+    float eps = 1e-6f, rope_theta = 1000000.0f;
+    int sliding_window = 0;
+    bool use_sliding_window = false;
+    std::vector<std::string> layer_types;
+    int ctx_dim() const { return in_channels - audio_dim; }
+};
+
+struct DevLayer {
+    uint16_t* w_qkv = nullptr;   // [(hq+2hkv)*D][H]
+    uint16_t* w_o = nullptr;     // [H][hq*D]
+    uint16_t* w_cq = nullptr;    // [hq*D][H]
+    uint16_t* w_ckv = nullptr;   // [2*hkv*D][H]
+    uint16_t* w_co = nullptr;    // [H][hq*D]
+    uint16_t* w_gu = nullptr;    // [2I][H] (16-row interleave)
+    uint16_t* w_down = nullptr;  // [H][I]
+    float* self_norm = nullptr;
+    float* cross_norm = nullptr;
+    float* mlp_norm = nullptr;
+    float* sq_norm = nullptr;
+    float* sk_norm = nullptr;
+    float* cq_norm = nullptr;
+    float* ck_norm = nullptr;
+    bool sliding = false;
+    bool cross = true;  // Layer::use_cross_attention default
+};
+
+struct DevTimestep {
+    uint16_t* w1 = nullptr;  // [H][256]
+    uint16_t* w2 = nullptr;  // [H][H]
+    uint16_t* wp = nullptr;  // [6H][H]
+    float* b1 = nullptr;
+    float* b2 = nullptr;
+    float* bp = nullptr;
+};
+
+struct DitModel {
+    DitConfig cfg;
+    ActType act = ActType::BF16;
+    uint16_t* proj_in_w = nullptr;   // [H][P*Cin], column k*Cin + c
+    float* proj_in_b = nullptr;
+    uint16_t* proj_out_w = nullptr;  // [P*audio][H], row o + k*audio
+    float* proj_out_b = nullptr;
+    uint16_t* cond_w = nullptr;      // [H][H]
+    float* cond_b = nullptr;
+    float* norm_out = nullptr;
+    float* out_table = nullptr;      // [2][H]
+    float* tables = nullptr;         // [layers][6][H]
+    DevTimestep te[2];               // time_embed, time_embed_r
+    std::vector<DevLayer> layers;
+    std::vector<void*> allocs;
+    size_t weight_bytes = 0;
+
+    ~DitModel();
+};
+
+// Throws std::runtime_error with a reference-style message on failure.
+// `status_hint` receives 3 (IO) or 4 (UNSUPPORTED) for the ABI status code.
+void load_config(const std::string& path, DitConfig& cfg);
+void load_dit_model(const std::string& dir, DitModel& m, int& status_hint);
+
+}  // namespace acemi

@@ -1,0 +1,135 @@
+// Kernel self-test entries (include/acestep_mi355x.h): run one gfx950 kernel on host
+// buffers so the GPU parity tests can compare it with an fp32 reference of the same op.
+#include <cstring>
+#include <vector>
+
+#include "../../../include/acestep_mi355x.h"
+#include "../kernels.h"
+
+namespace {
+
+struct DevMem {
+    void* p = nullptr;
+    explicit DevMem(size_t bytes) { ACEMI_HIP(hipMalloc(&p, bytes ? bytes : 16)); }
+    ~DevMem() {
+        if (p) (void)hipFree(p);
+    }
+    template <typename T>
+    T* as() {
+        return static_cast<T*>(p);
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+ace_ggml_status ace_mi_kernel_gemm(int32_t act_type, int32_t epi, int32_t M, int32_t N, int32_t K, const uint16_t* A,
+                                   const uint16_t* W, const float* bias, float* out_f32, uint16_t* out_u16) {
+    using namespace acemi;
+    if (!A || !W || M <= 0 || N % 128 != 0 || K % 64 != 0) return ACE_GGML_ERR_INVALID_ARG;
+    if (epi != EPI_STORE_F32 && epi != EPI_SWIGLU) return ACE_GGML_ERR_UNSUPPORTED;
+    if ((epi == EPI_STORE_F32 && !out_f32) || (epi == EPI_SWIGLU && !out_u16)) return ACE_GGML_ERR_INVALID_ARG;
+    try {
+        DevMem dA((size_t)M * K * 2), dW((size_t)N * K * 2), dB((size_t)N * 4), dC((size_t)M * N * 4);
+        ACEMI_HIP(hipMemcpy(dA.p, A, (size_t)M * K * 2, hipMemcpyHostToDevice));
+        ACEMI_HIP(hipMemcpy(dW.p, W, (size_t)N * K * 2, hipMemcpyHostToDevice));
+        if (bias) ACEMI_HIP(hipMemcpy(dB.p, bias, (size_t)N * 4, hipMemcpyHostToDevice));
+        GemmEpilogue e;
+        e.kind = epi;
+        e.bias = bias ? dB.as<float>() : nullptr;
+        if (epi == EPI_STORE_F32) {
+            e.c_f32 = dC.as<float>();
+            e.ldc = N;
+        } else {
+            e.c_act = dC.as<uint16_t>();
+            e.ldc = N / 2;
+        }
+        launch_gemm(act_type == 1 ? ActType::F16 : ActType::BF16, dA.as<uint16_t>(), K, dW.as<uint16_t>(), K, M, N,
+                    K, e, nullptr);
+        ACEMI_HIP(hipDeviceSynchronize());
+        if (epi == EPI_STORE_F32)
+            ACEMI_HIP(hipMemcpy(out_f32, dC.p, (size_t)M * N * 4, hipMemcpyDeviceToHost));
+        else
+            ACEMI_HIP(hipMemcpy(out_u16, dC.p, (size_t)M * (N / 2) * 2, hipMemcpyDeviceToHost));
+    } catch (const std::exception& ex) {
+        std::fprintf(stderr, "ace_mi_kernel_gemm: %s\n", ex.what());
+        return ACE_GGML_ERR;
+    }
+    return ACE_GGML_OK;
+}
+
+ace_ggml_status ace_mi_kernel_attention(int32_t B, int32_t Hq, int32_t Hkv, int32_t nq, int32_t nk, int32_t window,
+                                        float scale, const float* q, const float* kv, const int32_t* kmask,
+                                        float* out) {
+    using namespace acemi;
+    if (B <= 0 || Hq <= 0 || Hkv <= 0 || nq <= 0 || nk <= 0 || !q || !kv || !out) return ACE_GGML_ERR_INVALID_ARG;
+    try {
+        const int D = 128;
+        const int nq_pad = (int)round_up(nq, 128), nk_pad = (int)round_up(nk, 128);
+        const size_t nqf = (size_t)B * nq * Hq * D, nkvf = (size_t)B * nk * 2 * Hkv * D;
+        DevMem dq(nqf * 4), dkv(nkvf * 4), dm((size_t)B * nk * 4), dqh((size_t)B * Hq * nq_pad * D * 2),
+            dkh((size_t)B * Hkv * nk_pad * D * 2), dvt((size_t)B * Hkv * D * nk_pad * 2), dkb((size_t)B * nk_pad * 4),
+            dout(nqf * 2);
+        ACEMI_HIP(hipMemcpy(dq.p, q, nqf * 4, hipMemcpyHostToDevice));
+        ACEMI_HIP(hipMemcpy(dkv.p, kv, nkvf * 4, hipMemcpyHostToDevice));
+        if (kmask) ACEMI_HIP(hipMemcpy(dm.p, kmask, (size_t)B * nk * 4, hipMemcpyHostToDevice));
+        PrepArgs pq{};
+        pq.src = dq.as<float>();
+        pq.ld = Hq * D;
+        pq.q_col = 0;
+        pq.k_col = -1;
+        pq.v_col = -1;
+        pq.hq = Hq;
+        pq.hkv = Hkv;
+        pq.n_tok = nq;
+        pq.n_pad = nq_pad;
+        pq.B = B;
+        pq.qh = dqh.as<uint16_t>();
+        launch_attn_prep(pq, nullptr);
+        PrepArgs pk{};
+        pk.src = dkv.as<float>();
+        pk.ld = 2 * Hkv * D;
+        pk.q_col = -1;
+        pk.k_col = 0;
+        pk.v_col = Hkv * D;
+        pk.hq = Hq;
+        pk.hkv = Hkv;
+        pk.n_tok = nk;
+        pk.n_pad = nk_pad;
+        pk.B = B;
+        pk.kh = dkh.as<uint16_t>();
+        pk.vt = dvt.as<uint16_t>();
+        launch_attn_prep(pk, nullptr);
+        launch_key_bias(kmask ? dm.as<int32_t>() : nullptr, B, nk, 1, nk, nk_pad, dkb.as<float>(), nullptr);
+        AttnArgs a{};
+        a.q = dqh.as<uint16_t>();
+        a.k = dkh.as<uint16_t>();
+        a.vt = dvt.as<uint16_t>();
+        a.kbias = dkb.as<float>();
+        a.out = dout.as<uint16_t>();
+        a.B = B;
+        a.Hq = Hq;
+        a.Hkv = Hkv;
+        a.nq = nq;
+        a.nq_pad = nq_pad;
+        a.nk = nk;
+        a.nk_pad = nk_pad;
+        a.window = window;
+        a.scale = scale;
+        launch_attention(ActType::BF16, a, nullptr);
+        ACEMI_HIP(hipDeviceSynchronize());
+        std::vector<uint16_t> h(nqf);
+        ACEMI_HIP(hipMemcpy(h.data(), dout.p, nqf * 2, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < nqf; ++i) {
+            const uint32_t u = (uint32_t)h[i] << 16;
+            std::memcpy(&out[i], &u, 4);
+        }
+    } catch (const std::exception& ex) {
+        std::fprintf(stderr, "ace_mi_kernel_attention: %s\n", ex.what());
+        return ACE_GGML_ERR;
+    }
+    return ACE_GGML_OK;
+}
+
+}  // extern "C"

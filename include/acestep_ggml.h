@@ -1,0 +1,69 @@
+/*
+ * Drop-in C-ABI for the ACE-Step 1.5 DiT hot path, implemented on MI355X
+ * (gfx950) by libacestep_mi355x.so.
+ *
+ * Every declaration below has the exact name, argument order, types and
+ * status codes of the reference ABI it replaces, so existing callers
+ * (ctypes GGMLCAPIBridge, the C sampler, ace_ggml_cli --dit, compare_dit.py)
+ * can load this library instead of libacestep_ggml.so:
+ *
+ *   ace_ggml_status / ace_ggml_init_params   acestep_ggml/cpp/acestep_ggml.h:23-35
+ *   ace_ggml_create                          acestep_ggml/cpp/acestep_ggml.h:37
+ *   ace_ggml_destroy                         acestep_ggml/cpp/acestep_ggml.h:38
+ *   ace_ggml_last_error                      acestep_ggml/cpp/acestep_ggml.h:39
+ *   ace_ggml_load_dit                        acestep_ggml/cpp/acestep_ggml.h:43
+ *   ace_ggml_dit_forward                     acestep_ggml/cpp/acestep_ggml.h:96-108
+ *
+ * Semantics: host f32 row-major, time-major buffers; one sample
+ * per call; the caller owns every buffer; blocking; one context is not
+ * thread-safe.  `n_threads` and `use_metal` are accepted and ignored
+ * (the compute runs on the GPU); `compute_buffer_bytes` is ignored (the
+ * workspace is sized from the shapes).  The device is HIP device 0 unless
+ * ACE_MI_DEVICE is set, or ace_mi_create_on_device (acestep_mi355x.h) is used.
+ */
+#ifndef ACESTEP_GGML_H
+#define ACESTEP_GGML_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ACE_GGML_API __attribute__((visibility("default")))
+
+typedef struct ace_ggml_context ace_ggml_context;
+
+typedef enum ace_ggml_status {
+    ACE_GGML_OK = 0,
+    ACE_GGML_ERR = 1,
+    ACE_GGML_ERR_INVALID_ARG = 2,
+    ACE_GGML_ERR_IO = 3,
+    ACE_GGML_ERR_UNSUPPORTED = 4
+} ace_ggml_status;
+
+typedef struct ace_ggml_init_params {
+    int32_t n_threads;
+    int32_t use_metal;
+    size_t compute_buffer_bytes;
+} ace_ggml_init_params;
+
+ACE_GGML_API ace_ggml_status ace_ggml_create(const ace_ggml_init_params* params, ace_ggml_context** out_ctx);
+ACE_GGML_API void ace_ggml_destroy(ace_ggml_context* ctx);
+ACE_GGML_API const char* ace_ggml_last_error(const ace_ggml_context* ctx);
+
+ACE_GGML_API ace_ggml_status ace_ggml_load_dit(ace_ggml_context* ctx, const char* model_dir);
+
+ACE_GGML_API ace_ggml_status ace_ggml_dit_forward(ace_ggml_context* ctx, const float* hidden_states,
+                                                  const float* context_latents, const float* encoder_hidden_states,
+                                                  const int32_t* attention_mask,
+                                                  const int32_t* encoder_attention_mask, int32_t seq_len,
+                                                  int32_t enc_len, float timestep, float timestep_r, float* out,
+                                                  size_t out_size);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ACESTEP_GGML_H */

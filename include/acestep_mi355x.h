@@ -1,0 +1,99 @@
+/*
+ * MI355X extensions of the ACE-Step DiT C-ABI (libacestep_mi355x.so).
+ *
+ * These add what the reference ABI cannot express (SURVEY §8b "What the
+ * build adds"): a device-pointer, batched, stream-ordered forward that
+ * removes the per-step host round trip and the serial per-item loop of
+ * scripts/run_non_ggml_real_case.py:502-529, and a device-resident Euler
+ * sampler equivalent to the C sampler loop acestep_ggml.cpp:2042-2086.
+ * All pointers named d_* are HIP device pointers on the context's device;
+ * `stream` is a hipStream_t (NULL = the context's own stream).  Calls are
+ * asynchronous with respect to the host unless stated otherwise.
+ */
+#ifndef ACESTEP_MI355X_H
+#define ACESTEP_MI355X_H
+
+#include "acestep_ggml.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ace_mi_dit_info {
+    int32_t hidden_size;
+    int32_t intermediate_size;
+    int32_t num_layers;
+    int32_t num_heads;
+    int32_t num_kv_heads;
+    int32_t head_dim;
+    int32_t patch_size;
+    int32_t in_channels;
+    int32_t audio_dim;
+    int32_t sliding_window;
+    int32_t act_type;       /* 0 = bf16, 1 = fp16 */
+    int32_t device;
+    int64_t weight_bytes;
+} ace_mi_dit_info;
+
+/* Like ace_ggml_create, bound to HIP device `device`. */
+ACE_GGML_API ace_ggml_status ace_mi_create_on_device(const ace_ggml_init_params* params, int32_t device,
+                                                     ace_ggml_context** out_ctx);
+
+/* Model dimensions of the loaded DiT (ACE_GGML_ERR "dit not loaded" otherwise). */
+ACE_GGML_API ace_ggml_status ace_mi_dit_get_info(ace_ggml_context* ctx, ace_mi_dit_info* out);
+
+/* One denoising step for `batch` samples sharing (seq_len, enc_len).
+ * d_hidden [B][T][audio], d_context [B][T][in-audio] (either may be NULL = zeros),
+ * d_enc [B][L][hidden] (NULL only if enc_len == 0), d_mask [B][T] / d_enc_mask [B][L] int32
+ * (NULL = all valid), d_timestep / d_timestep_r [B] f32, d_out [B][T][audio] f32.
+ * Result equals `batch` calls of ace_ggml_dit_forward. */
+ACE_GGML_API ace_ggml_status ace_mi_dit_forward_batched(ace_ggml_context* ctx, int32_t batch, const float* d_hidden,
+                                                        const float* d_context, const float* d_enc,
+                                                        const int32_t* d_mask, const int32_t* d_enc_mask,
+                                                        int32_t seq_len, int32_t enc_len, const float* d_timestep,
+                                                        const float* d_timestep_r, float* d_out, void* stream);
+
+/* Euler ODE sampling on the device (acestep_ggml.cpp:2056-2086, mlx_dit/generate.py:154-197):
+ * for i in steps: v = DiT(xt, t_i, r = t_i); xt -= v * (t_i - t_{i+1}); last step xt -= v * t_i.
+ * d_xt [B][T][audio] holds the initial noise on entry and x0 on return.
+ * `schedule` is a HOST array of n_steps timesteps. */
+ACE_GGML_API ace_ggml_status ace_mi_dit_sample(ace_ggml_context* ctx, int32_t batch, float* d_xt,
+                                               const float* d_context, const float* d_enc, const int32_t* d_mask,
+                                               const int32_t* d_enc_mask, int32_t seq_len, int32_t enc_len,
+                                               const float* schedule, int32_t n_steps, void* stream);
+
+/* Per-kernel-class timing with hipEvents on the launch stream (adds a sync per kernel).
+ * ace_mi_profile_get copies up to `cap` entries: names (NUL-separated into `names`, `names_cap`
+ * bytes), total milliseconds and launch counts.  Returns the number of classes in *n_out. */
+ACE_GGML_API ace_ggml_status ace_mi_profile_enable(ace_ggml_context* ctx, int32_t on);
+ACE_GGML_API ace_ggml_status ace_mi_profile_reset(ace_ggml_context* ctx);
+ACE_GGML_API ace_ggml_status ace_mi_profile_get(ace_ggml_context* ctx, char* names, size_t names_cap, double* ms,
+                                                int32_t* counts, int32_t cap, int32_t* n_out);
+
+/* Launch `iters` copies of one DiT GEMM of layer 0 with M token rows on the context stream
+ * (which: 0 = MLP gate|up, 1 = MLP down).  Used by bench.py for the roofline probe. */
+ACE_GGML_API ace_ggml_status ace_mi_probe_gemm(ace_ggml_context* ctx, int32_t which, int32_t m_rows,
+                                               int32_t iters);
+
+/* Synchronise the context stream. */
+ACE_GGML_API ace_ggml_status ace_mi_synchronize(ace_ggml_context* ctx);
+
+/* ---- kernel self-test entries (blocking, host buffers; used by the -m gpu parity tests) ----
+ * GEMM: C = A[M][K] . W[N][K]^T with A, W raw 16-bit words of act_type (0 bf16, 1 fp16).
+ * epi 0: out_f32[M][N] = C (+ bias[N] if bias != NULL);
+ * epi 4: SwiGLU on 16-column interleaved gate|up weights, out_u16[M][N/2] raw act words. */
+ACE_GGML_API ace_ggml_status ace_mi_kernel_gemm(int32_t act_type, int32_t epi, int32_t M, int32_t N, int32_t K,
+                                                const uint16_t* A, const uint16_t* W, const float* bias,
+                                                float* out_f32, uint16_t* out_u16);
+/* Attention core only (no norm/RoPE): q [B][nq][Hq*128] f32, kv [B][nk][2*Hkv*128] f32 (K then V),
+ * kmask [B][nk] int32 or NULL, window > 0 = sliding |q-k| <= window; out [B][nq][Hq*128] f32
+ * (the kernel's bf16 output widened). */
+ACE_GGML_API ace_ggml_status ace_mi_kernel_attention(int32_t B, int32_t Hq, int32_t Hkv, int32_t nq, int32_t nk,
+                                                     int32_t window, float scale, const float* q, const float* kv,
+                                                     const int32_t* kmask, float* out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ACESTEP_MI355X_H */

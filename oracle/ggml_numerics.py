@@ -1,0 +1,305 @@
+"""ggml-cpu numeric semantics restated in numpy — TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).
+
+ggml 0.9.5 (the reference's absent submodule, `acestep_ggml/third_party/ggml`,
+version from `acestep_ggml/build_metal/CMakeCache.txt`) is not in the container.
+Its published algorithms are restated here:
+
+* `mul_mat(W, x)` converts the f32 activation `x` to the weight type's
+  `vec_dot_type` before the dot product and accumulates in f32:
+  BF16 -> bf16 (round-to-nearest-even), F16 -> fp16, Q8_0 -> Q8_0 blocks,
+  Q4_K -> Q8_K blocks, F32 -> f32 (no rounding).  Call sites:
+  `acestep_dit_model.cpp:1194-1196,1257,1295-1302,1381,1412,1528-1531,1551`.
+* Q8_0 block = {fp16 d; int8 qs[32]} (34 B / 32 weights),
+  `ggml-metal-embed.metal:222-227`; quantize d = amax/127, q = round(x/d)
+  (`:3110-3128`); dequant q*d (`:3328-3339`).
+* Q4_K super-block = {fp16 d, fp16 dmin, u8 scales[12], u8 qs[128]}
+  (144 B / 256 weights), `:298-309`; 6-bit scale/min unpack + dequant
+  `:3429-3451`.  The Q4_K *encoder* (`make_qkx2_quants`, ggml-quants.c) is not
+  in the container: it is restated from the published ggml source below and
+  is **parity unpinned** (GPU kernels are checked on identical packed bytes).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+QK8_0 = 32
+QK_K = 256
+
+
+# --------------------------------------------------------------------------
+# bf16 / fp16 rounding
+# --------------------------------------------------------------------------
+def f32_to_bf16_bits(x: np.ndarray) -> np.ndarray:
+    """ggml_compute_fp32_to_bf16: round-to-nearest-even on the f32 bits, NaN kept quiet."""
+    u = np.ascontiguousarray(x, dtype=np.float32).view(np.uint32)
+    nan = (u & np.uint32(0x7FFFFFFF)) > np.uint32(0x7F800000)
+    r = (u + (np.uint32(0x7FFF) + ((u >> np.uint32(16)) & np.uint32(1)))) >> np.uint32(16)
+    r = np.where(nan, (u >> np.uint32(16)) | np.uint32(64), r)
+    return r.astype(np.uint16)
+
+
+def bf16_bits_to_f32(b: np.ndarray) -> np.ndarray:
+    return (np.asarray(b, dtype=np.uint16).astype(np.uint32) << np.uint32(16)).view(np.float32)
+
+
+def round_bf16(x: np.ndarray) -> np.ndarray:
+    return bf16_bits_to_f32(f32_to_bf16_bits(x))
+
+
+def round_f16(x: np.ndarray) -> np.ndarray:
+    return np.asarray(x, dtype=np.float32).astype(np.float16).astype(np.float32)
+
+
+# --------------------------------------------------------------------------
+# Q8_0
+# --------------------------------------------------------------------------
+def quantize_q8_0_weights(w: np.ndarray):
+    """quantize_row_q8_0_ref (ggml_quantize_chunk path used by `try_quantize_matrix`,
+    acestep_dit_model.cpp:156-192): per 32-block d = amax/127, id = 1/d,
+    q = roundf(x*id) (round half away from zero), d stored as fp16.
+    Returns (d fp16 [rows, nb], qs int8 [rows, nb, 32])."""
+    w = np.asarray(w, dtype=np.float32)
+    rows, k = w.shape
+    assert k % QK8_0 == 0
+    blk = w.reshape(rows, k // QK8_0, QK8_0)
+    amax = np.max(np.abs(blk), axis=2)
+    d = (amax / np.float32(127.0)).astype(np.float32)
+    with np.errstate(divide="ignore"):
+        idv = np.where(d != 0, np.float32(1.0) / d, np.float32(0.0)).astype(np.float32)
+    x0 = blk * idv[:, :, None]
+    q = (np.sign(x0) * np.floor(np.abs(x0) + np.float32(0.5))).astype(np.int8)  # roundf
+    return d.astype(np.float16), q
+
+
+def dequantize_q8_0(d: np.ndarray, q: np.ndarray) -> np.ndarray:
+    rows, nb = d.shape
+    return (q.astype(np.float32) * d.astype(np.float32)[:, :, None]).reshape(rows, nb * QK8_0)
+
+
+def quantize_q8_0_activations(x: np.ndarray):
+    """x86 `quantize_row_q8_0` (AVX2 path, the vec_dot_type conversion of src1 in
+    mul_mat against Q8_0 weights): d = amax/127 stored fp16, id = 127/amax,
+    q = round-half-even(x*id).  Returns (d fp16, qs int8)."""
+    x = np.asarray(x, dtype=np.float32)
+    rows, k = x.shape
+    blk = x.reshape(rows, k // QK8_0, QK8_0)
+    amax = np.max(np.abs(blk), axis=2).astype(np.float32)
+    d = (amax / np.float32(127.0)).astype(np.float32)
+    with np.errstate(divide="ignore"):
+        idv = np.where(amax != 0, np.float32(127.0) / amax, np.float32(0.0)).astype(np.float32)
+    q = np.rint(blk * idv[:, :, None]).astype(np.int8)
+    return d.astype(np.float16), q
+
+
+def q8_0_activation_roundtrip(x: np.ndarray) -> np.ndarray:
+    d, q = quantize_q8_0_activations(x)
+    return dequantize_q8_0(d, q)
+
+
+def pack_q8_0(d: np.ndarray, q: np.ndarray) -> np.ndarray:
+    """Byte image of block_q8_0 rows: [rows, nb, 34] uint8 (fp16 d little-endian, then 32 x int8)."""
+    rows, nb = d.shape
+    out = np.empty((rows, nb, 34), dtype=np.uint8)
+    out[:, :, 0:2] = d.astype("<f2").view(np.uint8).reshape(rows, nb, 2)
+    out[:, :, 2:] = q.view(np.uint8)
+    return out
+
+
+def unpack_q8_0(raw: np.ndarray):
+    raw = np.asarray(raw, dtype=np.uint8)
+    d = raw[..., 0:2].copy().view("<f2")[..., 0]
+    q = raw[..., 2:].copy().view(np.int8)
+    return d.astype(np.float16), q
+
+
+# --------------------------------------------------------------------------
+# Q4_K (weights) and Q8_K (activations for Q4_K weights)
+# --------------------------------------------------------------------------
+def _nearest_int(f):
+    # ggml nearest_int: round-half-even via the 12582912 magic constant
+    return np.rint(np.asarray(f, dtype=np.float32)).astype(np.int32)
+
+
+def _make_qkx2_quants(x, weights, nmax=15, rmin=-1.0, rdelta=0.1, nstep=20):
+    """Vectorised make_qkx2_quants(n=32, use_mad=false) over a batch of sub-blocks.
+    x, weights: [S, 32] f32.  Returns (scale [S], the_min [S] (= -min), L [S,32])."""
+    x = x.astype(np.float32)
+    w = weights.astype(np.float32)
+    mn = np.minimum(np.min(x, axis=1), np.float32(0.0))
+    mx = np.max(x, axis=1)
+    sum_w = np.sum(w, axis=1, dtype=np.float32)
+    sum_x = np.sum(w * x, axis=1, dtype=np.float32)
+    flat = mx == mn
+    rng_ = np.where(flat, np.float32(1.0), mx - mn).astype(np.float32)
+    iscale = (np.float32(nmax) / rng_).astype(np.float32)
+    scale = (np.float32(1.0) / iscale).astype(np.float32)
+    L = np.clip(_nearest_int(iscale[:, None] * (x - mn[:, None])), 0, nmax)
+    diff = scale[:, None] * L + mn[:, None] - x
+    best = np.sum(w * diff * diff, axis=1, dtype=np.float32)
+    best_min = mn.copy()
+    for i_s in range(nstep + 1):
+        isc = ((np.float32(rmin) + np.float32(rdelta) * np.float32(i_s) + np.float32(nmax)) / rng_).astype(np.float32)
+        La = np.clip(_nearest_int(isc[:, None] * (x - mn[:, None])), 0, nmax).astype(np.float32)
+        sum_l = np.sum(w * La, axis=1, dtype=np.float32)
+        sum_l2 = np.sum(w * La * La, axis=1, dtype=np.float32)
+        sum_xl = np.sum(w * La * x, axis=1, dtype=np.float32)
+        D = sum_w * sum_l2 - sum_l * sum_l
+        ok = D > 0
+        Ds = np.where(ok, D, np.float32(1.0))
+        this_scale = (sum_w * sum_xl - sum_x * sum_l) / Ds
+        this_min = (sum_l2 * sum_x - sum_l * sum_xl) / Ds
+        pos = this_min > 0
+        this_min = np.where(pos, np.float32(0.0), this_min)
+        this_scale = np.where(pos, sum_xl / np.where(sum_l2 != 0, sum_l2, np.float32(1.0)), this_scale)
+        d2 = this_scale[:, None] * La + this_min[:, None] - x
+        mad = np.sum(w * d2 * d2, axis=1, dtype=np.float32)
+        better = ok & (mad < best)
+        L = np.where(better[:, None], La.astype(np.int32), L)
+        best = np.where(better, mad, best)
+        scale = np.where(better, this_scale, scale).astype(np.float32)
+        best_min = np.where(better, this_min, best_min).astype(np.float32)
+    scale = np.where(flat, np.float32(0.0), scale)
+    best_min = np.where(flat, mn, best_min)
+    L = np.where(flat[:, None], 0, L)
+    return scale.astype(np.float32), (-best_min).astype(np.float32), L
+
+
+def quantize_q4_k_weights(w: np.ndarray) -> np.ndarray:
+    """quantize_row_q4_K_ref (no imatrix).  Returns packed bytes [rows, nb, 144]."""
+    w = np.asarray(w, dtype=np.float32)
+    rows, k = w.shape
+    assert k % QK_K == 0
+    nb = k // QK_K
+    x = w.reshape(rows * nb, 8, 32)
+    sub = x.reshape(-1, 32)
+    av_x = np.sqrt(np.sum(sub * sub, axis=1, dtype=np.float32) / np.float32(32.0)).astype(np.float32)
+    weights = av_x[:, None] + np.abs(sub)
+    scales, mins, _ = _make_qkx2_quants(sub, weights)
+    scales = scales.reshape(-1, 8)
+    mins = mins.reshape(-1, 8)
+    max_scale = np.maximum(np.max(scales, axis=1), np.float32(0.0))
+    max_min = np.maximum(np.max(mins, axis=1), np.float32(0.0))
+    inv_scale = np.where(max_scale > 0, np.float32(63.0) / np.where(max_scale > 0, max_scale, 1), 0).astype(np.float32)
+    inv_min = np.where(max_min > 0, np.float32(63.0) / np.where(max_min > 0, max_min, 1), 0).astype(np.float32)
+    ls = np.minimum(_nearest_int(inv_scale[:, None] * scales), 63).astype(np.uint8)
+    lm = np.minimum(_nearest_int(inv_min[:, None] * mins), 63).astype(np.uint8)
+    sc = np.zeros((rows * nb, 12), dtype=np.uint8)
+    sc[:, 0:4] = ls[:, 0:4]
+    sc[:, 4:8] = lm[:, 0:4]
+    sc[:, 8:12] = (ls[:, 4:8] & 0xF) | ((lm[:, 4:8] & 0xF) << 4)
+    sc[:, 0:4] |= (ls[:, 4:8] >> 4) << 6
+    sc[:, 4:8] |= (lm[:, 4:8] >> 4) << 6
+    d = (max_scale / np.float32(63.0)).astype(np.float16)
+    dmin = (max_min / np.float32(63.0)).astype(np.float16)
+    scv, mv = _q4k_scale_min(sc)
+    dd = d.astype(np.float32)[:, None] * scv.astype(np.float32)
+    dm = dmin.astype(np.float32)[:, None] * mv.astype(np.float32)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        Lq = _nearest_int((x + dm[:, :, None]) / np.where(dd != 0, dd, 1)[:, :, None])
+    Lq = np.clip(Lq, 0, 15).astype(np.uint8)
+    Lq = np.where((dd != 0)[:, :, None], Lq, 0).astype(np.uint8).reshape(rows * nb, 256)
+    qs = np.empty((rows * nb, 128), dtype=np.uint8)
+    for j in range(4):
+        qs[:, 32 * j:32 * j + 32] = Lq[:, 64 * j:64 * j + 32] | (Lq[:, 64 * j + 32:64 * j + 64] << 4)
+    out = np.empty((rows * nb, 144), dtype=np.uint8)
+    out[:, 0:2] = d.astype("<f2").view(np.uint8).reshape(-1, 2)
+    out[:, 2:4] = dmin.astype("<f2").view(np.uint8).reshape(-1, 2)
+    out[:, 4:16] = sc
+    out[:, 16:] = qs
+    return out.reshape(rows, nb, 144)
+
+
+def _q4k_scale_min(sc: np.ndarray):
+    """get_scale_min_k4 for j = 0..7 (ggml-metal-embed.metal:3429-3432 restated)."""
+    scv = np.empty(sc.shape[:-1] + (8,), dtype=np.uint8)
+    mv = np.empty_like(scv)
+    scv[..., 0:4] = sc[..., 0:4] & 63
+    mv[..., 0:4] = sc[..., 4:8] & 63
+    scv[..., 4:8] = (sc[..., 8:12] & 0xF) | ((sc[..., 0:4] >> 6) << 4)
+    mv[..., 4:8] = (sc[..., 8:12] >> 4) | ((sc[..., 4:8] >> 6) << 4)
+    return scv, mv
+
+
+def dequantize_q4_k(raw: np.ndarray) -> np.ndarray:
+    """dequantize_row_q4_K: y = d*sc*q - dmin*m per 32-sub-block (`:3435-3451`)."""
+    raw = np.asarray(raw, dtype=np.uint8)
+    rows, nb, _ = raw.shape
+    r = raw.reshape(rows * nb, 144)
+    d = r[:, 0:2].copy().view("<f2")[:, 0].astype(np.float32)
+    dmin = r[:, 2:4].copy().view("<f2")[:, 0].astype(np.float32)
+    scv, mv = _q4k_scale_min(r[:, 4:16])
+    qs = r[:, 16:]
+    q = np.empty((rows * nb, 256), dtype=np.float32)
+    for j in range(4):
+        q[:, 64 * j:64 * j + 32] = (qs[:, 32 * j:32 * j + 32] & 0xF)
+        q[:, 64 * j + 32:64 * j + 64] = (qs[:, 32 * j:32 * j + 32] >> 4)
+    d1 = (d[:, None] * scv.astype(np.float32)).astype(np.float32)
+    m1 = (dmin[:, None] * mv.astype(np.float32)).astype(np.float32)
+    y = d1[:, :, None] * q.reshape(-1, 8, 32) - m1[:, :, None]
+    return y.reshape(rows, nb * 256).astype(np.float32)
+
+
+def q8_k_activation_roundtrip(x: np.ndarray) -> np.ndarray:
+    """quantize_row_q8_K_ref: per 256-block iscale = -127/max (max = signed value of
+    largest magnitude), q = min(127, nearest_int(iscale*x)), d = 1/iscale (f32)."""
+    x = np.asarray(x, dtype=np.float32)
+    rows, k = x.shape
+    blk = x.reshape(rows, k // QK_K, QK_K)
+    idx = np.argmax(np.abs(blk), axis=2)
+    mxv = np.take_along_axis(blk, idx[:, :, None], axis=2)[:, :, 0]
+    zero = mxv == 0
+    iscale = np.where(zero, np.float32(0.0), np.float32(-127.0) / np.where(zero, 1, mxv)).astype(np.float32)
+    q = np.minimum(_nearest_int(iscale[:, :, None] * blk), 127).astype(np.float32)
+    d = np.where(zero, np.float32(0.0), np.float32(1.0) / np.where(zero, 1, iscale)).astype(np.float32)
+    return (q * d[:, :, None]).reshape(rows, k).astype(np.float32)
+
+
+# --------------------------------------------------------------------------
+# Weight container with ggml storage semantics
+# --------------------------------------------------------------------------
+class GgmlWeight:
+    """A 2-D ggml weight W [out][in] (ggml ne0 = in).  `values` are the f32 values
+    ggml reads (dequantized for quant types); `wtype` selects the vec_dot_type."""
+
+    def __init__(self, values: np.ndarray, wtype: str, raw=None):
+        self.values = np.ascontiguousarray(values, dtype=np.float32)
+        self.wtype = wtype
+        self.raw = raw
+
+    @property
+    def shape(self):
+        return self.values.shape
+
+
+def convert_activation(x: np.ndarray, wtype: str) -> np.ndarray:
+    if wtype == "bf16":
+        return round_bf16(x)
+    if wtype == "f16":
+        return round_f16(x)
+    if wtype == "q8_0":
+        return q8_0_activation_roundtrip(x)
+    if wtype == "q4_k":
+        return q8_k_activation_roundtrip(x)
+    if wtype == "f32":
+        return np.asarray(x, dtype=np.float32)
+    raise ValueError(wtype)
+
+
+def mul_mat(w: GgmlWeight, x: np.ndarray) -> np.ndarray:
+    """ggml_mul_mat(W, x) -> x_conv @ W^T with f32 accumulation."""
+    xa = convert_activation(np.asarray(x, dtype=np.float32), w.wtype)
+    return np.matmul(xa, w.values.T).astype(np.float32)
+
+
+def make_weight(f32_values: np.ndarray, src_dtype: str, qtype: str | None) -> GgmlWeight:
+    """`load_tensor_2d_transposed` + `try_quantize_matrix` (acestep_dit_model.cpp:156-192,228-277):
+    quantize when a qtype is requested and in_dim % block == 0, else keep the file dtype."""
+    v = np.asarray(f32_values, dtype=np.float32)
+    if qtype == "q8_0" and v.shape[1] % QK8_0 == 0:
+        d, q = quantize_q8_0_weights(v)
+        return GgmlWeight(dequantize_q8_0(d, q), "q8_0", raw=pack_q8_0(d, q))
+    if qtype == "q4_k" and v.shape[1] % QK_K == 0:
+        raw = quantize_q4_k_weights(v)
+        return GgmlWeight(dequantize_q4_k(raw), "q4_k", raw=raw)
+    wt = {"BF16": "bf16", "F16": "f16", "F32": "f32"}[src_dtype]
+    return GgmlWeight(v, wt)

@@ -1,0 +1,191 @@
+"""GPU parity of the full DiT forward (ace_ggml_dit_forward and the MI355X extensions)
+against the oracle restatement of ace_dit::forward_dit.
+
+Tolerance (SURVEY §8d / BASELINE.json north_star "within 1e-3 relative"):
+  ||gpu - ref||_2 / ||ref||_2 <= 1e-3, and
+  max |gpu - ref| / |ref| <= REL_MAX over elements with |ref| > 1e-2 * rms(ref).
+"""
+import os
+import tempfile
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+REL_L2 = 1e-3
+REL_MAX = 1e-2
+
+
+def rel_errors(got, ref):
+    got = np.asarray(got, np.float64)
+    ref = np.asarray(ref, np.float64)
+    l2 = np.linalg.norm(got - ref) / np.linalg.norm(ref)
+    rms = np.sqrt(np.mean(ref * ref))
+    sel = np.abs(ref) > 1e-2 * rms
+    mx = float(np.max(np.abs(got - ref)[sel] / np.abs(ref[sel]))) if sel.any() else 0.0
+    return float(l2), mx
+
+
+@pytest.fixture(scope="module")
+def tiny_ckpt():
+    from acestep_mi355x.synthetic import TINY_CONFIG, write_checkpoint
+    d = tempfile.mkdtemp(prefix="acemi_tiny_")
+    write_checkpoint(d, TINY_CONFIG, seed=0, dtype="BF16")
+    return d
+
+
+@pytest.fixture(scope="module")
+def tiny_bridge(tiny_ckpt):
+    from acestep_mi355x.capi import GGMLCAPIBridge
+    br = GGMLCAPIBridge(n_threads=1, compute_buffer_mb=0)
+    br.load_dit(tiny_ckpt)
+    yield br
+    br.close()
+
+
+def test_golden_tiny_cases(tiny_bridge):
+    z = np.load(os.path.join(GOLDEN, "dit_tiny.npz"))
+    names = sorted({k.split("/")[0] for k in z.files})
+    for n in names:
+        T, L, t, r = z[f"{n}/meta"]
+        T, L = int(T), int(L)
+        m = z[f"{n}/mask"]
+        em = z[f"{n}/enc_mask"]
+        enc = z[f"{n}/enc"] if L > 0 else np.zeros((0, 256), np.float32)
+        got = tiny_bridge.dit_forward_tfirst(z[f"{n}/hidden"], z[f"{n}/context"], enc, m if m.size else None,
+                                             em if em.size else None, float(t), float(r))
+        l2, mx = rel_errors(got, z[f"{n}/out"])
+        assert l2 <= REL_L2 and mx <= REL_MAX, (n, l2, mx)
+
+
+def test_tiny_vs_live_oracle_long_sequence(tiny_ckpt, tiny_bridge):
+    from oracle.dit_oracle import DitWeights, forward_dit
+    W = DitWeights(tiny_ckpt)
+    rng = np.random.default_rng(99)
+    T, L = 1001, 130
+    h = rng.standard_normal((T, 64)).astype(np.float32)
+    c = rng.standard_normal((T, 128)).astype(np.float32)
+    e = rng.standard_normal((L, 256)).astype(np.float32)
+    mask = np.ones(T, np.int32)
+    mask[900:] = 0
+    emask = np.ones(L, np.int32)
+    emask[100:] = 0
+    ref = forward_dit(W, h, c, e, mask, emask, T, L, 0.8, 0.8)
+    got = tiny_bridge.dit_forward_tfirst(h, c, e, mask, emask, 0.8, 0.8)
+    l2, mx = rel_errors(got, ref)
+    assert l2 <= REL_L2 and mx <= REL_MAX, (l2, mx)
+
+
+def test_null_inputs_are_zeros(tiny_bridge):
+    """hidden/context NULL are treated as zeros (acestep_dit_model.cpp:1358-1377)."""
+    import ctypes
+    rng = np.random.default_rng(5)
+    T, L = 30, 4
+    e = rng.standard_normal((L, 256)).astype(np.float32)
+    zeros_h = np.zeros((T, 64), np.float32)
+    zeros_c = np.zeros((T, 128), np.float32)
+    a = tiny_bridge.dit_forward_tfirst(zeros_h, zeros_c, e, None, None, 0.5, 0.5)
+    out = np.empty((T, 64), np.float32)
+    fp = lambda x: x.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+    st = tiny_bridge.lib.ace_ggml_dit_forward(tiny_bridge.ctx, None, None, fp(e), None, None, T, L, 0.5, 0.5,
+                                              fp(out), out.nbytes)
+    assert st == 0
+    np.testing.assert_array_equal(a, out)
+    small = np.empty((T - 1, 64), np.float32)
+    st = tiny_bridge.lib.ace_ggml_dit_forward(tiny_bridge.ctx, None, None, fp(e), None, None, T, L, 0.5, 0.5,
+                                              fp(small), small.nbytes)
+    assert st == 2 and tiny_bridge._last_error() == "output buffer too small"
+    st = tiny_bridge.lib.ace_ggml_dit_forward(tiny_bridge.ctx, None, None, None, None, None, T, L, 0.5, 0.5,
+                                              fp(out), out.nbytes)
+    assert st == 1
+
+
+def test_batched_device_entry_equals_serial_calls(tiny_bridge):
+    import torch
+    rng = np.random.default_rng(17)
+    B, T, L = 3, 50, 7
+    h = rng.standard_normal((B, T, 64)).astype(np.float32)
+    c = rng.standard_normal((B, T, 128)).astype(np.float32)
+    e = rng.standard_normal((B, L, 256)).astype(np.float32)
+    ts = np.array([1.0, 0.6, 0.3], np.float32)
+    rs = np.array([1.0, 0.2, 0.3], np.float32)
+    mask = np.ones((B, T), np.int32)
+    mask[1, 40:] = 0
+    serial = np.stack([tiny_bridge.dit_forward_tfirst(h[b], c[b], e[b], mask[b], None, ts[b], rs[b])
+                       for b in range(B)])
+    dev = torch.device("cuda:0")
+    th = torch.from_numpy(h).to(dev)
+    tc = torch.from_numpy(c).to(dev)
+    te = torch.from_numpy(e).to(dev)
+    tm = torch.from_numpy(mask).to(dev)
+    tt = torch.from_numpy(ts).to(dev)
+    tr = torch.from_numpy(rs).to(dev)
+    out = torch.empty((B, T, 64), dtype=torch.float32, device=dev)
+    torch.cuda.synchronize()
+    tiny_bridge.dit_forward_batched_device(B, T, L, th.data_ptr(), tc.data_ptr(), te.data_ptr(), tm.data_ptr(), 0,
+                                           tt.data_ptr(), tr.data_ptr(), out.data_ptr(), 0)
+    tiny_bridge.synchronize()
+    got = out.cpu().numpy()
+    for b in range(B):
+        l2, mx = rel_errors(got[b], serial[b])
+        assert l2 < 1e-6, (b, l2, mx)
+
+
+def test_device_sampler_equals_host_euler_loop(tiny_bridge):
+    import torch
+    from acestep_mi355x.schedule import get_timestep_schedule
+    rng = np.random.default_rng(23)
+    B, T, L = 2, 40, 6
+    x0 = rng.standard_normal((B, T, 64)).astype(np.float32)
+    c = rng.standard_normal((B, T, 128)).astype(np.float32)
+    e = rng.standard_normal((B, L, 256)).astype(np.float32)
+    sched = get_timestep_schedule(3.0)
+    # host loop through the reference-ABI entry (acestep_ggml.cpp:2056-2086 order)
+    ref = x0.copy()
+    for b in range(B):
+        xt = ref[b]
+        for i, t in enumerate(sched):
+            vt = tiny_bridge.dit_forward_tfirst(xt, c[b], e[b], None, None, t, t)
+            dt = np.float32(t) if i + 1 == len(sched) else np.float32(np.float32(t) - np.float32(sched[i + 1]))
+            xt = (xt - vt * dt).astype(np.float32)
+        ref[b] = xt
+    dev = torch.device("cuda:0")
+    xt_d = torch.from_numpy(x0).to(dev)
+    tc = torch.from_numpy(c).to(dev)
+    te = torch.from_numpy(e).to(dev)
+    torch.cuda.synchronize()
+    tiny_bridge.dit_sample_device(B, T, L, xt_d.data_ptr(), tc.data_ptr(), te.data_ptr(), 0, 0, sched)
+    tiny_bridge.synchronize()
+    got = xt_d.cpu().numpy()
+    l2, _ = rel_errors(got, ref)
+    assert l2 < 1e-5, l2
+
+
+@pytest.mark.slow
+def test_full_width_two_layers_240s(monkeypatch):
+    """Full DiT width (2048/6144, 16/8 heads) at the 240 s workload (T = 6000 frames at 25 Hz,
+    N = 3000 tokens, L = 512), first 2 layers (ACE_GGML_DIT_MAX_LAYERS, :1457-1464): one
+    sliding + one full layer, vs the oracle."""
+    from acestep_mi355x.capi import GGMLCAPIBridge
+    from acestep_mi355x.synthetic import cached_checkpoint, make_config
+    from oracle.dit_oracle import DitWeights, forward_dit
+    cfg = make_config(num_hidden_layers=2)
+    d = cached_checkpoint(cfg, seed=0)
+    monkeypatch.setenv("ACE_GGML_DIT_MAX_LAYERS", "2")
+    br = GGMLCAPIBridge()
+    br.load_dit(d)
+    rng = np.random.default_rng(1234)
+    T, L = 6000, 512
+    h = rng.standard_normal((T, 64)).astype(np.float32)
+    c = np.concatenate([rng.standard_normal((T, 64)), np.ones((T, 64))], axis=1).astype(np.float32)
+    e = rng.standard_normal((L, 2048)).astype(np.float32)
+    got = br.dit_forward_tfirst(h, c, e, None, None, 0.9, 0.9)
+    br.close()
+    W = DitWeights(d)
+    ref = forward_dit(W, h, c, e, None, None, T, L, 0.9, 0.9, max_layers=2)
+    l2, mx = rel_errors(got, ref)
+    print(f"full-width 2-layer 240s: rel_l2={l2:.3e} rel_max={mx:.3e}")
+    assert l2 <= REL_L2, (l2, mx)

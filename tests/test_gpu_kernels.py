@@ -1,0 +1,127 @@
+"""GPU parity of the individual gfx950 kernels (through the C-ABI self-test entries)
+against an fp32 numpy reference of the same op on the same (already rounded) inputs."""
+import numpy as np
+import pytest
+
+from oracle.ggml_numerics import bf16_bits_to_f32, f32_to_bf16_bits, round_f16
+
+pytestmark = pytest.mark.gpu
+
+
+def _capi():
+    from acestep_mi355x import capi
+    return capi
+
+
+def _bits(x, act):
+    if act == 0:
+        return f32_to_bf16_bits(x)
+    return np.asarray(x, np.float32).astype(np.float16).view(np.uint16)
+
+
+def _vals(bits, act):
+    if act == 0:
+        return bf16_bits_to_f32(bits)
+    return bits.view(np.float16).astype(np.float32)
+
+
+@pytest.mark.parametrize("act", [0, 1])
+@pytest.mark.parametrize("M,N,K", [(1, 128, 64), (127, 256, 384), (300, 1024, 256), (1000, 384, 2048),
+                                   (4100, 128, 128)])
+def test_gemm_store_f32(act, M, N, K):
+    rng = np.random.default_rng(M + N + K + act)
+    a = _bits(rng.standard_normal((M, K)).astype(np.float32), act)
+    w = _bits((rng.standard_normal((N, K)) * 0.05).astype(np.float32), act)
+    bias = rng.standard_normal(N).astype(np.float32)
+    got = _capi().kernel_gemm(a, w, act_type=act, epi=0, bias=bias)
+    ref = (_vals(a, act).astype(np.float64) @ _vals(w, act).astype(np.float64).T + bias).astype(np.float32)
+    scale = np.abs(_vals(a, act)).astype(np.float64) @ np.abs(_vals(w, act)).astype(np.float64).T
+    assert np.all(np.abs(got - ref) <= 2e-6 * scale + 1e-6), np.max(np.abs(got - ref) / (scale + 1e-6))
+
+
+def test_gemm_asymmetric_identity():
+    """A = I (padded), W asymmetric: catches a transposed C write (guide §3)."""
+    M, N, K = 128, 128, 128
+    a = np.eye(M, K, dtype=np.float32)
+    w = (np.arange(N)[:, None] * 1000 + np.arange(K)[None, :]).astype(np.float32) / 4096.0
+    got = _capi().kernel_gemm(_bits(a, 0), _bits(w, 0), act_type=0, epi=0)
+    np.testing.assert_array_equal(got, _vals(_bits(w, 0), 0).T[:M, :N])
+
+
+@pytest.mark.parametrize("act", [0, 1])
+def test_gemm_swiglu_epilogue(act):
+    M, I, K = 200, 256, 512
+    rng = np.random.default_rng(11)
+    a = _bits(rng.standard_normal((M, K)).astype(np.float32), act)
+    g = (rng.standard_normal((I, K)) * 0.05).astype(np.float32)
+    u = (rng.standard_normal((I, K)) * 0.05).astype(np.float32)
+    # 16-row interleave [g0..15, u0..15, g16..31, ...] (runtime/model.cpp)
+    wi = np.empty((2 * I, K), np.float32)
+    for r in range(2 * I):
+        grp, w16 = divmod(r, 32)
+        wi[r] = (g if w16 < 16 else u)[grp * 16 + (w16 % 16)]
+    wb = _bits(wi, act)
+    got = _vals(_capi().kernel_gemm(a, wb, act_type=act, epi=4), act)
+    av = _vals(a, act).astype(np.float64)
+    gv = av @ _vals(_bits(g, act), act).astype(np.float64).T
+    uv = av @ _vals(_bits(u, act), act).astype(np.float64).T
+    ref = (gv / (1 + np.exp(-gv))) * uv
+    ulp = 2.0 ** (-8 if act == 0 else -11)
+    np.testing.assert_allclose(got, ref, rtol=ulp, atol=1e-5)
+
+
+def _attn_ref(q, kv, hq, hkv, window, kmask, scale):
+    B, nq, _ = q.shape
+    nk = kv.shape[1]
+    D = 128
+    qh = round_f16(q).reshape(B, nq, hq, D)
+    k = round_f16(kv[:, :, :hkv * D]).reshape(B, nk, hkv, D)
+    v = round_f16(kv[:, :, hkv * D:]).reshape(B, nk, hkv, D)
+    out = np.zeros((B, nq, hq, D), np.float64)
+    rep = hq // hkv
+    for b in range(B):
+        allow = np.ones((nq, nk), bool)
+        if window > 0:
+            allow &= np.abs(np.arange(nq)[:, None] - np.arange(nk)[None, :]) <= window
+        if kmask is not None:
+            allow &= kmask[b][None, :] != 0
+        for h in range(hq):
+            s = qh[b, :, h].astype(np.float64) @ k[b, :, h // rep].astype(np.float64).T * scale
+            s = np.where(allow, s, -np.inf)
+            m = s.max(axis=1, keepdims=True)
+            p = np.exp(s - m)
+            p /= p.sum(axis=1, keepdims=True)
+            out[b, :, h] = p @ v[b, :, h // rep].astype(np.float64)
+    return out.reshape(B, nq, hq * D)
+
+
+@pytest.mark.parametrize("B,hq,hkv,nq,nk,window,masked", [
+    (1, 2, 1, 64, 64, 0, False),
+    (2, 4, 2, 200, 200, 0, False),
+    (1, 4, 2, 333, 333, 16, False),
+    (2, 16, 8, 300, 77, 0, True),
+    (1, 2, 2, 130, 130, 128, True),
+    (1, 4, 1, 97, 500, 0, False),
+])
+def test_attention_vs_fp64(B, hq, hkv, nq, nk, window, masked):
+    rng = np.random.default_rng(B * 1000 + nq + nk)
+    q = rng.standard_normal((B, nq, hq * 128)).astype(np.float32) * 0.3
+    kv = rng.standard_normal((B, nk, 2 * hkv * 128)).astype(np.float32) * 0.3
+    kmask = None
+    if masked:
+        kmask = (rng.random((B, nk)) > 0.3).astype(np.int32)
+        kmask[:, 0] = 1
+    scale = 1.0 / np.sqrt(128.0)
+    got = _capi().kernel_attention(q, kv, hq, hkv, window=window, kmask=kmask, scale=scale)
+    ref = _attn_ref(q, kv, hq, hkv, window, kmask, scale)
+    err = np.abs(got - ref)
+    # fp16 operands + bf16 output rounding: |err| <= 2^-8 |ref| + small absolute term
+    assert np.all(err <= 2.0 ** -8 * np.abs(ref) + 2e-3), float(err.max())
+
+
+def test_attention_fully_masked_row_is_nan():
+    """ggml soft_max of an all -inf row gives NaN (acestep_dit_model.cpp:1245); so does the kernel."""
+    q = np.ones((1, 8, 128), np.float32)
+    kv = np.ones((1, 8, 256), np.float32)
+    got = _capi().kernel_attention(q, kv, 1, 1, window=0, kmask=np.zeros((1, 8), np.int32))
+    assert np.isnan(got).all()
