@@ -62,6 +62,13 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     if not os.path.exists(p):
         raise RuntimeError(f"libacestep_mi355x.so not found at {p}: run __graft_entry__.build() / make -C "
                            "ace-step-1.5-ggml_amd/csrc")
+    # One HIP runtime per process: torch ships its own libamdhip64 (same SONAME
+    # libamdhip64.so.7).  Loading torch first makes this library bind to that
+    # already-loaded runtime, so torch device pointers and our kernels share it.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(p)
     vp, i32, f32, sz = ctypes.c_void_p, ctypes.c_int32, ctypes.c_float, ctypes.c_size_t
     fp = ctypes.POINTER(ctypes.c_float)
@@ -97,7 +104,7 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     u16p = ctypes.POINTER(ctypes.c_uint16)
     lib.ace_mi_kernel_gemm.argtypes = [i32, i32, i32, i32, i32, u16p, u16p, fp, fp, u16p]
     lib.ace_mi_kernel_gemm.restype = ctypes.c_int
-    lib.ace_mi_kernel_attention.argtypes = [i32, i32, i32, i32, i32, i32, f32, fp, fp, ip, fp]
+    lib.ace_mi_kernel_attention.argtypes = [i32, i32, i32, i32, i32, i32, f32, i32, fp, fp, ip, fp]
     lib.ace_mi_kernel_attention.restype = ctypes.c_int
     if path is None:
         _LIB = lib
@@ -241,7 +248,8 @@ def kernel_gemm(a_bits: np.ndarray, w_bits: np.ndarray, act_type: int = 0, epi: 
 
 
 def kernel_attention(q: np.ndarray, kv: np.ndarray, hq: int, hkv: int, window: int = 0,
-                     kmask: Optional[np.ndarray] = None, scale: Optional[float] = None) -> np.ndarray:
+                     kmask: Optional[np.ndarray] = None, scale: Optional[float] = None,
+                     split: bool = True) -> np.ndarray:
     """q [B][nq][hq*128] f32, kv [B][nk][2*hkv*128] f32 -> out [B][nq][hq*128] f32 (bf16-rounded)."""
     lib = load_library()
     q = np.ascontiguousarray(q, dtype=np.float32)
@@ -251,7 +259,8 @@ def kernel_attention(q: np.ndarray, kv: np.ndarray, hq: int, hkv: int, window: i
     km = None if kmask is None else np.ascontiguousarray(kmask, dtype=np.int32)
     out = np.empty_like(q)
     sc = float(scale) if scale is not None else 1.0 / np.sqrt(128.0)
-    st = lib.ace_mi_kernel_attention(B, hq, hkv, nq, nk, int(window), sc, _fptr(q), _fptr(kv), _iptr(km), _fptr(out))
+    st = lib.ace_mi_kernel_attention(B, hq, hkv, nq, nk, int(window), sc, 1 if split else 0, _fptr(q), _fptr(kv),
+                                     _iptr(km), _fptr(out))
     if st != ACE_GGML_OK:
         raise RuntimeError(f"ace_mi_kernel_attention failed (status={st})")
     return out

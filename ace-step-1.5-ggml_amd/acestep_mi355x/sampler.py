@@ -1,0 +1,108 @@
+"""Batch-sharded diffusion sampling across the GPUs of one node.
+
+The reference samples batch items serially on one host thread
+(scripts/run_non_ggml_real_case.py:518-527; C sampler acestep_ggml.cpp:2042-2086).
+Each item's whole denoising loop is independent, so here rank k owns
+items {b : b % world == k}: rank 0 broadcasts the per-request conditioning
+(encoder states, masks, context latents, initial noise) once over RCCL/xGMI, every
+rank runs its shard's Euler loop on its own GPU with no data-path collective, and
+the final latents are gathered back to rank 0.  No tensor parallelism.
+
+Works with any torch.distributed backend: "nccl" (= RCCL on ROCm) on the GPU node,
+"gloo" for the CPU tests; world_size 1 needs no process group at all.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+
+def dist_info():
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+def shard_indices(global_batch: int, world: int, rank: int) -> List[int]:
+    """Items owned by `rank`: b % world == rank (round-robin keeps shards within one item)."""
+    if world <= 0 or not (0 <= rank < world):
+        raise ValueError("bad world/rank")
+    return [b for b in range(global_batch) if b % world == rank]
+
+
+@dataclass
+class Conditioning:
+    """Per-request inputs of the sampling loop for the whole (global) batch."""
+    noise: torch.Tensor                 # [B][T][audio] f32 initial x_t
+    context: torch.Tensor               # [B][T][ctx] f32 (silence latent | chunk mask)
+    enc: torch.Tensor                   # [B][L][H] f32 encoder hidden states
+    enc_mask: Optional[torch.Tensor] = None   # [B][L] int32
+    mask: Optional[torch.Tensor] = None       # [B][T] int32
+
+
+def broadcast_conditioning(cond: Optional[Conditioning], shapes: dict, device, src: int = 0) -> Conditioning:
+    """Rank `src` holds `cond`; every rank returns a full copy on `device`.  `shapes` (known to all
+    ranks from the request) gives B, T, L, audio, ctx, H and which masks exist."""
+    rank, world = dist_info()
+    B, T, L = shapes["B"], shapes["T"], shapes["L"]
+    audio, ctx, H = shapes["audio"], shapes["ctx"], shapes["H"]
+
+    def buf(shape, dtype, have):
+        if rank == src:
+            return have.to(device=device, dtype=dtype).contiguous()
+        return torch.empty(shape, dtype=dtype, device=device)
+
+    out = Conditioning(
+        noise=buf((B, T, audio), torch.float32, cond.noise if cond else None),
+        context=buf((B, T, ctx), torch.float32, cond.context if cond else None),
+        enc=buf((B, L, H), torch.float32, cond.enc if cond else None),
+        enc_mask=buf((B, L), torch.int32, cond.enc_mask if cond else None) if shapes.get("enc_mask") else None,
+        mask=buf((B, T), torch.int32, cond.mask if cond else None) if shapes.get("mask") else None,
+    )
+    if world > 1:
+        for t in (out.noise, out.context, out.enc, out.enc_mask, out.mask):
+            if t is not None:
+                dist.broadcast(t, src=src)
+    return out
+
+
+def gather_latents(x_local: torch.Tensor, global_batch: int, dst: int = 0) -> Optional[torch.Tensor]:
+    """Collect every rank's [b_local][T][C] shard into [B][T][C] (item order restored) on `dst`."""
+    rank, world = dist_info()
+    if world == 1:
+        return x_local
+    n_max = (global_batch + world - 1) // world
+    pad = torch.zeros((n_max,) + tuple(x_local.shape[1:]), dtype=x_local.dtype, device=x_local.device)
+    pad[: x_local.shape[0]] = x_local
+    parts = [torch.empty_like(pad) for _ in range(world)] if rank == dst else None
+    dist.gather(pad, parts, dst=dst)
+    if rank != dst:
+        return None
+    out = torch.empty((global_batch,) + tuple(x_local.shape[1:]), dtype=x_local.dtype, device=x_local.device)
+    for r in range(world):
+        for j, b in enumerate(shard_indices(global_batch, world, r)):
+            out[b] = parts[r][j]
+    return out
+
+
+def euler_sample_local(bridge, cond: Conditioning, items: Sequence[int], schedule: Sequence[float],
+                       stream: int = 0) -> torch.Tensor:
+    """Run the ODE loop (acestep_ggml.cpp:2056-2086) for `items` on this rank's GPU through
+    `ace_mi_dit_sample`; returns x0 [len(items)][T][audio]."""
+    idx = torch.tensor(list(items), dtype=torch.long, device=cond.noise.device)
+    xt = cond.noise.index_select(0, idx).contiguous()
+    ctx = cond.context.index_select(0, idx).contiguous()
+    enc = cond.enc.index_select(0, idx).contiguous()
+    em = cond.enc_mask.index_select(0, idx).contiguous() if cond.enc_mask is not None else None
+    mk = cond.mask.index_select(0, idx).contiguous() if cond.mask is not None else None
+    B, T, _ = xt.shape
+    L = enc.shape[1]
+    torch.cuda.current_stream().synchronize()
+    bridge.dit_sample_device(B, T, L, xt.data_ptr(), ctx.data_ptr(), enc.data_ptr(),
+                             mk.data_ptr() if mk is not None else 0, em.data_ptr() if em is not None else 0,
+                             list(schedule), stream)
+    bridge.synchronize()
+    return xt

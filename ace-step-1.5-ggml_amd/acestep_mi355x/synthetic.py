@@ -94,8 +94,11 @@ def _encode(values: np.ndarray, dtype: str) -> bytes:
     raise ValueError(dtype)
 
 
-def write_checkpoint(out_dir: str, cfg: dict, seed: int = 0, dtype: str = "BF16", std: float = 0.02) -> str:
-    """Write config.json + model.safetensors into out_dir; returns out_dir."""
+def write_checkpoint(out_dir: str, cfg: dict, seed: int = 0, dtype: str = "BF16", std: float = 0.02,
+                     backend: str = "numpy") -> str:
+    """Write config.json + model.safetensors into out_dir; returns out_dir.
+    backend "numpy" (default, used by the golden fixtures) or "torch" (multi-threaded, ~10x
+    faster for the 1.5 B-parameter benchmark checkpoint; different random values)."""
     os.makedirs(out_dir, exist_ok=True)
     with open(os.path.join(out_dir, "config.json"), "w", encoding="utf-8") as f:
         json.dump(cfg, f, indent=1)
@@ -110,11 +113,23 @@ def write_checkpoint(out_dir: str, cfg: dict, seed: int = 0, dtype: str = "BF16"
     hjson = json.dumps(header, separators=(",", ":")).encode("utf-8")
     hjson += b" " * ((8 - len(hjson) % 8) % 8)
     rng = np.random.default_rng(seed)
+    gen = None
+    if backend == "torch":
+        import torch
+        gen = torch.Generator().manual_seed(seed)
     tmp = os.path.join(out_dir, "model.safetensors.tmp")
     with open(tmp, "wb") as f:
         f.write(struct.pack("<Q", len(hjson)))
         f.write(hjson)
         for name, shape, kind in specs:
+            if gen is not None:
+                import torch
+                t = torch.randn(shape, generator=gen, dtype=torch.float32) * std
+                if kind == "norm":
+                    t = t + 1.0
+                tt = {"BF16": torch.bfloat16, "F16": torch.float16, "F32": torch.float32}[dtype]
+                f.write(t.to(tt).view(torch.int16 if dtype != "F32" else torch.int32).numpy().tobytes())
+                continue
             v = rng.standard_normal(size=shape, dtype=np.float32) * np.float32(std)
             if kind == "norm":
                 v = v + np.float32(1.0)
@@ -123,11 +138,12 @@ def write_checkpoint(out_dir: str, cfg: dict, seed: int = 0, dtype: str = "BF16"
     return out_dir
 
 
-def cached_checkpoint(cfg: dict, seed: int = 0, dtype: str = "BF16", root: str | None = None) -> str:
-    """Write the checkpoint once per (cfg, seed, dtype) under a cache dir and reuse it."""
-    key = hashlib.sha1(json.dumps([cfg, seed, dtype], sort_keys=True).encode()).hexdigest()[:16]
+def cached_checkpoint(cfg: dict, seed: int = 0, dtype: str = "BF16", root: str | None = None,
+                      backend: str = "numpy") -> str:
+    """Write the checkpoint once per (cfg, seed, dtype, backend) under a cache dir and reuse it."""
+    key = hashlib.sha1(json.dumps([cfg, seed, dtype, backend], sort_keys=True).encode()).hexdigest()[:16]
     root = root or os.environ.get("ACE_MI_SYNTH_DIR") or os.path.join(tempfile.gettempdir(), "acestep_mi355x_synth")
     d = os.path.join(root, key)
     if not os.path.exists(os.path.join(d, "model.safetensors")):
-        write_checkpoint(d, cfg, seed=seed, dtype=dtype)
+        write_checkpoint(d, cfg, seed=seed, dtype=dtype, backend=backend)
     return d

@@ -50,6 +50,8 @@ struct AttnArgs {
     int nq, nq_pad, nk, nk_pad;
     int window;  // >0: bidirectional sliding window |q-k| <= window
     float scale;
+    bool split = true;                 // hi/lo fp16 operands (see attention.hip)
+    int64_t q_plane = 0, k_plane = 0, v_plane = 0;  // element offset of the lo planes
 };
 void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s);
 
@@ -79,6 +81,7 @@ struct PrepArgs {
     uint16_t* qh;
     uint16_t* kh;
     uint16_t* vt;
+    int64_t q_plane = 0, k_plane = 0, v_plane = 0;  // >0: also write lo = f16(x - f16(x)) planes
 };
 void launch_attn_prep(const PrepArgs& a, hipStream_t s);
 // kbias[b][k] = (k < nk && pooled mask) ? 0 : -inf ; mask [B][nk*patch-ish frames] or null.

@@ -8,10 +8,16 @@
 // |q-k| <= w).  Scores never touch HBM; the sliding layers visit only the
 // key tiles inside the window.
 //
-// Numerics: operands fp16 (11-bit mantissa), products accumulated in f32 by
-// v_mfma_f32_32x32x16_f16, online softmax in f32 (exp2 domain).  A row whose
-// keys are all masked yields 0/0 = NaN exactly like ggml's soft_max of an
-// all -inf row.
+// Numerics: the reference runs attention in F32.  SPLIT=true (default) keeps
+// every operand as an fp16 pair x = hi + lo (hi = fp16(x), lo = fp16(x - hi))
+// and forms each product as hi*hi + hi*lo + lo*hi with three
+// v_mfma_f32_32x32x16_f16 (f32 accumulate) -> ~22-bit operands, so the bf16
+// rounding of the attention output (the o_proj vec_dot conversion) flips
+// almost never relative to the F32 reference.  SPLIT=false is the plain fp16
+// fast path (ACE_MI_ATTN_FAST=1).  P is formed as exp2(s - m + 12) (scaled by
+// 2^12 so its lo part stays a normal fp16; O and l carry the same factor).
+// Online softmax in f32 (exp2 domain).  A row whose keys are all masked
+// yields 0/0 = NaN exactly like ggml's soft_max of an all -inf row.
 //
 // Structure: one workgroup = 4 waves = (batch item, kv head, 128 query rows
 // spread over the n_rep q heads sharing that kv head), so each K/V tile is
@@ -36,7 +42,17 @@ constexpr int D = 128;
 constexpr int KT = 64;                    // keys per tile
 constexpr int K_BYTES = KT * D * 2;       // 16 KiB
 constexpr int V_BYTES = D * KT * 2;       // 16 KiB
-constexpr int STAGE = K_BYTES + V_BYTES + KT * 4;
+constexpr float PSCALE_LOG2 = 12.0f;
+
+template <bool SPLIT>
+struct Stage {
+    static constexpr int K_HI = 0;
+    static constexpr int K_LO = K_BYTES;
+    static constexpr int V_HI = SPLIT ? 2 * K_BYTES : K_BYTES;
+    static constexpr int V_LO = V_HI + V_BYTES;
+    static constexpr int KB = SPLIT ? 2 * (K_BYTES + V_BYTES) : K_BYTES + V_BYTES;
+    static constexpr int BYTES = KB + KT * 4;
+};
 
 __device__ __forceinline__ f32x16 mfma32(const uint4& a, const uint4& b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0,
@@ -65,8 +81,15 @@ __device__ __forceinline__ uint16_t to_act(float f) {
     }
 }
 
-template <bool F16OUT>
+__device__ __forceinline__ uint32_t pack_f16x2_lo(float a, float b) {
+    const _Float16 ha = (_Float16)a, hb = (_Float16)b;
+    return pack_f16x2(a - (float)ha, b - (float)hb);
+}
+
+template <bool F16OUT, bool SPLIT>
 __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
+    using ST = Stage<SPLIT>;
+    constexpr int STAGE = ST::BYTES;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -99,9 +122,13 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
 
     // ---- Q fragments (B operand of S^T = K Q^T): Q[q][16ks + 8h + j]
     const uint16_t* qptr = a.q + (((int64_t)b * a.Hq + head) * a.nq_pad + qrow) * D + 8 * h;
-    uint4 qf[8];
+    uint4 qf[8], qfl[8];
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) qf[ks] = *(const uint4*)(qptr + 16 * ks);
+    if constexpr (SPLIT) {
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) qfl[ks] = *(const uint4*)(qptr + a.q_plane + 16 * ks);
+    }
 
     const uint16_t* kbase = a.k + ((int64_t)b * a.Hkv + kvh) * a.nk_pad * D;
     const uint16_t* vbase = a.vt + ((int64_t)b * a.Hkv + kvh) * D * a.nk_pad;
@@ -115,20 +142,25 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
             const int g = wid + 4 * j;
             const int row = 4 * g + (lane >> 4);
             const int ch = (lane & 15) ^ (row & 15);
-            __builtin_amdgcn_global_load_lds((const void*)(kbase + (int64_t)(k0 + row) * D + ch * 8),
-                                             (lds_void*)(base + g * 1024), 16, 0, 0);
+            const uint16_t* src = kbase + (int64_t)(k0 + row) * D + ch * 8;
+            __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(base + ST::K_HI + g * 1024), 16, 0, 0);
+            if constexpr (SPLIT)
+                __builtin_amdgcn_global_load_lds((const void*)(src + a.k_plane), (lds_void*)(base + ST::K_LO + g * 1024),
+                                                 16, 0, 0);
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {  // V^T: 16 instr of 8 d-rows
             const int g = wid + 4 * j;
             const int d = 8 * g + (lane >> 3);
             const int ch = (lane & 7) ^ ((d >> 1) & 7);
-            __builtin_amdgcn_global_load_lds((const void*)(vbase + (int64_t)d * a.nk_pad + k0 + ch * 8),
-                                             (lds_void*)(base + K_BYTES + g * 1024), 16, 0, 0);
+            const uint16_t* src = vbase + (int64_t)d * a.nk_pad + k0 + ch * 8;
+            __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(base + ST::V_HI + g * 1024), 16, 0, 0);
+            if constexpr (SPLIT)
+                __builtin_amdgcn_global_load_lds((const void*)(src + a.v_plane), (lds_void*)(base + ST::V_LO + g * 1024),
+                                                 16, 0, 0);
         }
         if (kb && wid == 0) {
-            __builtin_amdgcn_global_load_lds((const void*)(kb + k0 + lane), (lds_void*)(base + K_BYTES + V_BYTES),
-                                             4, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void*)(kb + k0 + lane), (lds_void*)(base + ST::KB), 4, 0, 0);
         }
     };
 
@@ -150,9 +182,11 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
     for (int kt = kt_begin; kt < kt_end; ++kt) {
         const int cur = (kt - kt_begin) & 1;
         if (kt + 1 < kt_end) stage(cur ^ 1, kt + 1);
-        const char* Ks = smem + cur * STAGE;
-        const char* Vs = Ks + K_BYTES;
-        const float* KBs = (const float*)(Vs + V_BYTES);
+        const char* Ks = smem + cur * STAGE + ST::K_HI;
+        const char* Ksl = smem + cur * STAGE + ST::K_LO;
+        const char* Vs = smem + cur * STAGE + ST::V_HI;
+        const char* Vsl = smem + cur * STAGE + ST::V_LO;
+        const float* KBs = (const float*)(smem + cur * STAGE + ST::KB);
         const int k0 = kt * KT;
 
         // ---- S^T = K . Q^T (two 32-key tiles)
@@ -167,6 +201,11 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
                 const int ch = (2 * ks + h) ^ (key & 15);
                 const uint4 kf = *(const uint4*)(Ks + key * 256 + ch * 16);
                 s[t] = mfma32(kf, qf[ks], s[t]);
+                if constexpr (SPLIT) {
+                    const uint4 kfl = *(const uint4*)(Ksl + key * 256 + ch * 16);
+                    s[t] = mfma32(kf, qfl[ks], s[t]);
+                    s[t] = mfma32(kfl, qf[ks], s[t]);
+                }
             }
         }
 
@@ -190,11 +229,11 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
         }
         mloc = fmaxf(mloc, __shfl_xor(mloc, 32));
         const float m_new = fmaxf(m_run, mloc);
-        const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-        const float alpha = __builtin_amdgcn_exp2f(m_run - m_use);
+        const float m_use = ((m_new == -INFINITY) ? 0.f : m_new) - PSCALE_LOG2;
+        const float alpha = __builtin_amdgcn_exp2f(m_run - PSCALE_LOG2 - m_use);
         m_run = m_new;
         float lsum = 0.f;
-        uint4 pf[4];
+        uint4 pf[4], pfl[4];
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
 #pragma unroll
@@ -211,6 +250,14 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
                 f.z = pack_f16x2(s[t][8 * ss + 4], s[t][8 * ss + 5]);
                 f.w = pack_f16x2(s[t][8 * ss + 6], s[t][8 * ss + 7]);
                 pf[2 * t + ss] = f;
+                if constexpr (SPLIT) {
+                    uint4 fl;
+                    fl.x = pack_f16x2_lo(s[t][8 * ss + 0], s[t][8 * ss + 1]);
+                    fl.y = pack_f16x2_lo(s[t][8 * ss + 2], s[t][8 * ss + 3]);
+                    fl.z = pack_f16x2_lo(s[t][8 * ss + 4], s[t][8 * ss + 5]);
+                    fl.w = pack_f16x2_lo(s[t][8 * ss + 6], s[t][8 * ss + 7]);
+                    pfl[2 * t + ss] = fl;
+                }
             }
         }
         l_run = l_run * alpha + lsum;
@@ -228,6 +275,11 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
                 const int ch = (2 * g + h) ^ ((d >> 1) & 7);
                 const uint4 vf = *(const uint4*)(Vs + d * 128 + ch * 16);
                 o[dt] = mfma32(vf, pf[g], o[dt]);
+                if constexpr (SPLIT) {
+                    const uint4 vfl = *(const uint4*)(Vsl + d * 128 + ch * 16);
+                    o[dt] = mfma32(vf, pfl[g], o[dt]);
+                    o[dt] = mfma32(vfl, pf[g], o[dt]);
+                }
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -266,11 +318,20 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s) {
     const int n_qt = (a.nq + qpb - 1) / qpb;
     ACEMI_CHECK(a.nq_pad >= n_qt * qpb, "attention: nq_pad too small");
     const dim3 grid(a.B * a.Hkv * n_qt);
-    const size_t lds = 2 * STAGE;
-    if (out_t == ActType::F16)
-        hipLaunchKernelGGL(attn_kernel<true>, grid, dim3(256), lds, s, a);
-    else
-        hipLaunchKernelGGL(attn_kernel<false>, grid, dim3(256), lds, s, a);
+    if (a.split) {
+        ACEMI_CHECK(a.q_plane > 0 && a.k_plane > 0 && a.v_plane > 0, "attention: split mode needs lo planes");
+        const size_t lds = 2 * Stage<true>::BYTES;
+        if (out_t == ActType::F16)
+            hipLaunchKernelGGL((attn_kernel<true, true>), grid, dim3(256), lds, s, a);
+        else
+            hipLaunchKernelGGL((attn_kernel<false, true>), grid, dim3(256), lds, s, a);
+    } else {
+        const size_t lds = 2 * Stage<false>::BYTES;
+        if (out_t == ActType::F16)
+            hipLaunchKernelGGL((attn_kernel<true, false>), grid, dim3(256), lds, s, a);
+        else
+            hipLaunchKernelGGL((attn_kernel<false, false>), grid, dim3(256), lds, s, a);
+    }
     ACEMI_HIP(hipGetLastError());
 }
 

@@ -161,8 +161,14 @@ __global__ void __launch_bounds__(256) attn_prep_kernel(PrepArgs a) {
         }
         uint16_t* dst = isq ? a.qh + (((int64_t)b * a.hq + head) * a.n_pad + n) * 128
                             : a.kh + (((int64_t)b * a.hkv + head) * a.n_pad + n) * 128;
-        dst[lane] = f32_to_f16(r0);
-        dst[lane + 64] = f32_to_f16(r1);
+        const uint16_t h0 = f32_to_f16(r0), h1 = f32_to_f16(r1);
+        dst[lane] = h0;
+        dst[lane + 64] = h1;
+        const int64_t plane = isq ? a.q_plane : a.k_plane;
+        if (plane > 0) {
+            dst[plane + lane] = f32_to_f16(r0 - (float)__builtin_bit_cast(_Float16, h0));
+            dst[plane + lane + 64] = f32_to_f16(r1 - (float)__builtin_bit_cast(_Float16, h1));
+        }
     }
     if (a.v_col < 0) return;
     for (int hk = 0; hk < a.hkv; ++hk) {
@@ -181,15 +187,19 @@ __global__ void __launch_bounds__(256) attn_prep_kernel(PrepArgs a) {
         uint16_t* dst = a.vt + (((int64_t)b * a.hkv + hk) * 128 + d) * a.n_pad + n0 + half * 32;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-            uint32_t wv[4];
+            uint32_t wv[4], wl[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int p0 = half * 32 + c * 8 + 2 * j;
                 const float v0 = vs[vperm(p0)][d];
                 const float v1 = vs[vperm(p0 + 1)][d];
-                wv[j] = (uint32_t)f32_to_f16(v0) | ((uint32_t)f32_to_f16(v1) << 16);
+                const uint16_t h0 = f32_to_f16(v0), h1 = f32_to_f16(v1);
+                wv[j] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+                wl[j] = (uint32_t)f32_to_f16(v0 - (float)__builtin_bit_cast(_Float16, h0)) |
+                        ((uint32_t)f32_to_f16(v1 - (float)__builtin_bit_cast(_Float16, h1)) << 16);
             }
             *(uint4*)(dst + c * 8) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+            if (a.v_plane > 0) *(uint4*)(dst + a.v_plane + c * 8) = make_uint4(wl[0], wl[1], wl[2], wl[3]);
         }
     }
 }

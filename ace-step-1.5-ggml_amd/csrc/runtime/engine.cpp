@@ -3,10 +3,16 @@
 #include "engine.h"
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 
 namespace acemi {
+
+DitEngine::DitEngine(int device) : device_(device) {
+    const char* f = std::getenv("ACE_MI_ATTN_FAST");
+    attn_split_ = !(f && f[0] && f[0] != '0');
+}
 
 DitEngine::~DitEngine() {
     for (Buf* b : {&a0_, &x_, &act_, &attn_, &act2_, &qkv_, &qh_, &kh_, &vt_, &kbias_, &enc_act_, &encp_, &ckv_, &kc_,
@@ -78,9 +84,9 @@ void DitEngine::prepare_shape(int B, int Np, int L) {
     ensure(attn_, M * qd * act);
     ensure(act2_, M * I * act);
     ensure(qkv_, M * (qd + 2 * kd) * 4);
-    ensure(qh_, (size_t)B * c.hq * Npad * D * 2);
-    ensure(kh_, (size_t)B * c.hkv * Npad * D * 2);
-    ensure(vt_, (size_t)B * c.hkv * D * Npad * 2);
+    ensure(qh_, (size_t)2 * B * c.hq * Npad * D * 2);   // hi + lo planes
+    ensure(kh_, (size_t)2 * B * c.hkv * Npad * D * 2);
+    ensure(vt_, (size_t)2 * B * c.hkv * D * Npad * 2);
     ensure(kbias_, (size_t)B * Npad * 4);
     if (L > 0) {
         const int64_t Lpad = round_up(L, 64);
@@ -88,8 +94,8 @@ void DitEngine::prepare_shape(int B, int Np, int L) {
         ensure(enc_act_, Me * H * act);
         ensure(encp_, Me * H * act);
         ensure(ckv_, Me * 2 * kd * 4);
-        ensure(kc_, (size_t)c.layers * B * c.hkv * Lpad * D * 2);
-        ensure(vc_, (size_t)c.layers * B * c.hkv * D * Lpad * 2);
+        ensure(kc_, (size_t)2 * c.layers * B * c.hkv * Lpad * D * 2);
+        ensure(vc_, (size_t)2 * c.layers * B * c.hkv * D * Lpad * 2);
         ensure(kbias_c_, (size_t)B * Lpad * 4);
     }
     ensure(freq_, (size_t)B * 256 * 4);
@@ -139,6 +145,10 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
     const int Npad = (int)round_up(Np, 128);
     const int Lpad = (int)round_up(std::max(L, 1), 64);
     const int qd = c.hq * D, kd = c.hkv * D;
+    const bool split = attn_split_;
+    const int64_t q_plane = (int64_t)B * c.hq * Npad * D;        // lo plane offsets (elements)
+    const int64_t k_plane = (int64_t)B * c.hkv * Npad * D;
+    const int64_t kc_plane = (int64_t)c.layers * B * c.hkv * Lpad * D;
     ACEMI_CHECK(B >= 1 && B <= 8, "batch must be 1..8 per GPU");
     ACEMI_CHECK(T >= 1, "seq_len must be > 0");
     ACEMI_CHECK(L == 0 || io.enc != nullptr, "encoder_hidden_states required when enc_len > 0");
@@ -239,6 +249,8 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
             pa.eps = c.eps;
             pa.kh = get<uint16_t>(kc_) + (size_t)li * B * c.hkv * Lpad * D;
             pa.vt = get<uint16_t>(vc_) + (size_t)li * B * c.hkv * D * Lpad;
+            pa.k_plane = split ? kc_plane : 0;
+            pa.v_plane = split ? kc_plane : 0;
             tic(s);
             launch_attn_prep(pa, s);
             toc("attn_prep", s);
@@ -292,6 +304,9 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
             pa.qh = get<uint16_t>(qh_);
             pa.kh = get<uint16_t>(kh_);
             pa.vt = get<uint16_t>(vt_);
+            pa.q_plane = split ? q_plane : 0;
+            pa.k_plane = split ? k_plane : 0;
+            pa.v_plane = split ? k_plane : 0;
             tic(s);
             launch_attn_prep(pa, s);
             toc("attn_prep", s);
@@ -313,6 +328,10 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
             aa.window = ly.sliding ? std::max(c.sliding_window, 0) : 0;
             if (ly.sliding && c.sliding_window <= 0) aa.window = 0;
             aa.scale = scale;
+            aa.split = split;
+            aa.q_plane = q_plane;
+            aa.k_plane = k_plane;
+            aa.v_plane = k_plane;
             tic(s);
             launch_attention(at, aa, s);
             toc(ly.sliding ? "attn_self_sliding" : "attn_self_full", s);
@@ -359,6 +378,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
                 pa.q_norm = ly.cq_norm;
                 pa.eps = c.eps;
                 pa.qh = get<uint16_t>(qh_);
+                pa.q_plane = split ? q_plane : 0;
                 tic(s);
                 launch_attn_prep(pa, s);
                 toc("attn_prep", s);
@@ -379,6 +399,10 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
                 aa.nk_pad = Lpad;
                 aa.window = 0;
                 aa.scale = scale;
+                aa.split = split;
+                aa.q_plane = q_plane;
+                aa.k_plane = kc_plane;
+                aa.v_plane = kc_plane;
                 tic(s);
                 launch_attention(at, aa, s);
                 toc("attn_cross", s);

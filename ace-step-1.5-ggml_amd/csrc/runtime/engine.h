@@ -37,7 +37,7 @@ struct KernelTimes {
 
 class DitEngine {
    public:
-    explicit DitEngine(int device) : device_(device) {}
+    explicit DitEngine(int device);
     ~DitEngine();
     DitModel& model() { return model_; }
     void forward(const ForwardIO& io, hipStream_t s);
@@ -69,6 +69,7 @@ class DitEngine {
     Buf a0_, x_, act_, attn_, act2_, qkv_, qh_, kh_, vt_, kbias_, enc_act_, encp_, ckv_, kc_, vc_, kbias_c_;
     Buf freq_, freq_act_, th_, th_act_, temb_t_, temb_r_, temb_act_, proj_, mods_, outmod_, cos_, sin_;
     int rope_np_ = -1;
+    bool attn_split_ = true;  // ACE_MI_ATTN_FAST=1 -> single fp16 operands
     // profiling
     bool profiling_ = false;
     hipEvent_t ev0_ = nullptr, ev1_ = nullptr;

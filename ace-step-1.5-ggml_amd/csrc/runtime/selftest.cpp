@@ -60,16 +60,16 @@ ace_ggml_status ace_mi_kernel_gemm(int32_t act_type, int32_t epi, int32_t M, int
 }
 
 ace_ggml_status ace_mi_kernel_attention(int32_t B, int32_t Hq, int32_t Hkv, int32_t nq, int32_t nk, int32_t window,
-                                        float scale, const float* q, const float* kv, const int32_t* kmask,
-                                        float* out) {
+                                        float scale, int32_t split, const float* q, const float* kv,
+                                        const int32_t* kmask, float* out) {
     using namespace acemi;
     if (B <= 0 || Hq <= 0 || Hkv <= 0 || nq <= 0 || nk <= 0 || !q || !kv || !out) return ACE_GGML_ERR_INVALID_ARG;
     try {
         const int D = 128;
         const int nq_pad = (int)round_up(nq, 128), nk_pad = (int)round_up(nk, 128);
         const size_t nqf = (size_t)B * nq * Hq * D, nkvf = (size_t)B * nk * 2 * Hkv * D;
-        DevMem dq(nqf * 4), dkv(nkvf * 4), dm((size_t)B * nk * 4), dqh((size_t)B * Hq * nq_pad * D * 2),
-            dkh((size_t)B * Hkv * nk_pad * D * 2), dvt((size_t)B * Hkv * D * nk_pad * 2), dkb((size_t)B * nk_pad * 4),
+        DevMem dq(nqf * 4), dkv(nkvf * 4), dm((size_t)B * nk * 4), dqh((size_t)2 * B * Hq * nq_pad * D * 2),
+            dkh((size_t)2 * B * Hkv * nk_pad * D * 2), dvt((size_t)2 * B * Hkv * D * nk_pad * 2), dkb((size_t)B * nk_pad * 4),
             dout(nqf * 2);
         ACEMI_HIP(hipMemcpy(dq.p, q, nqf * 4, hipMemcpyHostToDevice));
         ACEMI_HIP(hipMemcpy(dkv.p, kv, nkvf * 4, hipMemcpyHostToDevice));
@@ -86,6 +86,8 @@ ace_ggml_status ace_mi_kernel_attention(int32_t B, int32_t Hq, int32_t Hkv, int3
         pq.n_pad = nq_pad;
         pq.B = B;
         pq.qh = dqh.as<uint16_t>();
+        const int64_t qpl = (int64_t)B * Hq * nq_pad * D, kpl = (int64_t)B * Hkv * nk_pad * D;
+        pq.q_plane = split ? qpl : 0;
         launch_attn_prep(pq, nullptr);
         PrepArgs pk{};
         pk.src = dkv.as<float>();
@@ -100,6 +102,8 @@ ace_ggml_status ace_mi_kernel_attention(int32_t B, int32_t Hq, int32_t Hkv, int3
         pk.B = B;
         pk.kh = dkh.as<uint16_t>();
         pk.vt = dvt.as<uint16_t>();
+        pk.k_plane = split ? kpl : 0;
+        pk.v_plane = split ? kpl : 0;
         launch_attn_prep(pk, nullptr);
         launch_key_bias(kmask ? dm.as<int32_t>() : nullptr, B, nk, 1, nk, nk_pad, dkb.as<float>(), nullptr);
         AttnArgs a{};
@@ -117,6 +121,10 @@ ace_ggml_status ace_mi_kernel_attention(int32_t B, int32_t Hq, int32_t Hkv, int3
         a.nk_pad = nk_pad;
         a.window = window;
         a.scale = scale;
+        a.split = split != 0;
+        a.q_plane = qpl;
+        a.k_plane = kpl;
+        a.v_plane = kpl;
         launch_attention(ActType::BF16, a, nullptr);
         ACEMI_HIP(hipDeviceSynchronize());
         std::vector<uint16_t> h(nqf);

@@ -1,0 +1,248 @@
+#!/usr/bin/env python3
+"""Benchmark: ACE-Step 1.5 DiT denoising steps/s on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[2] shape at bf16, see DESIGN.md "Measurement"):
+240 s of audio = T = 6000 latent frames at 25 Hz (the DiT's frame rate; "5Hz" in
+BASELINE.json is the LM code rate) -> N = 3000 patch tokens, encoder
+length L = 512, full 24-layer DiT with synthetic bf16 weights of the real
+architecture, 27-step shifted-linear (shift 3) Euler sampling.  One "step" = one
+DiT forward over the local batch + the Euler update, all on the GPU.
+
+Multi-GPU (one process per GPU, torchrun): the batch is sharded across ranks
+(weak scaling, `--batch-per-gpu` items each); rank 0 broadcasts the conditioning
+once over RCCL before the timed region; no collective inside it.
+
+Prints ONE JSON line on rank 0 (driver contract), with `roofline` for the
+dominant kernel (the MLP gate|up GEMM, measured with HIP events on the launch
+stream) and `cpu_baseline` (the numpy oracle restatement of ggml's forward_dit on
+the host cores, one 240 s forward).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "ace-step-1.5-ggml_amd"))
+sys.path.insert(0, ROOT)
+
+METRIC = "DiT denoising steps/sec (240s@5Hz latent, bs=1..8) + single-step ms; 1/2/4/8 GPU"
+BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16/fp16 MFMA (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=27)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--seconds", type=float, default=240.0)
+    ap.add_argument("--batch-per-gpu", type=int, default=1)
+    ap.add_argument("--enc-len", type=int, default=512)
+    ap.add_argument("--sample-steps", type=int, default=27)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    from acestep_mi355x.capi import GGMLCAPIBridge
+    from acestep_mi355x.sampler import Conditioning, broadcast_conditioning, shard_indices
+    from acestep_mi355x.schedule import shifted_linear_schedule
+    from acestep_mi355x.synthetic import cached_checkpoint, make_config
+
+    cfg = make_config()
+    # rank 0 writes the synthetic checkpoint, the others wait for it
+    if rank == 0:
+        ckpt = cached_checkpoint(cfg, seed=0, backend="torch")
+    barrier()
+    if rank != 0:
+        ckpt = cached_checkpoint(cfg, seed=0, backend="torch")
+
+    br = GGMLCAPIBridge(device=local)
+    br.load_dit(ckpt)
+    info = br.info
+
+    T = int(round(args.seconds * 25))        # 25 Hz latent frames
+    L = args.enc_len
+    b_loc = args.batch_per_gpu
+    B = b_loc * world
+    audio, ctxd, H = info.audio_dim, info.in_channels - info.audio_dim, info.hidden_size
+    shapes = dict(B=B, T=T, L=L, audio=audio, ctx=ctxd, H=H, mask=False, enc_mask=False)
+    cond = None
+    if rank == 0:
+        g = torch.Generator().manual_seed(1234)
+        noise = torch.randn((B, T, audio), generator=g)
+        src = torch.randn((B, T, audio), generator=g)
+        context = torch.cat([src, torch.ones((B, T, ctxd - audio))], dim=-1)  # silence latent | chunk mask
+        enc = torch.randn((B, L, H), generator=g)
+        cond = Conditioning(noise=noise, context=context, enc=enc)
+    torch.cuda.synchronize()
+    cond = broadcast_conditioning(cond, shapes, dev)
+    items = shard_indices(B, world, rank)
+    idx = torch.tensor(items, device=dev)
+    xt = cond.noise.index_select(0, idx).contiguous()
+    ctx = cond.context.index_select(0, idx).contiguous()
+    enc = cond.enc.index_select(0, idx).contiguous()
+    v = torch.empty_like(xt)
+    tt = torch.empty((b_loc,), dtype=torch.float32, device=dev)
+    sched = shifted_linear_schedule(args.sample_steps, 3.0)
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def step(i):
+        j = i % len(sched)
+        t = sched[j]
+        tt.fill_(t)
+        br.dit_forward_batched_device(b_loc, T, L, xt.data_ptr(), ctx.data_ptr(), enc.data_ptr(), 0, 0,
+                                      tt.data_ptr(), tt.data_ptr(), v.data_ptr(), stream)
+        dt = t if j + 1 == len(sched) else t - sched[j + 1]
+        xt.add_(v, alpha=-dt)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        elapsed = float(el.item())
+    finite = bool(torch.isfinite(xt).all().item())
+
+    # ---- per-kernel timing (HIP events on the launch stream, one event pair per launch)
+    breakdown = {}
+    roofline = None
+    if not args.no_profile:
+        br.profile_enable(True)
+        br.profile_reset()
+        nprof = 2
+        for i in range(nprof):
+            step(i)
+        torch.cuda.synchronize()
+        prof = br.profile_get()
+        br.profile_enable(False)
+        for name, ms, cnt in prof:
+            breakdown[name] = {"ms_per_step": round(ms / nprof, 4), "launches_per_step": cnt // nprof,
+                               "avg_us": round(1000.0 * ms / max(cnt, 1), 2)}
+        gu = [p for p in prof if p[0] == "gemm_gate_up"]
+        if gu:
+            name, ms, cnt = gu[0]
+            M = b_loc * ((T + 1) // 2)
+            flops = 2.0 * M * (2 * info.intermediate_size) * info.hidden_size
+            avg_s = ms / cnt / 1000.0
+            ach = flops / avg_s / 1e12
+            roofline = {"kernel": "gemm_gate_up (MLP gate|up, bf16 MFMA, SwiGLU epilogue)", "bound": "mfma",
+                        "achieved": round(ach, 1), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": round(ach / BF16_PEAK_TFLOPS, 4), "traffic": None,
+                        "flops_per_launch": flops, "avg_launch_us": round(avg_s * 1e6, 2),
+                        "shape_MNK": [M, 2 * info.intermediate_size, info.hidden_size]}
+        lin = [p for p in prof if p[0].startswith("gemm_")]
+        if lin:
+            Np = (T + 1) // 2
+            M = b_loc * Np
+            H_, I_ = info.hidden_size, info.intermediate_size
+            qd, kd = info.num_heads * info.head_dim, info.num_kv_heads * info.head_dim
+            per_layer = 2.0 * M * H_ * ((qd + 2 * kd) + qd + qd + qd + 2 * I_) + 2.0 * M * I_ * H_
+            lin_ms = sum(p[1] for p in lin if p[0] in ("gemm_qkv", "gemm_o", "gemm_cross_q", "gemm_cross_o",
+                                                          "gemm_gate_up", "gemm_down")) / nprof
+            if lin_ms > 0:
+                breakdown["_dit_block_linears"] = {
+                    "tflops": round(per_layer * info.num_layers / (lin_ms / 1000.0) / 1e12, 1),
+                    "frac_of_bf16_peak": round(per_layer * info.num_layers / (lin_ms / 1000.0) / 1e12
+                                               / BF16_PEAK_TFLOPS, 4)}
+
+    # ---- CPU baseline: the numpy oracle (restatement of ggml forward_dit) on the host cores
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and os.environ.get("ACE_MI_CPU_BASELINE", "1") != "0":
+        try:
+            cpu = cpu_baseline(ckpt, T, L)
+        except Exception as e:  # noqa: BLE001  (reported, never fatal)
+            cpu = {"value": None, "error": str(e)[:200]}
+
+    if rank == 0:
+        ms_per_step = 1000.0 * elapsed / args.steps
+        value = B * args.steps / elapsed
+        line = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic: random N(0,0.02) bf16 weights with the real DiT tensor names/shapes; "
+                    "N(0,1) latents/conditioning",
+            "config": {
+                "workload": f"DiT {args.sample_steps}-step sample, {args.seconds:g} s audio "
+                            f"(T={T} latent frames @25 Hz, N={(T + 1) // 2} tokens), enc_len={L}, "
+                            f"bs={b_loc}/GPU, bf16 weights, f32-faithful fp16x3 attention",
+                "model": "ACE-Step 1.5 DiT (24 layers, hidden 2048, MLP 6144, 16/8 heads)",
+                "seconds": args.seconds, "latent_frames": T, "tokens": (T + 1) // 2, "enc_len": L,
+                "batch_per_gpu": b_loc, "global_batch": B, "seq_len": T,
+                "parallelism": f"dp{world} (batch-sharded, RCCL broadcast of conditioning)",
+            },
+            "finite": finite,
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "breakdown": breakdown,
+        }
+        print(json.dumps(line), flush=True)
+    br.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(ckpt, T, L):
+    """Time one 240 s DiT forward of the numpy oracle (the checker restatement of ggml's CPU graph,
+    oracle/dit_oracle.py) on the host; steps/s = 1 / seconds."""
+    import numpy as np
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    except Exception:  # noqa: BLE001
+        cores = os.cpu_count() or 1
+    from oracle.dit_oracle import DitWeights, forward_dit
+    W = DitWeights(ckpt)
+    rng = np.random.default_rng(1234)
+    h = rng.standard_normal((T, 64)).astype(np.float32)
+    c = np.concatenate([rng.standard_normal((T, 64)), np.ones((T, 64))], axis=1).astype(np.float32)
+    e = rng.standard_normal((L, W.cfg.hidden_size)).astype(np.float32)
+    t0 = time.perf_counter()
+    forward_dit(W, h, c, e, None, None, T, L, 0.9, 0.9)
+    sec = time.perf_counter() - t0
+    return {"value": round(1.0 / sec, 5), "unit": "steps/s", "cores": cores, "kind": "port",
+            "seconds_per_step": round(sec, 3),
+            "sample": f"1 full 24-layer DiT forward, T={T}, L={L}, bs=1 (numpy/OpenBLAS f32 restatement "
+                      "of acestep_ggml forward_dit with ggml's bf16 activation rounding)"}
+
+
+if __name__ == "__main__":
+    main()

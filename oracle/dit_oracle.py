@@ -15,6 +15,7 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
+from . import ggml_numerics
 from .ggml_numerics import GgmlWeight, make_weight, mul_mat, bf16_bits_to_f32
 
 # --------------------------------------------------------------------------
@@ -338,3 +339,19 @@ def forward_dit(W: DitWeights, hidden_states, context_latents, encoder_hidden_st
     y_lin = mul_mat(W.proj_out_w, y)  # [Np][P*audio], column o + k*audio
     y2 = y_lin.reshape(Np * P, audio) + W.proj_out_b
     return np.ascontiguousarray(y2[:seq_len].astype(np.float32))
+
+
+def forward_with_floor(W: DitWeights, *args, perturb: float = 1e-7, **kw):
+    """(out, floor): the oracle output and its relative L2 change when every mul_mat result is
+    perturbed by `perturb` (a stand-in for another f32 summation order).  bf16 activation
+    rounding turns such a change of e into ~sqrt(e * 2^-8) per rounding site, so this floor,
+    not 0, is what two correct implementations of the same graph can agree to."""
+    out = forward_dit(W, *args, **kw)
+    old = ggml_numerics.MULMAT_PERTURB
+    ggml_numerics.MULMAT_PERTURB = perturb
+    try:
+        pert = forward_dit(W, *args, **kw)
+    finally:
+        ggml_numerics.MULMAT_PERTURB = old
+    floor = float(np.linalg.norm(pert.astype(np.float64) - out) / np.linalg.norm(out.astype(np.float64)))
+    return out, floor

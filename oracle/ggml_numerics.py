@@ -285,10 +285,19 @@ def convert_activation(x: np.ndarray, wtype: str) -> np.ndarray:
     raise ValueError(wtype)
 
 
+# Test-only knob: relative perturbation applied to every mul_mat result.  Used to measure the
+# reference computation's own sensitivity to f32 summation order (a different order changes a
+# dot product by ~1e-7 relative), which is the floor any non-bit-identical implementation sits on.
+MULMAT_PERTURB = 0.0
+
+
 def mul_mat(w: GgmlWeight, x: np.ndarray) -> np.ndarray:
     """ggml_mul_mat(W, x) -> x_conv @ W^T with f32 accumulation."""
     xa = convert_activation(np.asarray(x, dtype=np.float32), w.wtype)
-    return np.matmul(xa, w.values.T).astype(np.float32)
+    y = np.matmul(xa, w.values.T).astype(np.float32)
+    if MULMAT_PERTURB:
+        y = (y.astype(np.float64) * (1.0 + MULMAT_PERTURB)).astype(np.float32)
+    return y
 
 
 def make_weight(f32_values: np.ndarray, src_dtype: str, qtype: str | None) -> GgmlWeight:

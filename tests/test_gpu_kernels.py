@@ -70,13 +70,13 @@ def test_gemm_swiglu_epilogue(act):
     np.testing.assert_allclose(got, ref, rtol=ulp, atol=1e-5)
 
 
-def _attn_ref(q, kv, hq, hkv, window, kmask, scale):
+def _attn_ref(q, kv, hq, hkv, window, kmask, scale, rnd=round_f16):
     B, nq, _ = q.shape
     nk = kv.shape[1]
     D = 128
-    qh = round_f16(q).reshape(B, nq, hq, D)
-    k = round_f16(kv[:, :, :hkv * D]).reshape(B, nk, hkv, D)
-    v = round_f16(kv[:, :, hkv * D:]).reshape(B, nk, hkv, D)
+    qh = rnd(q).reshape(B, nq, hq, D)
+    k = rnd(kv[:, :, :hkv * D]).reshape(B, nk, hkv, D)
+    v = rnd(kv[:, :, hkv * D:]).reshape(B, nk, hkv, D)
     out = np.zeros((B, nq, hq, D), np.float64)
     rep = hq // hkv
     for b in range(B):
@@ -103,25 +103,51 @@ def _attn_ref(q, kv, hq, hkv, window, kmask, scale):
     (1, 2, 2, 130, 130, 128, True),
     (1, 4, 1, 97, 500, 0, False),
 ])
-def test_attention_vs_fp64(B, hq, hkv, nq, nk, window, masked):
+@pytest.mark.parametrize("split", [True, False])
+def test_attention_vs_fp64(B, hq, hkv, nq, nk, window, masked, split):
     rng = np.random.default_rng(B * 1000 + nq + nk)
-    q = rng.standard_normal((B, nq, hq * 128)).astype(np.float32) * 0.3
+    q = rng.standard_normal((B, nq, hq * 128)).astype(np.float32) * 2.0
     kv = rng.standard_normal((B, nk, 2 * hkv * 128)).astype(np.float32) * 0.3
     kmask = None
     if masked:
         kmask = (rng.random((B, nk)) > 0.3).astype(np.int32)
         kmask[:, 0] = 1
     scale = 1.0 / np.sqrt(128.0)
-    got = _capi().kernel_attention(q, kv, hq, hkv, window=window, kmask=kmask, scale=scale)
-    ref = _attn_ref(q, kv, hq, hkv, window, kmask, scale)
-    err = np.abs(got - ref)
-    # fp16 operands + bf16 output rounding: |err| <= 2^-8 |ref| + small absolute term
-    assert np.all(err <= 2.0 ** -8 * np.abs(ref) + 2e-3), float(err.max())
+    got = _capi().kernel_attention(q, kv, hq, hkv, window=window, kmask=kmask, scale=scale, split=split)
+    if split:
+        # ~22-bit operands: the only visible error is the bf16 rounding of the output
+        ref = _attn_ref(q, kv, hq, hkv, window, kmask, scale, rnd=lambda x: np.asarray(x, np.float32))
+        err = np.abs(got - ref)
+        assert np.all(err <= 2.0 ** -8 * np.abs(ref) + 1e-5), float(err.max())
+        # and it is much closer to the f32 reference than a single-fp16 evaluation would be
+        mism = np.mean(got != bf16_bits_to_f32(f32_to_bf16_bits(ref.astype(np.float32))))
+        assert mism < 0.01, mism
+    else:
+        ref = _attn_ref(q, kv, hq, hkv, window, kmask, scale)
+        err = np.abs(got - ref)
+        # fp16 operands + bf16 output rounding
+        assert np.all(err <= 2.0 ** -8 * np.abs(ref) + 2e-3), float(err.max())
 
 
-def test_attention_fully_masked_row_is_nan():
+@pytest.mark.parametrize("split", [True, False])
+def test_attention_fully_masked_row_is_nan(split):
     """ggml soft_max of an all -inf row gives NaN (acestep_dit_model.cpp:1245); so does the kernel."""
     q = np.ones((1, 8, 128), np.float32)
     kv = np.ones((1, 8, 256), np.float32)
-    got = _capi().kernel_attention(q, kv, 1, 1, window=0, kmask=np.zeros((1, 8), np.int32))
+    got = _capi().kernel_attention(q, kv, 1, 1, window=0, kmask=np.zeros((1, 8), np.int32), split=split)
     assert np.isnan(got).all()
+
+
+def test_attention_split_handles_small_values():
+    """lo parts of small operands are fp16 subnormals: check they are not flushed."""
+    rng = np.random.default_rng(3)
+    q = rng.standard_normal((1, 64, 128)).astype(np.float32) * 3
+    kv = rng.standard_normal((1, 64, 256)).astype(np.float32)
+    kv[:, :, 128:] *= 1e-3
+    got = _capi().kernel_attention(q, kv, 1, 1, split=True)
+    ref = _attn_ref(q, kv, 1, 1, 0, None, 1 / np.sqrt(128), rnd=lambda x: np.asarray(x, np.float32))
+    assert np.all(np.abs(got - ref) <= 2.0 ** -7 * np.abs(ref) + 1e-9)
+    # with flushed lo parts V would carry only fp16 precision and ~10% of outputs would round
+    # to a different bf16 than the f32 reference
+    mism = np.mean(got != bf16_bits_to_f32(f32_to_bf16_bits(ref.astype(np.float32))))
+    assert mism < 0.02, mism
