@@ -67,38 +67,51 @@ __global__ void to_act_kernel(bool f16, const float* __restrict__ in, int64_t n,
 // rms_norm (:1097-1106) + AdaLN modulate (:1477-1481, :1522-1526, :1545-1549):
 // y = ((x * 1/sqrt(mean(x^2)+eps)) * w) * (1 + scale) + shift, written in the act type that the
 // following mul_mat converts it to.
-template <bool F16>
+template <bool F16, int VPT>
 __global__ void __launch_bounds__(256) rmsnorm_mod_kernel(const float* __restrict__ x, int H, const float* __restrict__ w,
                                                           const float* __restrict__ scale, const float* __restrict__ shift,
                                                           int64_t mod_stride, int rows_per_item, float eps,
                                                           uint16_t* __restrict__ out) {
+    // one row per workgroup, VPT float4 per thread kept in registers (H <= 1024 * VPT)
     const int m = blockIdx.x;
     const float* xr = x + (int64_t)m * H;
     __shared__ float red[4];
+    float4 v[VPT];
     float ss = 0.f;
-    for (int i = threadIdx.x * 4; i < H; i += 1024) {
-        const float4 v = *(const float4*)(xr + i);
-        ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+#pragma unroll
+    for (int k = 0; k < VPT; ++k) {
+        const int i = (threadIdx.x + k * 256) * 4;
+        v[k] = i < H ? *(const float4*)(xr + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+        ss += v[k].x * v[k].x + v[k].y * v[k].y + v[k].z * v[k].z + v[k].w * v[k].w;
     }
     ss = wave_sum(ss);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
     __syncthreads();
     const float tot = red[0] + red[1] + red[2] + red[3];
-    const float mean = tot / (float)H;
-    const float sc = 1.0f / sqrtf(mean + eps);
+    const float sc = 1.0f / sqrtf(tot / (float)H + eps);
     const int item = m / rows_per_item;
     const float* scp = scale ? scale + (int64_t)item * mod_stride : nullptr;
     const float* shp = shift ? shift + (int64_t)item * mod_stride : nullptr;
     uint16_t* orow = out + (int64_t)m * H;
-    for (int i = threadIdx.x * 4; i < H; i += 1024) {
-        const float4 v = *(const float4*)(xr + i);
-        float y[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < VPT; ++k) {
+        const int i = (threadIdx.x + k * 256) * 4;
+        if (i >= H) break;
+        const float4 wv = *(const float4*)(w + i);
+        float y[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+        const float ww[4] = {wv.x, wv.y, wv.z, wv.w};
+        float s4[4] = {0.f, 0.f, 0.f, 0.f}, h4[4] = {0.f, 0.f, 0.f, 0.f};
+        if (scp) {
+            const float4 a4 = *(const float4*)(scp + i);
+            const float4 b4 = *(const float4*)(shp + i);
+            s4[0] = a4.x; s4[1] = a4.y; s4[2] = a4.z; s4[3] = a4.w;
+            h4[0] = b4.x; h4[1] = b4.y; h4[2] = b4.z; h4[3] = b4.w;
+        }
         uint16_t o[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            float t = __fmul_rn(y[j], sc);
-            t = __fmul_rn(t, w[i + j]);
-            if (scp) t = __fadd_rn(__fmul_rn(t, __fadd_rn(scp[i + j], 1.0f)), shp[i + j]);
+            float t = __fmul_rn(__fmul_rn(y[j], sc), ww[j]);
+            if (scp) t = __fadd_rn(__fmul_rn(t, __fadd_rn(s4[j], 1.0f)), h4[j]);
             o[j] = F16 ? f32_to_f16(t) : f32_to_bf16_rne(t);
         }
         uint2 pk;
@@ -121,86 +134,93 @@ __device__ __forceinline__ int vperm(int k) {
     return (k & ~15) | (gp << 2) | (w & 3);
 }
 
+// grid: (n_pad/64 token tiles, nq + nk + nv head slots, B).  Slot < nq: one q head; < nq+nk: one k
+// head; else the V^T transpose of one kv head.  One workgroup = 64 tokens of one head.
 __global__ void __launch_bounds__(256) attn_prep_kernel(PrepArgs a) {
     __shared__ float vs[64][129];
-    const int b = blockIdx.y;
+    const int b = blockIdx.z;
     const int n0 = blockIdx.x * 64;
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     const int nq = a.q_col >= 0 ? a.hq : 0;
     const int nk = a.k_col >= 0 ? a.hkv : 0;
-    const int nh = nq + nk;
-    for (int idx = wid; idx < 64 * nh; idx += 4) {
-        const int tok = idx / nh;
-        const int hh = idx % nh;
-        const int n = n0 + tok;
-        const bool isq = hh < nq;
-        const int head = isq ? hh : hh - nq;
-        float r0 = 0.f, r1 = 0.f;
-        if (n < a.n_tok) {
-            const float* row = a.src + ((int64_t)b * a.n_tok + n) * a.ld + (isq ? a.q_col : a.k_col) + head * 128;
-            const float x0 = row[lane];
-            const float x1 = row[lane + 64];
-            const float* w = isq ? a.q_norm : a.k_norm;
-            float y0 = x0, y1 = x1;
-            if (w) {  // null weight: plain copy (kernel self-test entry)
-                const float ss = wave_sum(x0 * x0 + x1 * x1);
-                const float sc = 1.0f / sqrtf(ss / 128.0f + a.eps);
-                y0 = __fmul_rn(__fmul_rn(x0, sc), w[lane]);
-                y1 = __fmul_rn(__fmul_rn(x1, sc), w[lane + 64]);
-            }
-            if (a.rope_cos) {
-                const float c = a.rope_cos[(int64_t)n * 64 + lane];
-                const float s = a.rope_sin[(int64_t)n * 64 + lane];
-                r0 = __fsub_rn(__fmul_rn(y0, c), __fmul_rn(y1, s));
-                r1 = __fadd_rn(__fmul_rn(y0, s), __fmul_rn(y1, c));
-            } else {
-                r0 = y0;
-                r1 = y1;
-            }
-        }
-        uint16_t* dst = isq ? a.qh + (((int64_t)b * a.hq + head) * a.n_pad + n) * 128
-                            : a.kh + (((int64_t)b * a.hkv + head) * a.n_pad + n) * 128;
-        const uint16_t h0 = f32_to_f16(r0), h1 = f32_to_f16(r1);
-        dst[lane] = h0;
-        dst[lane + 64] = h1;
+    const int slot = blockIdx.y;
+    if (slot < nq + nk) {
+        const bool isq = slot < nq;
+        const int head = isq ? slot : slot - nq;
+        const float* w = isq ? a.q_norm : a.k_norm;
+        const int col = (isq ? a.q_col : a.k_col) + head * 128;
+        uint16_t* base = isq ? a.qh + ((int64_t)b * a.hq + head) * a.n_pad * 128
+                             : a.kh + ((int64_t)b * a.hkv + head) * a.n_pad * 128;
         const int64_t plane = isq ? a.q_plane : a.k_plane;
-        if (plane > 0) {
-            dst[plane + lane] = f32_to_f16(r0 - (float)__builtin_bit_cast(_Float16, h0));
-            dst[plane + lane + 64] = f32_to_f16(r1 - (float)__builtin_bit_cast(_Float16, h1));
+        const float w0 = w ? w[lane] : 1.f, w1 = w ? w[lane + 64] : 1.f;
+        for (int tok = wid; tok < 64; tok += 4) {
+            const int n = n0 + tok;
+            float r0 = 0.f, r1 = 0.f;
+            if (n < a.n_tok) {
+                const float* row = a.src + ((int64_t)b * a.n_tok + n) * a.ld + col;
+                const float x0 = row[lane];
+                const float x1 = row[lane + 64];
+                float y0 = x0, y1 = x1;
+                if (w) {  // null weight: plain copy (kernel self-test entry)
+                    const float ss = wave_sum(x0 * x0 + x1 * x1);
+                    const float sc = 1.0f / sqrtf(ss / 128.0f + a.eps);
+                    y0 = __fmul_rn(__fmul_rn(x0, sc), w0);
+                    y1 = __fmul_rn(__fmul_rn(x1, sc), w1);
+                }
+                if (a.rope_cos) {
+                    const float c = a.rope_cos[(int64_t)n * 64 + lane];
+                    const float s = a.rope_sin[(int64_t)n * 64 + lane];
+                    r0 = __fsub_rn(__fmul_rn(y0, c), __fmul_rn(y1, s));
+                    r1 = __fadd_rn(__fmul_rn(y0, s), __fmul_rn(y1, c));
+                } else {
+                    r0 = y0;
+                    r1 = y1;
+                }
+            }
+            uint16_t* dst = base + (int64_t)n * 128;
+            const uint16_t h0 = f32_to_f16(r0), h1 = f32_to_f16(r1);
+            dst[lane] = h0;
+            dst[lane + 64] = h1;
+            if (plane > 0) {
+                dst[plane + lane] = f32_to_f16(r0 - (float)__builtin_bit_cast(_Float16, h0));
+                dst[plane + lane + 64] = f32_to_f16(r1 - (float)__builtin_bit_cast(_Float16, h1));
+            }
         }
+        return;
     }
     if (a.v_col < 0) return;
-    for (int hk = 0; hk < a.hkv; ++hk) {
-        __syncthreads();
-        for (int i = threadIdx.x; i < 64 * 128; i += 256) {
-            const int tok = i >> 7;
-            const int d = i & 127;
-            const int n = n0 + tok;
-            float v = 0.f;
-            if (n < a.n_tok) v = a.src[((int64_t)b * a.n_tok + n) * a.ld + a.v_col + hk * 128 + d];
-            vs[tok][d] = v;
-        }
-        __syncthreads();
-        const int d = threadIdx.x >> 1;
-        const int half = threadIdx.x & 1;
-        uint16_t* dst = a.vt + (((int64_t)b * a.hkv + hk) * 128 + d) * a.n_pad + n0 + half * 32;
+    const int hk = slot - nq - nk;
+    for (int i = threadIdx.x; i < 64 * 32; i += 256) {
+        const int tok = i >> 5;
+        const int d4 = (i & 31) * 4;
+        const int n = n0 + tok;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (n < a.n_tok) v = *(const float4*)(a.src + ((int64_t)b * a.n_tok + n) * a.ld + a.v_col + hk * 128 + d4);
+        vs[tok][d4 + 0] = v.x;
+        vs[tok][d4 + 1] = v.y;
+        vs[tok][d4 + 2] = v.z;
+        vs[tok][d4 + 3] = v.w;
+    }
+    __syncthreads();
+    const int d = threadIdx.x >> 1;
+    const int half = threadIdx.x & 1;
+    uint16_t* dst = a.vt + (((int64_t)b * a.hkv + hk) * 128 + d) * a.n_pad + n0 + half * 32;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            uint32_t wv[4], wl[4];
+    for (int c = 0; c < 4; ++c) {
+        uint32_t wv[4], wl[4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int p0 = half * 32 + c * 8 + 2 * j;
-                const float v0 = vs[vperm(p0)][d];
-                const float v1 = vs[vperm(p0 + 1)][d];
-                const uint16_t h0 = f32_to_f16(v0), h1 = f32_to_f16(v1);
-                wv[j] = (uint32_t)h0 | ((uint32_t)h1 << 16);
-                wl[j] = (uint32_t)f32_to_f16(v0 - (float)__builtin_bit_cast(_Float16, h0)) |
-                        ((uint32_t)f32_to_f16(v1 - (float)__builtin_bit_cast(_Float16, h1)) << 16);
-            }
-            *(uint4*)(dst + c * 8) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
-            if (a.v_plane > 0) *(uint4*)(dst + a.v_plane + c * 8) = make_uint4(wl[0], wl[1], wl[2], wl[3]);
+        for (int j = 0; j < 4; ++j) {
+            const int p0 = half * 32 + c * 8 + 2 * j;
+            const float v0 = vs[vperm(p0)][d];
+            const float v1 = vs[vperm(p0 + 1)][d];
+            const uint16_t h0 = f32_to_f16(v0), h1 = f32_to_f16(v1);
+            wv[j] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+            wl[j] = (uint32_t)f32_to_f16(v0 - (float)__builtin_bit_cast(_Float16, h0)) |
+                    ((uint32_t)f32_to_f16(v1 - (float)__builtin_bit_cast(_Float16, h1)) << 16);
         }
+        *(uint4*)(dst + c * 8) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+        if (a.v_plane > 0) *(uint4*)(dst + a.v_plane + c * 8) = make_uint4(wl[0], wl[1], wl[2], wl[3]);
     }
 }
 
@@ -357,19 +377,38 @@ void launch_to_act(ActType t, const float* in, int64_t n, bool silu, uint16_t* o
 void launch_rmsnorm_mod(ActType t, const float* x, int M, int H, const float* w, const float* scale,
                         const float* shift, int64_t mod_stride, int rows_per_item, float eps, uint16_t* out,
                         hipStream_t s) {
-    ACEMI_CHECK(H % 4 == 0, "rmsnorm: H % 4");
-    if (t == ActType::F16)
-        hipLaunchKernelGGL(rmsnorm_mod_kernel<true>, dim3(M), dim3(256), 0, s, x, H, w, scale, shift, mod_stride,
-                           rows_per_item, eps, out);
-    else
-        hipLaunchKernelGGL(rmsnorm_mod_kernel<false>, dim3(M), dim3(256), 0, s, x, H, w, scale, shift, mod_stride,
-                           rows_per_item, eps, out);
+    ACEMI_CHECK(H % 4 == 0 && H <= 4096, "rmsnorm: H % 4 == 0 and H <= 4096");
+    const bool f16 = t == ActType::F16;
+    if (H <= 1024) {
+        if (f16)
+            hipLaunchKernelGGL((rmsnorm_mod_kernel<true, 1>), dim3(M), dim3(256), 0, s, x, H, w, scale, shift,
+                               mod_stride, rows_per_item, eps, out);
+        else
+            hipLaunchKernelGGL((rmsnorm_mod_kernel<false, 1>), dim3(M), dim3(256), 0, s, x, H, w, scale, shift,
+                               mod_stride, rows_per_item, eps, out);
+    } else if (H <= 2048) {
+        if (f16)
+            hipLaunchKernelGGL((rmsnorm_mod_kernel<true, 2>), dim3(M), dim3(256), 0, s, x, H, w, scale, shift,
+                               mod_stride, rows_per_item, eps, out);
+        else
+            hipLaunchKernelGGL((rmsnorm_mod_kernel<false, 2>), dim3(M), dim3(256), 0, s, x, H, w, scale, shift,
+                               mod_stride, rows_per_item, eps, out);
+    } else {
+        if (f16)
+            hipLaunchKernelGGL((rmsnorm_mod_kernel<true, 4>), dim3(M), dim3(256), 0, s, x, H, w, scale, shift,
+                               mod_stride, rows_per_item, eps, out);
+        else
+            hipLaunchKernelGGL((rmsnorm_mod_kernel<false, 4>), dim3(M), dim3(256), 0, s, x, H, w, scale, shift,
+                               mod_stride, rows_per_item, eps, out);
+    }
     ACEMI_HIP(hipGetLastError());
 }
 
 void launch_attn_prep(const PrepArgs& a, hipStream_t s) {
     ACEMI_CHECK(a.n_pad % 64 == 0, "attn_prep: n_pad % 64");
-    hipLaunchKernelGGL(attn_prep_kernel, dim3(a.n_pad / 64, a.B), dim3(256), 0, s, a);
+    const int slots = (a.q_col >= 0 ? a.hq : 0) + (a.k_col >= 0 ? a.hkv : 0) + (a.v_col >= 0 ? a.hkv : 0);
+    ACEMI_CHECK(a.ld % 4 == 0 && (a.v_col < 0 || a.v_col % 4 == 0), "attn_prep: alignment");
+    hipLaunchKernelGGL(attn_prep_kernel, dim3(a.n_pad / 64, slots, a.B), dim3(256), 0, s, a);
     ACEMI_HIP(hipGetLastError());
 }
 

@@ -146,7 +146,7 @@ def test_attention_split_handles_small_values():
     kv[:, :, 128:] *= 1e-3
     got = _capi().kernel_attention(q, kv, 1, 1, split=True)
     ref = _attn_ref(q, kv, 1, 1, 0, None, 1 / np.sqrt(128), rnd=lambda x: np.asarray(x, np.float32))
-    assert np.all(np.abs(got - ref) <= 2.0 ** -7 * np.abs(ref) + 1e-9)
+    assert np.all(np.abs(got - ref) <= 2.0 ** -8 * np.abs(ref) + 1e-4 * np.abs(ref).max())
     # with flushed lo parts V would carry only fp16 precision and ~10% of outputs would round
     # to a different bf16 than the f32 reference
     mism = np.mean(got != bf16_bits_to_f32(f32_to_bf16_bits(ref.astype(np.float32))))
