@@ -31,7 +31,8 @@ EXPORTED_SYMBOLS = (
     "ace_ggml_create", "ace_ggml_destroy", "ace_ggml_last_error", "ace_ggml_load_dit", "ace_ggml_dit_forward",
     "ace_mi_create_on_device", "ace_mi_dit_get_info", "ace_mi_dit_forward_batched", "ace_mi_dit_sample",
     "ace_mi_profile_enable", "ace_mi_profile_reset", "ace_mi_profile_get", "ace_mi_probe_gemm",
-    "ace_mi_synchronize", "ace_mi_kernel_gemm", "ace_mi_kernel_attention",
+    "ace_mi_synchronize", "ace_mi_kernel_gemm", "ace_mi_kernel_attention", "ace_mi_bench_gemm",
+    "ace_mi_gemm_variant",
 )
 
 
@@ -106,6 +107,10 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.ace_mi_kernel_gemm.restype = ctypes.c_int
     lib.ace_mi_kernel_attention.argtypes = [i32, i32, i32, i32, i32, i32, f32, i32, fp, fp, ip, fp]
     lib.ace_mi_kernel_attention.restype = ctypes.c_int
+    lib.ace_mi_bench_gemm.argtypes = [i32, i32, i32, i32, i32, i32, i32, fp]
+    lib.ace_mi_bench_gemm.restype = ctypes.c_int
+    lib.ace_mi_gemm_variant.argtypes = [i32]
+    lib.ace_mi_gemm_variant.restype = ctypes.c_int
     if path is None:
         _LIB = lib
     return lib
@@ -264,3 +269,19 @@ def kernel_attention(q: np.ndarray, kv: np.ndarray, hq: int, hkv: int, window: i
     if st != ACE_GGML_OK:
         raise RuntimeError(f"ace_mi_kernel_attention failed (status={st})")
     return out
+
+
+def bench_gemm(M: int, N: int, K: int, variant: int = -1, epi: int = 0, act_type: int = 0, iters: int = 20) -> float:
+    """Average ms per launch of the engine GEMM on random operands (GPU)."""
+    lib = load_library()
+    ms = ctypes.c_float(0.0)
+    st = lib.ace_mi_bench_gemm(act_type, epi, variant, M, N, K, iters, ctypes.byref(ms))
+    if st != ACE_GGML_OK:
+        raise RuntimeError(f"ace_mi_bench_gemm failed (status={st})")
+    return float(ms.value)
+
+
+def gemm_variant(variant: int) -> None:
+    lib = load_library()
+    if lib.ace_mi_gemm_variant(int(variant)) != ACE_GGML_OK:
+        raise ValueError(variant)

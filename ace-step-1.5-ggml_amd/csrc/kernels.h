@@ -34,6 +34,8 @@ struct GemmEpilogue {
 
 void launch_gemm(ActType t, const uint16_t* A, int lda, const uint16_t* W, int ldw, int M, int N, int K,
                  const GemmEpilogue& epi, hipStream_t s);
+// -1 = automatic tile choice; 0..3 force a kernel variant (micro-benchmarks / tests)
+void gemm_force_variant(int v);
 
 // ------------------------------------------------------------ attention
 // Flash-style fp16 attention, f32 softmax/accumulate.  D = 128.

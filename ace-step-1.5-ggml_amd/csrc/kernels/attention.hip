@@ -30,6 +30,7 @@
 // LDS and the per-row rescale factor is lane-local.  K/V^T tiles arrive by
 // global_load_lds into a double-buffered, XOR-swizzled LDS image.
 #include "../kernels.h"
+#include "lds_asm.h"
 
 namespace acemi {
 namespace {
@@ -179,37 +180,60 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
+    // Per-lane LDS read addressing.  K rows are 256 B with 16-B chunk c stored at c ^ (key & 15); the
+    // fragment chunk of k-step ks is 2*ks + h, so its physical chunk is (2*ks) ^ cK (cK lane constant).
+    // V^T rows are 128 B with chunk c at c ^ ((d >> 1) & 7): chunk of key-step g is (2*g) ^ cV.
+    const int cK = h ^ (lq & 15);
+    const int cV = h ^ ((lq >> 1) & 7);
+    const uint32_t smem_l = lds_addr(smem);
+
     for (int kt = kt_begin; kt < kt_end; ++kt) {
         const int cur = (kt - kt_begin) & 1;
         if (kt + 1 < kt_end) stage(cur ^ 1, kt + 1);
-        const char* Ks = smem + cur * STAGE + ST::K_HI;
-        const char* Ksl = smem + cur * STAGE + ST::K_LO;
-        const char* Vs = smem + cur * STAGE + ST::V_HI;
-        const char* Vsl = smem + cur * STAGE + ST::V_LO;
-        const float* KBs = (const float*)(smem + cur * STAGE + ST::KB);
+        const uint32_t st = smem_l + cur * STAGE;
         const int k0 = kt * KT;
 
-        // ---- S^T = K . Q^T (two 32-key tiles)
+        // ---- S^T = K . Q^T (two 32-key tiles); SPLIT: Kh.Qh + Kh.Ql + Kl.Qh
         f32x16 s[2];
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) s[t][r] = 0.f;
-            const int key = 32 * t + lq;
+            const uint32_t rowk = st + ST::K_HI + (32 * t + lq) * 256;
+            uint4 kf[8], kfl[8];
+#pragma unroll
+            for (int ks = 0; ks < 8; ++ks) kf[ks] = ds_read_b128_v(rowk + (((2 * ks) ^ cK) << 4));
+            if constexpr (SPLIT) {
+#pragma unroll
+                for (int ks = 0; ks < 8; ++ks)
+                    kfl[ks] = ds_read_b128_v(rowk + (ST::K_LO - ST::K_HI) + (((2 * ks) ^ cK) << 4));
+            }
+            lds_wait_all();
 #pragma unroll
             for (int ks = 0; ks < 8; ++ks) {
-                const int ch = (2 * ks + h) ^ (key & 15);
-                const uint4 kf = *(const uint4*)(Ks + key * 256 + ch * 16);
-                s[t] = mfma32(kf, qf[ks], s[t]);
+                s[t] = mfma32(kf[ks], qf[ks], s[t]);
                 if constexpr (SPLIT) {
-                    const uint4 kfl = *(const uint4*)(Ksl + key * 256 + ch * 16);
-                    s[t] = mfma32(kf, qfl[ks], s[t]);
-                    s[t] = mfma32(kfl, qf[ks], s[t]);
+                    s[t] = mfma32(kf[ks], qfl[ks], s[t]);
+                    s[t] = mfma32(kfl[ks], qf[ks], s[t]);
                 }
             }
         }
 
         // ---- scale, mask, online softmax (this lane: query qrow, 32 of the 64 keys)
+        float kbv[2][16];
+        if (kb) {
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int g4 = 0; g4 < 4; ++g4) {
+                    const uint4 v = ds_read_b128_v(st + ST::KB + (32 * t + 8 * g4 + 4 * h) * 4);
+                    kbv[t][4 * g4 + 0] = __uint_as_float(v.x);
+                    kbv[t][4 * g4 + 1] = __uint_as_float(v.y);
+                    kbv[t][4 * g4 + 2] = __uint_as_float(v.z);
+                    kbv[t][4 * g4 + 3] = __uint_as_float(v.w);
+                }
+            lds_wait_all();
+        }
         const bool need_window = a.window > 0 && (k0 < qw0 + 31 - a.window || k0 + KT - 1 > qw0 + a.window);
         float mloc = -INFINITY;
 #pragma unroll
@@ -218,7 +242,7 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
             for (int r = 0; r < 16; ++r) {
                 const int krel = 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h;
                 float x = s[t][r] * c_log2;
-                if (kb) x += KBs[krel];
+                if (kb) x += kbv[t][r];
                 if (need_window) {
                     const int d = qrow - (k0 + krel);
                     if (d > a.window || d < -a.window) x = -INFINITY;
@@ -266,24 +290,32 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
 
-        // ---- O^T += V^T . P^T
+        // ---- O^T += V^T . P^T ; SPLIT: Vh.Ph + Vh.Pl + Vl.Ph
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) {
-            const int d = 32 * dt + lq;
+            const uint32_t rowv = st + ST::V_HI + (32 * dt + lq) * 128;
+            uint4 vf[4], vfl[4];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) vf[g] = ds_read_b128_v(rowv + (((2 * g) ^ cV) << 4));
+            if constexpr (SPLIT) {
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+                    vfl[g] = ds_read_b128_v(rowv + (ST::V_LO - ST::V_HI) + (((2 * g) ^ cV) << 4));
+            }
+            lds_wait_all();
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-                const int ch = (2 * g + h) ^ ((d >> 1) & 7);
-                const uint4 vf = *(const uint4*)(Vs + d * 128 + ch * 16);
-                o[dt] = mfma32(vf, pf[g], o[dt]);
+                o[dt] = mfma32(vf[g], pf[g], o[dt]);
                 if constexpr (SPLIT) {
-                    const uint4 vfl = *(const uint4*)(Vsl + d * 128 + ch * 16);
-                    o[dt] = mfma32(vf, pfl[g], o[dt]);
-                    o[dt] = mfma32(vfl, pf[g], o[dt]);
+                    o[dt] = mfma32(vf[g], pfl[g], o[dt]);
+                    o[dt] = mfma32(vfl[g], pf[g], o[dt]);
                 }
             }
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+        if (kt + 1 < kt_end) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile kt+1 landed (issued a whole tile ago)
+            __builtin_amdgcn_s_barrier();                     // ... for every wave; buffer `cur` released
+        }
     }
 
     // ---- normalise and store O[q][head*128 + d]

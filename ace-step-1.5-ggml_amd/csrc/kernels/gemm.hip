@@ -16,6 +16,8 @@
 // ds_read, which makes every ds_read_b128 lane group conflict-free.
 // Blocks are remapped XCD-aware (blocks b, b+8 share an XCD) and grouped
 // along M so co-resident tiles share weight panels in L2.
+#include <cmath>
+
 #include "../kernels.h"
 
 namespace acemi {
@@ -67,7 +69,50 @@ __device__ __forceinline__ f32x4 mfma16(const uint4& a, const uint4& b, f32x4 c)
 // chunk swizzle of a 128-byte LDS row
 __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 
-template <int BM, int BN, int WM, int WN, bool F16, int EPI>
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+
+// ds_read_b128 hidden from the compiler's waitcnt pass (it would otherwise drain every in-flight
+// LDS-DMA with vmcnt(0) before the read, serialising the prefetch).  The caller waits with
+// lds_wait_all() + sched_barrier before consuming the registers (guide §5.7 item 1, rule 18).
+template <int OFF>
+__device__ __forceinline__ uint4 ds_read_b128_off(uint32_t addr) {
+    u32x4 v;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
+    return make_uint4(v[0], v[1], v[2], v[3]);
+}
+__device__ __forceinline__ void lds_wait_all() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int I, int N, int STRIDE>
+struct ReadRows {  // dst[i] = 16 bytes at base + i*STRIDE, i = I..N-1 (compile-time offsets)
+    __device__ __forceinline__ static void run(uint32_t base, uint4 (&dst)[N][2], int kk) {
+        if (kk == 0)
+            dst[I][0] = ds_read_b128_off<I * STRIDE>(base);
+        else
+            dst[I][1] = ds_read_b128_off<I * STRIDE>(base);
+        ReadRows<I + 1, N, STRIDE>::run(base, dst, kk);
+    }
+};
+template <int N, int STRIDE>
+struct ReadRows<N, N, STRIDE> {
+    __device__ __forceinline__ static void run(uint32_t, uint4 (&)[N][2], int) {}
+};
+
+// s_waitcnt vmcnt(N) with N a compile-time constant (lgkmcnt/expcnt untouched)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
+__device__ __forceinline__ void wait_lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F); }
+
+// PIPE 0: stage(t+1) ; compute(t) ; vmcnt(0) ; __syncthreads        (2 LDS buffers)
+// PIPE 1: compute first half of tile t from registers read up front, release the LDS buffer with
+//         a raw s_barrier, stage tile t+2 into it, compute the second half, then a COUNTED
+//         vmcnt(G) retires tile t+1 while t+2 stays in flight across the next barrier.
+template <int BM, int BN, int WM, int WN, bool F16, int EPI, int PIPE>
 __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(GemmParams p) {
     constexpr int NW = WM * WN;
     constexpr int WTM = BM / WM;
@@ -81,7 +126,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(GemmParams p) {
     static_assert((BM + BN) % (8 * NW) == 0, "staging split");
     static_assert(EPI != EPI_SWIGLU || (TN % 2 == 0), "swiglu needs column pairs");
 
-    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -149,40 +194,98 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(GemmParams p) {
         for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     const int nk = p.K / BK;
-    stage(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-
     const int lrow = lane & 15;
     const int lchunk = lane >> 4;
 
-    for (int kt = 0; kt < nk; ++kt) {
-        const int cur = kt & 1;
-        if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
-        const char* As = smem + cur * STAGE;
+    auto read_frags = [&](int buf, uint4 (&a)[TM][2], uint4 (&b)[TN][2]) {
+        const char* As = smem + buf * STAGE;
         const char* Bs = As + BM * ROWB;
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
-            uint4 a[TM], b[TN];
-#pragma unroll
-            for (int i = 0; i < TM; ++i) {
-                const int row = wm0 + i * 16 + lrow;
-                const int ch = (kk * 4 + lchunk) ^ swz(row);
-                a[i] = *(const uint4*)(As + row * ROWB + ch * 16);
-            }
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
                 const int row = wn0 + j * 16 + lrow;
                 const int ch = (kk * 4 + lchunk) ^ swz(row);
-                b[j] = *(const uint4*)(Bs + row * ROWB + ch * 16);
+                b[j][kk] = *(const uint4*)(Bs + row * ROWB + ch * 16);
             }
 #pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<F16>(a[i], b[j], acc[i][j]);
+            for (int i = 0; i < TM; ++i) {
+                const int row = wm0 + i * 16 + lrow;
+                const int ch = (kk * 4 + lchunk) ^ swz(row);
+                a[i][kk] = *(const uint4*)(As + row * ROWB + ch * 16);
+            }
         }
+    };
+    // asm variant: row = w0 + i*16 + lrow has swz(row) = (lrow >> 1) & 7 for every i (w0, i*16 are
+    // multiples of 16), so fragment i sits at a lane base + i * 16 rows: one base per (operand, kk).
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+    auto read_frags_asm = [&](int buf, uint4 (&a)[TM][2], uint4 (&b)[TN][2]) {
+        const uint32_t sbase = lds0 + buf * STAGE;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int ch = (kk * 4 + lchunk) ^ ((lrow >> 1) & 7);
+            const uint32_t bb = sbase + BM * ROWB + (wn0 + lrow) * ROWB + ch * 16;
+            const uint32_t ab = sbase + (wm0 + lrow) * ROWB + ch * 16;
+            ReadRows<0, TN, 16 * ROWB>::run(bb, b, kk);
+            ReadRows<0, TM, 16 * ROWB>::run(ab, a, kk);
+        }
+        lds_wait_all();
+    };
+
+    if constexpr (PIPE == 0) {
+        stage(0, 0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        for (int kt = 0; kt < nk; ++kt) {
+            const int cur = kt & 1;
+            if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
+            uint4 a[TM][2], b[TN][2];
+            read_frags(cur, a, b);
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<F16>(a[i][kk], b[j][kk], acc[i][j]);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
+    } else {
+        stage(0, 0);
+        if (nk > 1) {
+            stage(1, 1);
+            wait_vmcnt<G_PER_WAVE>();
+        } else {
+            wait_vmcnt<0>();
+        }
+        __builtin_amdgcn_s_barrier();
+        for (int kt = 0; kt < nk; ++kt) {
+            const int cur = kt & 1;
+            uint4 a[TM][2], b[TN][2];
+            read_frags_asm(cur, a, b);
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+                for (int i = 0; i < TM / 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<F16>(a[i][kk], b[j][kk], acc[i][j]);
+            __builtin_amdgcn_s_barrier();  // every wave has its fragments of tile kt: buffer `cur` is free
+            const bool more = kt + 2 < nk;
+            if (more) stage(cur, kt + 2);
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+                for (int i = TM / 2; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<F16>(a[i][kk], b[j][kk], acc[i][j]);
+            if (kt + 1 < nk) {
+                if (more)
+                    wait_vmcnt<G_PER_WAVE>();  // tile kt+1 landed, kt+2 still in flight
+                else
+                    wait_vmcnt<0>();
+                __builtin_amdgcn_s_barrier();
+            }
+        }
     }
 
     // ---- epilogue.  C/D map of 16x16x32: col = lane & 15, row = (lane >> 4) * 4 + r.
@@ -238,27 +341,60 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(GemmParams p) {
     }
 }
 
-template <int BM, int BN, int WM, int WN, bool F16, int EPI>
+template <int BM, int BN, int WM, int WN, bool F16, int EPI, int PIPE>
 void launch_cfg(const GemmParams& p, hipStream_t s) {
     const int nbm = (p.M + BM - 1) / BM;
     const int nbn = p.N / BN;
     const dim3 grid(nbm * nbn);
     const dim3 block(WM * WN * 64);
-    const size_t lds = 2 * (BM + BN) * 128;
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, F16, EPI>), grid, block, lds, s, p);
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, F16, EPI, PIPE>), grid, block, 0, s, p);
+}
+
+// variant: 0 = 128x128 PIPE0, 1 = 128x128 PIPE1, 2 = 256x256 PIPE1 (8 waves 2x4), 3 = 256x128 PIPE1
+template <bool F16, int EPI>
+void launch_variant(int variant, const GemmParams& p, hipStream_t s) {
+    switch (variant) {
+        case 0: launch_cfg<128, 128, 2, 2, F16, EPI, 0>(p, s); break;
+        case 1: launch_cfg<128, 128, 2, 2, F16, EPI, 1>(p, s); break;
+        case 2: launch_cfg<256, 256, 2, 4, F16, EPI, 1>(p, s); break;
+        case 3: launch_cfg<256, 128, 2, 2, F16, EPI, 1>(p, s); break;
+        default: throw std::runtime_error("gemm: bad variant");
+    }
 }
 
 template <bool F16>
-void dispatch_epi(const GemmParams& p, hipStream_t s) {
+void dispatch_epi(int variant, const GemmParams& p, hipStream_t s) {
     switch (p.e.kind) {
-        case EPI_STORE_F32: launch_cfg<128, 128, 2, 2, F16, EPI_STORE_F32>(p, s); break;
-        case EPI_STORE_ACT: launch_cfg<128, 128, 2, 2, F16, EPI_STORE_ACT>(p, s); break;
-        case EPI_RESID_GATED: launch_cfg<128, 128, 2, 2, F16, EPI_RESID_GATED>(p, s); break;
-        case EPI_RESID: launch_cfg<128, 128, 2, 2, F16, EPI_RESID>(p, s); break;
-        case EPI_SWIGLU: launch_cfg<128, 128, 2, 2, F16, EPI_SWIGLU>(p, s); break;
-        case EPI_PROJ_OUT: launch_cfg<128, 128, 2, 2, F16, EPI_PROJ_OUT>(p, s); break;
+        case EPI_STORE_F32: launch_variant<F16, EPI_STORE_F32>(variant, p, s); break;
+        case EPI_STORE_ACT: launch_variant<F16, EPI_STORE_ACT>(variant, p, s); break;
+        case EPI_RESID_GATED: launch_variant<F16, EPI_RESID_GATED>(variant, p, s); break;
+        case EPI_RESID: launch_variant<F16, EPI_RESID>(variant, p, s); break;
+        case EPI_SWIGLU: launch_variant<F16, EPI_SWIGLU>(variant, p, s); break;
+        case EPI_PROJ_OUT: launch_variant<F16, EPI_PROJ_OUT>(variant, p, s); break;
         default: throw std::runtime_error("gemm: bad epilogue kind");
     }
+}
+
+int g_forced_variant = -1;
+
+// Tile choice: measured kernel ceiling (random bf16 operands, MI355X: v1 ~950, v2 ~1120 TFLOP/s at
+// large shapes) times the wave-quantization efficiency of the grid over 256 CUs (v1: 2 blocks/CU,
+// 64 KiB LDS each; v2: 1 block/CU, 128 KiB) and the M-edge utilisation.
+double predicted_tflops(int variant, int M, int N) {
+    const int bm = variant == 2 ? 256 : 128, bn = variant == 2 ? 256 : 128;
+    const double ceiling = variant == 2 ? 1120.0 : 950.0;
+    const int slots = variant == 2 ? 256 : 512;
+    const int64_t tiles = (int64_t)((M + bm - 1) / bm) * (N / bn);
+    const double waves = (double)tiles / slots;
+    const double eff = waves / std::ceil(waves);
+    const double medge = (double)M / (double)(((M + bm - 1) / bm) * bm);
+    return ceiling * eff * medge;
+}
+
+int pick_variant(int M, int N) {
+    if (g_forced_variant >= 0) return g_forced_variant;
+    if (N % 256 != 0) return 1;
+    return predicted_tflops(2, M, N) > predicted_tflops(1, M, N) ? 2 : 1;
 }
 
 }  // namespace
@@ -268,11 +404,14 @@ void launch_gemm(ActType t, const uint16_t* A, int lda, const uint16_t* W, int l
     ACEMI_CHECK(M >= 1 && N % 128 == 0 && K % 64 == 0 && K >= 64, "gemm: unsupported shape");
     ACEMI_CHECK(lda % 8 == 0 && ldw % 8 == 0, "gemm: leading dims must be multiples of 8");
     GemmParams p{A, W, lda, ldw, M, N, K, epi};
+    const int v = pick_variant(M, N);
     if (t == ActType::F16)
-        dispatch_epi<true>(p, s);
+        dispatch_epi<true>(v, p, s);
     else
-        dispatch_epi<false>(p, s);
+        dispatch_epi<false>(v, p, s);
     ACEMI_HIP(hipGetLastError());
 }
+
+void gemm_force_variant(int v) { g_forced_variant = v; }
 
 }  // namespace acemi

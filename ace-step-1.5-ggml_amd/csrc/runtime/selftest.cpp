@@ -141,3 +141,73 @@ ace_ggml_status ace_mi_kernel_attention(int32_t B, int32_t Hq, int32_t Hkv, int3
 }
 
 }  // extern "C"
+
+extern "C" {
+
+// GEMM micro-benchmark (random bf16/fp16 operands, device-resident): average ms per launch over
+// `iters` launches timed with hipEvents.  variant -1 = the engine's automatic choice.
+ace_ggml_status ace_mi_bench_gemm(int32_t act_type, int32_t epi, int32_t variant, int32_t M, int32_t N, int32_t K,
+                                  int32_t iters, float* avg_ms) {
+    using namespace acemi;
+    if (M <= 0 || N % 128 != 0 || K % 64 != 0 || iters <= 0 || !avg_ms) return ACE_GGML_ERR_INVALID_ARG;
+    try {
+        std::vector<uint16_t> ha((size_t)M * K), hw((size_t)N * K);
+        uint32_t st = 12345u;
+        auto rnd = [&]() {  // uniform in [-1, 1) as bf16 / fp16 bits
+            st = st * 1664525u + 1013904223u;
+            const float f = (float)(st >> 8) * (2.0f / 16777216.0f) - 1.0f;
+            if (act_type == 1) {
+                _Float16 h = (_Float16)f;
+                return __builtin_bit_cast(uint16_t, h);
+            }
+            uint32_t u;
+            std::memcpy(&u, &f, 4);
+            return (uint16_t)(u >> 16);
+        };
+        for (auto& v : ha) v = rnd();
+        for (auto& v : hw) v = rnd();
+        DevMem dA(ha.size() * 2), dW(hw.size() * 2), dC((size_t)M * N * 4), dG((size_t)N * 4);
+        ACEMI_HIP(hipMemcpy(dA.p, ha.data(), ha.size() * 2, hipMemcpyHostToDevice));
+        ACEMI_HIP(hipMemcpy(dW.p, hw.data(), hw.size() * 2, hipMemcpyHostToDevice));
+        ACEMI_HIP(hipMemset(dC.p, 0, (size_t)M * N * 4));
+        ACEMI_HIP(hipMemset(dG.p, 0, (size_t)N * 4));
+        GemmEpilogue e;
+        e.kind = epi;
+        e.ldc = (epi == EPI_SWIGLU) ? N / 2 : N;
+        e.c_f32 = dC.as<float>();
+        e.c_act = dC.as<uint16_t>();
+        e.gate = dG.as<float>();
+        e.rows_per_item = M;
+        const ActType at = act_type == 1 ? ActType::F16 : ActType::BF16;
+        gemm_force_variant(variant);
+        hipEvent_t e0, e1;
+        ACEMI_HIP(hipEventCreate(&e0));
+        ACEMI_HIP(hipEventCreate(&e1));
+        for (int i = 0; i < 3; ++i) launch_gemm(at, dA.as<uint16_t>(), K, dW.as<uint16_t>(), K, M, N, K, e, nullptr);
+        ACEMI_HIP(hipEventRecord(e0, nullptr));
+        for (int i = 0; i < iters; ++i)
+            launch_gemm(at, dA.as<uint16_t>(), K, dW.as<uint16_t>(), K, M, N, K, e, nullptr);
+        ACEMI_HIP(hipEventRecord(e1, nullptr));
+        ACEMI_HIP(hipEventSynchronize(e1));
+        float ms = 0.f;
+        ACEMI_HIP(hipEventElapsedTime(&ms, e0, e1));
+        *avg_ms = ms / iters;
+        gemm_force_variant(-1);
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+    } catch (const std::exception& ex) {
+        gemm_force_variant(-1);
+        std::fprintf(stderr, "ace_mi_bench_gemm: %s\n", ex.what());
+        return ACE_GGML_ERR;
+    }
+    return ACE_GGML_OK;
+}
+
+// Force a GEMM kernel variant for subsequent launches (-1 = automatic).
+ace_ggml_status ace_mi_gemm_variant(int32_t variant) {
+    if (variant < -1 || variant > 3) return ACE_GGML_ERR_INVALID_ARG;
+    acemi::gemm_force_variant(variant);
+    return ACE_GGML_OK;
+}
+
+}  // extern "C"

@@ -92,6 +92,14 @@ ACE_GGML_API ace_ggml_status ace_mi_kernel_attention(int32_t B, int32_t Hq, int3
                                                      int32_t window, float scale, int32_t split, const float* q,
                                                      const float* kv, const int32_t* kmask, float* out);
 
+/* GEMM micro-benchmark on random device operands: average ms per launch (HIP events) of the
+ * engine's GEMM for act_type (0 bf16, 1 fp16), epilogue `epi` (0 f32 store, 2 gated residual,
+ * 4 SwiGLU), kernel `variant` (-1 automatic, 0..3 forced). */
+ACE_GGML_API ace_ggml_status ace_mi_bench_gemm(int32_t act_type, int32_t epi, int32_t variant, int32_t M, int32_t N,
+                                               int32_t K, int32_t iters, float* avg_ms);
+/* Force the GEMM kernel variant of all later launches in this process (-1 = automatic). */
+ACE_GGML_API ace_ggml_status ace_mi_gemm_variant(int32_t variant);
+
 #ifdef __cplusplus
 }
 #endif

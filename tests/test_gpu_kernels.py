@@ -151,3 +151,32 @@ def test_attention_split_handles_small_values():
     # to a different bf16 than the f32 reference
     mism = np.mean(got != bf16_bits_to_f32(f32_to_bf16_bits(ref.astype(np.float32))))
     assert mism < 0.02, mism
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("M,N,K", [(1, 256, 64), (300, 512, 128), (1000, 768, 2048), (513, 256, 6144)])
+def test_gemm_all_variants(variant, M, N, K):
+    """Every GEMM kernel variant (128x128 / 256x256 / 256x128, both pipelines), incl. M edges and
+    K = 1, 2 and many tiles (pipeline prologue/epilogue paths)."""
+    capi = _capi()
+    if N % 256 and variant == 2:
+        pytest.skip("256-wide tiles need N % 256 == 0")
+    rng = np.random.default_rng(variant * 7 + M)
+    a = _bits(rng.standard_normal((M, K)).astype(np.float32), 0)
+    w = _bits((rng.standard_normal((N, K)) * 0.05).astype(np.float32), 0)
+    capi.gemm_variant(variant)
+    try:
+        got = capi.kernel_gemm(a, w, act_type=0, epi=0)
+        wi = w.copy()
+        got_sw = capi.kernel_gemm(a, wi, act_type=0, epi=4)
+    finally:
+        capi.gemm_variant(-1)
+    av, wv = _vals(a, 0).astype(np.float64), _vals(w, 0).astype(np.float64)
+    ref = av @ wv.T
+    scale = np.abs(av) @ np.abs(wv).T
+    assert np.all(np.abs(got - ref) <= 2e-6 * scale + 1e-6)
+    # SwiGLU epilogue on the same accumulators: columns 32g..32g+15 gate, 32g+16.. up
+    g = ref.reshape(M, N // 32, 2, 16)[:, :, 0, :].reshape(M, N // 2)
+    u = ref.reshape(M, N // 32, 2, 16)[:, :, 1, :].reshape(M, N // 2)
+    sw = (g / (1 + np.exp(-g))) * u
+    np.testing.assert_allclose(_vals(got_sw, 0), sw, rtol=2.0 ** -8, atol=1e-4)
