@@ -228,3 +228,34 @@ def test_full_model_24_layers_20s():
     br.close()
     ref, floor = forward_with_floor(DitWeights(d), h, c, e, None, None, T, L, 0.6428571429, 0.6428571429)
     check(got, ref, floor, "full 24-layer 20s")
+
+
+def test_decoder_forward_hook_device_path(tiny_bridge):
+    """install_dit_backend on cuda tensors (device pointers, one batched call) == the reference
+    host-pointer ABI per item; bf16 in/out like the PyTorch pipeline."""
+    import types
+
+    import torch
+    from acestep_mi355x.hook import install_dit_backend
+    dec = types.SimpleNamespace(forward=None)
+    handler = types.SimpleNamespace(model=types.SimpleNamespace(decoder=dec))
+    install_dit_backend(handler, tiny_bridge)
+    rng = np.random.default_rng(41)
+    B, T, L = 2, 44, 9
+    h = rng.standard_normal((B, T, 64)).astype(np.float32)
+    c = rng.standard_normal((B, T, 128)).astype(np.float32)
+    e = rng.standard_normal((B, L, 256)).astype(np.float32)
+    em = np.ones((B, L), np.int64)
+    em[0, 6:] = 0
+    dev = torch.device("cuda:0")
+    t = torch.tensor([0.9, 0.4], device=dev)
+    pred, _ = handler.model.decoder.forward(
+        hidden_states=torch.from_numpy(h).to(dev), timestep=t, timestep_r=t, attention_mask=None,
+        encoder_hidden_states=torch.from_numpy(e).to(dev), encoder_attention_mask=torch.from_numpy(em).to(dev),
+        context_latents=torch.from_numpy(c).to(dev))
+    torch.cuda.synchronize()
+    got = pred.cpu().numpy()
+    for b in range(B):
+        ref = tiny_bridge.dit_forward_tfirst(h[b], c[b], e[b], None, em[b].astype(np.int32), float(t[b]), float(t[b]))
+        l2, _ = rel_errors(got[b], ref)
+        assert l2 < 1e-6, (b, l2)
