@@ -32,8 +32,11 @@ EXPORTED_SYMBOLS = (
     "ace_mi_create_on_device", "ace_mi_dit_get_info", "ace_mi_dit_forward_batched", "ace_mi_dit_sample",
     "ace_mi_profile_enable", "ace_mi_profile_reset", "ace_mi_profile_get", "ace_mi_probe_gemm",
     "ace_mi_synchronize", "ace_mi_kernel_gemm", "ace_mi_kernel_attention", "ace_mi_bench_gemm",
-    "ace_mi_gemm_variant",
+    "ace_mi_gemm_variant", "ace_mi_quantize", "ace_mi_dequantize", "ace_mi_kernel_gemm_q", "ace_mi_bench_gemm_q",
 )
+
+# qtype codes of ace_mi_quantize & co. (names as parse_quant_type, acestep_dit_model.cpp:27-37)
+QTYPES = {"q8_0": 1, "q4_k": 2, "q6_k": 3}
 
 
 class AceInitParams(ctypes.Structure):
@@ -111,6 +114,15 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.ace_mi_bench_gemm.restype = ctypes.c_int
     lib.ace_mi_gemm_variant.argtypes = [i32]
     lib.ace_mi_gemm_variant.restype = ctypes.c_int
+    i64, u8p = ctypes.c_int64, ctypes.POINTER(ctypes.c_uint8)
+    lib.ace_mi_quantize.argtypes = [i32, fp, i64, i64, u8p, sz]
+    lib.ace_mi_quantize.restype = ctypes.c_int64
+    lib.ace_mi_dequantize.argtypes = [i32, u8p, i64, i64, fp]
+    lib.ace_mi_dequantize.restype = ctypes.c_int
+    lib.ace_mi_kernel_gemm_q.argtypes = [i32, i32, i32, i32, i32, i32, u16p, u8p, fp, fp, u16p]
+    lib.ace_mi_kernel_gemm_q.restype = ctypes.c_int
+    lib.ace_mi_bench_gemm_q.argtypes = [i32, i32, i32, i32, i32, i32, i32, fp]
+    lib.ace_mi_bench_gemm_q.restype = ctypes.c_int
     if path is None:
         _LIB = lib
     return lib
@@ -278,6 +290,69 @@ def bench_gemm(M: int, N: int, K: int, variant: int = -1, epi: int = 0, act_type
     st = lib.ace_mi_bench_gemm(act_type, epi, variant, M, N, K, iters, ctypes.byref(ms))
     if st != ACE_GGML_OK:
         raise RuntimeError(f"ace_mi_bench_gemm failed (status={st})")
+    return float(ms.value)
+
+
+_BLOCK = {"q8_0": (32, 34), "q4_k": (256, 144), "q6_k": (256, 210)}
+
+
+def quantize(x: np.ndarray, qtype: str) -> np.ndarray:
+    """The loader's ggml block encoder on host rows: f32 [rows][cols] -> uint8 [rows][nb][block bytes]."""
+    lib = load_library()
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    rows, cols = x.shape
+    qk, bb = _BLOCK[qtype]
+    out = np.empty((rows, cols // qk, bb), dtype=np.uint8)
+    n = lib.ace_mi_quantize(QTYPES[qtype], _fptr(x), rows, cols, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
+                            out.nbytes)
+    if n != out.nbytes:
+        raise ValueError(f"ace_mi_quantize failed ({qtype}, cols={cols})")
+    return out
+
+
+def dequantize(raw: np.ndarray, qtype: str) -> np.ndarray:
+    lib = load_library()
+    raw = np.ascontiguousarray(raw, dtype=np.uint8)
+    rows, nb, _ = raw.shape
+    cols = nb * _BLOCK[qtype][0]
+    out = np.empty((rows, cols), dtype=np.float32)
+    st = lib.ace_mi_dequantize(QTYPES[qtype], raw.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), rows, cols,
+                               _fptr(out))
+    if st != ACE_GGML_OK:
+        raise ValueError(f"ace_mi_dequantize failed (status={st})")
+    return out
+
+
+def kernel_gemm_q(a_bits: np.ndarray, w_blocks: np.ndarray, qtype: str, epi: int = 0, variant: int = -1,
+                  bias: Optional[np.ndarray] = None) -> np.ndarray:
+    """Dequant-fused GEMM: a_bits bf16 words [M][K], w_blocks ggml block bytes [N][nb][bb]."""
+    lib = load_library()
+    a = np.ascontiguousarray(a_bits, dtype=np.uint16)
+    w = np.ascontiguousarray(w_blocks, dtype=np.uint8)
+    M, K = a.shape
+    N = w.shape[0]
+    u16p = ctypes.POINTER(ctypes.c_uint16)
+    u8p = ctypes.POINTER(ctypes.c_uint8)
+    b = None if bias is None else np.ascontiguousarray(bias, dtype=np.float32)
+    if epi == 0:
+        out = np.empty((M, N), dtype=np.float32)
+        st = lib.ace_mi_kernel_gemm_q(QTYPES[qtype], epi, variant, M, N, K, a.ctypes.data_as(u16p),
+                                      w.ctypes.data_as(u8p), _fptr(b), _fptr(out), None)
+    else:
+        out = np.empty((M, N // 2), dtype=np.uint16)
+        st = lib.ace_mi_kernel_gemm_q(QTYPES[qtype], epi, variant, M, N, K, a.ctypes.data_as(u16p),
+                                      w.ctypes.data_as(u8p), _fptr(b), None, out.ctypes.data_as(u16p))
+    if st != ACE_GGML_OK:
+        raise RuntimeError(f"ace_mi_kernel_gemm_q failed (status={st})")
+    return out
+
+
+def bench_gemm_q(M: int, N: int, K: int, qtype: str, variant: int = -1, epi: int = 0, iters: int = 20) -> float:
+    lib = load_library()
+    ms = ctypes.c_float(0.0)
+    st = lib.ace_mi_bench_gemm_q(QTYPES[qtype], epi, variant, M, N, K, iters, ctypes.byref(ms))
+    if st != ACE_GGML_OK:
+        raise RuntimeError(f"ace_mi_bench_gemm_q failed (status={st})")
     return float(ms.value)
 
 

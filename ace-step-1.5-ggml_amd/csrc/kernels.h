@@ -32,6 +32,23 @@ struct GemmEpilogue {
     int patch = 2;        // EPI_PROJ_OUT
 };
 
+// Weight operand.  Dense: 16-bit [N][ld] in the activation type.  Quantized (ggml block formats
+// re-laid out at load, runtime/quant.h): q = int8 / nibble plane, s = f32 scales; the kernel
+// dequantizes each 32-value block to bf16 while staging it into LDS and multiplies it with a bf16
+// activation (`Q -> bf16 dequant-fused` MFMA GEMM).
+enum WeightFormat : int { WF_BF16 = 0, WF_F16 = 1, WF_Q8_0 = 2, WF_Q4_K = 3, WF_Q6_K = 4 };
+struct WeightView {
+    int fmt = WF_BF16;
+    const void* q = nullptr;   // dense uint16 [N][ld] | Q8_0/Q6_K int8 [N][K] | Q4_K u8 [N][K/2]
+    const float* s = nullptr;  // Q8_0 [N][K/32] | Q4_K [N][K/32][2] (d*sc, dmin*m) | Q6_K [N][K/16]
+    int ld = 0;                // dense leading dimension (elements)
+};
+inline ActType weight_act(int fmt) { return fmt == WF_F16 ? ActType::F16 : ActType::BF16; }
+inline bool weight_quantized(int fmt) { return fmt >= WF_Q8_0; }
+
+void launch_gemm(const uint16_t* A, int lda, const WeightView& W, int M, int N, int K, const GemmEpilogue& epi,
+                 hipStream_t s);
+// dense shorthand: W 16-bit of type t
 void launch_gemm(ActType t, const uint16_t* A, int lda, const uint16_t* W, int ldw, int M, int N, int K,
                  const GemmEpilogue& epi, hipStream_t s);
 // -1 = automatic tile choice; 0..3 force a kernel variant (micro-benchmarks / tests)

@@ -31,7 +31,9 @@ typedef __attribute__((address_space(3))) void lds_void;
 
 struct GemmParams {
     const uint16_t* A;
-    const uint16_t* W;
+    const uint16_t* W;   // dense weight
+    const void* Wq;      // quantized weight planes (runtime/quant.h)
+    const float* Ws;
     int lda, ldw, M, N, K;
     GemmEpilogue e;
 };
@@ -108,6 +110,85 @@ __device__ __forceinline__ void wait_vmcnt() {
 }
 __device__ __forceinline__ void wait_lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F); }
 
+// block -> tile: XCD-aware bijective remap (blocks b, b+8 share an XCD), then M-grouped order
+template <int BM, int BN>
+__device__ __forceinline__ void block_tile(const GemmParams& p, int& m0, int& n0) {
+    const int nbm = (p.M + BM - 1) / BM;
+    const int nbn = p.N / BN;
+    const int nwg = gridDim.x;
+    int bid = blockIdx.x;
+    {
+        const int xcd = bid & 7;
+        const int q = nwg >> 3, r = nwg & 7;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    }
+    constexpr int GM = 8;
+    const int group = bid / (GM * nbn);
+    const int first_m = group * GM;
+    const int gm = min(nbm - first_m, GM);
+    const int bm = first_m + (bid % (GM * nbn)) % gm;
+    const int bn = (bid % (GM * nbn)) / gm;
+    m0 = bm * BM;
+    n0 = bn * BN;
+}
+
+// Fused epilogue of one wave's TM x TN grid of 16x16 accumulators at (mw, nw).
+// C/D map of 16x16x32: col = lane & 15, row = (lane >> 4) * 4 + r.
+template <int TM, int TN, bool F16, int EPI>
+__device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[TM][TN], int mw, int nw, int lane) {
+    const GemmEpilogue& e = p.e;
+    const int M = p.M;
+    const int ccol = lane & 15;
+    const int crow = (lane >> 4) * 4;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int m = mw + i * 16 + crow + r;
+            if (m >= M) continue;
+            if constexpr (EPI == EPI_SWIGLU) {
+#pragma unroll
+                for (int j = 0; j < TN; j += 2) {
+                    const int n = nw + j * 16;  // multiple of 32
+                    const float g = acc[i][j][r];
+                    const float u = acc[i][j + 1][r];
+                    e.c_act[(int64_t)m * e.ldc + (n >> 1) + ccol] = to_act<F16>(silu_f(g) * u);
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const int n = nw + j * 16 + ccol;
+                    float v = acc[i][j][r];
+                    if constexpr (EPI == EPI_STORE_F32) {
+                        if (e.bias) v = v + e.bias[n];
+                        e.c_f32[(int64_t)m * e.ldc + n] = v;
+                    } else if constexpr (EPI == EPI_STORE_ACT) {
+                        if (e.bias) v = v + e.bias[n];
+                        e.c_act[(int64_t)m * e.ldc + n] = to_act<F16>(v);
+                    } else if constexpr (EPI == EPI_RESID_GATED) {
+                        const int item = m / e.rows_per_item;
+                        float* xp = e.c_f32 + (int64_t)m * e.ldc + n;
+                        const float gated = __fmul_rn(v, e.gate[(int64_t)item * e.gate_stride + n]);
+                        *xp = __fadd_rn(*xp, gated);
+                    } else if constexpr (EPI == EPI_RESID) {
+                        float* xp = e.c_f32 + (int64_t)m * e.ldc + n;
+                        *xp = __fadd_rn(*xp, v);
+                    } else if constexpr (EPI == EPI_PROJ_OUT) {
+                        const int item = m / e.rows_per_item;
+                        const int pp = m - item * e.rows_per_item;
+                        const int kpos = n / e.out_ch;
+                        const int c = n - kpos * e.out_ch;
+                        const int t = pp * e.patch + kpos;
+                        if (t < e.out_T) {
+                            e.c_f32[((int64_t)item * e.out_T + t) * e.out_ch + c] = __fadd_rn(v, e.bias[c]);
+                        }
+                    }
+                }
+            }
+        }
+    }
+}
+
 // PIPE 0: stage(t+1) ; compute(t) ; vmcnt(0) ; __syncthreads        (2 LDS buffers)
 // PIPE 1: compute first half of tile t from registers read up front, release the LDS buffer with
 //         a raw s_barrier, stage tile t+2 into it, compute the second half, then a COUNTED
@@ -132,24 +213,8 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(GemmParams p) {
     const int lane = tid & 63;
     const int wid = tid >> 6;
 
-    // ---- block -> tile (XCD-aware bijective remap, then M-grouped order)
-    const int nbm = (p.M + BM - 1) / BM;
-    const int nbn = p.N / BN;
-    const int nwg = gridDim.x;
-    int bid = blockIdx.x;
-    {
-        const int xcd = bid & 7;
-        const int q = nwg >> 3, r = nwg & 7;
-        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-    }
-    constexpr int GM = 8;
-    const int group = bid / (GM * nbn);
-    const int first_m = group * GM;
-    const int gm = min(nbm - first_m, GM);
-    const int bm = first_m + (bid % (GM * nbn)) % gm;
-    const int bn = (bid % (GM * nbn)) / gm;
-    const int m0 = bm * BM;
-    const int n0 = bn * BN;
+    int m0, n0;
+    block_tile<BM, BN>(p, m0, n0);
 
     const int wm = wid / WN;
     const int wn = wid % WN;
@@ -288,57 +353,276 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(GemmParams p) {
         }
     }
 
-    // ---- epilogue.  C/D map of 16x16x32: col = lane & 15, row = (lane >> 4) * 4 + r.
-    const GemmEpilogue& e = p.e;
-    const int ccol = lane & 15;
-    const int crow = (lane >> 4) * 4;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int m = m0 + wm0 + i * 16 + crow + r;
-            if (m >= M) continue;
-            if constexpr (EPI == EPI_SWIGLU) {
-#pragma unroll
-                for (int j = 0; j < TN; j += 2) {
-                    const int n = n0 + wn0 + j * 16;  // multiple of 32
-                    const float g = acc[i][j][r];
-                    const float u = acc[i][j + 1][r];
-                    e.c_act[(int64_t)m * e.ldc + (n >> 1) + ccol] = to_act<F16>(silu_f(g) * u);
-                }
-            } else {
-#pragma unroll
-                for (int j = 0; j < TN; ++j) {
-                    const int n = n0 + wn0 + j * 16 + ccol;
-                    float v = acc[i][j][r];
-                    if constexpr (EPI == EPI_STORE_F32) {
-                        if (e.bias) v = v + e.bias[n];
-                        e.c_f32[(int64_t)m * e.ldc + n] = v;
-                    } else if constexpr (EPI == EPI_STORE_ACT) {
-                        if (e.bias) v = v + e.bias[n];
-                        e.c_act[(int64_t)m * e.ldc + n] = to_act<F16>(v);
-                    } else if constexpr (EPI == EPI_RESID_GATED) {
-                        const int item = m / e.rows_per_item;
-                        float* xp = e.c_f32 + (int64_t)m * e.ldc + n;
-                        const float gated = __fmul_rn(v, e.gate[(int64_t)item * e.gate_stride + n]);
-                        *xp = __fadd_rn(*xp, gated);
-                    } else if constexpr (EPI == EPI_RESID) {
-                        float* xp = e.c_f32 + (int64_t)m * e.ldc + n;
-                        *xp = __fadd_rn(*xp, v);
-                    } else if constexpr (EPI == EPI_PROJ_OUT) {
-                        const int item = m / e.rows_per_item;
-                        const int pp = m - item * e.rows_per_item;
-                        const int kpos = n / e.out_ch;
-                        const int c = n - kpos * e.out_ch;
-                        const int t = pp * e.patch + kpos;
-                        if (t < e.out_T) {
-                            e.c_f32[((int64_t)item * e.out_T + t) * e.out_ch + c] = __fadd_rn(v, e.bias[c]);
-                        }
-                    }
-                }
-            }
+    gemm_epilogue<TM, TN, F16, EPI>(p, acc, m0 + wm0, n0 + wn0, lane);
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// Dequant-fused variant: W arrives as a ggml block format re-laid out at load (runtime/quant.h).
+// Each thread owns one 32-value block of the BN x 64 weight tile (BN*2 == threads): it loads the
+// block's bytes + scale(s) into registers one k-tile ahead, turns them into bf16 with the exact
+// ggml dequant arithmetic (q*d, d*sc*q - dmin*m, (d*sc)*q; one f32 rounding, then RNE bf16) and
+// writes the bf16 image into the same swizzled LDS layout the dense kernel reads.  A (bf16
+// activations) is still staged by LDS-DMA.  Pipeline (PIPE 1 shape): fragments of tile t are read
+// up front, a raw barrier frees the buffer, A(t+2) is DMA'd and W(t+2) dequantized into it while
+// the second half of tile t's MFMAs runs, and W(t+3)'s bytes are requested.
+struct WRaw {
+    u32x4 q0, q1;
+    float s0, s1;
+};
+
+__device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) {
+    typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+    bf16x2_t v;
+    v[0] = (__bf16)lo;
+    v[1] = (__bf16)hi;
+    return __builtin_bit_cast(uint32_t, v);
+}
+
+__device__ __forceinline__ void ds_write_b128_v(uint32_t addr, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    u32x4 v = {a, b, c, d};
+    asm volatile("ds_write_b128 %0, %1" : : "v"(addr), "v"(v) : "memory");
+}
+
+// Weight bytes are fetched with inline-asm loads the compiler does not track, so its waitcnt pass
+// cannot drain the whole queue (A's LDS-DMA included) with vmcnt(0) at the loop-carried use; the
+// kernel retires them with a counted vmcnt that also pins the registers (wait_w).
+typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
+__device__ __forceinline__ u32x4 gload_b128(const void* p) {
+    u32x4 v;
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p));
+    return v;
+}
+__device__ __forceinline__ u32x2 gload_b64(const void* p) {
+    u32x2 v;
+    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p));
+    return v;
+}
+__device__ __forceinline__ float gload_b32(const void* p) {
+    float v;
+    asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(p));
+    return v;
+}
+
+// vector-memory instructions issued per load_wq
+template <int WQ>
+constexpr int w_ops() { return WQ == WF_Q4_K ? 2 : 3; }
+
+template <int WQ>
+__device__ __forceinline__ WRaw load_wq(const char* qbase, const float* sbase, int kt) {
+    WRaw r;
+    if constexpr (WQ == WF_Q4_K) {
+        r.q0 = gload_b128(qbase + kt * 32);
+        const u32x2 sm = gload_b64(sbase + kt * 4);
+        r.s0 = __uint_as_float(sm[0]);
+        r.s1 = __uint_as_float(sm[1]);
+    } else {
+        r.q0 = gload_b128(qbase + kt * 64);
+        r.q1 = gload_b128(qbase + kt * 64 + 16);
+        if constexpr (WQ == WF_Q8_0) {
+            r.s0 = gload_b32(sbase + kt * 2);
+            r.s1 = r.s0;
+        } else {
+            const u32x2 sc = gload_b64(sbase + kt * 4);
+            r.s0 = __uint_as_float(sc[0]);
+            r.s1 = __uint_as_float(sc[1]);
         }
     }
+    return r;
+}
+
+// s_waitcnt vmcnt(N) that the registers of `r` depend on (no consumer can be hoisted above it)
+template <int WQ, int N>
+__device__ __forceinline__ void wait_w(WRaw& r) {
+    static_assert(N >= 0 && N < 16, "vmcnt range");
+    if constexpr (WQ == WF_Q4_K) {
+        uint32_t s0 = __float_as_uint(r.s0), s1 = __float_as_uint(r.s1);
+        asm volatile("s_waitcnt vmcnt(%3)" : "+v"(r.q0), "+v"(s0), "+v"(s1) : "i"(N));
+        r.s0 = __uint_as_float(s0);
+        r.s1 = __uint_as_float(s1);
+    } else {
+        uint32_t s0 = __float_as_uint(r.s0), s1 = __float_as_uint(r.s1);
+        asm volatile("s_waitcnt vmcnt(%4)" : "+v"(r.q0), "+v"(r.q1), "+v"(s0), "+v"(s1) : "i"(N));
+        r.s0 = __uint_as_float(s0);
+        r.s1 = __uint_as_float(s1);
+    }
+}
+
+// signed bytes of w (k order b0..b3) * s, via the unsigned-byte converts: (u - 128) * s = fma(u, s, -128 s)
+__device__ __forceinline__ void deq_i8x4(uint32_t w, float s, float c, uint32_t& o0, uint32_t& o1) {
+    const uint32_t u = w ^ 0x80808080u;
+    const float f0 = fmaf((float)(u & 0xffu), s, c);
+    const float f1 = fmaf((float)((u >> 8) & 0xffu), s, c);
+    const float f2 = fmaf((float)((u >> 16) & 0xffu), s, c);
+    const float f3 = fmaf((float)(u >> 24), s, c);
+    o0 = pk_bf16(f0, f1);
+    o1 = pk_bf16(f2, f3);
+}
+// unsigned nibble bytes (0..15) of w * d - m
+__device__ __forceinline__ void deq_u4x4(uint32_t w, float d, float nm, uint32_t& o0, uint32_t& o1) {
+    const float f0 = fmaf((float)(w & 0xffu), d, nm);
+    const float f1 = fmaf((float)((w >> 8) & 0xffu), d, nm);
+    const float f2 = fmaf((float)((w >> 16) & 0xffu), d, nm);
+    const float f3 = fmaf((float)(w >> 24), d, nm);
+    o0 = pk_bf16(f0, f1);
+    o1 = pk_bf16(f2, f3);
+}
+
+// dequantize one 32-value block and store it as 4 swizzled 16-byte chunks of an LDS row
+template <int WQ>
+__device__ __forceinline__ void dequant_store(const WRaw& r, uint32_t row_addr, int wh, int sw) {
+    uint32_t o[16];
+    if constexpr (WQ == WF_Q4_K) {
+        const float d = r.s0, nm = -r.s1;
+        const uint32_t w[4] = {r.q0[0], r.q0[1], r.q0[2], r.q0[3]};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {  // dword i: k = 8i..8i+3 in low nibbles, 8i+4..8i+7 in high nibbles
+            deq_u4x4(w[i] & 0x0f0f0f0fu, d, nm, o[4 * i + 0], o[4 * i + 1]);
+            deq_u4x4((w[i] >> 4) & 0x0f0f0f0fu, d, nm, o[4 * i + 2], o[4 * i + 3]);
+        }
+    } else {
+        const uint32_t w[8] = {r.q0[0], r.q0[1], r.q0[2], r.q0[3], r.q1[0], r.q1[1], r.q1[2], r.q1[3]};
+        const float c0 = -128.0f * r.s0, c1 = -128.0f * r.s1;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const float s = i < 4 ? r.s0 : r.s1;
+            const float c = i < 4 ? c0 : c1;
+            deq_i8x4(w[i], s, c, o[2 * i], o[2 * i + 1]);
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+        ds_write_b128_v(row_addr + (((wh * 4 + c) ^ sw) * 16), o[4 * c], o[4 * c + 1], o[4 * c + 2], o[4 * c + 3]);
+}
+
+template <int BM, int BN, int WM, int WN, int EPI, int WQ>
+__global__ void __launch_bounds__(WM * WN * 64) gemm_q_kernel(GemmParams p) {
+    constexpr int NW = WM * WN;
+    constexpr int WTM = BM / WM;
+    constexpr int WTN = BN / WN;
+    constexpr int TM = WTM / 16;
+    constexpr int TN = WTN / 16;
+    constexpr int BK = 64;
+    constexpr int ROWB = BK * 2;
+    constexpr int STAGE = (BM + BN) * ROWB;
+    constexpr int G_A = BM / 8 / NW;
+    static_assert(BM % (8 * NW) == 0, "A staging split");
+    static_assert(BN * 2 == NW * 64, "one 32-value weight block per thread");
+    static_assert(EPI != EPI_SWIGLU || (TN % 2 == 0), "swiglu needs column pairs");
+
+    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wid = tid >> 6;
+    int m0, n0;
+    block_tile<BM, BN>(p, m0, n0);
+    const int wm0 = (wid / WN) * WTM;
+    const int wn0 = (wid % WN) * WTN;
+    const int M = p.M, K = p.K;
+
+    // A staging sources (LDS-DMA, swizzled source chunk)
+    const uint16_t* src[G_A];
+#pragma unroll
+    for (int j = 0; j < G_A; ++j) {
+        const int row = (wid + NW * j) * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ swz(row);
+        src[j] = p.A + (int64_t)min(m0 + row, M - 1) * p.lda + c * 8;
+    }
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+    auto stage_a = [&](int buf, int kt) {
+        char* base = smem + buf * STAGE;
+#pragma unroll
+        for (int j = 0; j < G_A; ++j)
+            __builtin_amdgcn_global_load_lds((const void*)(src[j] + kt * BK), (lds_void*)(base + (wid + NW * j) * 1024),
+                                             16, 0, 0);
+    };
+
+    // W block owned by this thread: row wr of the tile, K half wh of each 64-wide k-tile
+    const int wr = tid >> 1, wh = tid & 1;
+    const int64_t grow = n0 + wr;
+    const char* qbase;
+    const float* sbase;
+    if constexpr (WQ == WF_Q4_K) {
+        qbase = (const char*)p.Wq + grow * (K / 2) + wh * 16;
+        sbase = p.Ws + (grow * (K / 32) + wh) * 2;
+    } else if constexpr (WQ == WF_Q8_0) {
+        qbase = (const char*)p.Wq + grow * K + wh * 32;
+        sbase = p.Ws + grow * (K / 32) + wh;
+    } else {
+        qbase = (const char*)p.Wq + grow * K + wh * 32;
+        sbase = p.Ws + grow * (K / 16) + wh * 2;
+    }
+    const int wsw = swz(wr);
+    const uint32_t wrow_off = BM * ROWB + wr * ROWB;
+
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int nk = K / BK;
+    const int lrow = lane & 15;
+    const int lchunk = lane >> 4;
+    auto read_frags_asm = [&](int buf, uint4 (&a)[TM][2], uint4 (&b)[TN][2]) {
+        const uint32_t sb = lds0 + buf * STAGE;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int ch = (kk * 4 + lchunk) ^ ((lrow >> 1) & 7);
+            const uint32_t bb = sb + BM * ROWB + (wn0 + lrow) * ROWB + ch * 16;
+            const uint32_t ab = sb + (wm0 + lrow) * ROWB + ch * 16;
+            ReadRows<0, TN, 16 * ROWB>::run(bb, b, kk);
+            ReadRows<0, TM, 16 * ROWB>::run(ab, a, kk);
+        }
+        lds_wait_all();
+    };
+
+    constexpr int WOPS = w_ops<WQ>();
+    // prologue: tiles 0 and 1 complete in LDS, W(min(2, nk-1)) requested
+    WRaw wnext = load_wq<WQ>(qbase, sbase, 0);
+    stage_a(0, 0);
+    wait_w<WQ, G_A>(wnext);
+    dequant_store<WQ>(wnext, lds0 + wrow_off, wh, wsw);
+    if (nk > 1) {
+        wnext = load_wq<WQ>(qbase, sbase, 1);
+        stage_a(1, 1);
+        wait_w<WQ, G_A>(wnext);
+        dequant_store<WQ>(wnext, lds0 + STAGE + wrow_off, wh, wsw);
+    }
+    wnext = load_wq<WQ>(qbase, sbase, min(2, nk - 1));
+    wait_vmcnt<WOPS>();  // A(0), A(1) landed
+    lds_wait_all();
+    __builtin_amdgcn_s_barrier();
+
+    auto mfma_half = [&](const uint4 (&a)[TM][2], const uint4 (&b)[TN][2], int i0) {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int i = i0; i < i0 + TM / 2; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<false>(a[i][kk], b[j][kk], acc[i][j]);
+    };
+
+    // One branch-free body for every tile: past the end, the tile indices clamp to nk-1, so the last
+    // two iterations re-stage the final tile into a buffer nobody reads again (harmless, and it keeps
+    // the accumulators in one loop so they stay put in AGPRs).
+    for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        uint4 a[TM][2], b[TN][2];
+        read_frags_asm(cur, a, b);
+        mfma_half(a, b, 0);
+        __builtin_amdgcn_s_barrier();  // every wave holds its fragments of tile kt: buffer `cur` is free
+        stage_a(cur, min(kt + 2, nk - 1));
+        wait_w<WQ, G_A>(wnext);        // W(kt+2) bytes, and the older A(kt+1) DMA, have landed
+        dequant_store<WQ>(wnext, lds0 + cur * STAGE + wrow_off, wh, wsw);
+        wnext = load_wq<WQ>(qbase, sbase, min(kt + 3, nk - 1));
+        mfma_half(a, b, TM / 2);
+        __builtin_amdgcn_s_barrier();
+    }
+    wait_vmcnt<0>();
+
+    gemm_epilogue<TM, TN, false, EPI>(p, acc, m0 + wm0, n0 + wn0, lane);
 }
 
 template <int BM, int BN, int WM, int WN, bool F16, int EPI, int PIPE>
@@ -375,6 +659,37 @@ void dispatch_epi(int variant, const GemmParams& p, hipStream_t s) {
     }
 }
 
+template <int BM, int BN, int WM, int WN, int EPI, int WQ>
+void launch_q_cfg(const GemmParams& p, hipStream_t s) {
+    const int nbm = (p.M + BM - 1) / BM;
+    const int nbn = p.N / BN;
+    hipLaunchKernelGGL((gemm_q_kernel<BM, BN, WM, WN, EPI, WQ>), dim3(nbm * nbn), dim3(WM * WN * 64), 0, s, p);
+}
+
+template <int EPI, int WQ>
+void launch_q_variant(int variant, const GemmParams& p, hipStream_t s) {
+    switch (variant) {
+        case 0:
+        case 1: launch_q_cfg<128, 128, 2, 2, EPI, WQ>(p, s); break;
+        case 2: launch_q_cfg<256, 256, 2, 4, EPI, WQ>(p, s); break;
+        case 3: launch_q_cfg<256, 128, 2, 2, EPI, WQ>(p, s); break;
+        default: throw std::runtime_error("gemm: bad variant");
+    }
+}
+
+template <int WQ>
+void dispatch_q_epi(int variant, const GemmParams& p, hipStream_t s) {
+    switch (p.e.kind) {
+        case EPI_STORE_F32: launch_q_variant<EPI_STORE_F32, WQ>(variant, p, s); break;
+        case EPI_STORE_ACT: launch_q_variant<EPI_STORE_ACT, WQ>(variant, p, s); break;
+        case EPI_RESID_GATED: launch_q_variant<EPI_RESID_GATED, WQ>(variant, p, s); break;
+        case EPI_RESID: launch_q_variant<EPI_RESID, WQ>(variant, p, s); break;
+        case EPI_SWIGLU: launch_q_variant<EPI_SWIGLU, WQ>(variant, p, s); break;
+        case EPI_PROJ_OUT: launch_q_variant<EPI_PROJ_OUT, WQ>(variant, p, s); break;
+        default: throw std::runtime_error("gemm: bad epilogue kind");
+    }
+}
+
 int g_forced_variant = -1;
 
 // Tile choice: measured kernel ceiling (random bf16 operands, MI355X: v1 ~950, v2 ~1120 TFLOP/s at
@@ -399,17 +714,46 @@ int pick_variant(int M, int N) {
 
 }  // namespace
 
+void launch_gemm(const uint16_t* A, int lda, const WeightView& W, int M, int N, int K, const GemmEpilogue& epi,
+                 hipStream_t s) {
+    ACEMI_CHECK(M >= 1 && N % 128 == 0 && K % 64 == 0 && K >= 64, "gemm: unsupported shape");
+    ACEMI_CHECK(lda % 8 == 0, "gemm: leading dims must be multiples of 8");
+    ACEMI_CHECK(W.q != nullptr, "gemm: null weight");
+    GemmParams p{A, (const uint16_t*)W.q, W.q, W.s, lda, W.ld, M, N, K, epi};
+    const int v = pick_variant(M, N);
+    switch (W.fmt) {
+        case WF_BF16:
+        case WF_F16:
+            ACEMI_CHECK(W.ld % 8 == 0, "gemm: leading dims must be multiples of 8");
+            if (W.fmt == WF_F16)
+                dispatch_epi<true>(v, p, s);
+            else
+                dispatch_epi<false>(v, p, s);
+            break;
+        case WF_Q8_0:
+            ACEMI_CHECK(W.s != nullptr, "gemm: null scales");
+            dispatch_q_epi<WF_Q8_0>(v, p, s);
+            break;
+        case WF_Q4_K:
+            ACEMI_CHECK(W.s != nullptr, "gemm: null scales");
+            dispatch_q_epi<WF_Q4_K>(v, p, s);
+            break;
+        case WF_Q6_K:
+            ACEMI_CHECK(W.s != nullptr, "gemm: null scales");
+            dispatch_q_epi<WF_Q6_K>(v, p, s);
+            break;
+        default: throw std::runtime_error("gemm: bad weight format");
+    }
+    ACEMI_HIP(hipGetLastError());
+}
+
 void launch_gemm(ActType t, const uint16_t* A, int lda, const uint16_t* W, int ldw, int M, int N, int K,
                  const GemmEpilogue& epi, hipStream_t s) {
-    ACEMI_CHECK(M >= 1 && N % 128 == 0 && K % 64 == 0 && K >= 64, "gemm: unsupported shape");
-    ACEMI_CHECK(lda % 8 == 0 && ldw % 8 == 0, "gemm: leading dims must be multiples of 8");
-    GemmParams p{A, W, lda, ldw, M, N, K, epi};
-    const int v = pick_variant(M, N);
-    if (t == ActType::F16)
-        dispatch_epi<true>(v, p, s);
-    else
-        dispatch_epi<false>(v, p, s);
-    ACEMI_HIP(hipGetLastError());
+    WeightView w;
+    w.fmt = t == ActType::F16 ? WF_F16 : WF_BF16;
+    w.q = W;
+    w.ld = ldw;
+    launch_gemm(A, lda, w, M, N, K, epi, s);
 }
 
 void gemm_force_variant(int v) { g_forced_variant = v; }

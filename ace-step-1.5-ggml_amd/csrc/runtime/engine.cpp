@@ -167,7 +167,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
 
     // ---- input pack + proj_in (:1343-1382)
     tic(s);
-    launch_pack_input(at, io.hidden, io.context, B, T, Np, P, c.audio_dim, c.ctx_dim(), a0, s);
+    launch_pack_input(m.proj_in_w.act(), io.hidden, io.context, B, T, Np, P, c.audio_dim, c.ctx_dim(), a0, s);
     toc("pack_input", s);
     {
         GemmEpilogue e;
@@ -176,7 +176,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
         e.c_f32 = x;
         e.ldc = H;
         tic(s);
-        launch_gemm(at, a0, P * c.in_channels, m.proj_in_w, P * c.in_channels, (int)M, H, P * c.in_channels, e, s);
+        launch_gemm(a0, P * c.in_channels, m.proj_in_w.view(), (int)M, H, P * c.in_channels, e, s);
         toc("gemm_proj_in", s);
     }
 
@@ -193,12 +193,13 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
         for (int e = 0; e < 2; ++e) {
             float* temb = get<float>(e == 0 ? temb_t_ : temb_r_);
             launch_timestep_freq(io.t, e == 0 ? nullptr : io.r, B, 256, 1000.0f, log_max, freq, s);
-            launch_to_act(at, freq, (int64_t)B * 256, false, freq_act, s);
-            launch_gemv(at, freq_act, B, m.te[e].w1, H, 256, m.te[e].b1, true, false, th, s);
-            launch_to_act(at, th, (int64_t)B * H, false, th_act, s);
-            launch_gemv(at, th_act, B, m.te[e].w2, H, H, m.te[e].b2, false, false, temb, s);
-            launch_to_act(at, temb, (int64_t)B * H, true, temb_act, s);
-            launch_gemv(at, temb_act, B, m.te[e].wp, 6 * H, H, m.te[e].bp, false, e == 1, proj, s);
+            const ActType ta = m.te[e].act;
+            launch_to_act(ta, freq, (int64_t)B * 256, false, freq_act, s);
+            launch_gemv(ta, freq_act, B, m.te[e].w1, H, 256, m.te[e].b1, true, false, th, s);
+            launch_to_act(ta, th, (int64_t)B * H, false, th_act, s);
+            launch_gemv(ta, th_act, B, m.te[e].w2, H, H, m.te[e].b2, false, false, temb, s);
+            launch_to_act(ta, temb, (int64_t)B * H, true, temb_act, s);
+            launch_gemv(ta, temb_act, B, m.te[e].wp, 6 * H, H, m.te[e].bp, false, e == 1, proj, s);
         }
         launch_layer_mods(m.tables, proj, n_layers, B, H, get<float>(mods_), s);
         launch_out_mods(m.out_table, get<float>(temb_t_), get<float>(temb_r_), B, H, get<float>(outmod_), s);
@@ -223,7 +224,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
         e.bias = m.cond_b;
         e.c_act = encp;
         e.ldc = H;
-        launch_gemm(at, enc_act, H, m.cond_w, H, (int)Me, H, H, e, s);
+        launch_gemm(enc_act, H, m.cond_w.view(), (int)Me, H, H, e, s);
         toc("gemm_condition", s);
         for (int li = 0; li < n_layers; ++li) {
             const DevLayer& ly = m.layers[li];
@@ -232,7 +233,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
             ek.c_f32 = get<float>(ckv_);
             ek.ldc = 2 * kd;
             tic(s);
-            launch_gemm(at, encp, H, ly.w_ckv, H, (int)Me, 2 * kd, H, ek, s);
+            launch_gemm(encp, H, ly.w_ckv.view(), (int)Me, 2 * kd, H, ek, s);
             toc("gemm_cross_kv", s);
             PrepArgs pa{};
             pa.src = get<float>(ckv_);
@@ -281,7 +282,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
             e.c_f32 = qkv;
             e.ldc = qd + 2 * kd;
             tic(s);
-            launch_gemm(at, act, H, ly.w_qkv, H, (int)M, qd + 2 * kd, H, e, s);
+            launch_gemm(act, H, ly.w_qkv.view(), (int)M, qd + 2 * kd, H, e, s);
             toc("gemm_qkv", s);
         }
         {
@@ -345,7 +346,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
             e.gate_stride = mstride;
             e.rows_per_item = Np;
             tic(s);
-            launch_gemm(at, attn, qd, ly.w_o, qd, (int)M, H, qd, e, s);
+            launch_gemm(attn, qd, ly.w_o.view(), (int)M, H, qd, e, s);
             toc("gemm_o", s);
         }
 
@@ -360,7 +361,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
                 e.c_f32 = qkv;
                 e.ldc = qd;
                 tic(s);
-                launch_gemm(at, act, H, ly.w_cq, H, (int)M, qd, H, e, s);
+                launch_gemm(act, H, ly.w_cq.view(), (int)M, qd, H, e, s);
                 toc("gemm_cross_q", s);
             }
             {
@@ -413,7 +414,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
                 e.c_f32 = x;
                 e.ldc = H;
                 tic(s);
-                launch_gemm(at, attn, qd, ly.w_co, qd, (int)M, H, qd, e, s);
+                launch_gemm(attn, qd, ly.w_co.view(), (int)M, H, qd, e, s);
                 toc("gemm_cross_o", s);
             }
         }
@@ -428,7 +429,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
             e.c_act = act2;
             e.ldc = I;
             tic(s);
-            launch_gemm(at, act, H, ly.w_gu, H, (int)M, 2 * I, H, e, s);
+            launch_gemm(act, H, ly.w_gu.view(), (int)M, 2 * I, H, e, s);
             toc("gemm_gate_up", s);
         }
         {
@@ -440,7 +441,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
             e.gate_stride = mstride;
             e.rows_per_item = Np;
             tic(s);
-            launch_gemm(at, act2, I, ly.w_down, I, (int)M, H, I, e, s);
+            launch_gemm(act2, I, ly.w_down.view(), (int)M, H, I, e, s);
             toc("gemm_down", s);
         }
     }
@@ -460,7 +461,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
         e.out_ch = c.audio_dim;
         e.patch = P;
         tic(s);
-        launch_gemm(at, act, H, m.proj_out_w, H, (int)M, P * c.audio_dim, H, e, s);
+        launch_gemm(act, H, m.proj_out_w.view(), (int)M, P * c.audio_dim, H, e, s);
         toc("gemm_proj_out", s);
     }
 }
@@ -478,7 +479,7 @@ void DitEngine::probe_gemm(int which, int M, int iters, hipStream_t s) {
             e.c_act = get<uint16_t>(act2_);
             e.ldc = I;
             tic(s);
-            launch_gemm(m.act, get<uint16_t>(act_), H, ly.w_gu, H, M, 2 * I, H, e, s);
+            launch_gemm(get<uint16_t>(act_), H, ly.w_gu.view(), M, 2 * I, H, e, s);
             toc("probe_gemm_gate_up", s);
         } else {
             e.kind = EPI_RESID_GATED;
@@ -488,7 +489,7 @@ void DitEngine::probe_gemm(int which, int M, int iters, hipStream_t s) {
             e.gate_stride = 0;
             e.rows_per_item = M;
             tic(s);
-            launch_gemm(m.act, get<uint16_t>(act2_), I, ly.w_down, I, M, H, I, e, s);
+            launch_gemm(get<uint16_t>(act2_), I, ly.w_down.view(), M, H, I, e, s);
             toc("probe_gemm_down", s);
         }
     }

@@ -11,6 +11,7 @@
 #include <sstream>
 
 #include "json.h"
+#include "quant.h"
 
 namespace acemi {
 namespace {
@@ -147,10 +148,29 @@ std::string upper(const char* v) {
     return s;
 }
 
+// A 2-D weight as read from the file: raw 16-bit values, or f32 (F32 files / quantization input).
+struct Mat {
+    std::string dtype;  // BF16 | F16 | F32
+    int64_t rows = 0, cols = 0;
+    std::vector<uint16_t> u16;
+    std::vector<float> f32;
+    float at(size_t i) const {
+        if (dtype == "F32") return f32[i];
+        if (dtype == "BF16") {
+            uint32_t u = static_cast<uint32_t>(u16[i]) << 16;
+            float r;
+            std::memcpy(&r, &u, 4);
+            return r;
+        }
+        return half_to_f32(u16[i]);
+    }
+};
+
 struct Loader {
     DitModel& m;
     StFile st;
-    std::string wdtype;  // dtype of the 2-D weights (BF16 or F16)
+    std::string wdtype;  // dtype of the 16-bit 2-D weights (BF16 or F16)
+    quant::QType qt = quant::QNONE;
     explicit Loader(DitModel& mm) : m(mm) {}
 
     template <typename T>
@@ -168,8 +188,8 @@ struct Loader {
         auto v = to_f32(t, st.read(t));
         return upload<float>(v.data(), v.size() * 4);
     }
-    // raw 16-bit matrix [rows][cols]
-    std::vector<uint16_t> mat16(const std::string& name, int64_t rows, int64_t cols) {
+    // matrix [rows][cols] (2-D, or 3-D flattened over the last two dims)
+    Mat mat(const std::string& name, int64_t rows, int64_t cols) {
         const auto& t = st.get(name);
         int64_t r = 1, c = 1;
         if (t.shape.size() == 2) {
@@ -182,16 +202,118 @@ struct Loader {
             throw IoError("invalid tensor shape for " + name);
         }
         if (r != rows || c != cols) throw IoError("invalid tensor shape for " + name);
-        if (t.dtype != "BF16" && t.dtype != "F16")
-            throw Unsupported("DiT 2-D weight " + name + " has dtype " + t.dtype + " (BF16/F16 supported)");
-        if (wdtype.empty()) wdtype = t.dtype;
-        if (t.dtype != wdtype) throw Unsupported("mixed 2-D weight dtypes are not supported (" + name + ")");
+        Mat out;
+        out.dtype = t.dtype;
+        out.rows = rows;
+        out.cols = cols;
         auto raw = st.read(t);
-        std::vector<uint16_t> out(static_cast<size_t>(rows * cols));
-        std::memcpy(out.data(), raw.data(), out.size() * 2);
+        if (t.dtype == "BF16" || t.dtype == "F16") {
+            if (wdtype.empty()) wdtype = t.dtype;
+            if (t.dtype != wdtype) throw Unsupported("mixed 2-D weight dtypes are not supported (" + name + ")");
+            out.u16.resize(static_cast<size_t>(rows * cols));
+            std::memcpy(out.u16.data(), raw.data(), out.u16.size() * 2);
+        } else if (t.dtype == "F32" && qt != quant::QNONE) {
+            out.f32 = to_f32(t, raw);
+        } else {
+            throw Unsupported("DiT 2-D weight " + name + " has dtype " + t.dtype +
+                              " (BF16/F16, or F32 with online quantization)");
+        }
         return out;
     }
-    uint16_t* up16(const std::vector<uint16_t>& v) { return upload<uint16_t>(v.data(), v.size() * 2); }
+    // new matrix whose row r is row src_row(r) of `a`, with columns permuted by src_col(c)
+    template <typename RowF, typename ColF>
+    static Mat permute(const Mat& a, int64_t rows, int64_t cols, RowF src_row, ColF src_col) {
+        Mat o;
+        o.dtype = a.dtype;
+        o.rows = rows;
+        o.cols = cols;
+        if (a.dtype == "F32")
+            o.f32.resize(static_cast<size_t>(rows * cols));
+        else
+            o.u16.resize(static_cast<size_t>(rows * cols));
+        for (int64_t r = 0; r < rows; ++r)
+            for (int64_t c = 0; c < cols; ++c) {
+                const size_t si = static_cast<size_t>(src_row(r) * a.cols + src_col(c));
+                const size_t di = static_cast<size_t>(r * cols + c);
+                if (a.dtype == "F32")
+                    o.f32[di] = a.f32[si];
+                else
+                    o.u16[di] = a.u16[si];
+            }
+        return o;
+    }
+    static Mat concat_rows(const std::vector<const Mat*>& parts) {
+        Mat o;
+        o.dtype = parts[0]->dtype;
+        o.cols = parts[0]->cols;
+        for (const Mat* p : parts) {
+            o.rows += p->rows;
+            o.u16.insert(o.u16.end(), p->u16.begin(), p->u16.end());
+            o.f32.insert(o.f32.end(), p->f32.begin(), p->f32.end());
+        }
+        return o;
+    }
+    std::vector<float> values(const Mat& a) {
+        std::vector<float> v(static_cast<size_t>(a.rows * a.cols));
+        for (size_t i = 0; i < v.size(); ++i) v[i] = a.at(i);
+        return v;
+    }
+    // try_quantize_matrix (acestep_dit_model.cpp:156-192): quantize when requested and in-dim % block == 0
+    DevWeight finish(const Mat& a) {
+        DevWeight w;
+        w.rows = static_cast<int>(a.rows);
+        w.cols = static_cast<int>(a.cols);
+        if (quant::applies(qt, a.cols)) {
+            const auto v = values(a);
+            std::vector<uint8_t> blocks(static_cast<size_t>(a.rows) * quant::row_bytes(qt, a.cols));
+            quant::quantize_rows(qt, v.data(), a.rows, a.cols, blocks.data());
+            std::vector<uint8_t> qp(quant::q_plane_bytes(qt, a.rows, a.cols));
+            std::vector<float> sp(quant::s_plane_floats(qt, a.rows, a.cols));
+            quant::to_planes(qt, blocks.data(), a.rows, a.cols, qp.data(), sp.data());
+            w.fmt = qt == quant::Q8_0 ? WF_Q8_0 : (qt == quant::Q4_K ? WF_Q4_K : WF_Q6_K);
+            w.q = upload<uint8_t>(qp.data(), qp.size());
+            w.s = upload<float>(sp.data(), sp.size() * 4);
+            return w;
+        }
+        if (a.dtype == "F32") throw Unsupported("F32 2-D weights are only supported with online quantization");
+        w.fmt = a.dtype == "F16" ? WF_F16 : WF_BF16;
+        w.q = upload<uint16_t>(a.u16.data(), a.u16.size() * 2);
+        return w;
+    }
+    // dense 16-bit copy for the GEMV path: the file bits, or bf16(dequant(quant(w))) when quantizing
+    uint16_t* finish16(const Mat& a, ActType& act) {
+        if (quant::applies(qt, a.cols) || a.dtype == "F32") {
+            auto v = values(a);
+            if (quant::applies(qt, a.cols)) {
+                std::vector<uint8_t> blocks(static_cast<size_t>(a.rows) * quant::row_bytes(qt, a.cols));
+                quant::quantize_rows(qt, v.data(), a.rows, a.cols, blocks.data());
+                quant::dequantize_rows(qt, blocks.data(), a.rows, a.cols, v.data());
+            }
+            std::vector<uint16_t> b(v.size());
+            for (size_t i = 0; i < v.size(); ++i) {
+                uint32_t u;
+                std::memcpy(&u, &v[i], 4);
+                u += 0x7fffu + ((u >> 16) & 1u);  // RNE (finite values)
+                b[i] = static_cast<uint16_t>(u >> 16);
+            }
+            act = ActType::BF16;
+            return upload<uint16_t>(b.data(), b.size() * 2);
+        }
+        act = a.dtype == "F16" ? ActType::F16 : ActType::BF16;
+        return upload<uint16_t>(a.u16.data(), a.u16.size() * 2);
+    }
+    // cast_f32 of a table loaded by load_tensor_3d_as_2d: dequant(quant(t)) when it is quantized
+    std::vector<float> table(const std::string& name, int64_t rows, int64_t cols) {
+        const auto& t = st.get(name);
+        if (t.numel() != rows * cols) throw IoError("invalid tensor shape for " + name);
+        auto v = to_f32(t, st.read(t));
+        if (quant::applies(qt, cols)) {
+            std::vector<uint8_t> blocks(static_cast<size_t>(rows) * quant::row_bytes(qt, cols));
+            quant::quantize_rows(qt, v.data(), rows, cols, blocks.data());
+            quant::dequantize_rows(qt, blocks.data(), rows, cols, v.data());
+        }
+        return v;
+    }
 };
 
 }  // namespace
@@ -255,11 +377,8 @@ void load_dit_model(const std::string& dir, DitModel& m, int& status_hint) {
         }
         if ((p.extension() == ".gguf" && fs::exists(p)) || (fs::is_directory(p) && fs::exists(p / "model.gguf")))
             throw Unsupported("GGUF DiT weights are not supported by the MI355X engine yet");
-        // online quantization request (acestep_dit_model.cpp:27-45)
-        std::string q = upper(std::getenv("ACE_GGML_DIT_WEIGHT_QTYPE"));
-        if (q.empty()) q = upper(std::getenv("ACE_GGML_WEIGHT_QTYPE"));
-        if (q == "Q8" || q == "Q8_0" || q == "Q6" || q == "Q6_K" || q == "Q4" || q == "Q4_K" || q == "Q4_K_M")
-            throw Unsupported("quantized DiT weights (" + q + ") are not supported by the MI355X engine yet");
+        // online quantization request (get_quant_type_from_env, acestep_dit_model.cpp:27-45)
+        const quant::QType qt = quant::from_env();
 
         DitConfig& c = m.cfg;
         load_config((root / "config.json").string(), c);
@@ -272,34 +391,51 @@ void load_dit_model(const std::string& dir, DitModel& m, int& status_hint) {
         if ((c.patch * c.audio_dim) % 128 != 0) throw Unsupported("patch*audio_dim must be a multiple of 128");
 
         Loader L(m);
+        L.qt = qt;
+        m.qtype = qt;
         L.st.open((root / "model.safetensors").string());
         const int H = c.hidden, I = c.intermediate, D = c.head_dim, P = c.patch, Cin = c.in_channels, A = c.audio_dim;
         const int qd = c.hq * D, kd = c.hkv * D;
 
         // proj_in: conv1d [H][Cin][P] -> [H][P*Cin] (load_conv1d_weight_as_linear :334-411)
         {
-            auto w = L.mat16("decoder.proj_in.1.weight", H, (int64_t)Cin * P);
-            std::vector<uint16_t> r(w.size());
-            for (int o = 0; o < H; ++o)
-                for (int ci = 0; ci < Cin; ++ci)
-                    for (int k = 0; k < P; ++k) r[(size_t)o * P * Cin + k * Cin + ci] = w[((size_t)o * Cin + ci) * P + k];
-            m.proj_in_w = L.up16(r);
+            const Mat w = L.mat("decoder.proj_in.1.weight", H, (int64_t)Cin * P);
+            m.proj_in_w = L.finish(Loader::permute(
+                w, H, (int64_t)P * Cin, [](int64_t r) { return r; },
+                [&](int64_t col) { return (col % Cin) * P + col / Cin; }));
             m.proj_in_b = L.vec_f32("decoder.proj_in.1.bias", H);
         }
         // proj_out: convtranspose1d [H][A][P] -> [(o + k*A)][H] (load_convtranspose1d_weight_as_linear :413-490)
         {
-            auto w = L.mat16("decoder.proj_out.1.weight", H, (int64_t)A * P);
-            std::vector<uint16_t> r(w.size());
+            const Mat w = L.mat("decoder.proj_out.1.weight", H, (int64_t)A * P);
+            // source element (i, o, k) sits at row i, column o*P + k; target (o + k*A, i)
+            Mat wt;
+            wt.dtype = w.dtype;
+            wt.rows = (int64_t)A * P;
+            wt.cols = H;
+            if (w.dtype == "F32")
+                wt.f32.resize((size_t)wt.rows * H);
+            else
+                wt.u16.resize((size_t)wt.rows * H);
             for (int i = 0; i < H; ++i)
                 for (int o = 0; o < A; ++o)
-                    for (int k = 0; k < P; ++k) r[(size_t)(o + k * A) * H + i] = w[((size_t)i * A + o) * P + k];
-            m.proj_out_w = L.up16(r);
+                    for (int k = 0; k < P; ++k) {
+                        const size_t si = ((size_t)i * A + o) * P + k, di = (size_t)(o + k * A) * H + i;
+                        if (w.dtype == "F32")
+                            wt.f32[di] = w.f32[si];
+                        else
+                            wt.u16[di] = w.u16[si];
+                    }
+            m.proj_out_w = L.finish(wt);
             m.proj_out_b = L.vec_f32("decoder.proj_out.1.bias", A);
         }
-        m.cond_w = L.up16(L.mat16("decoder.condition_embedder.weight", H, H));
+        m.cond_w = L.finish(L.mat("decoder.condition_embedder.weight", H, H));
         m.cond_b = L.vec_f32("decoder.condition_embedder.bias", H);
         m.norm_out = L.vec_f32("decoder.norm_out.weight", H);
-        m.out_table = L.vec_f32("decoder.scale_shift_table", 2 * H);
+        {
+            auto ot = L.table("decoder.scale_shift_table", 2, H);
+            m.out_table = L.upload<float>(ot.data(), ot.size() * 4);
+        }
         const char* tags[2] = {"decoder.time_embed.", "decoder.time_embed_r."};
         for (int e = 0; e < 2; ++e) {
             const std::string p2 = tags[e];
@@ -307,12 +443,15 @@ void load_dit_model(const std::string& dir, DitModel& m, int& status_hint) {
             if (t1.shape.size() != 2 || t1.shape[0] != H) throw IoError("invalid tensor shape for " + p2 + "linear_1.weight");
             const int64_t fin = t1.shape[1];
             if (fin != 256) throw Unsupported("timestep embedding input dim must be 256");
-            m.te[e].w1 = L.up16(L.mat16(p2 + "linear_1.weight", H, fin));
+            ActType a1, a2, a3;
+            m.te[e].w1 = L.finish16(L.mat(p2 + "linear_1.weight", H, fin), a1);
             m.te[e].b1 = L.vec_f32(p2 + "linear_1.bias", H);
-            m.te[e].w2 = L.up16(L.mat16(p2 + "linear_2.weight", H, H));
+            m.te[e].w2 = L.finish16(L.mat(p2 + "linear_2.weight", H, H), a2);
             m.te[e].b2 = L.vec_f32(p2 + "linear_2.bias", H);
-            m.te[e].wp = L.up16(L.mat16(p2 + "time_proj.weight", 6LL * H, H));
+            m.te[e].wp = L.finish16(L.mat(p2 + "time_proj.weight", 6LL * H, H), a3);
             m.te[e].bp = L.vec_f32(p2 + "time_proj.bias", 6LL * H);
+            if (a1 != a2 || a2 != a3) throw Unsupported("mixed timestep weight types");
+            m.te[e].act = a1;
         }
         std::vector<float> tables((size_t)c.layers * 6 * H);
         m.layers.resize(c.layers);
@@ -327,51 +466,45 @@ void load_dit_model(const std::string& dir, DitModel& m, int& status_hint) {
             ly.cq_norm = L.vec_f32(p2 + "cross_attn.q_norm.weight", D);
             ly.ck_norm = L.vec_f32(p2 + "cross_attn.k_norm.weight", D);
             {
-                auto wq = L.mat16(p2 + "self_attn.q_proj.weight", qd, H);
-                auto wk = L.mat16(p2 + "self_attn.k_proj.weight", kd, H);
-                auto wv = L.mat16(p2 + "self_attn.v_proj.weight", kd, H);
-                std::vector<uint16_t> cat;
-                cat.reserve(wq.size() + wk.size() + wv.size());
-                cat.insert(cat.end(), wq.begin(), wq.end());
-                cat.insert(cat.end(), wk.begin(), wk.end());
-                cat.insert(cat.end(), wv.begin(), wv.end());
-                ly.w_qkv = L.up16(cat);
+                const Mat wq = L.mat(p2 + "self_attn.q_proj.weight", qd, H);
+                const Mat wk = L.mat(p2 + "self_attn.k_proj.weight", kd, H);
+                const Mat wv = L.mat(p2 + "self_attn.v_proj.weight", kd, H);
+                ly.w_qkv = L.finish(Loader::concat_rows({&wq, &wk, &wv}));
             }
-            ly.w_o = L.up16(L.mat16(p2 + "self_attn.o_proj.weight", H, qd));
-            ly.w_cq = L.up16(L.mat16(p2 + "cross_attn.q_proj.weight", qd, H));
+            ly.w_o = L.finish(L.mat(p2 + "self_attn.o_proj.weight", H, qd));
+            ly.w_cq = L.finish(L.mat(p2 + "cross_attn.q_proj.weight", qd, H));
             {
-                auto wk = L.mat16(p2 + "cross_attn.k_proj.weight", kd, H);
-                auto wv = L.mat16(p2 + "cross_attn.v_proj.weight", kd, H);
-                std::vector<uint16_t> cat;
-                cat.reserve(wk.size() + wv.size());
-                cat.insert(cat.end(), wk.begin(), wk.end());
-                cat.insert(cat.end(), wv.begin(), wv.end());
-                ly.w_ckv = L.up16(cat);
+                const Mat wk = L.mat(p2 + "cross_attn.k_proj.weight", kd, H);
+                const Mat wv = L.mat(p2 + "cross_attn.v_proj.weight", kd, H);
+                ly.w_ckv = L.finish(Loader::concat_rows({&wk, &wv}));
             }
-            ly.w_co = L.up16(L.mat16(p2 + "cross_attn.o_proj.weight", H, qd));
+            ly.w_co = L.finish(L.mat(p2 + "cross_attn.o_proj.weight", H, qd));
             {
-                auto wg = L.mat16(p2 + "mlp.gate_proj.weight", I, H);
-                auto wu = L.mat16(p2 + "mlp.up_proj.weight", I, H);
-                std::vector<uint16_t> gu((size_t)2 * I * H);
-                for (int r = 0; r < 2 * I; ++r) {
-                    const int grp = r / 32, w = r % 32;
-                    const auto& src = (w < 16) ? wg : wu;
-                    const int srow = grp * 16 + (w % 16);
-                    std::memcpy(&gu[(size_t)r * H], &src[(size_t)srow * H], (size_t)H * 2);
-                }
-                ly.w_gu = L.up16(gu);
+                const Mat wg = L.mat(p2 + "mlp.gate_proj.weight", I, H);
+                const Mat wu = L.mat(p2 + "mlp.up_proj.weight", I, H);
+                const Mat gu = Loader::concat_rows({&wg, &wu});
+                // rows interleaved in groups of 16: [g0..15, u0..15, g16..31, ...]
+                ly.w_gu = L.finish(Loader::permute(
+                    gu, 2LL * I, H,
+                    [&](int64_t r) {
+                        const int64_t grp = r / 32, w = r % 32;
+                        return (w < 16 ? 0 : (int64_t)I) + grp * 16 + (w % 16);
+                    },
+                    [](int64_t col) { return col; }));
             }
-            ly.w_down = L.up16(L.mat16(p2 + "mlp.down_proj.weight", H, I));
+            ly.w_down = L.finish(L.mat(p2 + "mlp.down_proj.weight", H, I));
             {
-                const auto& t = L.st.get(p2 + "scale_shift_table");
-                if (t.numel() != 6LL * H) throw IoError("invalid tensor shape for " + p2 + "scale_shift_table");
-                auto v = to_f32(t, L.st.read(t));
+                auto v = L.table(p2 + "scale_shift_table", 6, H);
                 std::memcpy(&tables[(size_t)i * 6 * H], v.data(), v.size() * 4);
             }
             ly.sliding = i < (int)c.layer_types.size() && c.layer_types[i] == "sliding_attention";
         }
         m.tables = L.upload<float>(tables.data(), tables.size() * 4);
-        m.act = (L.wdtype == "F16") ? ActType::F16 : ActType::BF16;
+        m.act = m.layers.empty() ? m.cond_w.act() : m.layers[0].w_qkv.act();
+        for (const DevLayer& ly : m.layers)
+            for (const DevWeight* w : {&ly.w_qkv, &ly.w_o, &ly.w_cq, &ly.w_ckv, &ly.w_co, &ly.w_gu, &ly.w_down})
+                if (w->act() != m.act) throw Unsupported("mixed DiT block weight types");
+        if (m.cond_w.act() != m.act || m.proj_out_w.act() != m.act) throw Unsupported("mixed DiT weight types");
     } catch (const Unsupported& e) {
         status_hint = 4;
         throw std::runtime_error(e.what());

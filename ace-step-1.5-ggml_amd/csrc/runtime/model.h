@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../common.h"
+#include "../kernels.h"
 
 namespace acemi {
 
@@ -27,14 +28,32 @@ struct DitConfig {
     int ctx_dim() const { return in_channels - audio_dim; }
 };
 
+// A 2-D linear weight [rows = out][cols = in] in HBM: dense 16-bit (file dtype) or one of the
+// ggml block formats re-laid out as q/s planes (runtime/quant.h) when online quantization is on.
+struct DevWeight {
+    int fmt = WF_BF16;
+    void* q = nullptr;
+    float* s = nullptr;
+    int rows = 0, cols = 0;
+    WeightView view() const {
+        WeightView v;
+        v.fmt = fmt;
+        v.q = q;
+        v.s = s;
+        v.ld = cols;
+        return v;
+    }
+    ActType act() const { return weight_act(fmt); }
+};
+
 struct DevLayer {
-    uint16_t* w_qkv = nullptr;   // [(hq+2hkv)*D][H]
-    uint16_t* w_o = nullptr;     // [H][hq*D]
-    uint16_t* w_cq = nullptr;    // [hq*D][H]
-    uint16_t* w_ckv = nullptr;   // [2*hkv*D][H]
-    uint16_t* w_co = nullptr;    // [H][hq*D]
-    uint16_t* w_gu = nullptr;    // [2I][H] (16-row interleave)
-    uint16_t* w_down = nullptr;  // [H][I]
+    DevWeight w_qkv;   // [(hq+2hkv)*D][H]
+    DevWeight w_o;     // [H][hq*D]
+    DevWeight w_cq;    // [hq*D][H]
+    DevWeight w_ckv;   // [2*hkv*D][H]
+    DevWeight w_co;    // [H][hq*D]
+    DevWeight w_gu;    // [2I][H] (16-row interleave)
+    DevWeight w_down;  // [H][I]
     float* self_norm = nullptr;
     float* cross_norm = nullptr;
     float* mlp_norm = nullptr;
@@ -46,7 +65,10 @@ struct DevLayer {
     bool cross = true;  // Layer::use_cross_attention default
 };
 
+// Timestep MLPs run as small-M GEMVs on dense 16-bit weights; when the checkpoint is quantized
+// online they hold bf16(dequant(q)) — the same values the dequant-fused GEMM feeds its MFMAs.
 struct DevTimestep {
+    ActType act = ActType::BF16;
     uint16_t* w1 = nullptr;  // [H][256]
     uint16_t* w2 = nullptr;  // [H][H]
     uint16_t* wp = nullptr;  // [6H][H]
@@ -57,12 +79,13 @@ struct DevTimestep {
 
 struct DitModel {
     DitConfig cfg;
-    ActType act = ActType::BF16;
-    uint16_t* proj_in_w = nullptr;   // [H][P*Cin], column k*Cin + c
+    ActType act = ActType::BF16;     // activation type of every GEMM except proj_in
+    int qtype = 0;                   // quant::QType of the online quantization (0 = none)
+    DevWeight proj_in_w;             // [H][P*Cin], column k*Cin + c
     float* proj_in_b = nullptr;
-    uint16_t* proj_out_w = nullptr;  // [P*audio][H], row o + k*audio
+    DevWeight proj_out_w;            // [P*audio][H], row o + k*audio
     float* proj_out_b = nullptr;
-    uint16_t* cond_w = nullptr;      // [H][H]
+    DevWeight cond_w;                // [H][H]
     float* cond_b = nullptr;
     float* norm_out = nullptr;
     float* out_table = nullptr;      // [2][H]

@@ -5,6 +5,7 @@
 
 #include "../../../include/acestep_mi355x.h"
 #include "../kernels.h"
+#include "quant.h"
 
 namespace {
 
@@ -207,6 +208,155 @@ ace_ggml_status ace_mi_bench_gemm(int32_t act_type, int32_t epi, int32_t variant
 ace_ggml_status ace_mi_gemm_variant(int32_t variant) {
     if (variant < -1 || variant > 3) return ACE_GGML_ERR_INVALID_ARG;
     acemi::gemm_force_variant(variant);
+    return ACE_GGML_OK;
+}
+
+}  // extern "C"
+
+extern "C" {
+
+// ggml block quantization of rows (the loader's encoders): returns bytes written, or -1.
+int64_t ace_mi_quantize(int32_t qtype, const float* src, int64_t rows, int64_t cols, uint8_t* dst, size_t dst_size) {
+    using namespace acemi;
+    const auto t = static_cast<quant::QType>(qtype);
+    if (!src || !dst || rows <= 0 || (t != quant::Q8_0 && t != quant::Q4_K && t != quant::Q6_K)) return -1;
+    if (!quant::applies(t, cols)) return -1;
+    const size_t need = (size_t)rows * quant::row_bytes(t, cols);
+    if (dst_size < need) return -1;
+    try {
+        quant::quantize_rows(t, src, rows, cols, dst);
+    } catch (const std::exception&) {
+        return -1;
+    }
+    return (int64_t)need;
+}
+
+ace_ggml_status ace_mi_dequantize(int32_t qtype, const uint8_t* src, int64_t rows, int64_t cols, float* dst) {
+    using namespace acemi;
+    const auto t = static_cast<quant::QType>(qtype);
+    if (!src || !dst || rows <= 0 || (t != quant::Q8_0 && t != quant::Q4_K && t != quant::Q6_K) ||
+        !quant::applies(t, cols))
+        return ACE_GGML_ERR_INVALID_ARG;
+    quant::dequantize_rows(t, src, rows, cols, dst);
+    return ACE_GGML_OK;
+}
+
+// Dequant-fused GEMM on ggml block rows W [N][K]: out = A(bf16) . bf16(dequant(W))^T (+ bias).
+ace_ggml_status ace_mi_kernel_gemm_q(int32_t qtype, int32_t epi, int32_t variant, int32_t M, int32_t N, int32_t K,
+                                     const uint16_t* A, const uint8_t* W_blocks, const float* bias, float* out_f32,
+                                     uint16_t* out_u16) {
+    using namespace acemi;
+    const auto t = static_cast<quant::QType>(qtype);
+    if (!A || !W_blocks || M <= 0 || N % 128 != 0 || K % 64 != 0) return ACE_GGML_ERR_INVALID_ARG;
+    if (t != quant::Q8_0 && t != quant::Q4_K && t != quant::Q6_K) return ACE_GGML_ERR_INVALID_ARG;
+    if (!quant::applies(t, K)) return ACE_GGML_ERR_INVALID_ARG;
+    if (epi != EPI_STORE_F32 && epi != EPI_SWIGLU) return ACE_GGML_ERR_UNSUPPORTED;
+    if ((epi == EPI_STORE_F32 && !out_f32) || (epi == EPI_SWIGLU && !out_u16)) return ACE_GGML_ERR_INVALID_ARG;
+    if (variant < -1 || variant > 3) return ACE_GGML_ERR_INVALID_ARG;
+    try {
+        std::vector<uint8_t> qp(quant::q_plane_bytes(t, N, K));
+        std::vector<float> sp(quant::s_plane_floats(t, N, K));
+        quant::to_planes(t, W_blocks, N, K, qp.data(), sp.data());
+        DevMem dA((size_t)M * K * 2), dQ(qp.size()), dS(sp.size() * 4), dB((size_t)N * 4), dC((size_t)M * N * 4);
+        ACEMI_HIP(hipMemcpy(dA.p, A, (size_t)M * K * 2, hipMemcpyHostToDevice));
+        ACEMI_HIP(hipMemcpy(dQ.p, qp.data(), qp.size(), hipMemcpyHostToDevice));
+        ACEMI_HIP(hipMemcpy(dS.p, sp.data(), sp.size() * 4, hipMemcpyHostToDevice));
+        if (bias) ACEMI_HIP(hipMemcpy(dB.p, bias, (size_t)N * 4, hipMemcpyHostToDevice));
+        GemmEpilogue e;
+        e.kind = epi;
+        e.bias = bias ? dB.as<float>() : nullptr;
+        if (epi == EPI_STORE_F32) {
+            e.c_f32 = dC.as<float>();
+            e.ldc = N;
+        } else {
+            e.c_act = dC.as<uint16_t>();
+            e.ldc = N / 2;
+        }
+        WeightView w;
+        w.fmt = t == quant::Q8_0 ? WF_Q8_0 : (t == quant::Q4_K ? WF_Q4_K : WF_Q6_K);
+        w.q = dQ.p;
+        w.s = dS.as<float>();
+        gemm_force_variant(variant);
+        launch_gemm(dA.as<uint16_t>(), K, w, M, N, K, e, nullptr);
+        gemm_force_variant(-1);
+        ACEMI_HIP(hipDeviceSynchronize());
+        if (epi == EPI_STORE_F32)
+            ACEMI_HIP(hipMemcpy(out_f32, dC.p, (size_t)M * N * 4, hipMemcpyDeviceToHost));
+        else
+            ACEMI_HIP(hipMemcpy(out_u16, dC.p, (size_t)M * (N / 2) * 2, hipMemcpyDeviceToHost));
+    } catch (const std::exception& ex) {
+        gemm_force_variant(-1);
+        std::fprintf(stderr, "ace_mi_kernel_gemm_q: %s\n", ex.what());
+        return ACE_GGML_ERR;
+    }
+    return ACE_GGML_OK;
+}
+
+// Dequant-fused GEMM micro-benchmark (random N(0, 0.02) weights quantized with the loader's encoder).
+ace_ggml_status ace_mi_bench_gemm_q(int32_t qtype, int32_t epi, int32_t variant, int32_t M, int32_t N, int32_t K,
+                                    int32_t iters, float* avg_ms) {
+    using namespace acemi;
+    const auto t = static_cast<quant::QType>(qtype);
+    if (M <= 0 || N % 128 != 0 || K % 64 != 0 || iters <= 0 || !avg_ms) return ACE_GGML_ERR_INVALID_ARG;
+    if (t != quant::Q8_0 && t != quant::Q4_K && t != quant::Q6_K) return ACE_GGML_ERR_INVALID_ARG;
+    if (!quant::applies(t, K)) return ACE_GGML_ERR_INVALID_ARG;
+    try {
+        uint32_t st = 777u;
+        auto rnd = [&]() {
+            st = st * 1664525u + 1013904223u;
+            return ((float)(st >> 8) * (2.0f / 16777216.0f) - 1.0f);
+        };
+        std::vector<uint16_t> ha((size_t)M * K);
+        for (auto& v : ha) {
+            const float f = rnd();
+            uint32_t u;
+            std::memcpy(&u, &f, 4);
+            v = (uint16_t)(u >> 16);
+        }
+        std::vector<float> hw((size_t)N * K);
+        for (auto& v : hw) v = 0.02f * rnd();
+        std::vector<uint8_t> blocks((size_t)N * quant::row_bytes(t, K));
+        quant::quantize_rows(t, hw.data(), N, K, blocks.data());
+        std::vector<uint8_t> qp(quant::q_plane_bytes(t, N, K));
+        std::vector<float> sp(quant::s_plane_floats(t, N, K));
+        quant::to_planes(t, blocks.data(), N, K, qp.data(), sp.data());
+        DevMem dA(ha.size() * 2), dQ(qp.size()), dS(sp.size() * 4), dC((size_t)M * N * 4), dG((size_t)N * 4);
+        ACEMI_HIP(hipMemcpy(dA.p, ha.data(), ha.size() * 2, hipMemcpyHostToDevice));
+        ACEMI_HIP(hipMemcpy(dQ.p, qp.data(), qp.size(), hipMemcpyHostToDevice));
+        ACEMI_HIP(hipMemcpy(dS.p, sp.data(), sp.size() * 4, hipMemcpyHostToDevice));
+        ACEMI_HIP(hipMemset(dC.p, 0, (size_t)M * N * 4));
+        ACEMI_HIP(hipMemset(dG.p, 0, (size_t)N * 4));
+        GemmEpilogue e;
+        e.kind = epi;
+        e.ldc = (epi == EPI_SWIGLU) ? N / 2 : N;
+        e.c_f32 = dC.as<float>();
+        e.c_act = dC.as<uint16_t>();
+        e.gate = dG.as<float>();
+        e.rows_per_item = M;
+        WeightView w;
+        w.fmt = t == quant::Q8_0 ? WF_Q8_0 : (t == quant::Q4_K ? WF_Q4_K : WF_Q6_K);
+        w.q = dQ.p;
+        w.s = dS.as<float>();
+        gemm_force_variant(variant);
+        hipEvent_t e0, e1;
+        ACEMI_HIP(hipEventCreate(&e0));
+        ACEMI_HIP(hipEventCreate(&e1));
+        for (int i = 0; i < 3; ++i) launch_gemm(dA.as<uint16_t>(), K, w, M, N, K, e, nullptr);
+        ACEMI_HIP(hipEventRecord(e0, nullptr));
+        for (int i = 0; i < iters; ++i) launch_gemm(dA.as<uint16_t>(), K, w, M, N, K, e, nullptr);
+        ACEMI_HIP(hipEventRecord(e1, nullptr));
+        ACEMI_HIP(hipEventSynchronize(e1));
+        float ms = 0.f;
+        ACEMI_HIP(hipEventElapsedTime(&ms, e0, e1));
+        *avg_ms = ms / iters;
+        gemm_force_variant(-1);
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+    } catch (const std::exception& ex) {
+        gemm_force_variant(-1);
+        std::fprintf(stderr, "ace_mi_bench_gemm_q: %s\n", ex.what());
+        return ACE_GGML_ERR;
+    }
     return ACE_GGML_OK;
 }
 

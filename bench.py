@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--sample-steps", type=int, default=27)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--qtype", default="", choices=["", "q8_0", "q4_k", "q6_k"],
+                    help="online weight quantization (ACE_GGML_DIT_WEIGHT_QTYPE): BASELINE configs[2] is q8_0")
     return ap.parse_args()
 
 
@@ -76,8 +78,14 @@ def main():
     if rank != 0:
         ckpt = cached_checkpoint(cfg, seed=0, backend="torch")
 
+    if args.qtype:
+        os.environ["ACE_GGML_DIT_WEIGHT_QTYPE"] = args.qtype
+    else:
+        os.environ.pop("ACE_GGML_DIT_WEIGHT_QTYPE", None)
+        os.environ.pop("ACE_GGML_WEIGHT_QTYPE", None)
     br = GGMLCAPIBridge(device=local)
     br.load_dit(ckpt)
+    wdesc = f"{args.qtype.upper()} dequant-fused (bf16 MFMA)" if args.qtype else "bf16"
     info = br.info
 
     T = int(round(args.seconds * 25))        # 25 Hz latent frames
@@ -155,7 +163,8 @@ def main():
             flops = 2.0 * M * (2 * info.intermediate_size) * info.hidden_size
             avg_s = ms / cnt / 1000.0
             ach = flops / avg_s / 1e12
-            roofline = {"kernel": "gemm_gate_up (MLP gate|up, bf16 MFMA, SwiGLU epilogue)", "bound": "mfma",
+            roofline = {"kernel": f"gemm_gate_up (MLP gate|up, {wdesc} weights, bf16 MFMA, SwiGLU epilogue)",
+                        "bound": "mfma",
                         "achieved": round(ach, 1), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                         "frac": round(ach / BF16_PEAK_TFLOPS, 4), "traffic": None,
                         "flops_per_launch": flops, "avg_launch_us": round(avg_s * 1e6, 2),
@@ -179,7 +188,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and os.environ.get("ACE_MI_CPU_BASELINE", "1") != "0":
         try:
-            cpu = cpu_baseline(ckpt, T, L)
+            cpu = cpu_baseline(ckpt, T, L, args.qtype or None)
         except Exception as e:  # noqa: BLE001  (reported, never fatal)
             cpu = {"value": None, "error": str(e)[:200]}
 
@@ -203,7 +212,8 @@ def main():
             "config": {
                 "workload": f"DiT {args.sample_steps}-step sample, {args.seconds:g} s audio "
                             f"(T={T} latent frames @25 Hz, N={(T + 1) // 2} tokens), enc_len={L}, "
-                            f"bs={b_loc}/GPU, bf16 weights, f32-faithful fp16x3 attention",
+                            f"bs={b_loc}/GPU, {wdesc} weights, f32-faithful fp16x3 attention",
+                "weights": args.qtype or "bf16",
                 "model": "ACE-Step 1.5 DiT (24 layers, hidden 2048, MLP 6144, 16/8 heads)",
                 "seconds": args.seconds, "latent_frames": T, "tokens": (T + 1) // 2, "enc_len": L,
                 "batch_per_gpu": b_loc, "global_batch": B, "seq_len": T,
@@ -220,7 +230,7 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(ckpt, T, L):
+def cpu_baseline(ckpt, T, L, qtype=None):
     """Time one 240 s DiT forward of the numpy oracle (the checker restatement of ggml's CPU graph,
     oracle/dit_oracle.py) on the host; steps/s = 1 / seconds."""
     import numpy as np
@@ -230,7 +240,9 @@ def cpu_baseline(ckpt, T, L):
     except Exception:  # noqa: BLE001
         cores = os.cpu_count() or 1
     from oracle.dit_oracle import DitWeights, forward_dit
-    W = DitWeights(ckpt)
+    if qtype not in (None, "q8_0"):
+        qtype = None  # the numpy K-quant encoder is too slow for 1.5 B weights; time the bf16 graph
+    W = DitWeights(ckpt, qtype=qtype)
     rng = np.random.default_rng(1234)
     h = rng.standard_normal((T, 64)).astype(np.float32)
     c = np.concatenate([rng.standard_normal((T, 64)), np.ones((T, 64))], axis=1).astype(np.float32)
@@ -241,7 +253,8 @@ def cpu_baseline(ckpt, T, L):
     return {"value": round(1.0 / sec, 5), "unit": "steps/s", "cores": cores, "kind": "port",
             "seconds_per_step": round(sec, 3),
             "sample": f"1 full 24-layer DiT forward, T={T}, L={L}, bs=1 (numpy/OpenBLAS f32 restatement "
-                      "of acestep_ggml forward_dit with ggml's bf16 activation rounding)"}
+                      f"of acestep_ggml forward_dit, {qtype or 'bf16'} weights, ggml's activation rounding for "
+                      "that weight type)"}
 
 
 if __name__ == "__main__":

@@ -100,6 +100,23 @@ ACE_GGML_API ace_ggml_status ace_mi_bench_gemm(int32_t act_type, int32_t epi, in
 /* Force the GEMM kernel variant of all later launches in this process (-1 = automatic). */
 ACE_GGML_API ace_ggml_status ace_mi_gemm_variant(int32_t variant);
 
+/* ggml block quantization (qtype 1 = Q8_0, 2 = Q4_K, 3 = Q6_K) with the encoders the loader uses for
+ * ACE_GGML_DIT_WEIGHT_QTYPE (try_quantize_matrix, acestep_dit_model.cpp:156-192): rows x cols f32 ->
+ * ggml block bytes.  Returns the byte count written, or -1 (bad type / cols % block / dst too small). */
+ACE_GGML_API int64_t ace_mi_quantize(int32_t qtype, const float* src, int64_t rows, int64_t cols, uint8_t* dst,
+                                     size_t dst_size);
+/* ggml dequantize_row_* of block rows to f32. */
+ACE_GGML_API ace_ggml_status ace_mi_dequantize(int32_t qtype, const uint8_t* src, int64_t rows, int64_t cols,
+                                               float* dst);
+/* Dequant-fused GEMM on ggml block rows W [N][K]: out = A . bf16(dequant(W))^T (+ bias), A bf16 [M][K];
+ * epi 0 (f32 store) or 4 (SwiGLU, bf16 out [M][N/2]); variant -1 automatic, 0..3 forced. */
+ACE_GGML_API ace_ggml_status ace_mi_kernel_gemm_q(int32_t qtype, int32_t epi, int32_t variant, int32_t M, int32_t N,
+                                                  int32_t K, const uint16_t* A, const uint8_t* W_blocks,
+                                                  const float* bias, float* out_f32, uint16_t* out_u16);
+/* Dequant-fused GEMM micro-benchmark: average ms per launch (HIP events). */
+ACE_GGML_API ace_ggml_status ace_mi_bench_gemm_q(int32_t qtype, int32_t epi, int32_t variant, int32_t M, int32_t N,
+                                                 int32_t K, int32_t iters, float* avg_ms);
+
 #ifdef __cplusplus
 }
 #endif

@@ -67,7 +67,9 @@ def quantize_q8_0_weights(w: np.ndarray):
     with np.errstate(divide="ignore"):
         idv = np.where(d != 0, np.float32(1.0) / d, np.float32(0.0)).astype(np.float32)
     x0 = blk * idv[:, :, None]
-    q = (np.sign(x0) * np.floor(np.abs(x0) + np.float32(0.5))).astype(np.int8)  # roundf
+    ax = np.abs(x0)
+    fl = np.floor(ax)
+    q = (np.sign(x0) * (fl + ((ax - fl) >= np.float32(0.5)))).astype(np.int8)  # roundf, exact
     return d.astype(np.float16), q
 
 
@@ -120,6 +122,12 @@ def _nearest_int(f):
     return np.rint(np.asarray(f, dtype=np.float32)).astype(np.int32)
 
 
+def _seqsum(a: np.ndarray) -> np.ndarray:
+    """Row sums in float32 accumulated left to right, like ggml's scalar `for` loops
+    (np.sum would use pairwise summation and round differently)."""
+    return np.add.accumulate(np.asarray(a, dtype=np.float32), axis=1, dtype=np.float32)[:, -1]
+
+
 def _make_qkx2_quants(x, weights, nmax=15, rmin=-1.0, rdelta=0.1, nstep=20):
     """Vectorised make_qkx2_quants(n=32, use_mad=false) over a batch of sub-blocks.
     x, weights: [S, 32] f32.  Returns (scale [S], the_min [S] (= -min), L [S,32])."""
@@ -127,22 +135,25 @@ def _make_qkx2_quants(x, weights, nmax=15, rmin=-1.0, rdelta=0.1, nstep=20):
     w = weights.astype(np.float32)
     mn = np.minimum(np.min(x, axis=1), np.float32(0.0))
     mx = np.max(x, axis=1)
-    sum_w = np.sum(w, axis=1, dtype=np.float32)
-    sum_x = np.sum(w * x, axis=1, dtype=np.float32)
+    sum_w = _seqsum(w)
+    sum_x = _seqsum(w * x)
     flat = mx == mn
     rng_ = np.where(flat, np.float32(1.0), mx - mn).astype(np.float32)
     iscale = (np.float32(nmax) / rng_).astype(np.float32)
     scale = (np.float32(1.0) / iscale).astype(np.float32)
     L = np.clip(_nearest_int(iscale[:, None] * (x - mn[:, None])), 0, nmax)
-    diff = scale[:, None] * L + mn[:, None] - x
-    best = np.sum(w * diff * diff, axis=1, dtype=np.float32)
+    diff = scale[:, None] * L.astype(np.float32) + mn[:, None] - x
+    best = _seqsum(w * (diff * diff))
     best_min = mn.copy()
     for i_s in range(nstep + 1):
-        isc = ((np.float32(rmin) + np.float32(rdelta) * np.float32(i_s) + np.float32(nmax)) / rng_).astype(np.float32)
-        La = np.clip(_nearest_int(isc[:, None] * (x - mn[:, None])), 0, nmax).astype(np.float32)
-        sum_l = np.sum(w * La, axis=1, dtype=np.float32)
-        sum_l2 = np.sum(w * La * La, axis=1, dtype=np.float32)
-        sum_xl = np.sum(w * La * x, axis=1, dtype=np.float32)
+        # ggml updates `min` in place when a better fit is found, so later search points use the
+        # current best min in both the range (max - min) and the offset (x - min)
+        rng_cur = np.where(flat, np.float32(1.0), mx - best_min).astype(np.float32)
+        isc = ((np.float32(rmin) + np.float32(rdelta) * np.float32(i_s) + np.float32(nmax)) / rng_cur).astype(np.float32)
+        La = np.clip(_nearest_int(isc[:, None] * (x - best_min[:, None])), 0, nmax).astype(np.float32)
+        sum_l = _seqsum(w * La)
+        sum_l2 = _seqsum(w * La * La)
+        sum_xl = _seqsum(w * La * x)
         D = sum_w * sum_l2 - sum_l * sum_l
         ok = D > 0
         Ds = np.where(ok, D, np.float32(1.0))
@@ -152,7 +163,7 @@ def _make_qkx2_quants(x, weights, nmax=15, rmin=-1.0, rdelta=0.1, nstep=20):
         this_min = np.where(pos, np.float32(0.0), this_min)
         this_scale = np.where(pos, sum_xl / np.where(sum_l2 != 0, sum_l2, np.float32(1.0)), this_scale)
         d2 = this_scale[:, None] * La + this_min[:, None] - x
-        mad = np.sum(w * d2 * d2, axis=1, dtype=np.float32)
+        mad = _seqsum(w * (d2 * d2))
         better = ok & (mad < best)
         L = np.where(better[:, None], La.astype(np.int32), L)
         best = np.where(better, mad, best)
@@ -172,9 +183,9 @@ def quantize_q4_k_weights(w: np.ndarray) -> np.ndarray:
     nb = k // QK_K
     x = w.reshape(rows * nb, 8, 32)
     sub = x.reshape(-1, 32)
-    av_x = np.sqrt(np.sum(sub * sub, axis=1, dtype=np.float32) / np.float32(32.0)).astype(np.float32)
+    av_x = np.sqrt(_seqsum(sub * sub) / np.float32(32.0)).astype(np.float32)
     weights = av_x[:, None] + np.abs(sub)
-    scales, mins, _ = _make_qkx2_quants(sub, weights)
+    scales, mins, L0 = _make_qkx2_quants(sub, weights)
     scales = scales.reshape(-1, 8)
     mins = mins.reshape(-1, 8)
     max_scale = np.maximum(np.max(scales, axis=1), np.float32(0.0))
@@ -197,7 +208,8 @@ def quantize_q4_k_weights(w: np.ndarray) -> np.ndarray:
     with np.errstate(divide="ignore", invalid="ignore"):
         Lq = _nearest_int((x + dm[:, :, None]) / np.where(dd != 0, dd, 1)[:, :, None])
     Lq = np.clip(Lq, 0, 15).astype(np.uint8)
-    Lq = np.where((dd != 0)[:, :, None], Lq, 0).astype(np.uint8).reshape(rows * nb, 256)
+    # `if (!d) continue;` keeps make_qkx2_quants' L for that sub-block
+    Lq = np.where((dd != 0)[:, :, None], Lq, L0.reshape(-1, 8, 32)).astype(np.uint8).reshape(rows * nb, 256)
     qs = np.empty((rows * nb, 128), dtype=np.uint8)
     for j in range(4):
         qs[:, 32 * j:32 * j + 32] = Lq[:, 64 * j:64 * j + 32] | (Lq[:, 64 * j + 32:64 * j + 64] << 4)
@@ -255,6 +267,124 @@ def q8_k_activation_roundtrip(x: np.ndarray) -> np.ndarray:
 
 
 # --------------------------------------------------------------------------
+# Q6_K (weights; activations -> Q8_K like Q4_K)
+# --------------------------------------------------------------------------
+GROUP_MAX_EPS = np.float32(1e-15)
+
+
+def _make_qx_quants_rmse1(x: np.ndarray, nmax: int = 32):
+    """make_qx_quants(n=16, nmax, x, L, rmse_type=1, qw=NULL) over a batch of sub-blocks
+    (ggml-quants.c, restated): weights w = x*x, sequential float sums, 18-point scale search.
+    Returns (scale [S] f32, L [S,16] in 0..2*nmax-1)."""
+    x = np.asarray(x, dtype=np.float32)
+    S, n = x.shape
+    ax = np.abs(x)
+    # first index of the largest |x| (strict '>' scan from i = 0)
+    imax = np.argmax(ax, axis=1)
+    amax = ax[np.arange(S), imax]
+    mx = x[np.arange(S), imax]
+    zero = amax < GROUP_MAX_EPS
+    mxs = np.where(zero, np.float32(1.0), mx).astype(np.float32)
+    w = x * x
+
+    def quant(iscale):
+        lf = _nearest_int(iscale[:, None] * x)
+        return np.clip(lf, -nmax, nmax - 1)
+
+    iscale = (np.float32(-nmax) / mxs).astype(np.float32)
+    l = quant(iscale)
+    L = (l + nmax).astype(np.int32)
+    lf = l.astype(np.float32)
+    sumlx = _seqsum(w * x * lf)
+    suml2 = _seqsum(w * lf * lf)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        scale = np.where(suml2 != 0, sumlx / np.where(suml2 != 0, suml2, 1), np.float32(0.0)).astype(np.float32)
+    best = (scale * sumlx).astype(np.float32)
+    for i_s in range(-9, 10):
+        if i_s == 0:
+            continue
+        isc = (-(np.float32(nmax) + np.float32(0.1) * np.float32(i_s)) / mxs).astype(np.float32)
+        l2 = quant(isc)
+        lf2 = l2.astype(np.float32)
+        slx = _seqsum(w * x * lf2)
+        sl2 = _seqsum(w * lf2 * lf2)
+        better = (sl2 > 0) & (slx * slx > best * sl2)
+        L = np.where(better[:, None], l2 + nmax, L)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            sc2 = (slx / np.where(sl2 != 0, sl2, 1)).astype(np.float32)
+        scale = np.where(better, sc2, scale).astype(np.float32)
+        best = np.where(better, (sc2 * slx).astype(np.float32), best).astype(np.float32)
+    scale = np.where(zero, np.float32(0.0), scale).astype(np.float32)
+    L = np.where(zero[:, None], 0, L)
+    return scale, L
+
+
+def quantize_q6_k_weights(w: np.ndarray) -> np.ndarray:
+    """quantize_row_q6_K_ref (no imatrix), restated from the published ggml source
+    (parity unpinned; block layout {ql[128], qh[64], int8 scales[16], fp16 d} =
+    ggml-metal-embed.metal:329-338).  Returns packed bytes [rows, nb, 210]."""
+    w = np.asarray(w, dtype=np.float32)
+    rows, k = w.shape
+    assert k % QK_K == 0
+    nb = k // QK_K
+    x = w.reshape(rows * nb, 16, 16)
+    scales, L0 = _make_qx_quants_rmse1(x.reshape(-1, 16))
+    scales = scales.reshape(-1, 16)
+    L0 = L0.reshape(-1, 16, 16)
+    ab = np.abs(scales)
+    imax = np.argmax(ab, axis=1)
+    max_abs = ab[np.arange(len(ab)), imax]
+    max_scale = scales[np.arange(len(ab)), imax]
+    zero = max_abs < GROUP_MAX_EPS
+    iscale = np.where(zero, np.float32(0.0), np.float32(-128.0) / np.where(zero, 1, max_scale)).astype(np.float32)
+    with np.errstate(divide="ignore"):
+        d = np.where(zero, np.float32(0.0), np.float32(1.0) / np.where(zero, 1, iscale)).astype(np.float16)
+    sc = np.minimum(_nearest_int(iscale[:, None] * scales), 127).astype(np.int8)
+    dd = d.astype(np.float32)[:, None] * sc.astype(np.float32)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        lq = _nearest_int(x / np.where(dd != 0, dd, 1)[:, :, None])
+    lq = np.clip(lq, -32, 31) + 32
+    L = np.where((dd != 0)[:, :, None], lq, L0).astype(np.uint8).reshape(-1, 256)
+    ql = np.zeros((len(L), 128), dtype=np.uint8)
+    qh = np.zeros((len(L), 64), dtype=np.uint8)
+    for h in range(2):
+        j = 128 * h
+        Lh = L[:, j:j + 128]
+        q1, q2, q3, q4 = Lh[:, 0:32], Lh[:, 32:64], Lh[:, 64:96], Lh[:, 96:128]
+        ql[:, 64 * h:64 * h + 32] = (q1 & 0xF) | ((q3 & 0xF) << 4)
+        ql[:, 64 * h + 32:64 * h + 64] = (q2 & 0xF) | ((q4 & 0xF) << 4)
+        qh[:, 32 * h:32 * h + 32] = (q1 >> 4) | ((q2 >> 4) << 2) | ((q3 >> 4) << 4) | ((q4 >> 4) << 6)
+    out = np.zeros((len(L), 210), dtype=np.uint8)
+    out[:, 0:128] = ql
+    out[:, 128:192] = qh
+    out[:, 192:208] = sc.view(np.uint8)
+    out[:, 208:210] = d.astype("<f2").view(np.uint8).reshape(-1, 2)
+    out[zero] = 0  # memset(&y[i], 0, sizeof(block_q6_K))
+    return out.reshape(rows, nb, 210)
+
+
+def dequantize_q6_k(raw: np.ndarray) -> np.ndarray:
+    """dequantize_row_q6_K: y = d * sc[l/16] * (q - 32) with q = ql nibble | qh 2 bits << 4."""
+    raw = np.asarray(raw, dtype=np.uint8)
+    rows, nb, _ = raw.shape
+    r = raw.reshape(rows * nb, 210)
+    ql, qh = r[:, 0:128], r[:, 128:192]
+    sc = r[:, 192:208].copy().view(np.int8).astype(np.float32)
+    d = r[:, 208:210].copy().view("<f2")[:, 0].astype(np.float32)
+    q = np.empty((len(r), 256), dtype=np.float32)
+    for h in range(2):
+        a, b, hh = ql[:, 64 * h:64 * h + 32], ql[:, 64 * h + 32:64 * h + 64], qh[:, 32 * h:32 * h + 32]
+        base = 128 * h
+        q[:, base + 0:base + 32] = ((a & 0xF) | (((hh >> 0) & 3) << 4)).astype(np.float32) - 32
+        q[:, base + 32:base + 64] = ((b & 0xF) | (((hh >> 2) & 3) << 4)).astype(np.float32) - 32
+        q[:, base + 64:base + 96] = ((a >> 4) | (((hh >> 4) & 3) << 4)).astype(np.float32) - 32
+        q[:, base + 96:base + 128] = ((b >> 4) | (((hh >> 6) & 3) << 4)).astype(np.float32) - 32
+    ds = (d[:, None] * sc).astype(np.float32)  # d * sc[is] first, then * q (float)
+    y = ds[:, :, None] * q.reshape(-1, 16, 16)
+    return y.reshape(rows, nb * 256).astype(np.float32)
+
+
+# --------------------------------------------------------------------------
 # Weight container with ggml storage semantics
 # --------------------------------------------------------------------------
 class GgmlWeight:
@@ -278,7 +408,7 @@ def convert_activation(x: np.ndarray, wtype: str) -> np.ndarray:
         return round_f16(x)
     if wtype == "q8_0":
         return q8_0_activation_roundtrip(x)
-    if wtype == "q4_k":
+    if wtype in ("q4_k", "q6_k"):
         return q8_k_activation_roundtrip(x)
     if wtype == "f32":
         return np.asarray(x, dtype=np.float32)
@@ -310,5 +440,8 @@ def make_weight(f32_values: np.ndarray, src_dtype: str, qtype: str | None) -> Gg
     if qtype == "q4_k" and v.shape[1] % QK_K == 0:
         raw = quantize_q4_k_weights(v)
         return GgmlWeight(dequantize_q4_k(raw), "q4_k", raw=raw)
+    if qtype == "q6_k" and v.shape[1] % QK_K == 0:
+        raw = quantize_q6_k_weights(v)
+        return GgmlWeight(dequantize_q6_k(raw), "q6_k", raw=raw)
     wt = {"BF16": "bf16", "F16": "f16", "F32": "f32"}[src_dtype]
     return GgmlWeight(v, wt)

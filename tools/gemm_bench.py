@@ -17,12 +17,18 @@ SHAPES = [  # (name, M, N, K, epi)
     ("square 8192", 8192, 8192, 8192, 0),
 ]
 variants = [int(v) for v in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["0", "1", "2", "3"])]
-res = []
-for name, M, N, K, epi in SHAPES:
-    row = {"shape": name, "MNK": [M, N, K]}
-    for v in variants:
-        if v == 2 and N % 256:
+qtypes = sys.argv[2].split(",") if len(sys.argv) > 2 else [""]
+for qt in qtypes:
+    for name, M, N, K, epi in SHAPES:
+        if qt and M > 8192:
             continue
-        ms = capi.bench_gemm(M, N, K, variant=v, epi=epi, iters=20)
-        row[f"v{v}"] = round(2.0 * M * N * K / (ms / 1e3) / 1e12, 1)
-    print(json.dumps(row), flush=True)
+        row = {"shape": name, "MNK": [M, N, K], "weights": qt or "bf16"}
+        for v in variants:
+            if v == 2 and N % 256:
+                continue
+            if qt:
+                ms = capi.bench_gemm_q(M, N, K, qt, variant=v, epi=epi, iters=20)
+            else:
+                ms = capi.bench_gemm(M, N, K, variant=v, epi=epi, iters=20)
+            row[f"v{v}"] = round(2.0 * M * N * K / (ms / 1e3) / 1e12, 1)
+        print(json.dumps(row), flush=True)
