@@ -32,7 +32,8 @@ EXPORTED_SYMBOLS = (
     "ace_mi_create_on_device", "ace_mi_dit_get_info", "ace_mi_dit_forward_batched", "ace_mi_dit_sample",
     "ace_mi_profile_enable", "ace_mi_profile_reset", "ace_mi_profile_get", "ace_mi_probe_gemm",
     "ace_mi_synchronize", "ace_mi_kernel_gemm", "ace_mi_kernel_attention", "ace_mi_bench_gemm",
-    "ace_mi_gemm_variant", "ace_mi_quantize", "ace_mi_dequantize", "ace_mi_kernel_gemm_q", "ace_mi_bench_gemm_q",
+    "ace_mi_gemm_variant", "ace_ggml_load_vae", "ace_ggml_vae_get_info", "ace_ggml_vae_decode",
+    "ace_mi_vae_out_len", "ace_mi_vae_decode_device", "ace_mi_quantize", "ace_mi_dequantize", "ace_mi_kernel_gemm_q", "ace_mi_bench_gemm_q",
 )
 
 # qtype codes of ace_mi_quantize & co. (names as parse_quant_type, acestep_dit_model.cpp:27-37)
@@ -115,6 +116,16 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.ace_mi_gemm_variant.argtypes = [i32]
     lib.ace_mi_gemm_variant.restype = ctypes.c_int
     i64, u8p = ctypes.c_int64, ctypes.POINTER(ctypes.c_uint8)
+    lib.ace_ggml_load_vae.argtypes = [vp, ctypes.c_char_p]
+    lib.ace_ggml_load_vae.restype = ctypes.c_int
+    lib.ace_ggml_vae_get_info.argtypes = [vp, ip, ip, ip]
+    lib.ace_ggml_vae_get_info.restype = ctypes.c_int
+    lib.ace_ggml_vae_decode.argtypes = [vp, fp, i32, fp, sz]
+    lib.ace_ggml_vae_decode.restype = ctypes.c_int
+    lib.ace_mi_vae_out_len.argtypes = [vp, i32, ctypes.POINTER(i64)]
+    lib.ace_mi_vae_out_len.restype = ctypes.c_int
+    lib.ace_mi_vae_decode_device.argtypes = [vp, vp, i32, vp, vp]
+    lib.ace_mi_vae_decode_device.restype = ctypes.c_int
     lib.ace_mi_quantize.argtypes = [i32, fp, i64, i64, u8p, sz]
     lib.ace_mi_quantize.restype = ctypes.c_int64
     lib.ace_mi_dequantize.argtypes = [i32, u8p, i64, i64, fp]
@@ -157,6 +168,9 @@ class GGMLCAPIBridge:
         self._ensure_ok(st, "ace_ggml_create")
         atexit.register(self.close)
         self.info: Optional[AceMiDitInfo] = None
+        self.audio_channels = 0
+        self.hop_length = 0
+        self.latent_channels = 0
 
     # -- reference surface -------------------------------------------------
     def _last_error(self) -> str:
@@ -198,7 +212,36 @@ class GGMLCAPIBridge:
         self._ensure_ok(st, "ace_ggml_dit_forward")
         return out
 
+    def load_vae(self, model_dir) -> None:
+        """ace_ggml_load_vae + ace_ggml_vae_get_info (run_non_ggml_real_case.py:243-253)."""
+        self._ensure_ok(self.lib.ace_ggml_load_vae(self.ctx, str(model_dir).encode("utf-8")), "ace_ggml_load_vae")
+        lat, aud, hop = ctypes.c_int32(0), ctypes.c_int32(0), ctypes.c_int32(0)
+        st = self.lib.ace_ggml_vae_get_info(self.ctx, ctypes.byref(lat), ctypes.byref(aud), ctypes.byref(hop))
+        self._ensure_ok(st, "ace_ggml_vae_get_info")
+        self.latent_channels, self.audio_channels, self.hop_length = int(lat.value), int(aud.value), int(hop.value)
+
+    def vae_decode_tfirst(self, latents_tfirst) -> np.ndarray:
+        """latents [T, C] f32 -> audio [T*hop, channels] f32 (host buffers; :283-305)."""
+        if self.audio_channels <= 0 or self.hop_length <= 0:
+            raise RuntimeError("VAE not initialized in ggml bridge")
+        lat = np.ascontiguousarray(latents_tfirst, dtype=np.float32)
+        n_frames = int(lat.shape[0])
+        out_samples = n_frames * self.hop_length
+        out = np.empty((out_samples * self.audio_channels,), dtype=np.float32)
+        st = self.lib.ace_ggml_vae_decode(self.ctx, _fptr(lat), n_frames, _fptr(out), out.nbytes)
+        self._ensure_ok(st, "ace_ggml_vae_decode")
+        return out.reshape(out_samples, self.audio_channels)
+
     # -- MI355X extensions ---------------------------------------------------
+    def vae_out_len(self, n_frames: int) -> int:
+        n = ctypes.c_int64(0)
+        self._ensure_ok(self.lib.ace_mi_vae_out_len(self.ctx, int(n_frames), ctypes.byref(n)), "ace_mi_vae_out_len")
+        return int(n.value)
+
+    def vae_decode_device(self, d_latents: int, n_frames: int, d_out: int, stream: int = 0) -> None:
+        st = self.lib.ace_mi_vae_decode_device(self.ctx, d_latents, int(n_frames), d_out, stream or None)
+        self._ensure_ok(st, "ace_mi_vae_decode_device")
+
     def dit_forward_batched_device(self, batch: int, seq_len: int, enc_len: int, d_hidden: int, d_context: int,
                                    d_enc: int, d_mask: int, d_enc_mask: int, d_t: int, d_r: int, d_out: int,
                                    stream: int = 0) -> None:

@@ -111,3 +111,72 @@ def install_dit_backend(dit_handler: Any, bridge) -> None:
     decoder.forward = types.MethodType(decoder_forward_mi355x, decoder)
     setattr(dit_handler, "_ggml_dit_backend", "mi355x-capi")
     setattr(dit_handler, "_ggml_dit_decoder_forward_hooked", True)
+
+
+def _tile_plan(T: int, chunk_size: int, overlap: int):
+    """Windows of the reference tiled decode (run_non_ggml_real_case.py:597-611): returns
+    (stride, [(core_start, core_end, win_start, win_end)])."""
+    max_overlap = max(0, (chunk_size // 2) - 1)
+    if overlap > max_overlap:
+        overlap = max_overlap
+    stride = chunk_size - 2 * overlap
+    if stride <= 0:
+        overlap = max(0, chunk_size // 4)
+        stride = chunk_size - 2 * overlap
+        if stride <= 0:
+            stride, overlap = max(1, chunk_size), 0
+    steps = -(-T // stride)
+    plan = []
+    for i in range(steps):
+        cs = i * stride
+        ce = min(cs + stride, T)
+        plan.append((cs, ce, max(0, cs - overlap), min(T, ce + overlap)))
+    return plan
+
+
+def vae_decode_torch(bridge, latents_bct, chunk_size: int, overlap: int):
+    """latents [B, C, T] (ROCm tensor) -> audio [B, channels, samples] on the same device, decoding
+    each window with ace_mi_vae_decode_device on torch's current stream (no host round trip).
+    Windowing and trimming are those of the reference tiled decode, so outputs match it."""
+    import torch
+    B, C, T = latents_bct.shape
+    dev = latents_bct.device
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    lat = latents_bct.detach().to(torch.float32)
+    outs = []
+    plan = [(0, T, 0, T)] if T <= chunk_size else _tile_plan(T, chunk_size, overlap)
+    for b in range(B):
+        parts = []
+        for cs, ce, ws, we in plan:
+            win = lat[b, :, ws:we].transpose(0, 1).contiguous()        # [frames, C]
+            n = we - ws
+            wav = torch.empty((bridge.vae_out_len(n), bridge.audio_channels), dtype=torch.float32, device=dev)
+            bridge.vae_decode_device(win.data_ptr(), n, wav.data_ptr(), stream)
+            up = float(wav.shape[0]) / float(max(1, n))
+            ts = int(round((cs - ws) * up))
+            te = int(round((we - ce) * up))
+            parts.append(wav[ts:wav.shape[0] - te if te > 0 else wav.shape[0]])
+        outs.append(torch.cat(parts, dim=0).transpose(0, 1))            # [channels, samples]
+    return torch.stack(outs, dim=0)
+
+
+def install_vae_backend(dit_handler: Any, bridge, chunk_size_default: int = 32, overlap_default: int = 8) -> None:
+    """Replace dit_handler.tiled_decode (the `_install_ggml_vae_backend` seam,
+    scripts/run_non_ggml_real_case.py:541-659) with the MI355X VAE decoder."""
+
+    def tiled_decode_mi355x(self, latents, chunk_size=None, overlap=None, offload_wav_to_cpu=None):
+        import torch
+        if not isinstance(latents, torch.Tensor):
+            raise TypeError(f"latents must be torch.Tensor, got {type(latents)!r}")
+        if latents.dim() != 3:
+            raise ValueError(f"latents must have shape [B,C,T], got {tuple(latents.shape)}")
+        cs = int(chunk_size) if chunk_size is not None and int(chunk_size) > 0 else int(chunk_size_default)
+        ov = int(overlap) if overlap is not None else int(overlap_default)
+        x = latents if latents.is_cuda else latents.to("cuda")
+        out = vae_decode_torch(bridge, x, cs, max(0, ov))
+        if offload_wav_to_cpu is None and hasattr(self, "_should_offload_wav_to_cpu"):
+            offload_wav_to_cpu = self._should_offload_wav_to_cpu()
+        return out.cpu() if offload_wav_to_cpu else out
+
+    dit_handler.tiled_decode = types.MethodType(tiled_decode_mi355x, dit_handler)
+    setattr(dit_handler, "_ggml_vae_backend", "mi355x-capi")

@@ -147,3 +147,81 @@ def cached_checkpoint(cfg: dict, seed: int = 0, dtype: str = "BF16", root: str |
     if not os.path.exists(os.path.join(d, "model.safetensors")):
         write_checkpoint(d, cfg, seed=seed, dtype=dtype, backend=backend)
     return d
+
+
+# ----------------------------------------------------------------------------- VAE (Oobleck)
+# diffusers AutoencoderOobleck layout read by acestep_vae_model.cpp:760-955 (decoder.* only: the
+# MI355X engine implements decode; encode is out of scope this round).
+VAE_FULL_CONFIG = dict(audio_channels=2, encoder_hidden_size=128, decoder_channels=128, decoder_input_channels=64,
+                       sampling_rate=48000, downsampling_ratios=[2, 4, 4, 6, 10], channel_multiples=[1, 2, 4, 8, 16])
+VAE_TINY_CONFIG = dict(VAE_FULL_CONFIG, downsampling_ratios=[2, 3], channel_multiples=[1, 2])
+
+
+def vae_tensor_specs(cfg: dict) -> Iterator[Tuple[str, Tuple[int, ...], str]]:
+    """(name, shape, kind) of every decoder tensor; kind in {g, v, b, snake}."""
+    ch, lat, aud = cfg["decoder_channels"], cfg["decoder_input_channels"], cfg["audio_channels"]
+    strides = list(reversed(cfg["downsampling_ratios"]))
+    cm = [1] + list(cfg["channel_multiples"])
+    n = len(strides)
+
+    def conv(prefix, cout, cin, k, bias=True, transposed=False):
+        d0 = cin if transposed else cout
+        yield prefix + ".weight_g", (d0, 1, 1), "g"
+        yield prefix + ".weight_v", ((cin, cout, k) if transposed else (cout, cin, k)), "v"
+        if bias:
+            yield prefix + ".bias", (cout,), "b"
+
+    def snk(prefix, c):
+        yield prefix + ".alpha", (1, c, 1), "snake"
+        yield prefix + ".beta", (1, c, 1), "snake"
+
+    yield from conv("decoder.conv1", ch * cm[-1], lat, 7)
+    for i, s in enumerate(strides):
+        cin, cout = ch * cm[n - i], ch * cm[n - i - 1]
+        p = f"decoder.block.{i}"
+        yield from snk(p + ".snake1", cin)
+        yield from conv(p + ".conv_t1", cout, cin, 2 * s, transposed=True)
+        for j in range(3):
+            q = f"{p}.res_unit{j + 1}"
+            yield from snk(q + ".snake1", cout)
+            yield from conv(q + ".conv1", cout, cout, 7)
+            yield from snk(q + ".snake2", cout)
+            yield from conv(q + ".conv2", cout, cout, 1)
+    yield from snk("decoder.snake1", ch)
+    yield from conv("decoder.conv2", aud, ch, 7, bias=False)
+
+
+def write_vae_checkpoint(out_dir: str, cfg: dict, seed: int = 0, dtype: str = "F32") -> str:
+    """config.json + diffusion_pytorch_model.safetensors with weight-normed convs: weight_v ~ N(0,1),
+    weight_g ~ 0.6 + U(0, 0.4) (keeps activations O(1) through the residual stack), biases ~ N(0, 0.02),
+    snake alpha/beta ~ N(0, 0.1)."""
+    os.makedirs(out_dir, exist_ok=True)
+    with open(os.path.join(out_dir, "config.json"), "w", encoding="utf-8") as f:
+        json.dump(cfg, f, indent=1)
+    specs = list(vae_tensor_specs(cfg))
+    esz = {"BF16": 2, "F16": 2, "F32": 4}[dtype]
+    header: Dict[str, dict] = {}
+    off = 0
+    for name, shape, _ in specs:
+        nb = int(np.prod(shape)) * esz
+        header[name] = {"dtype": dtype, "shape": list(shape), "data_offsets": [off, off + nb]}
+        off += nb
+    hjson = json.dumps(header, separators=(",", ":")).encode("utf-8")
+    hjson += b" " * ((8 - len(hjson) % 8) % 8)
+    rng = np.random.default_rng(seed)
+    tmp = os.path.join(out_dir, "diffusion_pytorch_model.safetensors.tmp")
+    with open(tmp, "wb") as f:
+        f.write(struct.pack("<Q", len(hjson)))
+        f.write(hjson)
+        for name, shape, kind in specs:
+            if kind == "v":
+                v = rng.standard_normal(size=shape, dtype=np.float32)
+            elif kind == "g":
+                v = (np.float32(0.6) + np.float32(0.4) * rng.random(size=shape, dtype=np.float32))
+            elif kind == "b":
+                v = rng.standard_normal(size=shape, dtype=np.float32) * np.float32(0.02)
+            else:
+                v = rng.standard_normal(size=shape, dtype=np.float32) * np.float32(0.1)
+            f.write(_encode(v, dtype))
+    os.replace(tmp, os.path.join(out_dir, "diffusion_pytorch_model.safetensors"))
+    return out_dir

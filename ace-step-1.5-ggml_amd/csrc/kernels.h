@@ -123,4 +123,29 @@ void launch_out_mods(const float* out_table, const float* temb_t, const float* t
 // xt -= v * dt
 void launch_euler(float* xt, const float* v, int64_t n, float dt, hipStream_t s);
 
+// ------------------------------------------------------------ VAE decoder (kernels/vae.hip)
+// Implicit-GEMM conv on fp16 time-major activations.  A row (m, tap) = S[m + tap*dil - pad]
+// (zero row outside [0, T_in)); W [N][taps*Cin] fp16.  up == 1: conv, (m, n) -> (u = m, co = n);
+// up = s > 1: transposed conv, n = r*Cout + co -> u = s*m + r - crop.  Epilogue on v = acc + bias:
+// resid: v = X[u][co] + v; store_x: X[u][co] = v; S_out: S_out[u][co] = f16(snake(v)) (or f16(v)
+// when snake_ea is null).
+struct ConvGemmArgs {
+    const uint16_t* S = nullptr;
+    const uint16_t* zero = nullptr;
+    const uint16_t* W = nullptr;
+    int T_in = 0, Cin = 0, taps = 1, dil = 1, pad = 0;
+    int M = 0, N = 0;
+    const float* bias = nullptr;
+    int Cout = 0, up = 1, crop = 0, T_out = 0;
+    float* X = nullptr;
+    int resid = 0, store_x = 0;
+    uint16_t* S_out = nullptr;
+    const float* snake_ea = nullptr;
+    const float* snake_eb = nullptr;
+};
+void launch_conv_gemm(const ConvGemmArgs& a, hipStream_t s);
+void launch_to_f16(const float* x, int64_t n, uint16_t* y, hipStream_t s);
+// out[t][o] = sum_k sum_c W[o][k][c] * S[t + k - 3][c]   (kernel 7, pad 3, no bias), f32 out
+void launch_conv_out(const uint16_t* S, int T, int C, const uint16_t* W, int out_ch, float* out, hipStream_t s);
+
 }  // namespace acemi

@@ -108,7 +108,6 @@ __device__ __forceinline__ void wait_vmcnt() {
     static_assert(N >= 0 && N < 64, "vmcnt range");
     __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
 }
-__device__ __forceinline__ void wait_lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F); }
 
 // block -> tile: XCD-aware bijective remap (blocks b, b+8 share an XCD), then M-grouped order
 template <int BM, int BN>
@@ -384,68 +383,30 @@ __device__ __forceinline__ void ds_write_b128_v(uint32_t addr, uint32_t a, uint3
     asm volatile("ds_write_b128 %0, %1" : : "v"(addr), "v"(v) : "memory");
 }
 
-// Weight bytes are fetched with inline-asm loads the compiler does not track, so its waitcnt pass
-// cannot drain the whole queue (A's LDS-DMA included) with vmcnt(0) at the loop-carried use; the
-// kernel retires them with a counted vmcnt that also pins the registers (wait_w).
-typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
-__device__ __forceinline__ u32x4 gload_b128(const void* p) {
-    u32x4 v;
-    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p));
-    return v;
-}
-__device__ __forceinline__ u32x2 gload_b64(const void* p) {
-    u32x2 v;
-    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p));
-    return v;
-}
-__device__ __forceinline__ float gload_b32(const void* p) {
-    float v;
-    asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(p));
-    return v;
-}
-
-// vector-memory instructions issued per load_wq
-template <int WQ>
-constexpr int w_ops() { return WQ == WF_Q4_K ? 2 : 3; }
-
+// Weight bytes are plain (compiler-tracked) loads issued one k-tile ahead; the loop consumes them
+// BEFORE it issues the next A DMA, so the vmcnt the compiler places at that use only drains what
+// must have landed by the end of the iteration anyway (tile kt+1's A, issued earlier).
 template <int WQ>
 __device__ __forceinline__ WRaw load_wq(const char* qbase, const float* sbase, int kt) {
     WRaw r;
     if constexpr (WQ == WF_Q4_K) {
-        r.q0 = gload_b128(qbase + kt * 32);
-        const u32x2 sm = gload_b64(sbase + kt * 4);
-        r.s0 = __uint_as_float(sm[0]);
-        r.s1 = __uint_as_float(sm[1]);
+        r.q0 = *(const u32x4*)(qbase + kt * 32);
+        const float2 sm = *(const float2*)(sbase + kt * 4);
+        r.s0 = sm.x;
+        r.s1 = sm.y;
     } else {
-        r.q0 = gload_b128(qbase + kt * 64);
-        r.q1 = gload_b128(qbase + kt * 64 + 16);
+        r.q0 = *(const u32x4*)(qbase + kt * 64);
+        r.q1 = *(const u32x4*)(qbase + kt * 64 + 16);
         if constexpr (WQ == WF_Q8_0) {
-            r.s0 = gload_b32(sbase + kt * 2);
+            r.s0 = sbase[kt * 2];
             r.s1 = r.s0;
         } else {
-            const u32x2 sc = gload_b64(sbase + kt * 4);
-            r.s0 = __uint_as_float(sc[0]);
-            r.s1 = __uint_as_float(sc[1]);
+            const float2 sc = *(const float2*)(sbase + kt * 4);
+            r.s0 = sc.x;
+            r.s1 = sc.y;
         }
     }
     return r;
-}
-
-// s_waitcnt vmcnt(N) that the registers of `r` depend on (no consumer can be hoisted above it)
-template <int WQ, int N>
-__device__ __forceinline__ void wait_w(WRaw& r) {
-    static_assert(N >= 0 && N < 16, "vmcnt range");
-    if constexpr (WQ == WF_Q4_K) {
-        uint32_t s0 = __float_as_uint(r.s0), s1 = __float_as_uint(r.s1);
-        asm volatile("s_waitcnt vmcnt(%3)" : "+v"(r.q0), "+v"(s0), "+v"(s1) : "i"(N));
-        r.s0 = __uint_as_float(s0);
-        r.s1 = __uint_as_float(s1);
-    } else {
-        uint32_t s0 = __float_as_uint(r.s0), s1 = __float_as_uint(r.s1);
-        asm volatile("s_waitcnt vmcnt(%4)" : "+v"(r.q0), "+v"(r.q1), "+v"(s0), "+v"(s1) : "i"(N));
-        r.s0 = __uint_as_float(s0);
-        r.s1 = __uint_as_float(s1);
-    }
 }
 
 // signed bytes of w (k order b0..b3) * s, via the unsigned-byte converts: (u - 128) * s = fma(u, s, -128 s)
@@ -578,20 +539,17 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_q_kernel(GemmParams p) {
         lds_wait_all();
     };
 
-    constexpr int WOPS = w_ops<WQ>();
     // prologue: tiles 0 and 1 complete in LDS, W(min(2, nk-1)) requested
     WRaw wnext = load_wq<WQ>(qbase, sbase, 0);
     stage_a(0, 0);
-    wait_w<WQ, G_A>(wnext);
     dequant_store<WQ>(wnext, lds0 + wrow_off, wh, wsw);
     if (nk > 1) {
         wnext = load_wq<WQ>(qbase, sbase, 1);
         stage_a(1, 1);
-        wait_w<WQ, G_A>(wnext);
         dequant_store<WQ>(wnext, lds0 + STAGE + wrow_off, wh, wsw);
     }
     wnext = load_wq<WQ>(qbase, sbase, min(2, nk - 1));
-    wait_vmcnt<WOPS>();  // A(0), A(1) landed
+    wait_vmcnt<0>();
     lds_wait_all();
     __builtin_amdgcn_s_barrier();
 
@@ -613,9 +571,9 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_q_kernel(GemmParams p) {
         read_frags_asm(cur, a, b);
         mfma_half(a, b, 0);
         __builtin_amdgcn_s_barrier();  // every wave holds its fragments of tile kt: buffer `cur` is free
-        stage_a(cur, min(kt + 2, nk - 1));
-        wait_w<WQ, G_A>(wnext);        // W(kt+2) bytes, and the older A(kt+1) DMA, have landed
+        // W(kt+2): waiting for its bytes also retires the older A(kt+1) DMA
         dequant_store<WQ>(wnext, lds0 + cur * STAGE + wrow_off, wh, wsw);
+        stage_a(cur, min(kt + 2, nk - 1));
         wnext = load_wq<WQ>(qbase, sbase, min(kt + 3, nk - 1));
         mfma_half(a, b, TM / 2);
         __builtin_amdgcn_s_barrier();

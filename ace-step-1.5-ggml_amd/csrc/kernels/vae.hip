@@ -1,0 +1,290 @@
+// Oobleck VAE decoder kernels (gfx950): the conv stack of ace_vae::forward_decode
+// (acestep_ggml/cpp/acestep_vae_model.cpp:682-742,957-1002) as implicit-GEMM fp16 MFMA.
+//
+// ggml runs every decoder conv as F16 x F16 with f32 accumulation (im2col to F16 for
+// ggml_conv_1d; the F16 kernel and an F16 copy of the input for ggml_conv_transpose_1d), so
+// v_mfma_f32_16x16x32_f16 reproduces its arithmetic: exact products, f32 sums.
+//
+// Layout: activations time-major [T][C] (channel-contiguous rows).  A conv with taps k and
+// dilation d is a GEMM over K = taps*Cin whose A row for output t and tap k is the input row
+// t + k*d - pad (a shifted view, or a zero row at the edges), staged into LDS by LDS-DMA exactly
+// like the DiT GEMM.  A ConvTranspose1d with kernel 2s, stride s is ONE GEMM too: output time
+// u = s*j + r takes input rows j (kernel tap r) and j-1 (tap r+s), so with N = s*Cout columns
+// (r, co) the GEMM's row-major output IS the [T_out][Cout] layout, shifted by the center crop.
+// Epilogues fuse what follows each conv in the graph: bias, the residual add, the f32 store of
+// the running activation, and the NEXT Snake (x + sin^2(e^a x)/e^b, f32) written as the fp16
+// operand of the next conv.
+#include <cmath>
+
+#include "../kernels.h"
+#include "lds_asm.h"
+
+namespace acemi {
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+__device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
+
+__device__ __forceinline__ uint16_t f32_to_f16(float f) {
+    _Float16 h = (_Float16)f;
+    return __builtin_bit_cast(uint16_t, h);
+}
+
+// snake_forward (:682-692) with ea = exp(alpha), eb = exp(beta) precomputed on the host (expf)
+__device__ __forceinline__ float snake_f(float x, float ea, float eb) {
+    float s = sinf(__fmul_rn(ea, x));
+    s = __fmul_rn(s, s);
+    s = __fdiv_rn(s, eb);
+    return __fadd_rn(x, s);
+}
+
+template <int I, int N, int STRIDE>
+struct ReadRows {
+    __device__ __forceinline__ static void run(uint32_t base, uint4 (&dst)[N][2], int kk) {
+        if (kk == 0)
+            dst[I][0] = ds_read_b128_at<I * STRIDE>(base);
+        else
+            dst[I][1] = ds_read_b128_at<I * STRIDE>(base);
+        ReadRows<I + 1, N, STRIDE>::run(base, dst, kk);
+    }
+};
+template <int N, int STRIDE>
+struct ReadRows<N, N, STRIDE> {
+    __device__ __forceinline__ static void run(uint32_t, uint4 (&)[N][2], int) {}
+};
+
+__global__ void __launch_bounds__(256) conv_gemm_kernel(ConvGemmArgs p) {
+    constexpr int BM = 128, BN = 128, WM = 2, WN = 2, NW = 4;
+    constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
+    constexpr int BK = 64, ROWB = BK * 2, STAGE = (BM + BN) * ROWB;
+    constexpr int G_PER_WAVE = (BM + BN) / 8 / NW;  // 8
+
+    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+
+    // block -> tile: XCD-aware bijective remap, then M-grouped order
+    const int nbm = (p.M + BM - 1) / BM;
+    const int nbn = p.N / BN;
+    int bid = blockIdx.x;
+    {
+        const int nwg = gridDim.x, xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    }
+    constexpr int GM = 8;
+    const int group = bid / (GM * nbn);
+    const int first_m = group * GM;
+    const int gm = min(nbm - first_m, GM);
+    const int m0 = (first_m + (bid % (GM * nbn)) % gm) * BM;
+    const int n0 = ((bid % (GM * nbn)) / gm) * BN;
+    const int wm0 = (wid / WN) * WTM, wn0 = (wid % WN) * WTN;
+
+    const int cblocks = p.Cin / BK;
+    const int nk = p.taps * cblocks;
+    const int K = p.taps * p.Cin;
+
+    // per-lane staging rows (fixed) and swizzled 16-byte chunk
+    int srow[G_PER_WAVE];
+    int schunk[G_PER_WAVE];
+#pragma unroll
+    for (int j = 0; j < G_PER_WAVE; ++j) {
+        const int row = (wid + NW * j) * 8 + (lane >> 3);
+        srow[j] = row;
+        schunk[j] = (lane & 7) ^ swz(row);
+    }
+    auto stage = [&](int buf, int kt) {
+        char* base = smem + buf * STAGE;
+        const int tap = kt / cblocks;
+        const int c0 = (kt - tap * cblocks) * BK;
+        const int shift = tap * p.dil - p.pad;
+#pragma unroll
+        for (int j = 0; j < G_PER_WAVE; ++j) {
+            const int row = srow[j];
+            const uint16_t* src;
+            if (row < BM) {
+                const int m = m0 + row;
+                const int t = m + shift;
+                src = (m < p.M && t >= 0 && t < p.T_in) ? p.S + (int64_t)t * p.Cin + c0 + schunk[j] * 8
+                                                        : p.zero + schunk[j] * 8;
+            } else {
+                src = p.W + (int64_t)(n0 + row - BM) * K + kt * BK + schunk[j] * 8;
+            }
+            __builtin_amdgcn_global_load_lds((const void*)src,
+                                             (__attribute__((address_space(3))) void*)(base + (wid + NW * j) * 1024),
+                                             16, 0, 0);
+        }
+    };
+
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const uint32_t lds0 = lds_addr(smem);
+    const int lrow = lane & 15, lchunk = lane >> 4;
+    auto read_frags = [&](int buf, uint4 (&a)[TM][2], uint4 (&b)[TN][2]) {
+        const uint32_t sb = lds0 + buf * STAGE;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int ch = (kk * 4 + lchunk) ^ ((lrow >> 1) & 7);
+            ReadRows<0, TN, 16 * ROWB>::run(sb + BM * ROWB + (wn0 + lrow) * ROWB + ch * 16, b, kk);
+            ReadRows<0, TM, 16 * ROWB>::run(sb + (wm0 + lrow) * ROWB + ch * 16, a, kk);
+        }
+        lds_wait_all();
+    };
+    auto mma = [&](const uint4 (&a)[TM][2], const uint4 (&b)[TN][2], int i0) {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int i = i0; i < i0 + TM / 2; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a[i][kk]),
+                                                                       __builtin_bit_cast(f16x8, b[j][kk]),
+                                                                       acc[i][j], 0, 0, 0);
+    };
+
+    // PIPE-1 schedule of the DiT GEMM (gemm.hip): fragments read up front, raw barrier frees the
+    // buffer, tile kt+2 staged during the second half, counted vmcnt retires kt+1.
+    stage(0, 0);
+    if (nk > 1) {
+        stage(1, 1);
+        wait_vmcnt<G_PER_WAVE>();
+    } else {
+        wait_vmcnt<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        uint4 a[TM][2], b[TN][2];
+        read_frags(cur, a, b);
+        mma(a, b, 0);
+        __builtin_amdgcn_s_barrier();
+        const bool more = kt + 2 < nk;
+        if (more) stage(cur, kt + 2);
+        mma(a, b, TM / 2);
+        if (kt + 1 < nk) {
+            if (more)
+                wait_vmcnt<G_PER_WAVE>();
+            else
+                wait_vmcnt<0>();
+            __builtin_amdgcn_s_barrier();
+        }
+    }
+
+    // epilogue: (m, n) -> output time u and channel co; bias, residual, store, next Snake
+    const int ccol = lane & 15, crow = (lane >> 4) * 4;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int m = m0 + wm0 + i * 16 + crow + r;
+            if (m >= p.M) continue;
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int n = n0 + wn0 + j * 16 + ccol;
+                int u, co;
+                if (p.up > 1) {
+                    const int rr = n / p.Cout;
+                    co = n - rr * p.Cout;
+                    u = m * p.up + rr - p.crop;
+                } else {
+                    co = n;
+                    u = m;
+                }
+                if (u < 0 || u >= p.T_out) continue;
+                float v = acc[i][j][r];
+                if (p.bias) v = __fadd_rn(v, p.bias[co]);
+                const int64_t o = (int64_t)u * p.Cout + co;
+                if (p.resid) v = __fadd_rn(p.X[o], v);
+                if (p.store_x) p.X[o] = v;
+                if (p.S_out) p.S_out[o] = f32_to_f16(p.snake_ea ? snake_f(v, p.snake_ea[co], p.snake_eb[co]) : v);
+            }
+        }
+    }
+}
+
+// f32 -> fp16 copy (the latents' im2col conversion of decoder.conv1)
+__global__ void to_f16_kernel(const float* __restrict__ x, int64_t n, uint16_t* __restrict__ y) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        y[i] = f32_to_f16(x[i]);
+}
+
+// decoder.conv2: C -> out_ch (2), kernel 7, pad 3, no bias, on the fp16 Snake output.  Too narrow
+// for MFMA tiles: one thread per output time, the 7 input rows read as 16-byte vectors (shared
+// through L1/L2 by neighbouring threads), weights staged in LDS; f32 accumulation of exact
+// fp16 products.
+template <int OUT>
+__global__ void __launch_bounds__(256) conv_out_kernel(const uint16_t* __restrict__ S, int T, int C,
+                                                       const uint16_t* __restrict__ W, float* __restrict__ out) {
+    extern __shared__ float wsh[];  // [7][C][OUT] as f32
+    for (int i = threadIdx.x; i < 7 * C * OUT; i += blockDim.x) {
+        const int o = i % OUT, c = (i / OUT) % C, k = i / (OUT * C);
+        wsh[i] = (float)__builtin_bit_cast(_Float16, W[((int64_t)o * 7 + k) * C + c]);
+    }
+    __syncthreads();
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    float acc[OUT];
+#pragma unroll
+    for (int o = 0; o < OUT; ++o) acc[o] = 0.f;
+    for (int k = 0; k < 7; ++k) {
+        const int ti = t + k - 3;
+        if (ti < 0 || ti >= T) continue;
+        const uint4* row = (const uint4*)(S + (int64_t)ti * C);
+        for (int c8 = 0; c8 < C / 8; ++c8) {
+            const uint4 v = row[c8];
+            const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+                const float x0 = (float)__builtin_bit_cast(_Float16, (uint16_t)(w4[h] & 0xffffu));
+                const float x1 = (float)__builtin_bit_cast(_Float16, (uint16_t)(w4[h] >> 16));
+                const int c = c8 * 8 + 2 * h;
+#pragma unroll
+                for (int o = 0; o < OUT; ++o) {
+                    acc[o] = fmaf(x0, wsh[(k * C + c) * OUT + o], acc[o]);
+                    acc[o] = fmaf(x1, wsh[(k * C + c + 1) * OUT + o], acc[o]);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int o = 0; o < OUT; ++o) out[(int64_t)t * OUT + o] = acc[o];
+}
+
+}  // namespace
+
+void launch_conv_gemm(const ConvGemmArgs& a, hipStream_t s) {
+    ACEMI_CHECK(a.Cin % 64 == 0 && a.N % 128 == 0 && a.M >= 1 && a.taps >= 1, "conv_gemm: unsupported shape");
+    ACEMI_CHECK(a.S && a.W && a.zero, "conv_gemm: null operand");
+    ACEMI_CHECK(a.up <= 1 || a.N == a.up * a.Cout, "conv_gemm: transposed conv needs N = stride * Cout");
+    ACEMI_CHECK(a.up > 1 || a.N == a.Cout, "conv_gemm: N must equal Cout");
+    ACEMI_CHECK(!(a.resid || a.store_x) || a.X, "conv_gemm: null X");
+    const int nbm = (a.M + 127) / 128, nbn = a.N / 128;
+    hipLaunchKernelGGL(conv_gemm_kernel, dim3(nbm * nbn), dim3(256), 0, s, a);
+    ACEMI_HIP(hipGetLastError());
+}
+
+void launch_to_f16(const float* x, int64_t n, uint16_t* y, hipStream_t s) {
+    const int grid = (int)std::min<int64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(to_f16_kernel, dim3(std::max(grid, 1)), dim3(256), 0, s, x, n, y);
+    ACEMI_HIP(hipGetLastError());
+}
+
+void launch_conv_out(const uint16_t* S, int T, int C, const uint16_t* W, int out_ch, float* out, hipStream_t s) {
+    ACEMI_CHECK(C % 8 == 0, "conv_out: channels must be a multiple of 8");
+    const size_t shm = (size_t)7 * C * out_ch * 4;
+    ACEMI_CHECK(shm <= 64 * 1024, "conv_out: weights do not fit LDS");
+    const dim3 grid((T + 255) / 256);
+    if (out_ch == 1)
+        hipLaunchKernelGGL(conv_out_kernel<1>, grid, dim3(256), shm, s, S, T, C, W, out);
+    else if (out_ch == 2)
+        hipLaunchKernelGGL(conv_out_kernel<2>, grid, dim3(256), shm, s, S, T, C, W, out);
+    else
+        throw std::runtime_error("conv_out: audio_channels must be 1 or 2");
+    ACEMI_HIP(hipGetLastError());
+}
+
+}  // namespace acemi

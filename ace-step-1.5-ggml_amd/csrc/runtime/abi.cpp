@@ -13,6 +13,7 @@
 
 #include "../../../include/acestep_mi355x.h"
 #include "engine.h"
+#include "vae.h"
 
 struct ace_ggml_context {
     int32_t n_threads = 0;
@@ -22,6 +23,9 @@ struct ace_ggml_context {
     int device = -1;
     hipStream_t stream = nullptr;
     std::unique_ptr<acemi::DitEngine> dit;
+    std::unique_ptr<acemi::VaeEngine> vae;
+    void* d_vae = nullptr;  // host-ABI staging for ace_ggml_vae_decode
+    size_t d_vae_bytes = 0;
     // host-ABI staging (device)
     void* d_in = nullptr;
     size_t d_in_bytes = 0;
@@ -114,6 +118,8 @@ void ace_ggml_destroy(ace_ggml_context* ctx) {
     if (ctx->device >= 0) (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     ctx->dit.reset();
+    ctx->vae.reset();
+    if (ctx->d_vae) (void)hipFree(ctx->d_vae);
     if (ctx->d_in) (void)hipFree(ctx->d_in);
     if (ctx->d_v) (void)hipFree(ctx->d_v);
     if (ctx->d_sched) (void)hipFree(ctx->d_sched);
@@ -385,6 +391,107 @@ ace_ggml_status ace_mi_synchronize(ace_ggml_context* ctx) {
         }
     } catch (const std::exception& e) {
         return set_error(ctx, ACE_GGML_ERR, e.what());
+    }
+    return ACE_GGML_OK;
+}
+
+}  // extern "C"
+
+extern "C" {
+
+// ------------------------------------------------------------------ VAE decoder
+// ace_ggml_load_vae / vae_get_info / vae_decode (acestep_ggml.cpp:545-974, acestep_ggml.h:44-55)
+ace_ggml_status ace_ggml_load_vae(ace_ggml_context* ctx, const char* model_dir) {
+    if (!ctx || !model_dir) return ACE_GGML_ERR_INVALID_ARG;
+    int hint = 3;
+    try {
+        bind_device(ctx);
+        ACEMI_HIP(hipStreamSynchronize(ctx->stream));
+        ctx->vae.reset();
+        auto eng = std::make_unique<acemi::VaeEngine>(ctx->device);
+        acemi::load_vae_model(model_dir, eng->model(), hint);
+        ctx->vae = std::move(eng);
+    } catch (const acemi::HipError& e) {
+        ctx->vae.reset();
+        return set_error(ctx, ACE_GGML_ERR, e.what());
+    } catch (const std::exception& e) {
+        ctx->vae.reset();
+        return set_error(ctx, hint == 4 ? ACE_GGML_ERR_UNSUPPORTED : (hint == 1 ? ACE_GGML_ERR : ACE_GGML_ERR_IO),
+                         e.what());
+    }
+    return ACE_GGML_OK;
+}
+
+ace_ggml_status ace_ggml_vae_get_info(ace_ggml_context* ctx, int32_t* latent_channels, int32_t* audio_channels,
+                                      int32_t* hop_length) {
+    if (!ctx) return ACE_GGML_ERR_INVALID_ARG;
+    if (!ctx->vae) return set_error(ctx, ACE_GGML_ERR, "vae not loaded");
+    const auto& c = ctx->vae->model().cfg;
+    if (latent_channels) *latent_channels = c.decoder_input_channels;
+    if (audio_channels) *audio_channels = c.audio_channels;
+    if (hop_length) *hop_length = c.hop_length;
+    return ACE_GGML_OK;
+}
+
+ace_ggml_status ace_ggml_vae_decode(ace_ggml_context* ctx, const float* latents, int32_t n_frames, float* out,
+                                    size_t out_size) {
+    if (!ctx || !latents || !out || n_frames <= 0) return ACE_GGML_ERR_INVALID_ARG;
+    if (!ctx->vae) return set_error(ctx, ACE_GGML_ERR, "vae not loaded");
+    const auto& c = ctx->vae->model().cfg;
+    const size_t expected = (size_t)n_frames * (size_t)c.hop_length * (size_t)c.audio_channels * sizeof(float);
+    if (out_size < expected) return set_error(ctx, ACE_GGML_ERR_INVALID_ARG, "output buffer too small");
+    const bool profile = env_enabled("ACE_GGML_VAE_PROFILE");
+    try {
+        const auto t0 = std::chrono::steady_clock::now();
+        bind_device(ctx);
+        hipStream_t s = ctx->stream;
+        const int64_t out_len = ctx->vae->out_len(n_frames);
+        const size_t needed = (size_t)out_len * (size_t)c.audio_channels * sizeof(float);
+        if (out_size < needed) return set_error(ctx, ACE_GGML_ERR_INVALID_ARG, "output buffer too small for actual output");
+        const size_t n_in = (size_t)n_frames * c.decoder_input_channels * sizeof(float);
+        const size_t o_out = (n_in + 255) & ~size_t(255);
+        ensure_dev(ctx->d_vae, ctx->d_vae_bytes, o_out + needed);
+        char* base = static_cast<char*>(ctx->d_vae);
+        ACEMI_HIP(hipMemcpyAsync(base, latents, n_in, hipMemcpyHostToDevice, s));
+        ACEMI_HIP(hipStreamSynchronize(s));
+        const auto t1 = std::chrono::steady_clock::now();
+        ctx->vae->decode(reinterpret_cast<const float*>(base), n_frames, reinterpret_cast<float*>(base + o_out), s);
+        ACEMI_HIP(hipStreamSynchronize(s));
+        const auto t2 = std::chrono::steady_clock::now();
+        ACEMI_HIP(hipMemcpyAsync(out, base + o_out, needed, hipMemcpyDeviceToHost, s));
+        ACEMI_HIP(hipStreamSynchronize(s));
+        const auto t3 = std::chrono::steady_clock::now();
+        if (profile) {
+            using ms = std::chrono::duration<double, std::milli>;
+            std::fprintf(stderr,
+                         "ace_ggml_vae_decode profile: backend=mi355x frames=%d out_len=%lld device=%d upload_ms=%.3f "
+                         "compute_ms=%.3f copy_ms=%.3f total_ms=%.3f\n",
+                         n_frames, (long long)out_len, ctx->device, ms(t1 - t0).count(), ms(t2 - t1).count(),
+                         ms(t3 - t2).count(), ms(t3 - t0).count());
+        }
+    } catch (const std::exception& e) {
+        return set_error(ctx, ACE_GGML_ERR, std::string("graph compute failed: ") + e.what());
+    }
+    return ACE_GGML_OK;
+}
+
+ace_ggml_status ace_mi_vae_out_len(ace_ggml_context* ctx, int32_t n_frames, int64_t* out_len) {
+    if (!ctx || !out_len || n_frames <= 0) return ACE_GGML_ERR_INVALID_ARG;
+    if (!ctx->vae) return set_error(ctx, ACE_GGML_ERR, "vae not loaded");
+    *out_len = ctx->vae->out_len(n_frames);
+    return ACE_GGML_OK;
+}
+
+ace_ggml_status ace_mi_vae_decode_device(ace_ggml_context* ctx, const float* d_latents, int32_t n_frames, float* d_out,
+                                         void* stream) {
+    if (!ctx || !d_latents || !d_out || n_frames <= 0) return ACE_GGML_ERR_INVALID_ARG;
+    if (!ctx->vae) return set_error(ctx, ACE_GGML_ERR, "vae not loaded");
+    try {
+        bind_device(ctx);
+        hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+        ctx->vae->decode(d_latents, n_frames, d_out, s);
+    } catch (const std::exception& e) {
+        return set_error(ctx, ACE_GGML_ERR, std::string("graph compute failed: ") + e.what());
     }
     return ACE_GGML_OK;
 }

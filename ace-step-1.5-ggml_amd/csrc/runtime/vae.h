@@ -1,0 +1,85 @@
+// Oobleck VAE decoder resident in HBM + decode orchestration (ace_vae::forward_decode,
+// acestep_ggml/cpp/acestep_vae_model.cpp:957-1002, loaded like load_model_from_dir :760-955).
+//
+// Weights: weight-norm folded at load exactly as load_conv_weight_norm (:520-588) and stored
+// fp16 in the implicit-GEMM layouts of kernels/vae.hip:
+//   conv (k taps):      W [Cout][k][Cin]          (K index = tap*Cin + ci)
+//   conv_t (2s, s):     W [s*Cout][2][Cin]         W[r*Cout+co][tap*Cin+ci] = w[ci][co][r + tap*s]
+// Snake parameters as exp(alpha), exp(beta) (expf on the host, as ggml_exp does on the CPU).
+#pragma once
+
+#include <string>
+#include <vector>
+
+#include "../common.h"
+#include "../kernels.h"
+
+namespace acemi {
+
+struct VaeConfig {
+    int audio_channels = 2, encoder_hidden_size = 128, decoder_channels = 128, decoder_input_channels = 64;
+    int sampling_rate = 48000;
+    std::vector<int> downsampling_ratios, upsampling_ratios, channel_multiples;
+    int hop_length = 1;
+};
+
+struct VaeConv {
+    uint16_t* w = nullptr;
+    float* b = nullptr;
+    int cin = 0, cout = 0, taps = 1, dil = 1, pad = 0, stride = 1;
+    bool transposed = false;
+};
+struct VaeSnake {
+    float* ea = nullptr;
+    float* eb = nullptr;
+    int C = 0;
+};
+struct VaeRes {
+    VaeSnake s1, s2;
+    VaeConv c1, c2;
+    int dil = 1;
+};
+struct VaeBlock {
+    VaeSnake s1;
+    VaeConv ct;
+    VaeRes res[3];
+    int stride = 1;
+};
+
+struct VaeModel {
+    VaeConfig cfg;
+    VaeConv conv1;
+    std::vector<VaeBlock> blocks;
+    VaeSnake snake1;
+    VaeConv conv2;
+    std::vector<void*> allocs;
+    size_t weight_bytes = 0;
+    ~VaeModel();
+};
+
+// Throws std::runtime_error; status_hint 3 (IO) / 4 (UNSUPPORTED) / 1 (ERR).
+void load_vae_model(const std::string& dir, VaeModel& m, int& status_hint);
+
+class VaeEngine {
+public:
+    explicit VaeEngine(int device) : device_(device) {}
+    ~VaeEngine();
+    VaeModel& model() { return model_; }
+    // samples produced for n_frames latent frames (= n_frames * hop for even strides; PyTorch
+    // ConvTranspose1d lengths for odd ones)
+    int64_t out_len(int n_frames) const;
+    // latents [n_frames][latent_channels] f32 -> out [out_len][audio_channels] f32, device pointers
+    void decode(const float* d_latents, int n_frames, float* d_out, hipStream_t s);
+
+private:
+    struct Buf {
+        void* p = nullptr;
+        size_t bytes = 0;
+    };
+    void ensure(Buf& b, size_t bytes);
+    int device_;
+    VaeModel model_;
+    Buf x_, sa_, sb_, sc_, lat_, zero_;
+};
+
+}  // namespace acemi

@@ -13,6 +13,9 @@
  *   ace_ggml_last_error                      acestep_ggml/cpp/acestep_ggml.h:39
  *   ace_ggml_load_dit                        acestep_ggml/cpp/acestep_ggml.h:43
  *   ace_ggml_dit_forward                     acestep_ggml/cpp/acestep_ggml.h:96-108
+ *   ace_ggml_load_vae                        acestep_ggml/cpp/acestep_ggml.h:44
+ *   ace_ggml_vae_get_info                    acestep_ggml/cpp/acestep_ggml.h:45-49
+ *   ace_ggml_vae_decode                      acestep_ggml/cpp/acestep_ggml.h:50-55
  *
  * Semantics: host f32 row-major, time-major buffers; one sample
  * per call; the caller owns every buffer; blocking; one context is not
@@ -61,6 +64,15 @@ ACE_GGML_API ace_ggml_status ace_ggml_dit_forward(ace_ggml_context* ctx, const f
                                                   const int32_t* encoder_attention_mask, int32_t seq_len,
                                                   int32_t enc_len, float timestep, float timestep_r, float* out,
                                                   size_t out_size);
+
+/* Oobleck VAE decoder (diffusion_pytorch_model.safetensors + config.json).  Decode: latents
+ * [n_frames][latent_channels] f32 -> audio [n_frames*hop][audio_channels] f32 interleaved;
+ * INVALID_ARG "output buffer too small" if out_size < n_frames*hop*audio_channels*4. */
+ACE_GGML_API ace_ggml_status ace_ggml_load_vae(ace_ggml_context* ctx, const char* model_dir);
+ACE_GGML_API ace_ggml_status ace_ggml_vae_get_info(ace_ggml_context* ctx, int32_t* latent_channels,
+                                                   int32_t* audio_channels, int32_t* hop_length);
+ACE_GGML_API ace_ggml_status ace_ggml_vae_decode(ace_ggml_context* ctx, const float* latents, int32_t n_frames,
+                                                 float* out, size_t out_size);
 
 #ifdef __cplusplus
 }

@@ -100,6 +100,12 @@ ACE_GGML_API ace_ggml_status ace_mi_bench_gemm(int32_t act_type, int32_t epi, in
 /* Force the GEMM kernel variant of all later launches in this process (-1 = automatic). */
 ACE_GGML_API ace_ggml_status ace_mi_gemm_variant(int32_t variant);
 
+/* VAE decode on device pointers, stream-ordered: latents [n_frames][latent_channels] f32 ->
+ * out [out_len][audio_channels] f32 (out_len from ace_mi_vae_out_len: n_frames*hop for even strides). */
+ACE_GGML_API ace_ggml_status ace_mi_vae_out_len(ace_ggml_context* ctx, int32_t n_frames, int64_t* out_len);
+ACE_GGML_API ace_ggml_status ace_mi_vae_decode_device(ace_ggml_context* ctx, const float* d_latents,
+                                                      int32_t n_frames, float* d_out, void* stream);
+
 /* ggml block quantization (qtype 1 = Q8_0, 2 = Q4_K, 3 = Q6_K) with the encoders the loader uses for
  * ACE_GGML_DIT_WEIGHT_QTYPE (try_quantize_matrix, acestep_dit_model.cpp:156-192): rows x cols f32 ->
  * ggml block bytes.  Returns the byte count written, or -1 (bad type / cols % block / dst too small). */

@@ -1,0 +1,195 @@
+"""numpy restatement of the Oobleck VAE decoder (`ace_vae::forward_decode`) — TEST INFRASTRUCTURE
+ONLY (see oracle/__init__.py).
+
+Follows `acestep_ggml/cpp/acestep_vae_model.cpp`:
+  * config (`load_config` :55-125): upsampling_ratios = reversed(downsampling_ratios),
+    hop_length = prod(downsampling_ratios);
+  * weight-norm fold at load (`load_conv_weight_norm` :520-588): per slice i of dim 0,
+    ss = sum(v^2) in double, scale = g_i / sqrtf((float)ss + 1e-12f), w = v * scale, stored F16
+    (conv_t too, unless ACE_GGML_VAE_TRANSPOSE_CONV_F32);
+  * snake (`snake_forward` :682-692): x + sin(exp(alpha) * x)^2 / exp(beta), all f32 (no 1e-9);
+  * conv (`conv_forward` :694-712): ggml_conv_1d = im2col to F16 + F16 mul_mat with f32
+    accumulation; ggml_conv_transpose_1d with p0 = 0 (input rounded to F16, f32 accumulation),
+    then a center crop to the PyTorch output length; bias added after;
+  * residual unit (:724-733), decoder block (:735-742), decode (:957-1002): latents
+    [T][64] -> audio [T*hop][audio_channels] (`ace_ggml_vae_decode` returns it time-major,
+    acestep_ggml.cpp:936-940).
+Parity: ggml cannot be built here -> parity unpinned against real ggml; the Snake
+form is cross-checked against `acestep/mlx_vae/model.py:24-56` (which adds 1e-9 to beta; the
+ggml path does not).
+"""
+from __future__ import annotations
+
+import json
+import os
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from .dit_oracle import read_safetensors
+from .ggml_numerics import round_f16
+
+
+# Test-only knob (as ggml_numerics.MULMAT_PERTURB): relative perturbation of every conv result, used
+# to measure the decoder's own sensitivity to f32 summation order (fp16 re-rounding of every conv
+# input amplifies it) -- the floor two correct implementations agree to.
+CONV_PERTURB = 0.0
+
+
+def _perturb(y):
+    if CONV_PERTURB:
+        return (y.astype(np.float64) * (1.0 + CONV_PERTURB)).astype(np.float32)
+    return y
+
+
+@dataclass
+class VaeConfig:
+    audio_channels: int
+    decoder_channels: int
+    decoder_input_channels: int
+    downsampling_ratios: list
+    channel_multiples: list
+    upsampling_ratios: list = field(default_factory=list)
+    hop_length: int = 1
+
+    @staticmethod
+    def load(path: str) -> "VaeConfig":
+        o = json.load(open(path))
+        c = VaeConfig(audio_channels=int(o["audio_channels"]), decoder_channels=int(o["decoder_channels"]),
+                      decoder_input_channels=int(o["decoder_input_channels"]),
+                      downsampling_ratios=[int(v) for v in o["downsampling_ratios"]],
+                      channel_multiples=[int(v) for v in o["channel_multiples"]])
+        c.upsampling_ratios = list(reversed(c.downsampling_ratios))  # :119-120
+        c.hop_length = int(np.prod(c.downsampling_ratios))           # :121-124
+        return c
+
+
+def fold_weight_norm(g: np.ndarray, v: np.ndarray) -> np.ndarray:
+    """`load_conv_weight_norm` (:541-555) -> the f32 values of the F16 weight."""
+    v = np.asarray(v, np.float32)
+    d0 = v.shape[0]
+    flat = v.reshape(d0, -1)
+    ss = np.sum(flat.astype(np.float64) ** 2, axis=1)
+    scale = (np.asarray(g, np.float32).reshape(d0) / np.sqrt((ss.astype(np.float32) + np.float32(1e-12))
+                                                            .astype(np.float32))).astype(np.float32)
+    w = (flat * scale[:, None]).astype(np.float32)
+    return round_f16(w).reshape(v.shape)
+
+
+def snake(x, alpha, beta):
+    """snake_forward (:682-692): per channel (last axis of x [T][C])."""
+    a = np.exp(np.asarray(alpha, np.float32).reshape(-1)).astype(np.float32)
+    b = np.exp(np.asarray(beta, np.float32).reshape(-1)).astype(np.float32)
+    s = (a[None, :] * x).astype(np.float32)
+    s = np.sin(s).astype(np.float32)
+    s = (s * s).astype(np.float32)
+    s = (s / b[None, :]).astype(np.float32)
+    return (x + s).astype(np.float32)
+
+
+def conv1d(x, w, bias, dilation=1, padding=0):
+    """ggml_conv_1d(w [Cout][Cin][K], x [T][Cin], s0=1, p0=padding, d0=dilation): F16 operands,
+    f32 accumulation; + bias.  Output length T + 2p - d(K-1)."""
+    xh = round_f16(x).astype(np.float32)
+    T, cin = xh.shape
+    cout, cin2, K = w.shape
+    assert cin == cin2
+    T_out = T + 2 * padding - dilation * (K - 1)
+    xp = np.zeros((T + 2 * padding, cin), np.float32)
+    xp[padding:padding + T] = xh
+    out = np.zeros((T_out, cout), np.float32)
+    for k in range(K):
+        out += xp[k * dilation:k * dilation + T_out] @ w[:, :, k].T.astype(np.float32)
+    out = _perturb(out)
+    if bias is not None:
+        out += np.asarray(bias, np.float32)[None, :]
+    return out
+
+
+def conv_transpose1d(x, w, bias, stride, padding):
+    """ggml_conv_transpose_1d(w [Cin][Cout][K], x, s0=stride, p0=0) + center crop (:697-708) + bias."""
+    xh = round_f16(x).astype(np.float32)
+    T, cin = xh.shape
+    cin2, cout, K = w.shape
+    assert cin == cin2
+    full_len = (T - 1) * stride + K
+    full = np.zeros((full_len, cout), np.float32)
+    for k in range(K):
+        full[k:k + (T - 1) * stride + 1:stride] += xh @ w[:, :, k].astype(np.float32)
+    full = _perturb(full)
+    target = (T - 1) * stride - 2 * padding + (K - 1) + 1
+    if padding > 0 and 0 < target < full_len:
+        start = (full_len - target) // 2
+        full = full[start:start + target]
+    if bias is not None:
+        full = full + np.asarray(bias, np.float32)[None, :]
+    return full.astype(np.float32)
+
+
+class VaeWeights:
+    """Decoder weights as ggml holds them (F16 folded conv weights, f32 snake params/biases)."""
+
+    def __init__(self, model_dir: str):
+        self.cfg = VaeConfig.load(os.path.join(model_dir, "config.json"))
+        st = read_safetensors(os.path.join(model_dir, "diffusion_pytorch_model.safetensors"))
+
+        def arr(name):
+            dt, shape, v = st[name]
+            return v.astype(np.float32).reshape(shape)
+
+        def conv(prefix, bias=True):
+            w = fold_weight_norm(arr(prefix + ".weight_g"), arr(prefix + ".weight_v"))
+            return dict(w=w, b=arr(prefix + ".bias").reshape(-1) if bias else None)
+
+        def snk(prefix):
+            return dict(alpha=arr(prefix + ".alpha").reshape(-1), beta=arr(prefix + ".beta").reshape(-1))
+
+        self.conv1 = conv("decoder.conv1")
+        self.blocks = []
+        for i, s in enumerate(self.cfg.upsampling_ratios):
+            p = f"decoder.block.{i}"
+            blk = dict(stride=s, snake1=snk(p + ".snake1"), conv_t1=conv(p + ".conv_t1"), res=[])
+            for j, dil in enumerate((1, 3, 9)):
+                q = f"{p}.res_unit{j + 1}"
+                blk["res"].append(dict(dil=dil, snake1=snk(q + ".snake1"), conv1=conv(q + ".conv1"),
+                                       snake2=snk(q + ".snake2"), conv2=conv(q + ".conv2")))
+            self.blocks.append(blk)
+        self.snake1 = snk("decoder.snake1")
+        self.conv2 = conv("decoder.conv2", bias=False)
+
+
+def residual_unit(ru, x):
+    """residual_forward (:724-733)."""
+    y = conv1d(snake(x, **ru["snake1"]), ru["conv1"]["w"], ru["conv1"]["b"], ru["dil"], 3 * ru["dil"])
+    y = conv1d(snake(y, **ru["snake2"]), ru["conv2"]["w"], ru["conv2"]["b"], 1, 0)
+    n = min(len(x), len(y))
+    cx, cy = (len(x) - n) // 2, (len(y) - n) // 2
+    return (x[cx:cx + n] + y[cy:cy + n]).astype(np.float32)
+
+
+def decode(W: VaeWeights, latents: np.ndarray) -> np.ndarray:
+    """forward_decode (:957-1002): latents [T][C_lat] -> audio [T*hop][audio_channels]."""
+    x = conv1d(np.asarray(latents, np.float32), W.conv1["w"], W.conv1["b"], 1, 3)
+    for blk in W.blocks:
+        s = blk["stride"]
+        x = snake(x, **blk["snake1"])
+        x = conv_transpose1d(x, blk["conv_t1"]["w"], blk["conv_t1"]["b"], s, (s + 1) // 2)
+        for ru in blk["res"]:
+            x = residual_unit(ru, x)
+    x = snake(x, **W.snake1)
+    return conv1d(x, W.conv2["w"], None, 1, 3)
+
+
+def decode_with_floor(W: VaeWeights, latents, perturb: float = 1e-6):
+    """(audio, floor): decode() and its relative L2 change under a `perturb` relative change of
+    every conv result (see CONV_PERTURB)."""
+    global CONV_PERTURB
+    out = decode(W, latents)
+    old = CONV_PERTURB
+    CONV_PERTURB = perturb
+    try:
+        pert = decode(W, latents)
+    finally:
+        CONV_PERTURB = old
+    floor = float(np.linalg.norm(pert.astype(np.float64) - out) / np.linalg.norm(out.astype(np.float64)))
+    return out, floor

@@ -1,0 +1,133 @@
+"""GPU parity of the Oobleck VAE decoder (ace_ggml_vae_decode and the device entry) against the
+oracle restatement of ace_vae::forward_decode (oracle/vae_oracle.py).
+
+Tolerance: every conv re-rounds its input to fp16 (ggml im2col), so any f32 difference (summation
+order, a 1-ulp sinf) can flip an fp16 rounding and propagate; the bound is
+max(1e-3, FLOOR_K * floor), floor = the oracle's own rel-L2 change when every conv result is
+perturbed by 1e-6 (vae_oracle.decode_with_floor)."""
+import tempfile
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REL_L2 = 1e-3
+FLOOR_K = 1.5
+
+
+def _ckpt(cfg):
+    from acestep_mi355x.synthetic import write_vae_checkpoint
+    d = tempfile.mkdtemp(prefix="acemi_vae_")
+    write_vae_checkpoint(d, cfg, seed=0)
+    return d
+
+
+@pytest.fixture(scope="module")
+def tiny_vae():
+    from acestep_mi355x.capi import GGMLCAPIBridge
+    from acestep_mi355x.synthetic import VAE_TINY_CONFIG
+    d = _ckpt(VAE_TINY_CONFIG)
+    br = GGMLCAPIBridge()
+    br.load_vae(d)
+    yield d, br
+    br.close()
+
+
+def _check(got, ref, floor, tag):
+    got = np.asarray(got, np.float64)
+    ref = np.asarray(ref, np.float64)
+    assert got.shape == ref.shape, (got.shape, ref.shape)
+    l2 = float(np.linalg.norm(got - ref) / np.linalg.norm(ref))
+    bound = max(REL_L2, FLOOR_K * floor)
+    print(f"{tag}: rel_l2={l2:.3e} floor={floor:.3e} bound={bound:.3e} max_abs={np.abs(got - ref).max():.3e}")
+    assert np.isfinite(l2) and l2 <= bound, (tag, l2, floor)
+
+
+@pytest.mark.parametrize("T", [1, 20, 37])
+def test_tiny_vae_decode_odd_stride(tiny_vae, T):
+    from oracle.vae_oracle import VaeWeights, decode_with_floor
+    d, br = tiny_vae
+    assert (br.latent_channels, br.audio_channels, br.hop_length) == (64, 2, 6)
+    lat = np.random.default_rng(T).standard_normal((T, 64)).astype(np.float32)
+    ref, floor = decode_with_floor(VaeWeights(d), lat)
+    n = br.vae_out_len(T)
+    assert n == ref.shape[0]
+    got = br.vae_decode_tfirst(lat)           # [T*hop, 2]; odd strides fill only the first n samples
+    _check(got[:n], ref, floor, f"tiny VAE T={T}")
+
+
+def test_vae_error_paths(tiny_vae):
+    import ctypes
+    from acestep_mi355x.capi import GGMLCAPIBridge
+    d, br = tiny_vae
+    lat = np.zeros((10, 64), np.float32)
+    out = np.zeros((10 * 6 - 1, 2), np.float32)
+    fp = lambda x: x.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+    assert br.lib.ace_ggml_vae_decode(br.ctx, fp(lat), 10, fp(out), out.nbytes) == 2
+    assert br._last_error() == "output buffer too small"
+    assert br.lib.ace_ggml_vae_decode(br.ctx, None, 10, fp(out), out.nbytes) == 2
+    assert br.lib.ace_ggml_vae_decode(br.ctx, fp(lat), 0, fp(out), out.nbytes) == 2
+    fresh = GGMLCAPIBridge()
+    assert fresh.lib.ace_ggml_vae_decode(fresh.ctx, fp(lat), 10, fp(out), out.nbytes) == 1
+    assert fresh._last_error() == "vae not loaded"
+    assert fresh.lib.ace_ggml_vae_get_info(fresh.ctx, None, None, None) == 1
+    assert fresh.lib.ace_ggml_load_vae(fresh.ctx, b"/nonexistent/vae") == 3
+    fresh.close()
+
+
+def test_device_entry_equals_host_entry(tiny_vae):
+    import torch
+    d, br = tiny_vae
+    lat = np.random.default_rng(9).standard_normal((33, 64)).astype(np.float32)
+    host = br.vae_decode_tfirst(lat)
+    n = br.vae_out_len(33)
+    dl = torch.from_numpy(lat).cuda()
+    out = torch.empty((n, 2), dtype=torch.float32, device="cuda")
+    br.vae_decode_device(dl.data_ptr(), 33, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy(), host[:n])
+
+
+def test_tiled_decode_hook_matches_windowed_oracle(tiny_vae):
+    """install_vae_backend: dit_handler.tiled_decode on ROCm tensors, reference window plan."""
+    import types
+    import torch
+    from acestep_mi355x.hook import _tile_plan, install_vae_backend
+    from oracle.vae_oracle import VaeWeights, decode
+    d, br = tiny_vae
+    handler = types.SimpleNamespace()
+    install_vae_backend(handler, br, chunk_size_default=16, overlap_default=4)
+    B, T = 2, 40
+    lat = np.random.default_rng(5).standard_normal((B, 64, T)).astype(np.float32)
+    got = handler.tiled_decode(torch.from_numpy(lat).cuda(), offload_wav_to_cpu=True).numpy()
+    W = VaeWeights(d)
+    for b in range(B):
+        parts = []
+        for cs, ce, ws, we in _tile_plan(T, 16, 4):
+            wav = decode(W, lat[b, :, ws:we].T)
+            up = wav.shape[0] / max(1, we - ws)
+            ts, te = int(round((cs - ws) * up)), int(round((we - ce) * up))
+            parts.append(wav[ts:wav.shape[0] - te if te > 0 else wav.shape[0]])
+        ref = np.concatenate(parts, axis=0).T
+        assert got[b].shape == ref.shape
+        l2 = np.linalg.norm(got[b] - ref) / np.linalg.norm(ref)
+        print(f"tiled hook b={b}: rel_l2={l2:.3e}")
+        assert l2 < 5e-3
+
+
+@pytest.mark.slow
+def test_full_size_vae_decode():
+    """The real ACE-Step 1.5 decoder shape (128 x [1,2,4,8,16] channels, strides 10,6,4,4,2,
+    hop 1920) on 6 latent frames (11520 samples)."""
+    from acestep_mi355x.capi import GGMLCAPIBridge
+    from acestep_mi355x.synthetic import VAE_FULL_CONFIG
+    from oracle.vae_oracle import VaeWeights, decode_with_floor
+    d = _ckpt(VAE_FULL_CONFIG)
+    br = GGMLCAPIBridge()
+    br.load_vae(d)
+    lat = np.random.default_rng(11).standard_normal((6, 64)).astype(np.float32)
+    got = br.vae_decode_tfirst(lat)
+    br.close()
+    ref, floor = decode_with_floor(VaeWeights(d), lat)
+    _check(got, ref, floor, "full VAE T=6")
