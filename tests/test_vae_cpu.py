@@ -101,3 +101,69 @@ def test_synthetic_vae_checkpoint_decodes_in_oracle():
     y = V.decode(W, lat)
     # odd stride 3: PyTorch ConvTranspose1d length (20+1)*3 - 2*2 = 59, then (59+1)*2 - 2 = 118
     assert y.shape == (118, 2) and np.all(np.isfinite(y))
+
+
+def test_implicit_gemm_formulation_reproduces_the_oracle():
+    """The layouts and index maps used by kernels/vae.hip + runtime/vae.cpp, restated in numpy:
+    weights re-laid out as the loader does, A rows gathered as conv_gemm_kernel's stage() does
+    (row m, tap -> input row m + tap*dil - pad, zero outside), output columns mapped as its epilogue
+    does (conv_t: n = r*Cout + co -> u = s*m + r - crop).  Must reproduce the oracle's decoder."""
+    from acestep_mi355x.synthetic import VAE_TINY_CONFIG, write_vae_checkpoint
+    d = tempfile.mkdtemp()
+    write_vae_checkpoint(d, VAE_TINY_CONFIG)
+    W = V.VaeWeights(d)
+
+    def gemm_conv(S, Wm, taps, dil, pad, M, T_in, Cin):
+        A = np.zeros((M, taps * Cin), np.float64)
+        for m in range(M):
+            for tap in range(taps):
+                t = m + tap * dil - pad
+                if 0 <= t < T_in:
+                    A[m, tap * Cin:(tap + 1) * Cin] = S[t]
+        return A @ Wm.T
+
+    def conv_layout(w):            # [Cout][Cin][K] -> [Cout][K*Cin]
+        return np.transpose(w, (0, 2, 1)).reshape(w.shape[0], -1).astype(np.float64)
+
+    def convt_layout(w, s):        # [Cin][Cout][2s] -> [s*Cout][2*Cin]
+        cin, cout, _ = w.shape
+        out = np.zeros((s * cout, 2 * cin))
+        for r in range(s):
+            for tap in range(2):
+                out[r * cout:(r + 1) * cout, tap * cin:(tap + 1) * cin] = w[:, :, r + tap * s].T
+        return out
+
+    def snake(v, sn):
+        return V.snake(v.astype(np.float32), sn["alpha"], sn["beta"])
+
+    lat = np.random.default_rng(1).standard_normal((13, 64)).astype(np.float32)
+    S = round_f16(lat).astype(np.float64)
+    X = gemm_conv(S, conv_layout(W.conv1["w"]), 7, 1, 3, 13, 13, 64) + W.conv1["b"]
+    L = 13
+    for blk in W.blocks:
+        s = blk["stride"]
+        p = (s + 1) // 2
+        Sa = round_f16(snake(X, blk["snake1"])).astype(np.float64)
+        full = (L + 1) * s
+        Lo = full - 2 * p
+        cout = blk["conv_t1"]["w"].shape[1]
+        G = gemm_conv(Sa, convt_layout(blk["conv_t1"]["w"], s), 2, -1, 0, L + 1, L, Sa.shape[1])
+        Xn = np.zeros((Lo, cout))
+        for m in range(L + 1):
+            for n in range(s * cout):
+                r, co = divmod(n, cout)
+                u = m * s + r - p
+                if 0 <= u < Lo:
+                    Xn[u, co] = G[m, n] + blk["conv_t1"]["b"][co]
+        X, L = Xn, Lo
+        for ru in blk["res"]:
+            Sb = round_f16(snake(X, ru["snake1"])).astype(np.float64)
+            Y = gemm_conv(Sb, conv_layout(ru["conv1"]["w"]), 7, ru["dil"], 3 * ru["dil"], L, L, Sb.shape[1])
+            Sc = round_f16(snake(Y + ru["conv1"]["b"], ru["snake2"])).astype(np.float64)
+            X = X + (gemm_conv(Sc, conv_layout(ru["conv2"]["w"]), 1, 1, 0, L, L, Sc.shape[1]) + ru["conv2"]["b"])
+    Sf = round_f16(snake(X, W.snake1)).astype(np.float64)
+    out = gemm_conv(Sf, conv_layout(W.conv2["w"]), 7, 1, 3, L, L, Sf.shape[1])
+    ref = V.decode(W, lat)
+    assert out.shape == ref.shape
+    rel = np.linalg.norm(out - ref) / np.linalg.norm(ref)
+    assert rel < 2e-3, rel
