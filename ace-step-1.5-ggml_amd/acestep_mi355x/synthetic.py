@@ -225,3 +225,80 @@ def write_vae_checkpoint(out_dir: str, cfg: dict, seed: int = 0, dtype: str = "F
             f.write(_encode(v, dtype))
     os.replace(tmp, os.path.join(out_dir, "diffusion_pytorch_model.safetensors"))
     return out_dir
+
+
+# ----------------------------------------------------------------------------- GGUF export
+GGML_TYPES = {"F32": 0, "F16": 1, "Q8_0": 8, "Q4_K": 12, "Q6_K": 14, "BF16": 30}
+_QUANT_ARG = {"F16": None, "Q8": "Q8_0", "Q8_0": "Q8_0", "Q6": "Q6_K", "Q6_K": "Q6_K", "Q4": "Q4_K", "Q4_K": "Q4_K"}
+_QBLOCK = {"Q8_0": 32, "Q4_K": 256, "Q6_K": 256}
+
+
+def _read_safetensors_f32(path: str) -> Dict[str, np.ndarray]:
+    with open(path, "rb") as f:
+        n = struct.unpack("<Q", f.read(8))[0]
+        header = json.loads(f.read(n))
+        base = 8 + n
+        out = {}
+        for name, info in header.items():
+            if name == "__metadata__":
+                continue
+            b0, b1 = info["data_offsets"]
+            f.seek(base + b0)
+            raw = f.read(b1 - b0)
+            dt = info["dtype"]
+            if dt == "F32":
+                v = np.frombuffer(raw, "<f4").astype(np.float32)
+            elif dt == "F16":
+                v = np.frombuffer(raw, "<f2").astype(np.float32)
+            elif dt == "BF16":
+                v = (np.frombuffer(raw, "<u2").astype(np.uint32) << 16).view(np.float32)
+            else:
+                raise ValueError(dt)
+            out[name] = v.reshape(info["shape"])
+    return out
+
+
+def write_gguf(safetensors_path: str, out_path: str, quant: str = "Q8", arch: str = "acestep") -> str:
+    """GGUF export with the rules of acestep_ggml/tools/export_safetensors_to_gguf.py:192-281: every
+    float tensor with >= 2 dims whose last dim is a multiple of the block size is quantized (Q8/Q6/Q4),
+    everything else is stored F16.  Block bytes come from this library's ggml encoders
+    (ace_mi_quantize; the reference script uses gguf-py / ggml's C quantizer).  GGUF v3, alignment 32,
+    numpy shape reversed into ggml ne order."""
+    from . import capi
+    qname = _QUANT_ARG[quant.upper()]
+    tensors = _read_safetensors_f32(safetensors_path)
+    entries = []
+    for name, v in tensors.items():
+        if qname and v.ndim >= 2 and v.shape[-1] % _QBLOCK[qname] == 0:
+            rows = int(np.prod(v.shape[:-1]))
+            data = capi.quantize(v.reshape(rows, v.shape[-1]), qname.lower()).tobytes()
+            entries.append((name, v.shape, GGML_TYPES[qname], data))
+        else:
+            entries.append((name, v.shape, GGML_TYPES["F16"], v.astype("<f2").tobytes()))
+
+    def s(x: str) -> bytes:
+        b = x.encode("utf-8")
+        return struct.pack("<Q", len(b)) + b
+
+    kv = [("general.architecture", 8, s(arch)), ("general.type", 8, s("model")),
+          ("general.quantization_version", 4, struct.pack("<I", 2))]
+    head = b"GGUF" + struct.pack("<IQQ", 3, len(entries), len(kv))
+    for k, t, val in kv:
+        head += s(k) + struct.pack("<I", t) + val
+    off = 0
+    infos = b""
+    for name, shape, gt, data in entries:
+        ne = list(reversed(shape))
+        infos += s(name) + struct.pack("<I", len(ne)) + b"".join(struct.pack("<Q", d) for d in ne)
+        infos += struct.pack("<IQ", gt, off)
+        off += (len(data) + 31) // 32 * 32
+    blob = head + infos
+    blob += b"\0" * ((32 - len(blob) % 32) % 32)
+    tmp = out_path + ".tmp"
+    with open(tmp, "wb") as f:
+        f.write(blob)
+        for _, _, _, data in entries:
+            f.write(data)
+            f.write(b"\0" * ((32 - len(data) % 32) % 32))
+    os.replace(tmp, out_path)
+    return out_path

@@ -36,14 +36,16 @@ struct GemmEpilogue {
 // re-laid out at load, runtime/quant.h): q = int8 / nibble plane, s = f32 scales; the kernel
 // dequantizes each 32-value block to bf16 while staging it into LDS and multiplies it with a bf16
 // activation (`Q -> bf16 dequant-fused` MFMA GEMM).
-enum WeightFormat : int { WF_BF16 = 0, WF_F16 = 1, WF_Q8_0 = 2, WF_Q4_K = 3, WF_Q6_K = 4 };
+// WF_F32X3: an F32 weight as the fp16 triple [hi | lo | hi] along K (ld = 3K), multiplied with an
+// activation written as [hi | hi | lo] (Ah.Wh + Ah.Wl + Al.Wh) by the plain fp16 GEMM over 3K.
+enum WeightFormat : int { WF_BF16 = 0, WF_F16 = 1, WF_Q8_0 = 2, WF_Q4_K = 3, WF_Q6_K = 4, WF_F32X3 = 5 };
 struct WeightView {
     int fmt = WF_BF16;
     const void* q = nullptr;   // dense uint16 [N][ld] | Q8_0/Q6_K int8 [N][K] | Q4_K u8 [N][K/2]
     const float* s = nullptr;  // Q8_0 [N][K/32] | Q4_K [N][K/32][2] (d*sc, dmin*m) | Q6_K [N][K/16]
     int ld = 0;                // dense leading dimension (elements)
 };
-inline ActType weight_act(int fmt) { return fmt == WF_F16 ? ActType::F16 : ActType::BF16; }
+inline ActType weight_act(int fmt) { return (fmt == WF_F16 || fmt == WF_F32X3) ? ActType::F16 : ActType::BF16; }
 inline bool weight_quantized(int fmt) { return fmt >= WF_Q8_0; }
 
 void launch_gemm(const uint16_t* A, int lda, const WeightView& W, int M, int N, int K, const GemmEpilogue& epi,
@@ -76,15 +78,16 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s);
 
 // ------------------------------------------------------------ elementwise
 // Pack [context | hidden] frames into patches: out act [B*Np][P*Cin].
+// x3: write the f32 value as the fp16 triple [hi | hi | lo] per row (input of a WF_F32X3 weight).
 void launch_pack_input(ActType t, const float* hidden, const float* context, int B, int T, int Np, int P,
-                       int audio_dim, int ctx_dim, uint16_t* out, hipStream_t s);
+                       int audio_dim, int ctx_dim, uint16_t* out, hipStream_t s, bool x3 = false);
 // f32 -> act conversion (row-major copy), optionally act(silu(x)).
 void launch_to_act(ActType t, const float* in, int64_t n, bool silu, uint16_t* out, hipStream_t s);
 // y = act( RMSNorm(x) * w * (1 + scale) + shift ); scale/shift optional, per item
 // (item = row / rows_per_item, stride mod_stride floats).
 void launch_rmsnorm_mod(ActType t, const float* x, int M, int H, const float* w, const float* scale,
                         const float* shift, int64_t mod_stride, int rows_per_item, float eps, uint16_t* out,
-                        hipStream_t s);
+                        hipStream_t s, bool x3 = false);
 // Per-head RMSNorm (+ NEOX RoPE) of the q/k sections and f16 re-layout for attention.
 struct PrepArgs {
     const float* src;

@@ -31,9 +31,10 @@ __device__ __forceinline__ float wave_sum(float v) {
 // ---------------------------------------------------------------- pack
 // input pack + patchify (acestep_dit_model.cpp:1350-1380): x0[t] = concat(context[t], hidden[t]),
 // zero padded to a multiple of the patch, viewed as [Np][P*Cin] (index k*Cin + c).
-__global__ void pack_input_kernel(bool f16, const float* __restrict__ hidden, const float* __restrict__ context,
+__global__ void pack_input_kernel(bool f16, bool x3, const float* __restrict__ hidden, const float* __restrict__ context,
                                   int B, int T, int Np, int P, int audio, int cdim, uint16_t* __restrict__ out) {
     const int cin = audio + cdim;
+    const int rowlen = P * cin;
     const int64_t total = (int64_t)B * Np * P * cin;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
         const int c = (int)(i % cin);
@@ -51,7 +52,16 @@ __global__ void pack_input_kernel(bool f16, const float* __restrict__ hidden, co
                 if (hidden) v = hidden[((int64_t)b * T + t) * audio + (c - cdim)];
             }
         }
-        out[i] = to_act(f16, v);
+        if (x3) {  // f32 operand as fp16 [hi | hi | lo] (WF_F32X3 weights)
+            const int64_t row = i / rowlen, col = i - row * rowlen;
+            uint16_t* o = out + row * 3 * rowlen + col;
+            const uint16_t hi = f32_to_f16(v);
+            o[0] = hi;
+            o[rowlen] = hi;
+            o[2 * rowlen] = f32_to_f16(v - (float)__builtin_bit_cast(_Float16, hi));
+        } else {
+            out[i] = to_act(f16, v);
+        }
     }
 }
 
@@ -67,7 +77,7 @@ __global__ void to_act_kernel(bool f16, const float* __restrict__ in, int64_t n,
 // rms_norm (:1097-1106) + AdaLN modulate (:1477-1481, :1522-1526, :1545-1549):
 // y = ((x * 1/sqrt(mean(x^2)+eps)) * w) * (1 + scale) + shift, written in the act type that the
 // following mul_mat converts it to.
-template <bool F16, int VPT>
+template <bool F16, int VPT, bool X3 = false>
 __global__ void __launch_bounds__(256) rmsnorm_mod_kernel(const float* __restrict__ x, int H, const float* __restrict__ w,
                                                           const float* __restrict__ scale, const float* __restrict__ shift,
                                                           int64_t mod_stride, int rows_per_item, float eps,
@@ -92,7 +102,7 @@ __global__ void __launch_bounds__(256) rmsnorm_mod_kernel(const float* __restric
     const int item = m / rows_per_item;
     const float* scp = scale ? scale + (int64_t)item * mod_stride : nullptr;
     const float* shp = shift ? shift + (int64_t)item * mod_stride : nullptr;
-    uint16_t* orow = out + (int64_t)m * H;
+    uint16_t* orow = out + (int64_t)m * H * (X3 ? 3 : 1);
 #pragma unroll
     for (int k = 0; k < VPT; ++k) {
         const int i = (threadIdx.x + k * 256) * 4;
@@ -107,12 +117,24 @@ __global__ void __launch_bounds__(256) rmsnorm_mod_kernel(const float* __restric
             s4[0] = a4.x; s4[1] = a4.y; s4[2] = a4.z; s4[3] = a4.w;
             h4[0] = b4.x; h4[1] = b4.y; h4[2] = b4.z; h4[3] = b4.w;
         }
-        uint16_t o[4];
+        uint16_t o[4], lo[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             float t = __fmul_rn(__fmul_rn(y[j], sc), ww[j]);
             if (scp) t = __fadd_rn(__fmul_rn(t, __fadd_rn(s4[j], 1.0f)), h4[j]);
-            o[j] = F16 ? f32_to_f16(t) : f32_to_bf16_rne(t);
+            o[j] = (F16 || X3) ? f32_to_f16(t) : f32_to_bf16_rne(t);
+            if (X3) lo[j] = f32_to_f16(t - (float)__builtin_bit_cast(_Float16, o[j]));
+        }
+        if constexpr (X3) {  // f32 operand as fp16 [hi | hi | lo] (WF_F32X3 weights)
+            uint2 ph, pl;
+            ph.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
+            ph.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
+            pl.x = (uint32_t)lo[0] | ((uint32_t)lo[1] << 16);
+            pl.y = (uint32_t)lo[2] | ((uint32_t)lo[3] << 16);
+            *(uint2*)(orow + i) = ph;
+            *(uint2*)(orow + H + i) = ph;
+            *(uint2*)(orow + 2 * H + i) = pl;
+            continue;
         }
         uint2 pk;
         pk.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
@@ -362,10 +384,10 @@ inline dim3 grid_for(int64_t n, int block = 256) {
 }  // namespace
 
 void launch_pack_input(ActType t, const float* hidden, const float* context, int B, int T, int Np, int P,
-                       int audio_dim, int ctx_dim, uint16_t* out, hipStream_t s) {
+                       int audio_dim, int ctx_dim, uint16_t* out, hipStream_t s, bool x3) {
     const int64_t n = (int64_t)B * Np * P * (audio_dim + ctx_dim);
-    hipLaunchKernelGGL(pack_input_kernel, grid_for(n), dim3(256), 0, s, t == ActType::F16, hidden, context, B, T, Np,
-                       P, audio_dim, ctx_dim, out);
+    hipLaunchKernelGGL(pack_input_kernel, grid_for(n), dim3(256), 0, s, t == ActType::F16, x3, hidden, context, B, T,
+                       Np, P, audio_dim, ctx_dim, out);
     ACEMI_HIP(hipGetLastError());
 }
 
@@ -376,31 +398,27 @@ void launch_to_act(ActType t, const float* in, int64_t n, bool silu, uint16_t* o
 
 void launch_rmsnorm_mod(ActType t, const float* x, int M, int H, const float* w, const float* scale,
                         const float* shift, int64_t mod_stride, int rows_per_item, float eps, uint16_t* out,
-                        hipStream_t s) {
+                        hipStream_t s, bool x3) {
     ACEMI_CHECK(H % 4 == 0 && H <= 4096, "rmsnorm: H % 4 == 0 and H <= 4096");
     const bool f16 = t == ActType::F16;
-    if (H <= 1024) {
-        if (f16)
-            hipLaunchKernelGGL((rmsnorm_mod_kernel<true, 1>), dim3(M), dim3(256), 0, s, x, H, w, scale, shift,
-                               mod_stride, rows_per_item, eps, out);
-        else
-            hipLaunchKernelGGL((rmsnorm_mod_kernel<false, 1>), dim3(M), dim3(256), 0, s, x, H, w, scale, shift,
-                               mod_stride, rows_per_item, eps, out);
-    } else if (H <= 2048) {
-        if (f16)
-            hipLaunchKernelGGL((rmsnorm_mod_kernel<true, 2>), dim3(M), dim3(256), 0, s, x, H, w, scale, shift,
-                               mod_stride, rows_per_item, eps, out);
-        else
-            hipLaunchKernelGGL((rmsnorm_mod_kernel<false, 2>), dim3(M), dim3(256), 0, s, x, H, w, scale, shift,
-                               mod_stride, rows_per_item, eps, out);
+    const int vpt = H <= 1024 ? 1 : (H <= 2048 ? 2 : 4);
+#define ACEMI_RMS(F, V, X)                                                                                   \
+    hipLaunchKernelGGL((rmsnorm_mod_kernel<F, V, X>), dim3(M), dim3(256), 0, s, x, H, w, scale, shift, mod_stride, \
+                       rows_per_item, eps, out)
+    if (x3) {
+        if (vpt == 1) ACEMI_RMS(true, 1, true);
+        else if (vpt == 2) ACEMI_RMS(true, 2, true);
+        else ACEMI_RMS(true, 4, true);
+    } else if (f16) {
+        if (vpt == 1) ACEMI_RMS(true, 1, false);
+        else if (vpt == 2) ACEMI_RMS(true, 2, false);
+        else ACEMI_RMS(true, 4, false);
     } else {
-        if (f16)
-            hipLaunchKernelGGL((rmsnorm_mod_kernel<true, 4>), dim3(M), dim3(256), 0, s, x, H, w, scale, shift,
-                               mod_stride, rows_per_item, eps, out);
-        else
-            hipLaunchKernelGGL((rmsnorm_mod_kernel<false, 4>), dim3(M), dim3(256), 0, s, x, H, w, scale, shift,
-                               mod_stride, rows_per_item, eps, out);
+        if (vpt == 1) ACEMI_RMS(false, 1, false);
+        else if (vpt == 2) ACEMI_RMS(false, 2, false);
+        else ACEMI_RMS(false, 4, false);
     }
+#undef ACEMI_RMS
     ACEMI_HIP(hipGetLastError());
 }
 

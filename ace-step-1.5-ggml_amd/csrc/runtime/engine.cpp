@@ -78,11 +78,11 @@ void DitEngine::prepare_shape(int B, int Np, int L) {
     const int64_t Npad = round_up(Np, 128);
     const int qd = c.hq * D, kd = c.hkv * D;
     const size_t act = 2;
-    ensure(a0_, M * c.patch * c.in_channels * act);
+    ensure(a0_, M * c.patch * c.in_channels * act * 3);                 // x3 layout for F32 proj_in
+    ensure(act2_, M * std::max(I, 3 * H) * act);                        // also the x3 proj_out input
     ensure(x_, M * H * 4);
     ensure(act_, M * std::max(H, qd) * act);
     ensure(attn_, M * qd * act);
-    ensure(act2_, M * I * act);
     ensure(qkv_, M * (qd + 2 * kd) * 4);
     ensure(qh_, (size_t)2 * B * c.hq * Npad * D * 2);   // hi + lo planes
     ensure(kh_, (size_t)2 * B * c.hkv * Npad * D * 2);
@@ -167,7 +167,9 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
 
     // ---- input pack + proj_in (:1343-1382)
     tic(s);
-    launch_pack_input(m.proj_in_w.act(), io.hidden, io.context, B, T, Np, P, c.audio_dim, c.ctx_dim(), a0, s);
+    const int kin = m.proj_in_w.k_mult();
+    launch_pack_input(m.proj_in_w.act(), io.hidden, io.context, B, T, Np, P, c.audio_dim, c.ctx_dim(), a0, s,
+                      kin == 3);
     toc("pack_input", s);
     {
         GemmEpilogue e;
@@ -176,7 +178,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
         e.c_f32 = x;
         e.ldc = H;
         tic(s);
-        launch_gemm(a0, P * c.in_channels, m.proj_in_w.view(), (int)M, H, P * c.in_channels, e, s);
+        launch_gemm(a0, kin * P * c.in_channels, m.proj_in_w.view(), (int)M, H, kin * P * c.in_channels, e, s);
         toc("gemm_proj_in", s);
     }
 
@@ -450,7 +452,10 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
     {
         const float* om = get<float>(outmod_);
         tic(s);
-        launch_rmsnorm_mod(at, x, (int)M, H, m.norm_out, om + H, om, 2LL * H, Np, c.eps, act, s);
+        const int kout = m.proj_out_w.k_mult();
+        uint16_t* head_in = kout == 3 ? get<uint16_t>(act2_) : act;  // act2_ is sized for M x 3H too
+        launch_rmsnorm_mod(m.proj_out_w.act(), x, (int)M, H, m.norm_out, om + H, om, 2LL * H, Np, c.eps, head_in, s,
+                           kout == 3);
         toc("rmsnorm_mod", s);
         GemmEpilogue e;
         e.kind = EPI_PROJ_OUT;
@@ -461,7 +466,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
         e.out_ch = c.audio_dim;
         e.patch = P;
         tic(s);
-        launch_gemm(act, H, m.proj_out_w.view(), (int)M, P * c.audio_dim, H, e, s);
+        launch_gemm(head_in, kout * H, m.proj_out_w.view(), (int)M, P * c.audio_dim, kout * H, e, s);
         toc("gemm_proj_out", s);
     }
 }

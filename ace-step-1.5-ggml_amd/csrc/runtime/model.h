@@ -37,12 +37,13 @@ struct DevWeight {
     int rows = 0, cols = 0;
     WeightView view() const {
         WeightView v;
-        v.fmt = fmt;
+        v.fmt = fmt == WF_F32X3 ? WF_F16 : fmt;
         v.q = q;
         v.s = s;
-        v.ld = cols;
+        v.ld = fmt == WF_F32X3 ? 3 * cols : cols;
         return v;
     }
+    int k_mult() const { return fmt == WF_F32X3 ? 3 : 1; }  // GEMM K = k_mult * cols
     ActType act() const { return weight_act(fmt); }
 };
 

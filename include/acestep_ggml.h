@@ -21,7 +21,10 @@
  * per call; the caller owns every buffer; blocking; one context is not
  * thread-safe.  `n_threads` and `use_metal` are accepted and ignored
  * (the compute runs on the GPU); `compute_buffer_bytes` is ignored (the
- * workspace is sized from the shapes).  The device is HIP device 0 unless
+ * workspace is sized from the shapes).  ace_ggml_load_dit accepts the reference's weight sources:
+ * model.safetensors (BF16/F16, optional online ACE_GGML_DIT_WEIGHT_QTYPE=Q8_0/Q6_K/Q4_K) and GGUF
+ * (ACE_GGML_DIT_GGUF[_PATH], <dir>.gguf or <dir>/model.gguf; F16/BF16/Q8_0/Q6_K/Q4_K tensors).
+ * The device is HIP device 0 unless
  * ACE_MI_DEVICE is set, or ace_mi_create_on_device (acestep_mi355x.h) is used.
  */
 #ifndef ACESTEP_GGML_H

@@ -95,33 +95,146 @@ def read_safetensors(path: str) -> dict:
 # --------------------------------------------------------------------------
 # weight loading  (acestep_dit_model.cpp:753-1088)
 # --------------------------------------------------------------------------
+def read_gguf(path: str) -> dict:
+    """Independent numpy GGUF v2/v3 reader (format of llama.cpp's GGUFWriter, used by
+    acestep_ggml/tools/export_safetensors_to_gguf.py): name -> (ggml type, ne list, raw bytes)."""
+    import struct as _st
+    data = open(path, "rb").read()
+    pos = 0
+
+    def rd(fmt):
+        nonlocal pos
+        v = _st.unpack_from("<" + fmt, data, pos)
+        pos += _st.calcsize("<" + fmt)
+        return v[0] if len(v) == 1 else v
+
+    def rstr():
+        nonlocal pos
+        n = rd("Q")
+        out = data[pos:pos + n].decode("utf-8")
+        pos += n
+        return out
+
+    sizes = {0: 1, 1: 1, 2: 2, 3: 2, 4: 4, 5: 4, 6: 4, 7: 1, 10: 8, 11: 8, 12: 8}
+
+    def skip_value(t):
+        nonlocal pos
+        if t == 8:
+            rstr()
+        elif t == 9:
+            et, n = rd("I"), rd("Q")
+            for _ in range(n):
+                skip_value(et)
+        else:
+            pos += sizes[t]
+
+    assert data[:4] == b"GGUF"
+    pos = 4
+    version, n_t, n_kv = rd("I"), rd("Q"), rd("Q")
+    assert version in (2, 3)
+    align = 32
+    for _ in range(n_kv):
+        key, t = rstr(), rd("I")
+        if key == "general.alignment" and t in (4, 5, 10, 11):
+            align = int(_st.unpack_from("<" + {4: "I", 5: "i", 10: "Q", 11: "q"}[t], data, pos)[0])
+        skip_value(t)
+    infos = []
+    for _ in range(n_t):
+        name = rstr()
+        nd = rd("I")
+        ne = [rd("Q") for _ in range(nd)]
+        gt, off = rd("I"), rd("Q")
+        infos.append((name, ne, gt, off))
+    base = (pos + align - 1) // align * align
+    row_bytes = {0: lambda n: 4 * n, 1: lambda n: 2 * n, 30: lambda n: 2 * n, 8: lambda n: n // 32 * 34,
+                 12: lambda n: n // 256 * 144, 14: lambda n: n // 256 * 210}
+    out = {}
+    for name, ne, gt, off in infos:
+        rows = int(np.prod(ne[1:])) if len(ne) > 1 else 1
+        nb = row_bytes[gt](ne[0]) * rows
+        out[name] = (gt, ne, data[base + off: base + off + nb])
+    return out
+
+
+_GGUF_QT = {8: "q8_0", 12: "q4_k", 14: "q6_k"}
+
+
+def _gguf_values(gt, ne, raw):
+    """f32 values of a GGUF tensor in numpy (row-major, reversed ne) shape."""
+    from .ggml_numerics import dequantize_q4_k, dequantize_q6_k, dequantize_q8_0, unpack_q8_0
+    shape = list(reversed(ne))
+    rows = int(np.prod(ne[1:])) if len(ne) > 1 else 1
+    if gt == 0:
+        v = np.frombuffer(raw, "<f4").astype(np.float32)
+    elif gt == 1:
+        v = np.frombuffer(raw, "<f2").astype(np.float32)
+    elif gt == 30:
+        v = (np.frombuffer(raw, "<u2").astype(np.uint32) << 16).view(np.float32)
+    elif gt == 8:
+        v = dequantize_q8_0(*unpack_q8_0(np.frombuffer(raw, np.uint8).reshape(rows, ne[0] // 32, 34)))
+    elif gt == 12:
+        v = dequantize_q4_k(np.frombuffer(raw, np.uint8).reshape(rows, ne[0] // 256, 144))
+    elif gt == 14:
+        v = dequantize_q6_k(np.frombuffer(raw, np.uint8).reshape(rows, ne[0] // 256, 210))
+    else:
+        raise ValueError(f"unsupported gguf type {gt}")
+    return np.asarray(v, np.float32).reshape(shape)
+
+
 class DitWeights:
-    def __init__(self, model_dir: str, qtype: str | None = None):
+    def __init__(self, model_dir: str, qtype: str | None = None, gguf: str | None = None):
+        """Weights of load_model_from_dir (acestep_dit_model.cpp:753-1088).  `gguf`: load the tensors
+        from a GGUF file instead (the `use_gguf` branch: types kept as stored, conv weights converted
+        to F32, no online quantization, :526-718)."""
         self.cfg = DitConfig.load(os.path.join(model_dir, "config.json"))
-        st = read_safetensors(os.path.join(model_dir, "model.safetensors"))
-        self.qtype = qtype
+        st = read_gguf(gguf) if gguf else read_safetensors(os.path.join(model_dir, "model.safetensors"))
+        self.qtype = None if gguf else qtype
+        qtype = self.qtype
         c = self.cfg
 
-        def w2(name):  # load_tensor_2d_transposed :228-277
-            dt, shape, v = st[name]
-            return make_weight(v.reshape(shape[0], shape[1]), dt, qtype)
+        if gguf:
+            def w2(name):  # load_tensor_2d_from_gguf: type kept
+                gt, ne, raw = st[name]
+                v = _gguf_values(gt, ne, raw).reshape(ne[1], ne[0])
+                wt = _GGUF_QT.get(gt) or {0: "f32", 1: "f16", 30: "bf16"}[gt]
+                return GgmlWeight(v, wt)
 
-        def w3as2(name):  # load_tensor_3d_as_2d :279-332 ([1, r, c] -> r rows of c)
-            dt, shape, v = st[name]
-            return make_weight(v.reshape(shape[1], shape[2]), dt, qtype)
+            def w3as2(name):  # load_tensor_3d_as_2d_from_gguf + cast_f32
+                gt, ne, raw = st[name]
+                return GgmlWeight(_gguf_values(gt, ne, raw).reshape(ne[1], ne[0]), "f32")
 
-        def v1(name):  # load_tensor_1d + cast_f32
-            return st[name][2].astype(np.float32).reshape(-1)
+            def v1(name):
+                gt, ne, raw = st[name]
+                return _gguf_values(gt, ne, raw).reshape(-1)
 
-        # proj_in: conv1d [out, in, k] -> linear [out][in + k*in]  (:334-411)
-        dt, (co, ci, kk), wv = st["decoder.proj_in.1.weight"]
+            def conv_w(name):  # read_gguf_tensor_as_f32 -> values, stored as an F32 matrix
+                gt, ne, raw = st[name]
+                return "F32", tuple(reversed(ne)), _gguf_values(gt, ne, raw)
+        else:
+            def w2(name):  # load_tensor_2d_transposed :228-277
+                dt, shape, v = st[name]
+                return make_weight(v.reshape(shape[0], shape[1]), dt, qtype)
+
+            def w3as2(name):  # load_tensor_3d_as_2d :279-332 ([1, r, c] -> r rows of c)
+                dt, shape, v = st[name]
+                return make_weight(v.reshape(shape[1], shape[2]), dt, qtype)
+
+            def v1(name):  # load_tensor_1d + cast_f32
+                return st[name][2].astype(np.float32).reshape(-1)
+
+            def conv_w(name):
+                dt, shape, v = st[name]
+                return dt, tuple(shape), np.asarray(v).reshape(shape)
+
+        # proj_in: conv1d [out, in, k] -> linear [out][in + k*in]  (:334-411; GGUF :602-637 -> F32)
+        dt, (co, ci, kk), wv = conv_w("decoder.proj_in.1.weight")
         mat = np.transpose(wv, (0, 2, 1)).reshape(co, kk * ci)  # index k*ci + c
-        self.proj_in_w = make_weight(mat, dt, qtype)
+        self.proj_in_w = GgmlWeight(mat, "f32") if gguf else make_weight(mat, dt, qtype)
         self.proj_in_b = v1("decoder.proj_in.1.bias")
-        # proj_out: convtranspose1d [in, out, k] -> linear [(out + k*out_ch)][in]  (:413-490)
-        dt, (ci2, co2, k2), wv = st["decoder.proj_out.1.weight"]
+        # proj_out: convtranspose1d [in, out, k] -> linear [(out + k*out_ch)][in]  (:413-490; GGUF :639-677)
+        dt, (ci2, co2, k2), wv = conv_w("decoder.proj_out.1.weight")
         mat = np.transpose(wv, (2, 1, 0)).reshape(k2 * co2, ci2)  # row o + k*co2
-        self.proj_out_w = make_weight(mat, dt, qtype)
+        self.proj_out_w = GgmlWeight(mat, "f32") if gguf else make_weight(mat, dt, qtype)
         self.proj_out_b = v1("decoder.proj_out.1.bias")
         self.condition_w = w2("decoder.condition_embedder.weight")
         self.condition_b = v1("decoder.condition_embedder.bias")

@@ -345,3 +345,31 @@ def test_quantized_full_width_vs_ggml_semantics(monkeypatch, qtype):
     assert l2 <= QUANT_FLOOR_K * floor and cos >= 0.999, (l2, floor, cos)
     eng = forward_with_floor(engine_view(W), h, c, e, None, None, T, L, 0.8, 0.8, max_layers=2)
     check(got, eng[0], eng[1], f"full-width {qtype} (dequant semantics)")
+
+
+# ---------------------------------------------------------------- GGUF weights (a14 / SURVEY §8f)
+@pytest.mark.parametrize("quant", ["Q8", "Q4", "F16"])
+def test_gguf_tiny_matches_oracle(tiny_ckpt, monkeypatch, quant):
+    """model.gguf next to config.json (resolve_gguf_path, acestep_dit_model.cpp:47-70): types kept as
+    stored, proj_in/proj_out converted to F32 (the engine's fp16 hi/lo triple GEMM), no online
+    quantization even if ACE_GGML_DIT_WEIGHT_QTYPE is set."""
+    import shutil
+    from acestep_mi355x.capi import GGMLCAPIBridge
+    from acestep_mi355x.synthetic import write_gguf
+    from oracle.dit_oracle import DitWeights, forward_with_floor
+    d = tempfile.mkdtemp(prefix="acemi_gguf_")
+    shutil.copy(os.path.join(tiny_ckpt, "config.json"), d)
+    path = write_gguf(os.path.join(tiny_ckpt, "model.safetensors"), os.path.join(d, "model.gguf"), quant=quant)
+    monkeypatch.setenv("ACE_GGML_DIT_WEIGHT_QTYPE", "q6_k")   # ignored on the GGUF path
+    br = GGMLCAPIBridge()
+    br.load_dit(d)
+    rng = np.random.default_rng(41)
+    T, L = 150, 12
+    h = rng.standard_normal((T, 64)).astype(np.float32)
+    c = rng.standard_normal((T, 128)).astype(np.float32)
+    e = rng.standard_normal((L, 256)).astype(np.float32)
+    got = br.dit_forward_tfirst(h, c, e, None, None, 0.6, 0.6)
+    br.close()
+    W = DitWeights(d, gguf=path)
+    ref, floor = forward_with_floor(engine_view(W), h, c, e, None, None, T, L, 0.6, 0.6)
+    check(got, ref, floor, f"tiny GGUF {quant}")
