@@ -33,7 +33,8 @@ EXPORTED_SYMBOLS = (
     "ace_mi_profile_enable", "ace_mi_profile_reset", "ace_mi_profile_get", "ace_mi_probe_gemm",
     "ace_mi_synchronize", "ace_mi_kernel_gemm", "ace_mi_kernel_attention", "ace_mi_bench_gemm",
     "ace_mi_gemm_variant", "ace_ggml_load_vae", "ace_ggml_vae_get_info", "ace_ggml_vae_decode",
-    "ace_mi_vae_out_len", "ace_mi_vae_decode_device", "ace_mi_quantize", "ace_mi_dequantize", "ace_mi_kernel_gemm_q", "ace_mi_bench_gemm_q",
+    "ace_mi_vae_out_len", "ace_mi_vae_decode_device", "ace_ggml_vae_encode", "ace_mi_vae_enc_out_len",
+    "ace_mi_vae_encode_device", "ace_mi_quantize", "ace_mi_dequantize", "ace_mi_kernel_gemm_q", "ace_mi_bench_gemm_q",
 )
 
 # qtype codes of ace_mi_quantize & co. (names as parse_quant_type, acestep_dit_model.cpp:27-37)
@@ -126,6 +127,12 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.ace_mi_vae_out_len.restype = ctypes.c_int
     lib.ace_mi_vae_decode_device.argtypes = [vp, vp, i32, vp, vp]
     lib.ace_mi_vae_decode_device.restype = ctypes.c_int
+    lib.ace_ggml_vae_encode.argtypes = [vp, fp, i32, fp, sz]
+    lib.ace_ggml_vae_encode.restype = ctypes.c_int
+    lib.ace_mi_vae_enc_out_len.argtypes = [vp, i32, ctypes.POINTER(i64)]
+    lib.ace_mi_vae_enc_out_len.restype = ctypes.c_int
+    lib.ace_mi_vae_encode_device.argtypes = [vp, vp, i32, vp, vp]
+    lib.ace_mi_vae_encode_device.restype = ctypes.c_int
     lib.ace_mi_quantize.argtypes = [i32, fp, i64, i64, u8p, sz]
     lib.ace_mi_quantize.restype = ctypes.c_int64
     lib.ace_mi_dequantize.argtypes = [i32, u8p, i64, i64, fp]
@@ -232,7 +239,28 @@ class GGMLCAPIBridge:
         self._ensure_ok(st, "ace_ggml_vae_decode")
         return out.reshape(out_samples, self.audio_channels)
 
+    def vae_encode_tfirst(self, audio_tfirst) -> np.ndarray:
+        """audio [samples, channels] f32 -> latent mean [samples // hop, latent_channels] (host buffers)."""
+        if self.latent_channels <= 0 or self.hop_length <= 0:
+            raise RuntimeError("VAE not initialized in ggml bridge")
+        a = np.ascontiguousarray(audio_tfirst, dtype=np.float32)
+        n = int(a.shape[0])
+        out = np.empty((n // self.hop_length, self.latent_channels), dtype=np.float32)
+        st = self.lib.ace_ggml_vae_encode(self.ctx, _fptr(a), n, _fptr(out), out.nbytes)
+        self._ensure_ok(st, "ace_ggml_vae_encode")
+        return out
+
     # -- MI355X extensions ---------------------------------------------------
+    def vae_enc_out_len(self, n_samples: int) -> int:
+        n = ctypes.c_int64(0)
+        st = self.lib.ace_mi_vae_enc_out_len(self.ctx, int(n_samples), ctypes.byref(n))
+        self._ensure_ok(st, "ace_mi_vae_enc_out_len")
+        return int(n.value)
+
+    def vae_encode_device(self, d_audio: int, n_samples: int, d_out: int, stream: int = 0) -> None:
+        st = self.lib.ace_mi_vae_encode_device(self.ctx, d_audio, int(n_samples), d_out, stream or None)
+        self._ensure_ok(st, "ace_mi_vae_encode_device")
+
     def vae_out_len(self, n_frames: int) -> int:
         n = ctypes.c_int64(0)
         self._ensure_ok(self.lib.ace_mi_vae_out_len(self.ctx, int(n_frames), ctypes.byref(n)), "ace_mi_vae_out_len")

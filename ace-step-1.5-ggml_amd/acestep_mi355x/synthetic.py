@@ -189,6 +189,23 @@ def vae_tensor_specs(cfg: dict) -> Iterator[Tuple[str, Tuple[int, ...], str]]:
             yield from conv(q + ".conv2", cout, cout, 1)
     yield from snk("decoder.snake1", ch)
     yield from conv("decoder.conv2", aud, ch, 7, bias=False)
+    # encoder (diffusers OobleckEncoder; acestep_vae_model.cpp:925-937)
+    eh = cfg["encoder_hidden_size"]
+    dn = list(cfg["downsampling_ratios"])
+    yield from conv("encoder.conv1", eh, aud, 7)
+    for i, s in enumerate(dn):
+        cin, cout = eh * cm[i], eh * cm[i + 1]
+        p = f"encoder.block.{i}"
+        for j in range(3):
+            q = f"{p}.res_unit{j + 1}"
+            yield from snk(q + ".snake1", cin)
+            yield from conv(q + ".conv1", cin, cin, 7)
+            yield from snk(q + ".snake2", cin)
+            yield from conv(q + ".conv2", cin, cin, 1)
+        yield from snk(p + ".snake1", cin)
+        yield from conv(p + ".conv1", cout, cin, 2 * s)
+    yield from snk("encoder.snake1", eh * cm[-1])
+    yield from conv("encoder.conv2", eh, eh * cm[-1], 3)
 
 
 def write_vae_checkpoint(out_dir: str, cfg: dict, seed: int = 0, dtype: str = "F32") -> str:

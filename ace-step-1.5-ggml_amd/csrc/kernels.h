@@ -137,6 +137,7 @@ struct ConvGemmArgs {
     const uint16_t* zero = nullptr;
     const uint16_t* W = nullptr;
     int T_in = 0, Cin = 0, taps = 1, dil = 1, pad = 0;
+    int in_stride = 1;  // strided conv: A row (m, tap) = S[m*in_stride + tap*dil - pad]
     int M = 0, N = 0;
     const float* bias = nullptr;
     int Cout = 0, up = 1, crop = 0, T_out = 0;
@@ -148,6 +149,8 @@ struct ConvGemmArgs {
 };
 void launch_conv_gemm(const ConvGemmArgs& a, hipStream_t s);
 void launch_to_f16(const float* x, int64_t n, uint16_t* y, hipStream_t s);
+// x [rows][C] f32 -> y [rows][Cpad] fp16, channels >= C zero
+void launch_pack_f16(const float* x, int64_t rows, int C, int Cpad, uint16_t* y, hipStream_t s);
 // out[t][o] = sum_k sum_c W[o][k][c] * S[t + k - 3][c]   (kernel 7, pad 3, no bias), f32 out
 void launch_conv_out(const uint16_t* S, int T, int C, const uint16_t* W, int out_ch, float* out, hipStream_t s);
 

@@ -98,13 +98,14 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(ConvGemmArgs p) {
         const int tap = kt / cblocks;
         const int c0 = (kt - tap * cblocks) * BK;
         const int shift = tap * p.dil - p.pad;
+        const int istr = p.in_stride;
 #pragma unroll
         for (int j = 0; j < G_PER_WAVE; ++j) {
             const int row = srow[j];
             const uint16_t* src;
             if (row < BM) {
                 const int m = m0 + row;
-                const int t = m + shift;
+                const int t = m * istr + shift;
                 src = (m < p.M && t >= 0 && t < p.T_in) ? p.S + (int64_t)t * p.Cin + c0 + schunk[j] * 8
                                                         : p.zero + schunk[j] * 8;
             } else {
@@ -212,6 +213,15 @@ __global__ void to_f16_kernel(const float* __restrict__ x, int64_t n, uint16_t* 
         y[i] = f32_to_f16(x[i]);
 }
 
+__global__ void pack_f16_kernel(const float* __restrict__ x, int64_t rows, int C, int Cpad, uint16_t* __restrict__ y) {
+    const int64_t n = rows * Cpad;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / Cpad;
+        const int c = (int)(i - r * Cpad);
+        y[i] = c < C ? f32_to_f16(x[r * C + c]) : (uint16_t)0;
+    }
+}
+
 // decoder.conv2: C -> out_ch (2), kernel 7, pad 3, no bias, on the fp16 Snake output.  Too narrow
 // for MFMA tiles: one thread per output time, the 7 input rows read as 16-byte vectors (shared
 // through L1/L2 by neighbouring threads), weights staged in LDS; f32 accumulation of exact
@@ -270,6 +280,13 @@ void launch_conv_gemm(const ConvGemmArgs& a, hipStream_t s) {
 void launch_to_f16(const float* x, int64_t n, uint16_t* y, hipStream_t s) {
     const int grid = (int)std::min<int64_t>((n + 255) / 256, 4096);
     hipLaunchKernelGGL(to_f16_kernel, dim3(std::max(grid, 1)), dim3(256), 0, s, x, n, y);
+    ACEMI_HIP(hipGetLastError());
+}
+
+void launch_pack_f16(const float* x, int64_t rows, int C, int Cpad, uint16_t* y, hipStream_t s) {
+    const int64_t n = rows * Cpad;
+    const int grid = (int)std::min<int64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(pack_f16_kernel, dim3(std::max(grid, 1)), dim3(256), 0, s, x, rows, C, Cpad, y);
     ACEMI_HIP(hipGetLastError());
 }
 

@@ -475,6 +475,59 @@ ace_ggml_status ace_ggml_vae_decode(ace_ggml_context* ctx, const float* latents,
     return ACE_GGML_OK;
 }
 
+// ace_ggml_vae_encode (acestep_ggml.cpp:975-1072): audio [n_samples][audio_channels] -> latent mean
+// [n_samples/hop][latent_channels]
+ace_ggml_status ace_ggml_vae_encode(ace_ggml_context* ctx, const float* audio, int32_t n_samples, float* out,
+                                    size_t out_size) {
+    if (!ctx || !audio || !out || n_samples <= 0) return ACE_GGML_ERR_INVALID_ARG;
+    if (!ctx->vae) return set_error(ctx, ACE_GGML_ERR, "vae not loaded");
+    const auto& c = ctx->vae->model().cfg;
+    const size_t expected = (size_t)(n_samples / c.hop_length) * (size_t)c.decoder_input_channels * sizeof(float);
+    if (out_size < expected) return set_error(ctx, ACE_GGML_ERR_INVALID_ARG, "output buffer too small");
+    if (!ctx->vae->model().has_encoder) return set_error(ctx, ACE_GGML_ERR, "vae encode failed: encoder weights not loaded");
+    try {
+        bind_device(ctx);
+        hipStream_t s = ctx->stream;
+        const int64_t out_len = ctx->vae->enc_out_len(n_samples);
+        if (out_len <= 0) return set_error(ctx, ACE_GGML_ERR, "unexpected vae output shape");
+        const size_t needed = (size_t)out_len * (size_t)c.decoder_input_channels * sizeof(float);
+        if (out_size < needed) return set_error(ctx, ACE_GGML_ERR_INVALID_ARG, "output buffer too small for actual output");
+        const size_t n_in = (size_t)n_samples * c.audio_channels * sizeof(float);
+        const size_t o_out = (n_in + 255) & ~size_t(255);
+        ensure_dev(ctx->d_vae, ctx->d_vae_bytes, o_out + needed);
+        char* base = static_cast<char*>(ctx->d_vae);
+        ACEMI_HIP(hipMemcpyAsync(base, audio, n_in, hipMemcpyHostToDevice, s));
+        ctx->vae->encode(reinterpret_cast<const float*>(base), n_samples, reinterpret_cast<float*>(base + o_out), s);
+        ACEMI_HIP(hipMemcpyAsync(out, base + o_out, needed, hipMemcpyDeviceToHost, s));
+        ACEMI_HIP(hipStreamSynchronize(s));
+    } catch (const std::exception& e) {
+        return set_error(ctx, ACE_GGML_ERR, std::string("graph compute failed: ") + e.what());
+    }
+    return ACE_GGML_OK;
+}
+
+ace_ggml_status ace_mi_vae_enc_out_len(ace_ggml_context* ctx, int32_t n_samples, int64_t* out_len) {
+    if (!ctx || !out_len || n_samples <= 0) return ACE_GGML_ERR_INVALID_ARG;
+    if (!ctx->vae) return set_error(ctx, ACE_GGML_ERR, "vae not loaded");
+    if (!ctx->vae->model().has_encoder) return set_error(ctx, ACE_GGML_ERR, "vae encoder weights not loaded");
+    *out_len = ctx->vae->enc_out_len(n_samples);
+    return ACE_GGML_OK;
+}
+
+ace_ggml_status ace_mi_vae_encode_device(ace_ggml_context* ctx, const float* d_audio, int32_t n_samples, float* d_out,
+                                         void* stream) {
+    if (!ctx || !d_audio || !d_out || n_samples <= 0) return ACE_GGML_ERR_INVALID_ARG;
+    if (!ctx->vae) return set_error(ctx, ACE_GGML_ERR, "vae not loaded");
+    try {
+        bind_device(ctx);
+        hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+        ctx->vae->encode(d_audio, n_samples, d_out, s);
+    } catch (const std::exception& e) {
+        return set_error(ctx, ACE_GGML_ERR, std::string("graph compute failed: ") + e.what());
+    }
+    return ACE_GGML_OK;
+}
+
 ace_ggml_status ace_mi_vae_out_len(ace_ggml_context* ctx, int32_t n_frames, int64_t* out_len) {
     if (!ctx || !out_len || n_frames <= 0) return ACE_GGML_ERR_INVALID_ARG;
     if (!ctx->vae) return set_error(ctx, ACE_GGML_ERR, "vae not loaded");

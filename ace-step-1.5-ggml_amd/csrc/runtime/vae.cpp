@@ -74,21 +74,24 @@ struct VaeLoader {
         if ((int64_t)b.size() != cout) throw IoError("invalid tensor shape for " + prefix + ".bias");
         return upload<float>(b.data(), b.size() * 4);
     }
-    // ggml_conv_1d weight [Cout][Cin][K] -> W [Cout][K][Cin] fp16
-    VaeConv conv(const std::string& prefix, bool with_bias, int dil, int pad) {
+    // ggml_conv_1d weight [Cout][Cin][K] -> W [Cout][K][Cin_pad] fp16 (zero columns past Cin)
+    VaeConv conv(const std::string& prefix, bool with_bias, int dil, int pad, int stride = 1, int cin_pad_to = 1) {
         std::vector<int64_t> sh;
         auto w = fold(prefix, sh);
         VaeConv c;
         c.cout = (int)sh[0];
-        c.cin = (int)sh[1];
+        c.cin_real = (int)sh[1];
+        c.cin = (c.cin_real + cin_pad_to - 1) / cin_pad_to * cin_pad_to;
         c.taps = (int)sh[2];
         c.dil = dil;
         c.pad = pad;
-        std::vector<uint16_t> h((size_t)c.cout * c.taps * c.cin);
+        c.stride = stride;
+        std::vector<uint16_t> h((size_t)c.cout * c.taps * c.cin, 0);
         for (int co = 0; co < c.cout; ++co)
-            for (int ci = 0; ci < c.cin; ++ci)
+            for (int ci = 0; ci < c.cin_real; ++ci)
                 for (int k = 0; k < c.taps; ++k)
-                    h[((size_t)co * c.taps + k) * c.cin + ci] = f32_to_f16_bits(w[((size_t)co * c.cin + ci) * c.taps + k]);
+                    h[((size_t)co * c.taps + k) * c.cin + ci] =
+                        f32_to_f16_bits(w[((size_t)co * c.cin_real + ci) * c.taps + k]);
         c.w = upload<uint16_t>(h.data(), h.size() * 2);
         if (with_bias) c.b = bias(prefix, c.cout);
         return c;
@@ -99,7 +102,7 @@ struct VaeLoader {
         auto w = fold(prefix, sh);
         VaeConv c;
         c.transposed = true;
-        c.cin = (int)sh[0];
+        c.cin = c.cin_real = (int)sh[0];
         c.cout = (int)sh[1];
         c.stride = stride;
         c.pad = (stride + 1) / 2;  // ceil(stride / 2) (:575)
@@ -224,6 +227,47 @@ void load_vae_model(const std::string& dir, VaeModel& m, int& status_hint) {
         if (m.conv2.cin != C || m.conv2.taps != 7 || m.conv2.cout != c.audio_channels)
             throw IoError("invalid decoder.conv2 shape");
         if (C % 8 != 0) throw Unsupported("decoder.conv2 input channels must be a multiple of 8");
+
+        // encoder (load_model_from_dir :925-937): conv1 (k7, pad 3), blocks (3 residual units, Snake,
+        // conv k=2s stride s pad ceil(s/2)), snake1, conv2 (k3, pad 1) -> [mean | scale]
+        if (L.st.has("encoder.conv1.weight_v")) {
+            m.enc_conv1 = L.conv("encoder.conv1", true, 1, 3, 1, 64);
+            if (m.enc_conv1.cin_real != c.audio_channels) throw IoError("encoder.conv1 input channels mismatch");
+            check_gemm_conv(m.enc_conv1, "encoder.conv1");
+            int Ce = m.enc_conv1.cout;
+            m.enc_blocks.resize(c.downsampling_ratios.size());
+            for (size_t i = 0; i < m.enc_blocks.size(); ++i) {
+                const std::string p2 = "encoder.block." + std::to_string(i);
+                VaeEncBlock& b = m.enc_blocks[i];
+                b.stride = c.downsampling_ratios[i];
+                const int dils[3] = {1, 3, 9};
+                for (int j = 0; j < 3; ++j) {
+                    const std::string q = p2 + ".res_unit" + std::to_string(j + 1);
+                    VaeRes& r = b.res[j];
+                    r.dil = dils[j];
+                    r.s1 = L.snake(q + ".snake1", Ce);
+                    r.c1 = L.conv(q + ".conv1", true, dils[j], ((7 - 1) * dils[j]) / 2);
+                    r.s2 = L.snake(q + ".snake2", Ce);
+                    r.c2 = L.conv(q + ".conv2", true, 1, 0);
+                    if (r.c1.cin != Ce || r.c1.cout != Ce || r.c2.cin != Ce || r.c2.cout != Ce || r.c1.taps != 7 ||
+                        r.c2.taps != 1)
+                        throw IoError("invalid residual unit shape at " + q);
+                    check_gemm_conv(r.c1, q + ".conv1");
+                    check_gemm_conv(r.c2, q + ".conv2");
+                }
+                b.s1 = L.snake(p2 + ".snake1", Ce);
+                b.conv = L.conv(p2 + ".conv1", true, 1, (b.stride + 1) / 2, b.stride);
+                if (b.conv.cin != Ce || b.conv.taps != 2 * b.stride) throw IoError("invalid shape at " + p2 + ".conv1");
+                check_gemm_conv(b.conv, p2 + ".conv1");
+                Ce = b.conv.cout;
+            }
+            m.enc_snake1 = L.snake("encoder.snake1", Ce);
+            m.enc_conv2 = L.conv("encoder.conv2", true, 1, 1);
+            if (m.enc_conv2.cin != Ce || m.enc_conv2.cout < c.decoder_input_channels)
+                throw IoError("invalid encoder.conv2 shape");
+            check_gemm_conv(m.enc_conv2, "encoder.conv2");
+            m.has_encoder = true;
+        }
     } catch (const Unsupported& e) {
         status_hint = 4;
         throw std::runtime_error(e.what());
@@ -265,92 +309,160 @@ int64_t VaeEngine::out_len(int n_frames) const {
     return L;
 }
 
+void VaeEngine::run_conv(const VaeConv& c, const uint16_t* S, int T_in, int T_out, float* X, bool resid, bool store,
+                         uint16_t* S_out, const VaeSnake* next, hipStream_t s) {
+    ConvGemmArgs a;
+    a.S = S;
+    a.zero = static_cast<const uint16_t*>(zero_.p);
+    a.W = c.w;
+    a.T_in = T_in;
+    a.Cin = c.cin;
+    a.taps = c.taps;
+    a.bias = c.b;
+    a.Cout = c.cout;
+    a.T_out = T_out;
+    if (c.transposed) {
+        a.dil = -1;  // tap 0 -> input row j, tap 1 -> row j-1
+        a.pad = 0;
+        a.M = T_in + 1;
+        a.N = c.stride * c.cout;
+        a.up = c.stride;
+        a.crop = c.pad;
+    } else {
+        a.dil = c.dil;
+        a.pad = c.pad;
+        a.in_stride = c.stride;
+        a.M = T_out;
+        a.N = c.cout;
+    }
+    a.X = X;
+    a.resid = resid ? 1 : 0;
+    a.store_x = store ? 1 : 0;
+    a.S_out = S_out;
+    if (next) {
+        a.snake_ea = next->ea;
+        a.snake_eb = next->eb;
+    }
+    launch_conv_gemm(a, s);
+}
+
+// residual_forward (:724-733): x += conv2(snake2(conv1(snake1(x)))); Sin holds snake1(x); the new x's
+// Snake for the next consumer goes to Snext_out
+void VaeEngine::run_res(const VaeRes& r, int L, float* X, uint16_t* Sin, uint16_t* Stmp, uint16_t* Snext_out,
+                        const VaeSnake* next, hipStream_t s) {
+    run_conv(r.c1, Sin, L, L, nullptr, false, false, Stmp, &r.s2, s);
+    run_conv(r.c2, Stmp, L, L, X, true, true, Snext_out, next, s);
+}
+
+namespace {
+int64_t convt_len(int64_t L, const VaeConv& c) {  // PyTorch ConvTranspose1d length (conv_forward :697-708)
+    const int64_t full = (L + 1) * c.stride, target = full - 2 * c.pad;
+    return (c.pad > 0 && target > 0 && target < full) ? target : full;
+}
+int64_t conv_len(int64_t L, const VaeConv& c) {  // ggml_conv_1d output length
+    return (L + 2 * c.pad - (int64_t)c.dil * (c.taps - 1) - 1) / c.stride + 1;
+}
+}  // namespace
+
 void VaeEngine::decode(const float* d_latents, int n_frames, float* d_out, hipStream_t s) {
     const VaeModel& m = model_;
     ACEMI_CHECK(n_frames >= 1, "vae decode: n_frames must be > 0");
     // buffer sizes: the largest (length x channels) over the stages
     int64_t L = n_frames, maxe = (int64_t)n_frames * m.conv1.cout;
-    int maxc = m.conv1.cout;
     for (const auto& b : m.blocks) {
-        const int64_t full = (L + 1) * b.stride, target = full - 2 * b.ct.pad;
-        L = (b.ct.pad > 0 && target > 0 && target < full) ? target : full;
+        L = convt_len(L, b.ct);
         maxe = std::max(maxe, L * b.ct.cout);
-        maxc = std::max(maxc, b.ct.cin);
     }
+    ACEMI_CHECK(L < (1LL << 31), "vae decode: sequence too long");
     ensure(x_, (size_t)maxe * 4);
     ensure(sa_, (size_t)maxe * 2);
     ensure(sb_, (size_t)maxe * 2);
     ensure(sc_, (size_t)maxe * 2);
     ensure(lat_, (size_t)n_frames * m.conv1.cin * 2);
-    ensure(zero_, (size_t)std::max(maxc, 64) * 2 * 2);  // hipMemset to 0 in ensure()
+    ensure(zero_, 4096);  // >= 64 fp16 zeros (hipMemset in ensure())
 
     float* X = static_cast<float*>(x_.p);
     uint16_t* Sa = static_cast<uint16_t*>(sa_.p);
     uint16_t* Sb = static_cast<uint16_t*>(sb_.p);
     uint16_t* Sc = static_cast<uint16_t*>(sc_.p);
-    const uint16_t* zero = static_cast<const uint16_t*>(zero_.p);
 
     // latents -> fp16 (ggml im2col of decoder.conv1's input)
     launch_to_f16(d_latents, (int64_t)n_frames * m.conv1.cin, static_cast<uint16_t*>(lat_.p), s);
-
-    auto conv = [&](const VaeConv& c, const uint16_t* S, int T_in, int T_out, float* Xp, bool resid, bool store,
-                    uint16_t* S_out, const VaeSnake* next) {
-        ConvGemmArgs a;
-        a.S = S;
-        a.zero = zero;
-        a.W = c.w;
-        a.T_in = T_in;
-        a.Cin = c.cin;
-        a.taps = c.taps;
-        a.bias = c.b;
-        a.Cout = c.cout;
-        a.T_out = T_out;
-        if (c.transposed) {
-            a.dil = -1;  // tap 0 -> input row j, tap 1 -> row j-1
-            a.pad = 0;
-            a.M = T_in + 1;
-            a.N = c.stride * c.cout;
-            a.up = c.stride;
-            a.crop = c.pad;
-        } else {
-            a.dil = c.dil;
-            a.pad = c.pad;
-            a.M = T_out;
-            a.N = c.cout;
-        }
-        a.X = Xp;
-        a.resid = resid ? 1 : 0;
-        a.store_x = store ? 1 : 0;
-        a.S_out = S_out;
-        if (next) {
-            a.snake_ea = next->ea;
-            a.snake_eb = next->eb;
-        }
-        launch_conv_gemm(a, s);
-    };
     const VaeSnake* first = m.blocks.empty() ? &m.snake1 : &m.blocks[0].s1;
     // decoder.conv1 -> X, Sa = snake(next)(X)
-    conv(m.conv1, static_cast<const uint16_t*>(lat_.p), n_frames, n_frames, X, false, true, Sa, first);
+    run_conv(m.conv1, static_cast<const uint16_t*>(lat_.p), n_frames, n_frames, X, false, true, Sa, first, s);
     L = n_frames;
     for (size_t i = 0; i < m.blocks.size(); ++i) {
         const VaeBlock& b = m.blocks[i];
-        const int64_t full = (L + 1) * b.stride, target = full - 2 * b.ct.pad;
-        const int64_t Lo = (b.ct.pad > 0 && target > 0 && target < full) ? target : full;
-        ACEMI_CHECK(Lo < (1LL << 31), "vae decode: sequence too long");
+        const int64_t Lo = convt_len(L, b.ct);
         // snake1 was applied by the producer of Sa; conv_t1 -> X, Sb = res1.snake1(X)
-        conv(b.ct, Sa, (int)L, (int)Lo, X, false, true, Sb, &b.res[0].s1);
+        run_conv(b.ct, Sa, (int)L, (int)Lo, X, false, true, Sb, &b.res[0].s1, s);
         L = Lo;
         for (int j = 0; j < 3; ++j) {
-            const VaeRes& r = b.res[j];
-            // conv1(snake1(x)) -> Sc = snake2(.)
-            conv(r.c1, Sb, (int)L, (int)L, nullptr, false, false, Sc, &r.s2);
-            // x += conv2(.) ; next consumer's Snake of the new x
             const VaeSnake* next = j < 2 ? &b.res[j + 1].s1 : (i + 1 < m.blocks.size() ? &m.blocks[i + 1].s1 : &m.snake1);
-            conv(r.c2, Sc, (int)L, (int)L, X, true, true, j < 2 ? Sb : Sa, next);
+            run_res(b.res[j], (int)L, X, Sb, Sc, j < 2 ? Sb : Sa, next, s);
         }
     }
     // decoder.snake1 (applied into Sa) -> decoder.conv2
     launch_conv_out(Sa, (int)L, m.conv2.cin, m.conv2.w, m.conv2.cout, d_out, s);
+}
+
+int64_t VaeEngine::enc_out_len(int n_samples) const {
+    const VaeModel& m = model_;
+    int64_t L = conv_len(n_samples, m.enc_conv1);
+    for (const auto& b : m.enc_blocks) L = conv_len(L, b.conv);
+    return conv_len(L, m.enc_conv2);
+}
+
+// forward_encode (acestep_vae_model.cpp:1004-1044)
+void VaeEngine::encode(const float* d_audio, int n_samples, float* d_out, hipStream_t s) {
+    const VaeModel& m = model_;
+    ACEMI_CHECK(m.has_encoder, "vae encoder weights not loaded");
+    ACEMI_CHECK(n_samples >= 1, "vae encode: n_samples must be > 0");
+    int64_t L = conv_len(n_samples, m.enc_conv1);
+    int64_t maxe = (int64_t)n_samples * m.enc_conv1.cin;  // padded input
+    maxe = std::max(maxe, L * m.enc_conv1.cout);
+    for (const auto& b : m.enc_blocks) {
+        maxe = std::max(maxe, L * b.conv.cin);
+        L = conv_len(L, b.conv);
+        ACEMI_CHECK(L >= 1, "vae encode: input too short");
+        maxe = std::max(maxe, L * b.conv.cout);
+    }
+    const int64_t Lf = conv_len(L, m.enc_conv2);
+    ACEMI_CHECK(Lf >= 1, "vae encode: input too short");
+    maxe = std::max(maxe, Lf * m.enc_conv2.cout);
+    ensure(x_, (size_t)maxe * 4);
+    ensure(sa_, (size_t)maxe * 2);
+    ensure(sb_, (size_t)maxe * 2);
+    ensure(sc_, (size_t)maxe * 2);
+    ensure(zero_, 4096);
+    float* X = static_cast<float*>(x_.p);
+    uint16_t* Sa = static_cast<uint16_t*>(sa_.p);
+    uint16_t* Sb = static_cast<uint16_t*>(sb_.p);
+    uint16_t* Sc = static_cast<uint16_t*>(sc_.p);
+
+    // audio [n][C] -> fp16 [n][64] (zero-padded channels; ggml im2col of encoder.conv1's input)
+    launch_pack_f16(d_audio, n_samples, m.enc_conv1.cin_real, m.enc_conv1.cin, Sa, s);
+    L = conv_len(n_samples, m.enc_conv1);
+    const VaeSnake* first = m.enc_blocks.empty() ? &m.enc_snake1 : &m.enc_blocks[0].res[0].s1;
+    run_conv(m.enc_conv1, Sa, n_samples, (int)L, X, false, true, Sb, first, s);
+    for (size_t i = 0; i < m.enc_blocks.size(); ++i) {
+        const VaeEncBlock& b = m.enc_blocks[i];
+        for (int j = 0; j < 3; ++j) {
+            const VaeSnake* next = j < 2 ? &b.res[j + 1].s1 : &b.s1;
+            run_res(b.res[j], (int)L, X, Sb, Sc, j < 2 ? Sb : Sa, next, s);
+        }
+        // block snake1 (in Sa) -> strided conv -> X, Sb = snake(next)(X)
+        const int64_t Lo = conv_len(L, b.conv);
+        const VaeSnake* next = i + 1 < m.enc_blocks.size() ? &m.enc_blocks[i + 1].res[0].s1 : &m.enc_snake1;
+        run_conv(b.conv, Sa, (int)L, (int)Lo, X, false, true, Sb, next, s);
+        L = Lo;
+    }
+    // encoder.snake1 (in Sb) -> conv2 -> X [Lf][2*latent]; keep the mean half (:1037-1043)
+    run_conv(m.enc_conv2, Sb, (int)L, (int)Lf, X, false, true, nullptr, nullptr, s);
+    const int lat = model_.cfg.decoder_input_channels;
+    ACEMI_HIP(hipMemcpy2DAsync(d_out, (size_t)lat * 4, X, (size_t)m.enc_conv2.cout * 4, (size_t)lat * 4, (size_t)Lf,
+                               hipMemcpyDeviceToDevice, s));
 }
 
 }  // namespace acemi

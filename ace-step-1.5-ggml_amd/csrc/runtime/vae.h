@@ -27,6 +27,7 @@ struct VaeConv {
     uint16_t* w = nullptr;
     float* b = nullptr;
     int cin = 0, cout = 0, taps = 1, dil = 1, pad = 0, stride = 1;
+    int cin_real = 0;  // < cin when the input channels were zero-padded to a multiple of 64
     bool transposed = false;
 };
 struct VaeSnake {
@@ -46,12 +47,25 @@ struct VaeBlock {
     int stride = 1;
 };
 
+struct VaeEncBlock {  // diffusers OobleckEncoderBlock: 3 residual units, Snake, strided conv (k 2s)
+    VaeRes res[3];
+    VaeSnake s1;
+    VaeConv conv;
+    int stride = 1;
+};
+
 struct VaeModel {
     VaeConfig cfg;
     VaeConv conv1;
     std::vector<VaeBlock> blocks;
     VaeSnake snake1;
     VaeConv conv2;
+    // encoder (optional: loaded when encoder.* tensors exist; required by encode)
+    bool has_encoder = false;
+    VaeConv enc_conv1;  // audio channels zero-padded to 64
+    std::vector<VaeEncBlock> enc_blocks;
+    VaeSnake enc_snake1;
+    VaeConv enc_conv2;
     std::vector<void*> allocs;
     size_t weight_bytes = 0;
     ~VaeModel();
@@ -70,6 +84,10 @@ public:
     int64_t out_len(int n_frames) const;
     // latents [n_frames][latent_channels] f32 -> out [out_len][audio_channels] f32, device pointers
     void decode(const float* d_latents, int n_frames, float* d_out, hipStream_t s);
+    // latent frames produced by encode (ggml_conv_1d output lengths of the strided convs)
+    int64_t enc_out_len(int n_samples) const;
+    // audio [n_samples][audio_channels] f32 -> latent mean [enc_out_len][latent_channels] f32
+    void encode(const float* d_audio, int n_samples, float* d_out, hipStream_t s);
 
 private:
     struct Buf {
@@ -80,6 +98,10 @@ private:
     int device_;
     VaeModel model_;
     Buf x_, sa_, sb_, sc_, lat_, zero_;
+    void run_conv(const VaeConv& c, const uint16_t* S, int T_in, int T_out, float* X, bool resid, bool store,
+                  uint16_t* S_out, const VaeSnake* next, hipStream_t s);
+    void run_res(const VaeRes& r, int L, float* X, uint16_t* Sin, uint16_t* Stmp, uint16_t* Snext_out,
+                 const VaeSnake* next, hipStream_t s);
 };
 
 }  // namespace acemi

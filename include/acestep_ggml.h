@@ -16,6 +16,7 @@
  *   ace_ggml_load_vae                        acestep_ggml/cpp/acestep_ggml.h:44
  *   ace_ggml_vae_get_info                    acestep_ggml/cpp/acestep_ggml.h:45-49
  *   ace_ggml_vae_decode                      acestep_ggml/cpp/acestep_ggml.h:50-55
+ *   ace_ggml_vae_encode                      acestep_ggml/cpp/acestep_ggml.h:56-61
  *
  * Semantics: host f32 row-major, time-major buffers; one sample
  * per call; the caller owns every buffer; blocking; one context is not
@@ -75,6 +76,10 @@ ACE_GGML_API ace_ggml_status ace_ggml_load_vae(ace_ggml_context* ctx, const char
 ACE_GGML_API ace_ggml_status ace_ggml_vae_get_info(ace_ggml_context* ctx, int32_t* latent_channels,
                                                    int32_t* audio_channels, int32_t* hop_length);
 ACE_GGML_API ace_ggml_status ace_ggml_vae_decode(ace_ggml_context* ctx, const float* latents, int32_t n_frames,
+                                                 float* out, size_t out_size);
+/* Encode: audio [n_samples][audio_channels] f32 -> latent mean [n_samples/hop][latent_channels] f32
+ * (needs the encoder.* tensors of the VAE checkpoint). */
+ACE_GGML_API ace_ggml_status ace_ggml_vae_encode(ace_ggml_context* ctx, const float* audio, int32_t n_samples,
                                                  float* out, size_t out_size);
 
 #ifdef __cplusplus

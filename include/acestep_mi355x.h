@@ -105,6 +105,10 @@ ACE_GGML_API ace_ggml_status ace_mi_gemm_variant(int32_t variant);
 ACE_GGML_API ace_ggml_status ace_mi_vae_out_len(ace_ggml_context* ctx, int32_t n_frames, int64_t* out_len);
 ACE_GGML_API ace_ggml_status ace_mi_vae_decode_device(ace_ggml_context* ctx, const float* d_latents,
                                                       int32_t n_frames, float* d_out, void* stream);
+/* VAE encode on device pointers: audio [n_samples][audio_channels] -> latent mean [enc_out_len][latent]. */
+ACE_GGML_API ace_ggml_status ace_mi_vae_enc_out_len(ace_ggml_context* ctx, int32_t n_samples, int64_t* out_len);
+ACE_GGML_API ace_ggml_status ace_mi_vae_encode_device(ace_ggml_context* ctx, const float* d_audio,
+                                                      int32_t n_samples, float* d_out, void* stream);
 
 /* ggml block quantization (qtype 1 = Q8_0, 2 = Q4_K, 3 = Q6_K) with the encoders the loader uses for
  * ACE_GGML_DIT_WEIGHT_QTYPE (try_quantize_matrix, acestep_dit_model.cpp:156-192): rows x cols f32 ->

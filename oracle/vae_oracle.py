@@ -87,19 +87,19 @@ def snake(x, alpha, beta):
     return (x + s).astype(np.float32)
 
 
-def conv1d(x, w, bias, dilation=1, padding=0):
-    """ggml_conv_1d(w [Cout][Cin][K], x [T][Cin], s0=1, p0=padding, d0=dilation): F16 operands,
-    f32 accumulation; + bias.  Output length T + 2p - d(K-1)."""
+def conv1d(x, w, bias, dilation=1, padding=0, stride=1):
+    """ggml_conv_1d(w [Cout][Cin][K], x [T][Cin], s0=stride, p0=padding, d0=dilation): F16 operands,
+    f32 accumulation; + bias.  Output length (T + 2p - d(K-1) - 1) / s + 1."""
     xh = round_f16(x).astype(np.float32)
     T, cin = xh.shape
     cout, cin2, K = w.shape
     assert cin == cin2
-    T_out = T + 2 * padding - dilation * (K - 1)
-    xp = np.zeros((T + 2 * padding, cin), np.float32)
+    T_out = (T + 2 * padding - dilation * (K - 1) - 1) // stride + 1
+    xp = np.zeros((T + 2 * padding + stride, cin), np.float32)
     xp[padding:padding + T] = xh
     out = np.zeros((T_out, cout), np.float32)
     for k in range(K):
-        out += xp[k * dilation:k * dilation + T_out] @ w[:, :, k].T.astype(np.float32)
+        out += xp[k * dilation:k * dilation + (T_out - 1) * stride + 1:stride] @ w[:, :, k].T.astype(np.float32)
     out = _perturb(out)
     if bias is not None:
         out += np.asarray(bias, np.float32)[None, :]
@@ -156,6 +156,19 @@ class VaeWeights:
             self.blocks.append(blk)
         self.snake1 = snk("decoder.snake1")
         self.conv2 = conv("decoder.conv2", bias=False)
+        # encoder (load_model_from_dir :925-937): optional here, required by encode()
+        self.enc = None
+        if "encoder.conv1.weight_v" in st:
+            enc = dict(conv1=conv("encoder.conv1"), blocks=[], snake1=snk("encoder.snake1"), conv2=conv("encoder.conv2"))
+            for i, s_ in enumerate(self.cfg.downsampling_ratios):
+                p = f"encoder.block.{i}"
+                blk = dict(stride=s_, res=[], snake1=snk(p + ".snake1"), conv1=conv(p + ".conv1"))
+                for j, dil in enumerate((1, 3, 9)):
+                    q = f"{p}.res_unit{j + 1}"
+                    blk["res"].append(dict(dil=dil, snake1=snk(q + ".snake1"), conv1=conv(q + ".conv1"),
+                                           snake2=snk(q + ".snake2"), conv2=conv(q + ".conv2")))
+                enc["blocks"].append(blk)
+            self.enc = enc
 
 
 def residual_unit(ru, x):
@@ -178,6 +191,22 @@ def decode(W: VaeWeights, latents: np.ndarray) -> np.ndarray:
             x = residual_unit(ru, x)
     x = snake(x, **W.snake1)
     return conv1d(x, W.conv2["w"], None, 1, 3)
+
+
+def encode(W: VaeWeights, audio: np.ndarray) -> np.ndarray:
+    """forward_encode (:1004-1044): audio [n_samples][audio_channels] -> latent mean
+    [n_frames][decoder_input_channels] (the first half of encoder.conv2's [mean, scale] channels)."""
+    E = W.enc
+    x = conv1d(np.asarray(audio, np.float32), E["conv1"]["w"], E["conv1"]["b"], 1, 3)
+    for blk in E["blocks"]:
+        for ru in blk["res"]:
+            x = residual_unit(ru, x)
+        s = blk["stride"]
+        x = snake(x, **blk["snake1"])
+        x = conv1d(x, blk["conv1"]["w"], blk["conv1"]["b"], 1, (s + 1) // 2, stride=s)
+    x = snake(x, **E["snake1"])
+    x = conv1d(x, E["conv2"]["w"], E["conv2"]["b"], 1, 1)
+    return x[:, :W.cfg.decoder_input_channels].copy()
 
 
 def decode_with_floor(W: VaeWeights, latents, perturb: float = 1e-6):

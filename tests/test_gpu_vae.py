@@ -131,3 +131,24 @@ def test_full_size_vae_decode():
     br.close()
     ref, floor = decode_with_floor(VaeWeights(d), lat)
     _check(got, ref, floor, "full VAE T=6")
+
+
+@pytest.mark.parametrize("n", [120, 126, 600])
+def test_tiny_vae_encode(tiny_vae, n):
+    """ace_ggml_vae_encode: encoder convs incl. the strided downsampling convs (the first conv's
+    2 audio channels zero-padded to 64 for the GEMM) vs the oracle."""
+    from oracle.vae_oracle import VaeWeights, encode
+    import oracle.vae_oracle as V
+    d, br = tiny_vae
+    audio = np.random.default_rng(n).standard_normal((n, 2)).astype(np.float32)
+    W = VaeWeights(d)
+    ref = encode(W, audio)
+    V.CONV_PERTURB = 1e-6
+    try:
+        pert = encode(W, audio)
+    finally:
+        V.CONV_PERTURB = 0.0
+    floor = float(np.linalg.norm(pert - ref) / np.linalg.norm(ref))
+    assert br.vae_enc_out_len(n) == ref.shape[0]
+    got = br.vae_encode_tfirst(audio)
+    _check(got[:ref.shape[0]], ref, floor, f"tiny VAE encode n={n}")

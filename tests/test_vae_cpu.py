@@ -167,3 +167,30 @@ def test_implicit_gemm_formulation_reproduces_the_oracle():
     assert out.shape == ref.shape
     rel = np.linalg.norm(out - ref) / np.linalg.norm(ref)
     assert rel < 2e-3, rel
+
+
+@pytest.mark.parametrize("stride", [2, 4, 6])
+def test_strided_conv_matches_torch(stride):
+    """encoder downsampling conv: ggml_conv_1d(s0=s, p0=ceil(s/2)), kernel 2s."""
+    rng = np.random.default_rng(stride + 10)
+    T, cin, cout = 61, 64, 32
+    x = rng.standard_normal((T, cin)).astype(np.float32)
+    w = round_f16(rng.standard_normal((cout, cin, 2 * stride)).astype(np.float32) * 0.05)
+    b = rng.standard_normal(cout).astype(np.float32)
+    pad = (stride + 1) // 2
+    got = V.conv1d(x, w, b, 1, pad, stride=stride)
+    ref = torch.nn.functional.conv1d(torch.from_numpy(round_f16(x).T[None].astype(np.float64)),
+                                     torch.from_numpy(w.astype(np.float64)), torch.from_numpy(b.astype(np.float64)),
+                                     stride=stride, padding=pad)[0].T.numpy()
+    assert got.shape == ref.shape
+    np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-4)
+
+
+def test_encoder_round_trip_shapes():
+    from acestep_mi355x.synthetic import VAE_TINY_CONFIG, write_vae_checkpoint
+    d = tempfile.mkdtemp()
+    write_vae_checkpoint(d, VAE_TINY_CONFIG)
+    W = V.VaeWeights(d)
+    audio = np.random.default_rng(2).standard_normal((120, 2)).astype(np.float32)
+    z = V.encode(W, audio)
+    assert z.shape == (20, 64) and np.all(np.isfinite(z))
