@@ -468,9 +468,16 @@ void load_dit_model(const std::string& dir, DitModel& m, int& status_hint) {
         const char* tags[2] = {"decoder.time_embed.", "decoder.time_embed_r."};
         for (int e = 0; e < 2; ++e) {
             const std::string p2 = tags[e];
-            const auto& t1 = L.st.get(p2 + "linear_1.weight");
-            if (t1.shape.size() != 2 || t1.shape[0] != H) throw IoError("invalid tensor shape for " + p2 + "linear_1.weight");
-            const int64_t fin = t1.shape[1];
+            int64_t fin = 0;
+            if (L.gguf) {
+                const auto& t1 = L.gg.get(p2 + "linear_1.weight");
+                if (t1.ne_at(1) != H || t1.ne_at(2) != 1) throw IoError("invalid tensor shape for " + p2 + "linear_1.weight");
+                fin = t1.ne_at(0);
+            } else {
+                const auto& t1 = L.st.get(p2 + "linear_1.weight");
+                if (t1.shape.size() != 2 || t1.shape[0] != H) throw IoError("invalid tensor shape for " + p2 + "linear_1.weight");
+                fin = t1.shape[1];
+            }
             if (fin != 256) throw Unsupported("timestep embedding input dim must be 256");
             ActType a1, a2, a3;
             m.te[e].w1 = L.finish16(L.mat(p2 + "linear_1.weight", H, fin), a1);
