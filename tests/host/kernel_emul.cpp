@@ -1,0 +1,475 @@
+// Host emulation of the gfx950 kernels (TEST INFRASTRUCTURE, never shipped): every launch_* entry of
+// csrc/kernels.h restated as plain C++ loops over "device" memory that is host memory, plus stub HIP
+// runtime functions.  Linked with the real runtime/*.cpp into libacestep_mi355x_host.so it runs the
+// product's host orchestration (ABI validation, loaders, buffer sizing, pointer offsets, the order and
+// arguments of every launch) on the CPU, so tests can compare whole forwards with the oracle without a
+// GPU.  The arithmetic follows each kernel's documented contract (bf16/fp16 operand rounding, f32
+// epilogues) with double accumulation; it says nothing about the kernels' own correctness, which the
+// -m gpu tests check.
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "kernels.h"
+
+extern "C" {
+hipError_t hipMalloc(void** p, size_t n) {
+    *p = std::calloc(1, n ? n : 1);
+    return *p ? hipSuccess : hipErrorOutOfMemory;
+}
+hipError_t hipFree(void* p) {
+    std::free(p);
+    return hipSuccess;
+}
+hipError_t hipMemcpy(void* d, const void* s, size_t n, hipMemcpyKind) {
+    std::memmove(d, s, n);
+    return hipSuccess;
+}
+hipError_t hipMemcpyAsync(void* d, const void* s, size_t n, hipMemcpyKind, hipStream_t) {
+    std::memmove(d, s, n);
+    return hipSuccess;
+}
+hipError_t hipMemcpy2DAsync(void* d, size_t dp, const void* s, size_t sp, size_t w, size_t h, hipMemcpyKind,
+                            hipStream_t) {
+    for (size_t r = 0; r < h; ++r) std::memmove((char*)d + r * dp, (const char*)s + r * sp, w);
+    return hipSuccess;
+}
+hipError_t hipMemset(void* d, int v, size_t n) {
+    std::memset(d, v, n);
+    return hipSuccess;
+}
+hipError_t hipDeviceSynchronize() { return hipSuccess; }
+hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
+hipError_t hipStreamCreateWithFlags(hipStream_t* s, unsigned int) {
+    *s = reinterpret_cast<hipStream_t>(0x1);
+    return hipSuccess;
+}
+hipError_t hipStreamDestroy(hipStream_t) { return hipSuccess; }
+hipError_t hipSetDevice(int) { return hipSuccess; }
+hipError_t hipGetDeviceCount(int* n) {
+    *n = 1;
+    return hipSuccess;
+}
+hipError_t hipEventCreate(hipEvent_t* e) {
+    *e = reinterpret_cast<hipEvent_t>(0x1);
+    return hipSuccess;
+}
+hipError_t hipEventDestroy(hipEvent_t) { return hipSuccess; }
+hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipSuccess; }
+hipError_t hipEventSynchronize(hipEvent_t) { return hipSuccess; }
+hipError_t hipEventElapsedTime(float* ms, hipEvent_t, hipEvent_t) {
+    *ms = 0.f;
+    return hipSuccess;
+}
+const char* hipGetErrorString(hipError_t) { return "host emulation"; }
+}
+
+namespace acemi {
+namespace {
+
+float bf16f(uint16_t b) {
+    uint32_t u = (uint32_t)b << 16;
+    float f;
+    std::memcpy(&f, &u, 4);
+    return f;
+}
+float f16f(uint16_t b) {
+    _Float16 h;
+    std::memcpy(&h, &b, 2);
+    return (float)h;
+}
+uint16_t to_bf16(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 64u);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+uint16_t to_f16(float f) {
+    _Float16 h = (_Float16)f;
+    uint16_t u;
+    std::memcpy(&u, &h, 2);
+    return u;
+}
+float act_val(bool f16, uint16_t b) { return f16 ? f16f(b) : bf16f(b); }
+uint16_t to_act(bool f16, float f) { return f16 ? to_f16(f) : to_bf16(f); }
+float silu(float x) { return x / (1.0f + expf(-x)); }
+int vperm(int k) {
+    const int w = k & 15, g = w >> 2;
+    const int gp = (g == 1) ? 2 : (g == 2 ? 1 : g);
+    return (k & ~15) | (gp << 2) | (w & 3);
+}
+
+// weight element (n, k) as the MFMA sees it
+float weight_val(const WeightView& W, int K, int n, int k) {
+    switch (W.fmt) {
+        case WF_BF16: return bf16f(((const uint16_t*)W.q)[(int64_t)n * W.ld + k]);
+        case WF_F16: return f16f(((const uint16_t*)W.q)[(int64_t)n * W.ld + k]);
+        case WF_Q8_0: {
+            const int8_t q = ((const int8_t*)W.q)[(int64_t)n * K + k];
+            return bf16f(to_bf16((float)q * W.s[(int64_t)n * (K / 32) + k / 32]));
+        }
+        case WF_Q6_K: {
+            const int8_t q = ((const int8_t*)W.q)[(int64_t)n * K + k];
+            return bf16f(to_bf16((float)q * W.s[(int64_t)n * (K / 16) + k / 16]));
+        }
+        case WF_Q4_K: {
+            const int blk = k / 32, i = k % 32;
+            const int dw = i / 8, r = i % 8;  // dword dw: low nibbles k 0..3, high nibbles k 4..7
+            const uint8_t byte = ((const uint8_t*)W.q)[(int64_t)n * (K / 2) + blk * 16 + dw * 4 + (r & 3)];
+            const int q = r < 4 ? (byte & 0xF) : (byte >> 4);
+            const float* sm = W.s + ((int64_t)n * (K / 32) + blk) * 2;
+            return bf16f(to_bf16(fmaf((float)q, sm[0], -sm[1])));
+        }
+        default: throw std::runtime_error("emul gemm: bad weight format");
+    }
+}
+
+}  // namespace
+
+void gemm_force_variant(int) {}
+
+void launch_gemm(const uint16_t* A, int lda, const WeightView& W, int M, int N, int K, const GemmEpilogue& e,
+                 hipStream_t) {
+    ACEMI_CHECK(M >= 1 && N % 128 == 0 && K % 64 == 0 && K >= 64, "gemm: unsupported shape");
+    const bool af16 = W.fmt == WF_F16;  // activation type of the kernel; quantized weights -> bf16
+    std::vector<float> wcol((size_t)K);
+    std::vector<double> acc((size_t)M * N);
+    std::vector<float> arow((size_t)K);
+    std::vector<float> wt((size_t)N * K);
+    for (int n = 0; n < N; ++n)
+        for (int k = 0; k < K; ++k) wt[(size_t)n * K + k] = weight_val(W, K, n, k);
+    for (int m = 0; m < M; ++m) {
+        for (int k = 0; k < K; ++k) arow[k] = act_val(af16, A[(int64_t)m * lda + k]);
+        for (int n = 0; n < N; ++n) {
+            double s = 0;
+            const float* w = &wt[(size_t)n * K];
+            for (int k = 0; k < K; ++k) s += (double)arow[k] * w[k];
+            acc[(size_t)m * N + n] = s;
+        }
+    }
+    for (int m = 0; m < M; ++m) {
+        if (e.kind == EPI_SWIGLU) {
+            for (int n = 0; n < N; n += 32)
+                for (int j = 0; j < 16; ++j) {
+                    const float g = (float)acc[(size_t)m * N + n + j], u = (float)acc[(size_t)m * N + n + 16 + j];
+                    e.c_act[(int64_t)m * e.ldc + (n >> 1) + j] = to_act(af16, silu(g) * u);
+                }
+            continue;
+        }
+        for (int n = 0; n < N; ++n) {
+            float v = (float)acc[(size_t)m * N + n];
+            switch (e.kind) {
+                case EPI_STORE_F32:
+                    if (e.bias) v += e.bias[n];
+                    e.c_f32[(int64_t)m * e.ldc + n] = v;
+                    break;
+                case EPI_STORE_ACT:
+                    if (e.bias) v += e.bias[n];
+                    e.c_act[(int64_t)m * e.ldc + n] = to_act(af16, v);
+                    break;
+                case EPI_RESID_GATED: {
+                    const int item = m / e.rows_per_item;
+                    float* xp = e.c_f32 + (int64_t)m * e.ldc + n;
+                    *xp = *xp + v * e.gate[(int64_t)item * e.gate_stride + n];
+                    break;
+                }
+                case EPI_RESID: e.c_f32[(int64_t)m * e.ldc + n] += v; break;
+                case EPI_PROJ_OUT: {
+                    const int item = m / e.rows_per_item, pp = m - item * e.rows_per_item;
+                    const int kpos = n / e.out_ch, c = n - kpos * e.out_ch, t = pp * e.patch + kpos;
+                    if (t < e.out_T) e.c_f32[((int64_t)item * e.out_T + t) * e.out_ch + c] = v + e.bias[c];
+                    break;
+                }
+                default: throw std::runtime_error("emul gemm: bad epilogue");
+            }
+        }
+    }
+}
+
+void launch_gemm(ActType t, const uint16_t* A, int lda, const uint16_t* W, int ldw, int M, int N, int K,
+                 const GemmEpilogue& epi, hipStream_t s) {
+    WeightView w;
+    w.fmt = t == ActType::F16 ? WF_F16 : WF_BF16;
+    w.q = W;
+    w.ld = ldw;
+    launch_gemm(A, lda, w, M, N, K, epi, s);
+}
+
+void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t) {
+    const int D = 128, rep = a.Hq / a.Hkv;
+    std::vector<double> s((size_t)a.nk_pad), o((size_t)D);
+    auto val = [&](const uint16_t* base, int64_t idx, int64_t plane) {
+        double v = f16f(base[idx]);
+        if (a.split && plane > 0) v += f16f(base[idx + plane]);
+        return v;
+    };
+    for (int b = 0; b < a.B; ++b)
+        for (int h = 0; h < a.Hq; ++h) {
+            const int hk = h / rep;
+            for (int q = 0; q < a.nq; ++q) {
+                const int64_t qb = (((int64_t)b * a.Hq + h) * a.nq_pad + q) * D;
+                double mx = -INFINITY;
+                for (int k = 0; k < a.nk_pad; ++k) {
+                    double bias = a.kbias ? a.kbias[(int64_t)b * a.nk_pad + k] : (k < a.nk ? 0.0 : -INFINITY);
+                    if (a.window > 0 && std::abs(q - k) > a.window) bias = -INFINITY;
+                    if (std::isinf(bias)) {
+                        s[k] = -INFINITY;
+                        continue;
+                    }
+                    const int64_t kb = (((int64_t)b * a.Hkv + hk) * a.nk_pad + k) * D;
+                    double dot = 0;
+                    for (int d = 0; d < D; ++d) dot += val(a.q, qb + d, a.q_plane) * val(a.k, kb + d, a.k_plane);
+                    s[k] = dot * a.scale + bias;
+                    mx = std::max(mx, s[k]);
+                }
+                std::fill(o.begin(), o.end(), 0.0);
+                double sum = 0;
+                for (int k = 0; k < a.nk_pad; ++k) {
+                    if (std::isinf(s[k])) continue;
+                    const double p = std::exp(s[k] - mx);
+                    sum += p;
+                    const int pk = vperm(k % 16) + (k / 16) * 16;  // V^T keys are stored permuted in 16-groups
+                    for (int d = 0; d < D; ++d)
+                        o[d] += p * val(a.vt, (((int64_t)b * a.Hkv + hk) * D + d) * a.nk_pad + pk, a.v_plane);
+                }
+                uint16_t* out = a.out + ((int64_t)b * a.nq + q) * a.Hq * D + h * D;
+                for (int d = 0; d < D; ++d) out[d] = to_act(out_t == ActType::F16, (float)(o[d] / sum));  // 0/0 -> NaN
+            }
+        }
+}
+
+void launch_pack_input(ActType t, const float* hidden, const float* context, int B, int T, int Np, int P, int audio,
+                       int cdim, uint16_t* out, hipStream_t, bool x3) {
+    const int cin = audio + cdim, rowlen = P * cin;
+    for (int b = 0; b < B; ++b)
+        for (int p = 0; p < Np; ++p)
+            for (int k = 0; k < P; ++k)
+                for (int c = 0; c < cin; ++c) {
+                    const int tt = p * P + k;
+                    float v = 0.f;
+                    if (tt < T) {
+                        if (c < cdim) {
+                            if (context) v = context[((int64_t)b * T + tt) * cdim + c];
+                        } else if (hidden) {
+                            v = hidden[((int64_t)b * T + tt) * audio + (c - cdim)];
+                        }
+                    }
+                    const int64_t row = (int64_t)b * Np + p, col = (int64_t)k * cin + c;
+                    if (x3) {
+                        uint16_t* o = out + row * 3 * rowlen + col;
+                        o[0] = o[rowlen] = to_f16(v);
+                        o[2 * rowlen] = to_f16(v - f16f(o[0]));
+                    } else {
+                        out[row * rowlen + col] = to_act(t == ActType::F16, v);
+                    }
+                }
+}
+
+void launch_to_act(ActType t, const float* in, int64_t n, bool sl, uint16_t* out, hipStream_t) {
+    for (int64_t i = 0; i < n; ++i) out[i] = to_act(t == ActType::F16, sl ? silu(in[i]) : in[i]);
+}
+
+void launch_rmsnorm_mod(ActType t, const float* x, int M, int H, const float* w, const float* scale, const float* shift,
+                        int64_t mod_stride, int rows_per_item, float eps, uint16_t* out, hipStream_t, bool x3) {
+    for (int m = 0; m < M; ++m) {
+        const float* xr = x + (int64_t)m * H;
+        double ss = 0;
+        for (int i = 0; i < H; ++i) ss += (double)xr[i] * xr[i];
+        const float sc = 1.0f / sqrtf((float)(ss / H) + eps);
+        const int item = m / rows_per_item;
+        uint16_t* o = out + (int64_t)m * H * (x3 ? 3 : 1);
+        for (int i = 0; i < H; ++i) {
+            float y = xr[i] * sc * w[i];
+            if (scale) y = y * (scale[(int64_t)item * mod_stride + i] + 1.0f) + shift[(int64_t)item * mod_stride + i];
+            if (x3) {
+                o[i] = o[H + i] = to_f16(y);
+                o[2 * H + i] = to_f16(y - f16f(o[i]));
+            } else {
+                o[i] = to_act(t == ActType::F16, y);
+            }
+        }
+    }
+}
+
+void launch_attn_prep(const PrepArgs& a, hipStream_t) {
+    auto head = [&](bool isq, int b, int h) {
+        const float* w = isq ? a.q_norm : a.k_norm;
+        const int col = (isq ? a.q_col : a.k_col) + h * 128;
+        uint16_t* base = isq ? a.qh + ((int64_t)b * a.hq + h) * a.n_pad * 128 : a.kh + ((int64_t)b * a.hkv + h) * a.n_pad * 128;
+        const int64_t plane = isq ? a.q_plane : a.k_plane;
+        for (int n = 0; n < a.n_pad; ++n) {
+            float y[128] = {};
+            if (n < a.n_tok) {
+                const float* row = a.src + ((int64_t)b * a.n_tok + n) * a.ld + col;
+                float ss = 0;
+                for (int d = 0; d < 128; ++d) ss += row[d] * row[d];
+                const float sc = 1.0f / sqrtf(ss / 128.0f + a.eps);
+                for (int d = 0; d < 128; ++d) y[d] = w ? row[d] * sc * w[d] : row[d];
+                if (a.rope_cos) {
+                    for (int d = 0; d < 64; ++d) {
+                        const float c = a.rope_cos[(int64_t)n * 64 + d], s = a.rope_sin[(int64_t)n * 64 + d];
+                        const float y0 = y[d], y1 = y[d + 64];
+                        y[d] = y0 * c - y1 * s;
+                        y[d + 64] = y0 * s + y1 * c;
+                    }
+                }
+            }
+            uint16_t* dst = base + (int64_t)n * 128;
+            for (int d = 0; d < 128; ++d) {
+                dst[d] = to_f16(y[d]);
+                if (plane > 0) dst[plane + d] = to_f16(y[d] - f16f(dst[d]));
+            }
+        }
+    };
+    for (int b = 0; b < a.B; ++b) {
+        if (a.q_col >= 0)
+            for (int h = 0; h < a.hq; ++h) head(true, b, h);
+        if (a.k_col >= 0)
+            for (int h = 0; h < a.hkv; ++h) head(false, b, h);
+        if (a.v_col >= 0)
+            for (int h = 0; h < a.hkv; ++h)
+                for (int d = 0; d < 128; ++d) {
+                    uint16_t* dst = a.vt + (((int64_t)b * a.hkv + h) * 128 + d) * a.n_pad;
+                    for (int p = 0; p < a.n_pad; ++p) {
+                        const int n = (p / 16) * 16 + vperm(p % 16);
+                        const float v = n < a.n_tok ? a.src[((int64_t)b * a.n_tok + n) * a.ld + a.v_col + h * 128 + d] : 0.f;
+                        dst[p] = to_f16(v);
+                        if (a.v_plane > 0) dst[a.v_plane + p] = to_f16(v - f16f(dst[p]));
+                    }
+                }
+    }
+}
+
+void launch_key_bias(const int32_t* mask, int B, int frames, int patch, int nk, int nk_pad, float* kbias, hipStream_t) {
+    for (int b = 0; b < B; ++b)
+        for (int k = 0; k < nk_pad; ++k) {
+            bool ok = k < nk;
+            if (ok && mask) {
+                bool any = false;
+                for (int j = 0; j < patch; ++j) {
+                    const int f = k * patch + j;
+                    if (f < frames && mask[(int64_t)b * frames + f] != 0) any = true;
+                }
+                ok = any;
+            }
+            kbias[(int64_t)b * nk_pad + k] = ok ? 0.f : -INFINITY;
+        }
+}
+
+void launch_timestep_freq(const float* t, const float* r, int B, int dim, float scale, float log_max, float* f,
+                          hipStream_t) {
+    const int half = dim / 2;
+    for (int b = 0; b < B; ++b) {
+        float tv = t[b];
+        if (r) tv = tv - r[b];
+        const float ts = tv * scale;
+        for (int i = 0; i < half; ++i) {
+            const float arg = ts * expf((-log_max * (float)i) / (float)half);
+            f[(int64_t)b * dim + i] = cosf(arg);
+            f[(int64_t)b * dim + i + half] = sinf(arg);
+        }
+        if (dim & 1) f[(int64_t)b * dim + dim - 1] = 0.f;
+    }
+}
+
+void launch_gemv(ActType t, const uint16_t* x, int M, const uint16_t* W, int N, int K, const float* bias, bool sl,
+                 bool accumulate, float* y, hipStream_t) {
+    const bool f16 = t == ActType::F16;
+    for (int m = 0; m < M; ++m)
+        for (int n = 0; n < N; ++n) {
+            double s = 0;
+            for (int k = 0; k < K; ++k) s += (double)act_val(f16, x[(int64_t)m * K + k]) * act_val(f16, W[(int64_t)n * K + k]);
+            float v = (float)s;
+            if (bias) v += bias[n];
+            if (sl) v = silu(v);
+            float* yp = y + (int64_t)m * N + n;
+            *yp = accumulate ? *yp + v : v;
+        }
+}
+
+void launch_layer_mods(const float* tables, const float* proj, int L, int B, int H, float* mod, hipStream_t) {
+    for (int l = 0; l < L; ++l)
+        for (int b = 0; b < B; ++b)
+            for (int j = 0; j < 6; ++j)
+                for (int c = 0; c < H; ++c)
+                    mod[(((int64_t)l * B + b) * 6 + j) * H + c] = tables[((int64_t)l * 6 + j) * H + c] + proj[((int64_t)b * 6 + j) * H + c];
+}
+
+void launch_out_mods(const float* table, const float* tt, const float* tr, int B, int H, float* om, hipStream_t) {
+    for (int b = 0; b < B; ++b)
+        for (int j = 0; j < 2; ++j)
+            for (int c = 0; c < H; ++c)
+                om[((int64_t)b * 2 + j) * H + c] = table[(int64_t)j * H + c] + (tt[(int64_t)b * H + c] + tr[(int64_t)b * H + c]);
+}
+
+void launch_euler(float* xt, const float* v, int64_t n, float dt, hipStream_t) {
+    for (int64_t i = 0; i < n; ++i) xt[i] = xt[i] - v[i] * dt;
+}
+
+// ---------------------------------------------------------------- VAE
+void launch_conv_gemm(const ConvGemmArgs& a, hipStream_t) {
+    ACEMI_CHECK(a.Cin % 64 == 0 && a.N % 128 == 0 && a.M >= 1 && a.taps >= 1, "conv_gemm: unsupported shape");
+    const int K = a.taps * a.Cin;
+    std::vector<float> row((size_t)K);
+    for (int m = 0; m < a.M; ++m) {
+        for (int tap = 0; tap < a.taps; ++tap) {
+            const int t = m * a.in_stride + tap * a.dil - a.pad;
+            for (int c = 0; c < a.Cin; ++c)
+                row[(size_t)tap * a.Cin + c] = (t >= 0 && t < a.T_in) ? f16f(a.S[(int64_t)t * a.Cin + c]) : 0.f;
+        }
+        for (int n = 0; n < a.N; ++n) {
+            double s = 0;
+            const uint16_t* w = a.W + (int64_t)n * K;
+            for (int k = 0; k < K; ++k) s += (double)row[k] * f16f(w[k]);
+            int u, co;
+            if (a.up > 1) {
+                const int rr = n / a.Cout;
+                co = n - rr * a.Cout;
+                u = m * a.up + rr - a.crop;
+            } else {
+                co = n;
+                u = m;
+            }
+            if (u < 0 || u >= a.T_out) continue;
+            float v = (float)s;
+            if (a.bias) v += a.bias[co];
+            const int64_t o = (int64_t)u * a.Cout + co;
+            if (a.resid) v = a.X[o] + v;
+            if (a.store_x) a.X[o] = v;
+            if (a.S_out) {
+                float y = v;
+                if (a.snake_ea) {
+                    float sv = sinf(a.snake_ea[co] * v);
+                    y = v + (sv * sv) / a.snake_eb[co];
+                }
+                a.S_out[o] = to_f16(y);
+            }
+        }
+    }
+}
+
+void launch_to_f16(const float* x, int64_t n, uint16_t* y, hipStream_t) {
+    for (int64_t i = 0; i < n; ++i) y[i] = to_f16(x[i]);
+}
+
+void launch_pack_f16(const float* x, int64_t rows, int C, int Cpad, uint16_t* y, hipStream_t) {
+    for (int64_t r = 0; r < rows; ++r)
+        for (int c = 0; c < Cpad; ++c) y[r * Cpad + c] = c < C ? to_f16(x[r * C + c]) : (uint16_t)0;
+}
+
+void launch_conv_out(const uint16_t* S, int T, int C, const uint16_t* W, int out_ch, float* out, hipStream_t) {
+    for (int t = 0; t < T; ++t)
+        for (int o = 0; o < out_ch; ++o) {
+            double s = 0;
+            for (int k = 0; k < 7; ++k) {
+                const int ti = t + k - 3;
+                if (ti < 0 || ti >= T) continue;
+                for (int c = 0; c < C; ++c) s += (double)f16f(S[(int64_t)ti * C + c]) * f16f(W[((int64_t)o * 7 + k) * C + c]);
+            }
+            out[(int64_t)t * out_ch + o] = (float)s;
+        }
+}
+
+}  // namespace acemi

@@ -1,0 +1,173 @@
+"""The product's host code (runtime/*.cpp: ABI, loaders, engine orchestration) linked against a host
+emulation of the kernels (tests/host/kernel_emul.cpp, each launch_* restated as plain loops on
+host memory) and driven through the same ctypes bridge as the GPU tests.  This checks on the CPU
+that every buffer, offset and launch argument of the DiT forward, the quantized and GGUF weight
+paths, the batched/sampler entries and the VAE decode/encode is wired as the oracle's graph says;
+the kernels themselves are checked by the -m gpu tests."""
+import os
+import shutil
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+CSRC = os.path.join(ROOT, "ace-step-1.5-ggml_amd", "csrc")
+CLANG = "/opt/rocm/llvm/bin/clang++"
+RUNTIME = ("json.cpp", "gguf.cpp", "quant.cpp", "model.cpp", "engine.cpp", "vae.cpp", "abi.cpp", "selftest.cpp")
+
+
+@pytest.fixture(scope="module")
+def host_lib():
+    if not os.path.exists(CLANG):
+        pytest.skip("host clang++ not available")
+    out = os.path.join(tempfile.mkdtemp(prefix="acemi_hl_"), "libacestep_mi355x_host.so")
+    srcs = [os.path.join(CSRC, "runtime", f) for f in RUNTIME] + [os.path.join(ROOT, "tests", "host", "kernel_emul.cpp")]
+    subprocess.run([CLANG, "-std=c++17", "-O2", "-fPIC", "-shared", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
+                    "-I" + CSRC, "-ffp-contract=off", "-pthread", "-Wno-unused-result", "-Wl,-Bsymbolic", *srcs,
+                    "-o", out], check=True)
+    return out
+
+
+@pytest.fixture(scope="module")
+def tiny_ckpt():
+    from acestep_mi355x.synthetic import TINY_CONFIG, write_checkpoint
+    d = tempfile.mkdtemp(prefix="acemi_he_")
+    write_checkpoint(d, TINY_CONFIG, seed=0, dtype="BF16")
+    return d
+
+
+def bridge(lib):
+    from acestep_mi355x.capi import GGMLCAPIBridge
+    return GGMLCAPIBridge(lib_path=lib)
+
+
+def rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / np.linalg.norm(b))
+
+
+def engine_view(W):
+    from test_gpu_forward import engine_view as ev
+    return ev(W)
+
+
+def inputs(seed, T, L, H=256):
+    rng = np.random.default_rng(seed)
+    return (rng.standard_normal((T, 64)).astype(np.float32), rng.standard_normal((T, 128)).astype(np.float32),
+            rng.standard_normal((L, H)).astype(np.float32))
+
+
+def test_dit_forward_bf16_with_masks(host_lib, tiny_ckpt):
+    from oracle.dit_oracle import DitWeights, forward_with_floor
+    br = bridge(host_lib)
+    br.load_dit(tiny_ckpt)
+    h, c, e = inputs(3, 77, 13)
+    mask = np.ones(77, np.int32)
+    mask[70:] = 0
+    emask = np.ones(13, np.int32)
+    emask[10:] = 0
+    got = br.dit_forward_tfirst(h, c, e, mask, emask, 0.8, 0.3)
+    ref, floor = forward_with_floor(DitWeights(tiny_ckpt), h, c, e, mask, emask, 77, 13, 0.8, 0.3)
+    assert rel(got, ref) <= max(1e-3, 1.5 * floor), (rel(got, ref), floor)
+    br.close()
+
+
+@pytest.mark.parametrize("qtype", ["q8_0", "q4_k", "q6_k"])
+def test_dit_forward_online_quantized(host_lib, tiny_ckpt, monkeypatch, qtype):
+    from oracle.dit_oracle import DitWeights, forward_with_floor
+    monkeypatch.setenv("ACE_GGML_DIT_WEIGHT_QTYPE", qtype)
+    br = bridge(host_lib)
+    br.load_dit(tiny_ckpt)
+    h, c, e = inputs(5, 64, 9)
+    got = br.dit_forward_tfirst(h, c, e, None, None, 0.6, 0.6)
+    ref, floor = forward_with_floor(engine_view(DitWeights(tiny_ckpt, qtype=qtype)), h, c, e, None, None, 64, 9,
+                                    0.6, 0.6)
+    assert rel(got, ref) <= max(1e-3, 1.5 * floor), (rel(got, ref), floor)
+    br.close()
+
+
+@pytest.mark.parametrize("quant", ["Q8", "Q4", "F16"])
+def test_dit_forward_gguf(host_lib, tiny_ckpt, quant):
+    from acestep_mi355x.synthetic import write_gguf
+    from oracle.dit_oracle import DitWeights, forward_with_floor
+    d = tempfile.mkdtemp(prefix="acemi_heg_")
+    shutil.copy(os.path.join(tiny_ckpt, "config.json"), d)
+    path = write_gguf(os.path.join(tiny_ckpt, "model.safetensors"), os.path.join(d, "model.gguf"), quant=quant)
+    br = bridge(host_lib)
+    br.load_dit(d)
+    h, c, e = inputs(7, 50, 6)
+    got = br.dit_forward_tfirst(h, c, e, None, None, 0.5, 0.5)
+    ref, floor = forward_with_floor(engine_view(DitWeights(d, gguf=path)), h, c, e, None, None, 50, 6, 0.5, 0.5)
+    assert rel(got, ref) <= max(1e-3, 1.5 * floor), (rel(got, ref), floor)
+    br.close()
+
+
+def test_batched_entry_and_sampler_wiring(host_lib, tiny_ckpt):
+    """ace_mi_dit_forward_batched / ace_mi_dit_sample on "device" pointers (host memory here)."""
+    br = bridge(host_lib)
+    br.load_dit(tiny_ckpt)
+    B, T, L = 3, 40, 7
+    rng = np.random.default_rng(11)
+    h = rng.standard_normal((B, T, 64)).astype(np.float32)
+    c = rng.standard_normal((B, T, 128)).astype(np.float32)
+    e = rng.standard_normal((B, L, 256)).astype(np.float32)
+    t = np.array([0.9, 0.5, 0.2], np.float32)
+    out = np.empty((B, T, 64), np.float32)
+    p = lambda a: a.ctypes.data
+    br.dit_forward_batched_device(B, T, L, p(h), p(c), p(e), 0, 0, p(t), p(t), p(out), 0)
+    for b in range(B):
+        ser = br.dit_forward_tfirst(h[b], c[b], e[b], None, None, float(t[b]), float(t[b]))
+        np.testing.assert_array_equal(out[b], ser)
+    # device sampler == host Euler loop
+    sched = [1.0, 0.75, 0.5, 0.25]
+    xt = h.copy()
+    br.dit_sample_device(B, T, L, p(xt), p(c), p(e), 0, 0, sched, 0)
+    ref = h.copy()
+    for i, ti in enumerate(sched):
+        for b in range(B):
+            v = br.dit_forward_tfirst(ref[b], c[b], e[b], None, None, ti, ti)
+            dt = ti if i + 1 == len(sched) else ti - sched[i + 1]
+            ref[b] = ref[b] - v * np.float32(dt)
+    np.testing.assert_allclose(xt, ref, rtol=1e-5, atol=1e-5)
+    br.close()
+
+
+def test_vae_decode_encode(host_lib):
+    from acestep_mi355x.synthetic import VAE_TINY_CONFIG, write_vae_checkpoint
+    from oracle.vae_oracle import VaeWeights, decode, decode_with_floor, encode
+    d = tempfile.mkdtemp(prefix="acemi_hev_")
+    write_vae_checkpoint(d, VAE_TINY_CONFIG, seed=1)
+    br = bridge(host_lib)
+    br.load_vae(d)
+    W = VaeWeights(d)
+    lat = np.random.default_rng(2).standard_normal((21, 64)).astype(np.float32)
+    ref, floor = decode_with_floor(W, lat)
+    n = br.vae_out_len(21)
+    got = br.vae_decode_tfirst(lat)[:n]
+    assert got.shape == ref.shape and rel(got, ref) <= max(1e-3, 1.5 * floor), (rel(got, ref), floor)
+    audio = np.random.default_rng(3).standard_normal((126, 2)).astype(np.float32)
+    z = br.vae_encode_tfirst(audio)
+    zr = encode(W, audio)
+    assert z.shape == zr.shape and rel(z, zr) < 2e-3, rel(z, zr)
+    br.close()
+
+
+def test_abi_error_paths(host_lib, tiny_ckpt):
+    import ctypes
+    br = bridge(host_lib)
+    fp = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+    out = np.zeros((10, 64), np.float32)
+    assert br.lib.ace_ggml_dit_forward(br.ctx, None, None, None, None, None, 10, 0, 0.5, 0.5, fp(out), out.nbytes) == 1
+    assert br._last_error() == "dit not loaded"
+    assert br.lib.ace_ggml_load_dit(br.ctx, b"/nonexistent") == 3
+    br.load_dit(tiny_ckpt)
+    assert br.lib.ace_ggml_dit_forward(br.ctx, None, None, None, None, None, 10, 0, 0.5, 0.5, fp(out),
+                                       out.nbytes - 4) == 2
+    assert br._last_error() == "output buffer too small"
+    assert br.lib.ace_ggml_dit_forward(br.ctx, None, None, None, None, None, 0, 0, 0.5, 0.5, fp(out), out.nbytes) == 2
+    # enc_len > 0 without encoder states
+    assert br.lib.ace_ggml_dit_forward(br.ctx, None, None, None, None, None, 10, 4, 0.5, 0.5, fp(out), out.nbytes) == 1
+    br.close()
