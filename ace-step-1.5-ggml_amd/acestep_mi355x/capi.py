@@ -30,6 +30,7 @@ ACE_GGML_ERR_UNSUPPORTED = 4
 EXPORTED_SYMBOLS = (
     "ace_ggml_create", "ace_ggml_destroy", "ace_ggml_last_error", "ace_ggml_load_dit", "ace_ggml_dit_forward",
     "ace_mi_create_on_device", "ace_mi_dit_get_info", "ace_mi_dit_forward_batched", "ace_mi_dit_sample",
+    "ace_mi_dit_sample_ex",
     "ace_mi_profile_enable", "ace_mi_profile_reset", "ace_mi_profile_get", "ace_mi_probe_gemm",
     "ace_mi_synchronize", "ace_mi_kernel_gemm", "ace_mi_kernel_attention", "ace_mi_bench_gemm",
     "ace_mi_gemm_variant", "ace_ggml_load_vae", "ace_ggml_vae_get_info", "ace_ggml_vae_decode",
@@ -97,6 +98,8 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.ace_mi_dit_forward_batched.restype = ctypes.c_int
     lib.ace_mi_dit_sample.argtypes = [vp, i32, vp, vp, vp, vp, vp, i32, i32, fp, i32, vp]
     lib.ace_mi_dit_sample.restype = ctypes.c_int
+    lib.ace_mi_dit_sample_ex.argtypes = [vp, i32, vp, vp, vp, vp, vp, i32, i32, fp, i32, i32, vp, i32, vp, vp, i32, vp]
+    lib.ace_mi_dit_sample_ex.restype = ctypes.c_int
     lib.ace_mi_profile_enable.argtypes = [vp, i32]
     lib.ace_mi_profile_enable.restype = ctypes.c_int
     lib.ace_mi_profile_reset.argtypes = [vp]
@@ -285,6 +288,19 @@ class GGMLCAPIBridge:
                                         d_mask or None, d_enc_mask or None, int(seq_len), int(enc_len),
                                         _fptr(sched), int(sched.shape[0]), stream or None)
         self._ensure_ok(st, "ace_mi_dit_sample")
+
+    def dit_sample_ex_device(self, batch: int, seq_len: int, enc_len: int, d_xt: int, d_context: int, d_enc: int,
+                             d_mask: int, d_enc_mask: int, schedule: List[float], sde: bool = False, d_noise: int = 0,
+                             cover_steps: int = -1, d_context_nc: int = 0, d_enc_nc: int = 0,
+                             cache_cross: bool = True, stream: int = 0) -> None:
+        """The MLX/PyTorch generation loop on the device (ace_mi_dit_sample_ex)."""
+        sched = np.ascontiguousarray(schedule, dtype=np.float32)
+        st = self.lib.ace_mi_dit_sample_ex(self.ctx, int(batch), d_xt, d_context or None, d_enc or None,
+                                           d_mask or None, d_enc_mask or None, int(seq_len), int(enc_len),
+                                           _fptr(sched), int(sched.shape[0]), 1 if sde else 0, d_noise or None,
+                                           int(cover_steps), d_context_nc or None, d_enc_nc or None,
+                                           1 if cache_cross else 0, stream or None)
+        self._ensure_ok(st, "ace_mi_dit_sample_ex")
 
     def synchronize(self) -> None:
         self._ensure_ok(self.lib.ace_mi_synchronize(self.ctx), "ace_mi_synchronize")

@@ -106,3 +106,38 @@ def euler_sample_local(bridge, cond: Conditioning, items: Sequence[int], schedul
                              list(schedule), stream)
     bridge.synchronize()
     return xt
+
+
+def generate_local(bridge, cond: Conditioning, items: Sequence[int], schedule: Sequence[float],
+                   infer_method: str = "ode", seed: Optional[int] = None, cover_steps: int = -1,
+                   cond_non_cover: Optional[Conditioning] = None, cache_cross: bool = True,
+                   stream: int = 0) -> torch.Tensor:
+    """The reference generation loop (acestep/mlx_dit/generate.py:143-199) for this rank's `items`
+    through `ace_mi_dit_sample_ex`: ODE or SDE stepping, the audio-cover switch to non-cover
+    conditions at `cover_steps`, and the cross-attention cache.  SDE re-noise draws come from a
+    torch generator seeded with `seed` on the device (the MLX draws cannot be reproduced)."""
+    dev = cond.noise.device
+    idx = torch.tensor(list(items), dtype=torch.long, device=dev)
+    sel = lambda t: t.index_select(0, idx).contiguous() if t is not None else None
+    xt = sel(cond.noise)
+    ctx, enc, em, mk = sel(cond.context), sel(cond.enc), sel(cond.enc_mask), sel(cond.mask)
+    ctx_nc = sel(cond_non_cover.context) if cond_non_cover is not None else None
+    enc_nc = sel(cond_non_cover.enc) if cond_non_cover is not None else None
+    B, T, C = xt.shape
+    L = enc.shape[1]
+    noise = None
+    if infer_method == "sde" and len(schedule) > 1:
+        g = torch.Generator(device=dev)
+        if seed is not None:
+            g.manual_seed(int(seed))
+        noise = torch.randn((len(schedule) - 1, B, T, C), generator=g, device=dev, dtype=torch.float32)
+    elif infer_method not in ("ode", "sde"):
+        raise ValueError(infer_method)
+    torch.cuda.current_stream().synchronize()
+    ptr = lambda t: t.data_ptr() if t is not None else 0
+    bridge.dit_sample_ex_device(B, T, L, xt.data_ptr(), ptr(ctx), ptr(enc), ptr(mk), ptr(em), list(schedule),
+                                sde=infer_method == "sde", d_noise=ptr(noise), cover_steps=cover_steps,
+                                d_context_nc=ptr(ctx_nc), d_enc_nc=ptr(enc_nc), cache_cross=cache_cross,
+                                stream=stream)
+    bridge.synchronize()
+    return xt

@@ -125,6 +125,8 @@ void launch_out_mods(const float* out_table, const float* temb_t, const float* t
                      float* outmod, hipStream_t s);
 // xt -= v * dt
 void launch_euler(float* xt, const float* v, int64_t n, float dt, hipStream_t s);
+// SDE re-noise step: xt = t_next * noise + (1 - t_next) * (xt - v * t)
+void launch_sde(float* xt, const float* v, const float* noise, int64_t n, float t, float t_next, hipStream_t s);
 
 // ------------------------------------------------------------ VAE decoder (kernels/vae.hip)
 // Implicit-GEMM conv on fp16 time-major activations.  A row (m, tap) = S[m + tap*dil - pad]

@@ -374,6 +374,17 @@ __global__ void euler_kernel(float* __restrict__ xt, const float* __restrict__ v
         xt[i] = __fsub_rn(xt[i], __fmul_rn(v[i], dt));
 }
 
+// SDE step of the reference generation loop (acestep/mlx_dit/generate.py:183-192):
+// x0 = xt - v*t ; xt = t_next*noise + (1 - t_next)*x0
+__global__ void sde_kernel(float* __restrict__ xt, const float* __restrict__ v, const float* __restrict__ noise,
+                           int64_t n, float t, float t_next) {
+    const float keep = __fsub_rn(1.0f, t_next);
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float x0 = __fsub_rn(xt[i], __fmul_rn(v[i], t));
+        xt[i] = __fadd_rn(__fmul_rn(t_next, noise[i]), __fmul_rn(keep, x0));
+    }
+}
+
 inline dim3 grid_for(int64_t n, int block = 256) {
     int64_t g = (n + block - 1) / block;
     if (g > 8192) g = 8192;
@@ -419,6 +430,11 @@ void launch_rmsnorm_mod(ActType t, const float* x, int M, int H, const float* w,
         else ACEMI_RMS(false, 4, false);
     }
 #undef ACEMI_RMS
+    ACEMI_HIP(hipGetLastError());
+}
+
+void launch_sde(float* xt, const float* v, const float* noise, int64_t n, float t, float t_next, hipStream_t s) {
+    hipLaunchKernelGGL(sde_kernel, grid_for(n), dim3(256), 0, s, xt, v, noise, n, t, t_next);
     ACEMI_HIP(hipGetLastError());
 }
 

@@ -283,13 +283,18 @@ ace_ggml_status ace_mi_dit_forward_batched(ace_ggml_context* ctx, int32_t batch,
     return ACE_GGML_OK;
 }
 
-ace_ggml_status ace_mi_dit_sample(ace_ggml_context* ctx, int32_t batch, float* d_xt, const float* d_context,
-                                  const float* d_enc, const int32_t* d_mask, const int32_t* d_enc_mask,
-                                  int32_t seq_len, int32_t enc_len, const float* schedule, int32_t n_steps,
-                                  void* stream) {
+namespace {
+// The generation loop shared by ace_mi_dit_sample (the C sampler, acestep_ggml.cpp:2042-2086) and
+// ace_mi_dit_sample_ex (the Python/MLX loop, acestep/mlx_dit/generate.py:143-199).
+ace_ggml_status run_sampler(ace_ggml_context* ctx, int32_t batch, float* d_xt, const float* d_context,
+                            const float* d_enc, const int32_t* d_mask, const int32_t* d_enc_mask, int32_t seq_len,
+                            int32_t enc_len, const float* schedule, int32_t n_steps, bool sde, const float* d_noise,
+                            int32_t cover_steps, const float* d_context_nc, const float* d_enc_nc, bool cache_cross,
+                            void* stream) {
     if (!ctx || !d_xt || seq_len <= 0 || batch <= 0 || !schedule || n_steps <= 0) return ACE_GGML_ERR_INVALID_ARG;
     if (!ctx->dit) return set_error(ctx, ACE_GGML_ERR, "dit not loaded");
     if (enc_len > 0 && !d_enc) return set_error(ctx, ACE_GGML_ERR_INVALID_ARG, "encoder_hidden_states is null");
+    if (sde && n_steps > 1 && !d_noise) return set_error(ctx, ACE_GGML_ERR_INVALID_ARG, "sde needs noise");
     try {
         bind_device(ctx);
         hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
@@ -318,16 +323,46 @@ ace_ggml_status ace_mi_dit_sample(ace_ggml_context* ctx, int32_t batch, float* d
         io.out = ctx->d_v;
         io.max_layers = max_layers_env();
         for (int i = 0; i < n_steps; ++i) {
+            bool fresh = (i == 0);
+            if (i == cover_steps && (d_enc_nc || d_context_nc)) {  // switch to the non-cover conditions
+                if (d_enc_nc) io.enc = d_enc_nc;
+                if (d_context_nc) io.context = d_context_nc;
+                fresh = true;
+            }
+            io.reuse_cross = cache_cross && !fresh;
             io.t = ctx->d_sched + (size_t)i * batch;
             io.r = io.t;
             ctx->dit->forward(io, s);
-            const float dt = (i + 1 == n_steps) ? schedule[i] : schedule[i] - schedule[i + 1];
-            acemi::launch_euler(d_xt, ctx->d_v, (int64_t)n, dt, s);
+            if (i + 1 == n_steps) {  // final step: x0 = xt - v * t
+                acemi::launch_euler(d_xt, ctx->d_v, (int64_t)n, schedule[i], s);
+            } else if (sde) {
+                acemi::launch_sde(d_xt, ctx->d_v, d_noise + (size_t)i * n, (int64_t)n, schedule[i], schedule[i + 1], s);
+            } else {
+                acemi::launch_euler(d_xt, ctx->d_v, (int64_t)n, schedule[i] - schedule[i + 1], s);
+            }
         }
     } catch (const std::exception& e) {
         return set_error(ctx, ACE_GGML_ERR, std::string("dit sample failed: ") + e.what());
     }
     return ACE_GGML_OK;
+}
+}  // namespace
+
+ace_ggml_status ace_mi_dit_sample(ace_ggml_context* ctx, int32_t batch, float* d_xt, const float* d_context,
+                                  const float* d_enc, const int32_t* d_mask, const int32_t* d_enc_mask,
+                                  int32_t seq_len, int32_t enc_len, const float* schedule, int32_t n_steps,
+                                  void* stream) {
+    return run_sampler(ctx, batch, d_xt, d_context, d_enc, d_mask, d_enc_mask, seq_len, enc_len, schedule, n_steps,
+                       false, nullptr, -1, nullptr, nullptr, false, stream);
+}
+
+ace_ggml_status ace_mi_dit_sample_ex(ace_ggml_context* ctx, int32_t batch, float* d_xt, const float* d_context,
+                                     const float* d_enc, const int32_t* d_mask, const int32_t* d_enc_mask,
+                                     int32_t seq_len, int32_t enc_len, const float* schedule, int32_t n_steps,
+                                     int32_t sde, const float* d_noise, int32_t cover_steps, const float* d_context_nc,
+                                     const float* d_enc_nc, int32_t cache_cross, void* stream) {
+    return run_sampler(ctx, batch, d_xt, d_context, d_enc, d_mask, d_enc_mask, seq_len, enc_len, schedule, n_steps,
+                       sde != 0, d_noise, cover_steps, d_context_nc, d_enc_nc, cache_cross != 0, stream);
 }
 
 ace_ggml_status ace_mi_profile_enable(ace_ggml_context* ctx, int32_t on) {

@@ -94,8 +94,11 @@ void DitEngine::prepare_shape(int B, int Np, int L) {
         ensure(enc_act_, Me * H * act);
         ensure(encp_, Me * H * act);
         ensure(ckv_, Me * 2 * kd * 4);
+        const void* kc_old = kc_.p;
+        const void* vc_old = vc_.p;
         ensure(kc_, (size_t)2 * c.layers * B * c.hkv * Lpad * D * 2);
         ensure(vc_, (size_t)2 * c.layers * B * c.hkv * D * Lpad * 2);
+        if (kc_.p != kc_old || vc_.p != vc_old) cross_key_.valid = false;
         ensure(kbias_c_, (size_t)B * Lpad * 4);
     }
     ensure(freq_, (size_t)B * 256 * 4);
@@ -215,7 +218,10 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
     toc("key_bias", s);
 
     // ---- condition embedder (:1384-1414) + per-layer cross K/V (constant over the layer loop)
-    if (L > 0) {
+    const bool reuse = io.reuse_cross && cross_key_.valid && cross_key_.B == B && cross_key_.L == L &&
+                       cross_key_.layers >= n_layers && cross_key_.enc == io.enc;
+    if (L > 0 && !reuse) {
+        cross_key_ = CrossKey{true, B, L, n_layers, io.enc};
         const int64_t Me = (int64_t)B * L;
         uint16_t* enc_act = get<uint16_t>(enc_act_);
         uint16_t* encp = get<uint16_t>(encp_);

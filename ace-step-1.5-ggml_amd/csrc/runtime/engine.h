@@ -26,6 +26,12 @@ struct ForwardIO {
     const float* r = nullptr;         // [B]
     float* out = nullptr;             // [B][T][audio]
     int max_layers = -1;              // ACE_GGML_DIT_MAX_LAYERS
+    // Reuse the encoder-side tensors (condition_embedder output, every layer's cross K/V) computed
+    // by the previous forward of this engine: the cross-attention cache of the reference generation
+    // loop (acestep/mlx_dit/generate.py:150-171, MLXCrossAttentionCache / use_cache=True).  Only
+    // valid when enc / enc_mask / B / L / layer count are those of that forward; the sampler entry
+    // guarantees it.
+    bool reuse_cross = false;
 };
 
 // Per-kernel-class timing, filled when profiling is enabled (hipEvents on the launch stream).
@@ -67,6 +73,11 @@ class DitEngine {
     DitModel model_;
     // workspace
     Buf a0_, x_, act_, attn_, act2_, qkv_, qh_, kh_, vt_, kbias_, enc_act_, encp_, ckv_, kc_, vc_, kbias_c_;
+    struct CrossKey {  // what kc_/vc_ currently hold (ForwardIO::reuse_cross)
+        bool valid = false;
+        int B = 0, L = 0, layers = 0;
+        const float* enc = nullptr;
+    } cross_key_;
     Buf freq_, freq_act_, th_, th_act_, temb_t_, temb_r_, temb_act_, proj_, mods_, outmod_, cos_, sin_;
     int rope_np_ = -1;
     bool attn_split_ = true;  // ACE_MI_ATTN_FAST=1 -> single fp16 operands

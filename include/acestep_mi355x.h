@@ -61,6 +61,19 @@ ACE_GGML_API ace_ggml_status ace_mi_dit_sample(ace_ggml_context* ctx, int32_t ba
                                                const float* d_context, const float* d_enc, const int32_t* d_mask,
                                                const int32_t* d_enc_mask, int32_t seq_len, int32_t enc_len,
                                                const float* schedule, int32_t n_steps, void* stream);
+/* The Python/MLX generation loop (acestep/mlx_dit/generate.py:143-199) on the device: ODE (sde = 0)
+ * or SDE (sde = 1: x0 = xt - v*t; xt = t_next*noise_i + (1 - t_next)*x0 with caller noise
+ * d_noise [n_steps-1][batch][seq_len][audio]); from step `cover_steps` on, the non-cover conditions
+ * d_context_nc / d_enc_nc (either may be NULL) replace d_context / d_enc; cache_cross = 1 reuses the
+ * encoder-side tensors (condition embedder + every layer's cross K/V) between steps with the same
+ * conditions, as MLXCrossAttentionCache (use_cache=True) does.  Last step: x0 = xt - v*t. */
+ACE_GGML_API ace_ggml_status ace_mi_dit_sample_ex(ace_ggml_context* ctx, int32_t batch, float* d_xt,
+                                                  const float* d_context, const float* d_enc, const int32_t* d_mask,
+                                                  const int32_t* d_enc_mask, int32_t seq_len, int32_t enc_len,
+                                                  const float* schedule, int32_t n_steps, int32_t sde,
+                                                  const float* d_noise, int32_t cover_steps,
+                                                  const float* d_context_nc, const float* d_enc_nc,
+                                                  int32_t cache_cross, void* stream);
 
 /* Per-kernel-class timing with hipEvents on the launch stream (adds a sync per kernel).
  * ace_mi_profile_get copies up to `cap` entries: names (NUL-separated into `names`, `names_cap`

@@ -408,6 +408,13 @@ void launch_euler(float* xt, const float* v, int64_t n, float dt, hipStream_t) {
     for (int64_t i = 0; i < n; ++i) xt[i] = xt[i] - v[i] * dt;
 }
 
+void launch_sde(float* xt, const float* v, const float* noise, int64_t n, float t, float t_next, hipStream_t) {
+    for (int64_t i = 0; i < n; ++i) {
+        const float x0 = xt[i] - v[i] * t;
+        xt[i] = t_next * noise[i] + (1.0f - t_next) * x0;
+    }
+}
+
 // ---------------------------------------------------------------- VAE
 void launch_conv_gemm(const ConvGemmArgs& a, hipStream_t) {
     ACEMI_CHECK(a.Cin % 64 == 0 && a.N % 128 == 0 && a.M >= 1 && a.taps >= 1, "conv_gemm: unsupported shape");

@@ -171,3 +171,44 @@ def test_abi_error_paths(host_lib, tiny_ckpt):
     # enc_len > 0 without encoder states
     assert br.lib.ace_ggml_dit_forward(br.ctx, None, None, None, None, None, 10, 4, 0.5, 0.5, fp(out), out.nbytes) == 1
     br.close()
+
+
+def test_generation_loop_ex_ode_sde_cover_and_cross_cache(host_lib, tiny_ckpt):
+    """ace_mi_dit_sample_ex == the reference loop of acestep/mlx_dit/generate.py:143-199 restated with
+    per-step forwards: ODE with the cross-attention cache, SDE with caller noise, and the cover switch."""
+    br = bridge(host_lib)
+    br.load_dit(tiny_ckpt)
+    B, T, L = 2, 30, 5
+    rng = np.random.default_rng(21)
+    x0 = rng.standard_normal((B, T, 64)).astype(np.float32)
+    c = rng.standard_normal((B, T, 128)).astype(np.float32)
+    e = rng.standard_normal((B, L, 256)).astype(np.float32)
+    c_nc = rng.standard_normal((B, T, 128)).astype(np.float32)
+    e_nc = rng.standard_normal((B, L, 256)).astype(np.float32)
+    sched = [1.0, 0.9, 0.75, 0.5, 0.3]
+    noise = rng.standard_normal((len(sched) - 1, B, T, 64)).astype(np.float32)
+    p = lambda a: a.ctypes.data
+
+    def ref_loop(sde, cover):
+        xt = x0.copy()
+        for i, t in enumerate(sched):
+            cc, ee = (c_nc, e_nc) if (cover is not None and i >= cover) else (c, e)
+            v = np.stack([br.dit_forward_tfirst(xt[b], cc[b], ee[b], None, None, t, t) for b in range(B)])
+            if i + 1 == len(sched):
+                xt = xt - v * np.float32(t)
+            elif sde:
+                xc = xt - v * np.float32(t)
+                tn = np.float32(sched[i + 1])
+                xt = tn * noise[i] + (np.float32(1.0) - tn) * xc
+            else:
+                xt = xt - v * np.float32(t - sched[i + 1])
+        return xt
+
+    for sde, cover, cache in ((False, None, True), (True, None, True), (False, 2, True), (True, 3, False)):
+        xt = x0.copy()
+        br.dit_sample_ex_device(B, T, L, p(xt), p(c), p(e), 0, 0, sched, sde=sde, d_noise=p(noise),
+                                cover_steps=-1 if cover is None else cover,
+                                d_context_nc=p(c_nc) if cover is not None else 0,
+                                d_enc_nc=p(e_nc) if cover is not None else 0, cache_cross=cache)
+        np.testing.assert_allclose(xt, ref_loop(sde, cover), rtol=1e-5, atol=1e-5, err_msg=str((sde, cover, cache)))
+    br.close()
