@@ -3,6 +3,7 @@
 // Status/error behaviour follows the reference implementation
 // (acestep_ggml/cpp/acestep_ggml.cpp:65-70 ace_set_error, :108-194 create,
 // :230-236 last_error, :260-357 load_dit, :1304-1482 dit_forward).
+#include <algorithm>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -307,7 +308,8 @@ ace_ggml_status run_sampler(ace_ggml_context* ctx, int32_t batch, float* d_xt, c
         for (int i = 0; i < n_steps; ++i)
             for (int b = 0; b < batch; ++b) tt[(size_t)i * batch + b] = schedule[i];
         void* sp = ctx->d_sched;
-        ensure_dev(sp, ctx->d_sched_bytes, tt.size() * 4);
+        // sized generously so a longer loop later does not reallocate (hipFree syncs the device)
+        ensure_dev(sp, ctx->d_sched_bytes, std::max<size_t>(tt.size() * 4, 64 * 1024));
         ctx->d_sched = static_cast<float*>(sp);
         ACEMI_HIP(hipMemcpyAsync(ctx->d_sched, tt.data(), tt.size() * 4, hipMemcpyHostToDevice, s));
         ACEMI_HIP(hipStreamSynchronize(s));

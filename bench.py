@@ -6,7 +6,10 @@ Workload (BASELINE.json configs[2] shape at bf16, see DESIGN.md "Measurement"):
 BASELINE.json is the LM code rate) -> N = 3000 patch tokens, encoder
 length L = 512, full 24-layer DiT with synthetic bf16 weights of the real
 architecture, 27-step shifted-linear (shift 3) Euler sampling.  One "step" = one
-DiT forward over the local batch + the Euler update, all on the GPU.
+DiT forward over the local batch + the Euler update, all on the GPU, run by the
+library's device-side generation loop (ace_mi_dit_sample_ex) with the encoder-side
+cross-attention K/V recomputed every step like the ggml C sampler (--cross-cache
+reuses them like the reference Python/MLX sampler does).
 
 Multi-GPU (one process per GPU, torchrun): the batch is sharded across ranks
 (weak scaling, `--batch-per-gpu` items each); rank 0 broadcasts the conditioning
@@ -43,6 +46,8 @@ def parse():
     ap.add_argument("--sample-steps", type=int, default=27)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--cross-cache", action="store_true",
+                    help="reuse cross-attention K/V across steps (MLXCrossAttentionCache); off = ggml C sampler")
     ap.add_argument("--qtype", default="", choices=["", "q8_0", "q4_k", "q6_k"],
                     help="online weight quantization (ACE_GGML_DIT_WEIGHT_QTYPE): BASELINE configs[2] is q8_0")
     return ap.parse_args()
@@ -109,28 +114,28 @@ def main():
     xt = cond.noise.index_select(0, idx).contiguous()
     ctx = cond.context.index_select(0, idx).contiguous()
     enc = cond.enc.index_select(0, idx).contiguous()
-    v = torch.empty_like(xt)
-    tt = torch.empty((b_loc,), dtype=torch.float32, device=dev)
     sched = shifted_linear_schedule(args.sample_steps, 3.0)
     stream = torch.cuda.current_stream().cuda_stream
 
-    def step(i):
-        j = i % len(sched)
-        t = sched[j]
-        tt.fill_(t)
-        br.dit_forward_batched_device(b_loc, T, L, xt.data_ptr(), ctx.data_ptr(), enc.data_ptr(), 0, 0,
-                                      tt.data_ptr(), tt.data_ptr(), v.data_ptr(), stream)
-        dt = t if j + 1 == len(sched) else t - sched[j + 1]
-        xt.add_(v, alpha=-dt)
+    def run(first, k):
+        """k denoising steps of the schedule (cyclic) in ONE device-side generation-loop call
+        (ace_mi_dit_sample_ex): per step one batched DiT forward + the Euler update, both HIP kernels.
+        Cross-attention K/V are recomputed every step (as the ggml C sampler does) unless
+        --cross-cache asks for the reference Python/MLX sampler's cache."""
+        sch = [sched[(first + i) % len(sched)] for i in range(k)]
+        br.dit_sample_ex_device(b_loc, T, L, xt.data_ptr(), ctx.data_ptr(), enc.data_ptr(), 0, 0, sch,
+                                cache_cross=args.cross_cache, stream=stream)
 
-    for i in range(args.warmup):
-        step(i)
+    def step(i):  # single step (profiling pass)
+        run(i, 1)
+
+    if args.warmup > 0:
+        run(0, args.warmup)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(args.warmup + i)
+    run(args.warmup, args.steps)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -214,6 +219,8 @@ def main():
                             f"(T={T} latent frames @25 Hz, N={(T + 1) // 2} tokens), enc_len={L}, "
                             f"bs={b_loc}/GPU, {wdesc} weights, f32-faithful fp16x3 attention",
                 "weights": args.qtype or "bf16",
+                "sampler": "ace_mi_dit_sample_ex (device loop: batched DiT forward + Euler kernel per step)",
+                "cross_attention_cache": bool(args.cross_cache),
                 "model": "ACE-Step 1.5 DiT (24 layers, hidden 2048, MLP 6144, 16/8 heads)",
                 "seconds": args.seconds, "latent_frames": T, "tokens": (T + 1) // 2, "enc_len": L,
                 "batch_per_gpu": b_loc, "global_batch": B, "seq_len": T,
