@@ -180,48 +180,3 @@ def test_gemm_all_variants(variant, M, N, K):
     u = ref.reshape(M, N // 32, 2, 16)[:, :, 1, :].reshape(M, N // 2)
     sw = (g / (1 + np.exp(-g))) * u
     np.testing.assert_allclose(_vals(got_sw, 0), sw, rtol=2.0 ** -8, atol=1e-4)
-
-
-# ---------------------------------------------------------------- dequant-fused GEMM
-def _q_ref(a_bits, w_blocks, qtype):
-    """fp64 product of the bf16 activations with bf16(dequant(W)) — the values the kernel's MFMAs see."""
-    from oracle import ggml_numerics as g
-    deq = {"q8_0": lambda r: g.dequantize_q8_0(*g.unpack_q8_0(r)), "q4_k": g.dequantize_q4_k,
-           "q6_k": g.dequantize_q6_k}[qtype](w_blocks)
-    wv = g.round_bf16(deq).astype(np.float64)
-    av = bf16_bits_to_f32(a_bits).astype(np.float64)
-    return av @ wv.T, np.abs(av) @ np.abs(wv).T
-
-
-@pytest.mark.parametrize("qtype", ["q8_0", "q4_k", "q6_k"])
-@pytest.mark.parametrize("variant", [-1, 1, 2, 3])
-@pytest.mark.parametrize("M,N,K", [(1, 256, 256), (300, 512, 512), (1000, 256, 2048), (129, 768, 6144)])
-def test_gemm_q_matches_dequantized_product(qtype, variant, M, N, K):
-    capi = _capi()
-    if variant == 2 and N % 256:
-        pytest.skip("256-wide tiles need N % 256 == 0")
-    rng = np.random.default_rng(M + K + variant)
-    a = f32_to_bf16_bits(rng.standard_normal((M, K)).astype(np.float32))
-    w = (rng.standard_normal((N, K)) * 0.02).astype(np.float32)
-    blocks = capi.quantize(w, qtype)
-    bias = rng.standard_normal(N).astype(np.float32)
-    got = capi.kernel_gemm_q(a, blocks, qtype, epi=0, variant=variant, bias=bias)
-    ref, scale = _q_ref(a, blocks, qtype)
-    ref = ref + bias
-    assert np.all(np.abs(got - ref) <= 2e-6 * scale + 1e-6), np.max(np.abs(got - ref) / (scale + 1e-6))
-
-
-@pytest.mark.parametrize("qtype", ["q8_0", "q4_k"])
-def test_gemm_q_swiglu_epilogue(qtype):
-    M, I, K = 200, 256, 512
-    rng = np.random.default_rng(21)
-    a = f32_to_bf16_bits(rng.standard_normal((M, K)).astype(np.float32))
-    w = (rng.standard_normal((2 * I, K)) * 0.05).astype(np.float32)
-    blocks = _capi().quantize(w, qtype)
-    got = bf16_bits_to_f32(_capi().kernel_gemm_q(a, blocks, qtype, epi=4))
-    ref, _ = _q_ref(a, blocks, qtype)
-    gcols = np.concatenate([np.arange(grp * 32, grp * 32 + 16) for grp in range(I // 16)])
-    ucols = gcols + 16
-    gv, uv = ref[:, gcols], ref[:, ucols]
-    sw = gv / (1.0 + np.exp(-gv)) * uv
-    np.testing.assert_allclose(got, sw, rtol=2 ** -7, atol=1e-3 * np.abs(sw).max())

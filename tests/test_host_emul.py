@@ -50,7 +50,7 @@ def rel(a, b):
 
 
 def engine_view(W):
-    from test_gpu_forward import engine_view as ev
+    from test_gpu_quant import engine_view as ev
     return ev(W)
 
 

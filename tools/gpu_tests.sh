@@ -1,12 +1,18 @@
 #!/bin/bash
+# GPU-box parity suite, one pytest process per file (dense paths first), each under its own time
+# limit.  Stops at the first crash / timeout (rc other than 0 = pass, 1 = test failures).
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 rocminfo 2>/dev/null | grep -m2 -E "gfx950|Marketing" > gpurun_out/dev.txt
-timeout -k 10 400 python -m pytest tests/test_gpu_kernels.py -q -m gpu > gpurun_out/k.log 2>&1
-rc=$?
-echo "kernels rc=$rc" >> gpurun_out/k.log
-if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-timeout -k 10 900 python -m pytest tests/test_gpu_forward.py -q -s -m "gpu" ${FWD_ARGS} > gpurun_out/f.log 2>&1
-rc=$?
-echo "forward rc=$rc" >> gpurun_out/f.log
-exit $rc
+worst=0
+for spec in kernels:400 forward:900 quant:900 sampler:300 vae:600; do
+    name=${spec%%:*}
+    lim=${spec##*:}
+    timeout -k 10 "$lim" python -m pytest "tests/test_gpu_${name}.py" -q -s -m gpu ${FWD_ARGS} \
+        > "gpurun_out/${name}.log" 2>&1
+    rc=$?
+    echo "${name} rc=$rc" >> "gpurun_out/${name}.log"
+    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+    if [ $rc -gt $worst ]; then worst=$rc; fi
+done
+exit $worst
