@@ -36,6 +36,8 @@ EXPORTED_SYMBOLS = (
     "ace_mi_gemm_variant", "ace_ggml_load_vae", "ace_ggml_vae_get_info", "ace_ggml_vae_decode",
     "ace_mi_vae_out_len", "ace_mi_vae_decode_device", "ace_ggml_vae_encode", "ace_mi_vae_enc_out_len",
     "ace_mi_vae_encode_device", "ace_mi_quantize", "ace_mi_dequantize", "ace_mi_kernel_gemm_q", "ace_mi_bench_gemm_q",
+    "ace_mi_cond_get_info", "ace_mi_text_project", "ace_mi_lyric_encode", "ace_mi_timbre_encode",
+    "ace_mi_build_condition",
 )
 
 # qtype codes of ace_mi_quantize & co. (names as parse_quant_type, acestep_dit_model.cpp:27-37)
@@ -55,6 +57,12 @@ class AceMiDitInfo(ctypes.Structure):
         "hidden_size", "intermediate_size", "num_layers", "num_heads", "num_kv_heads", "head_dim",
         "patch_size", "in_channels", "audio_dim", "sliding_window", "act_type", "device")] + [
         ("weight_bytes", ctypes.c_int64)]
+
+
+class AceMiCondInfo(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "hidden_size", "lyric_in_dim", "timbre_in_dim", "text_projector_in", "has_lyric_encoder", "lyric_layers",
+        "has_timbre_encoder", "timbre_layers")]
 
 
 _LIB = None
@@ -144,6 +152,16 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.ace_mi_kernel_gemm_q.restype = ctypes.c_int
     lib.ace_mi_bench_gemm_q.argtypes = [i32, i32, i32, i32, i32, i32, i32, fp]
     lib.ace_mi_bench_gemm_q.restype = ctypes.c_int
+    lib.ace_mi_cond_get_info.argtypes = [vp, ctypes.POINTER(AceMiCondInfo)]
+    lib.ace_mi_cond_get_info.restype = ctypes.c_int
+    lib.ace_mi_text_project.argtypes = [vp, fp, i32, i32, fp, sz]
+    lib.ace_mi_text_project.restype = ctypes.c_int
+    lib.ace_mi_lyric_encode.argtypes = [vp, fp, i32, fp, sz]
+    lib.ace_mi_lyric_encode.restype = ctypes.c_int
+    lib.ace_mi_timbre_encode.argtypes = [vp, fp, ip, i32, i32, fp, sz]
+    lib.ace_mi_timbre_encode.restype = ctypes.c_int
+    lib.ace_mi_build_condition.argtypes = [vp, fp, i32, fp, i32, i32, fp, ip, i32, i32, fp, sz, ip, sz, ip]
+    lib.ace_mi_build_condition.restype = ctypes.c_int
     if path is None:
         _LIB = lib
     return lib
@@ -252,6 +270,62 @@ class GGMLCAPIBridge:
         st = self.lib.ace_ggml_vae_encode(self.ctx, _fptr(a), n, _fptr(out), out.nbytes)
         self._ensure_ok(st, "ace_ggml_vae_encode")
         return out
+
+    # -- condition encoders (include/acestep_mi355x.h; acestep_ggml.cpp:1624-1899, :2414-2556) -------
+    def cond_info(self) -> AceMiCondInfo:
+        info = AceMiCondInfo()
+        self._ensure_ok(self.lib.ace_mi_cond_get_info(self.ctx, ctypes.byref(info)), "ace_mi_cond_get_info")
+        return info
+
+    def text_project(self, states) -> np.ndarray:
+        """encoder.text_projector: [n, in] -> [n, H]."""
+        x = np.ascontiguousarray(states, dtype=np.float32)
+        out = np.empty((x.shape[0], self.cond_info().hidden_size), np.float32)
+        st = self.lib.ace_mi_text_project(self.ctx, _fptr(x), int(x.shape[0]), int(x.shape[1]), _fptr(out), out.nbytes)
+        self._ensure_ok(st, "ace_mi_text_project")
+        return out
+
+    def lyric_encode(self, lyric_embeds) -> np.ndarray:
+        """Lyric encoder: token embeddings [n, text_hidden] -> [n, H]."""
+        x = np.ascontiguousarray(lyric_embeds, dtype=np.float32)
+        out = np.empty((x.shape[0], self.cond_info().hidden_size), np.float32)
+        st = self.lib.ace_mi_lyric_encode(self.ctx, _fptr(x), int(x.shape[0]), _fptr(out), out.nbytes)
+        self._ensure_ok(st, "ace_mi_lyric_encode")
+        return out
+
+    def timbre_encode(self, refer, order_mask=None) -> np.ndarray:
+        """Timbre encoder: references [n_refer, refer_len, timbre_in] -> [n_refer, H]."""
+        x = np.ascontiguousarray(refer, dtype=np.float32)
+        om = None if order_mask is None else np.ascontiguousarray(order_mask, dtype=np.int32)
+        out = np.empty((x.shape[0], self.cond_info().hidden_size), np.float32)
+        st = self.lib.ace_mi_timbre_encode(self.ctx, _fptr(x), _iptr(om), int(x.shape[0]), int(x.shape[1]),
+                                           _fptr(out), out.nbytes)
+        self._ensure_ok(st, "ace_mi_timbre_encode")
+        return out
+
+    def build_condition(self, style_states=None, lyric_embeds=None, refer=None, refer_order_mask=None,
+                        text_hidden: Optional[int] = None) -> Tuple[np.ndarray, np.ndarray]:
+        """(encoder_hidden_states [len, H], encoder_attention_mask [len]) from text-encoder style states,
+        lyric token embeddings and timbre references."""
+        ss = None if style_states is None else np.ascontiguousarray(style_states, dtype=np.float32)
+        le = None if lyric_embeds is None else np.ascontiguousarray(lyric_embeds, dtype=np.float32)
+        rf = None if refer is None else np.ascontiguousarray(refer, dtype=np.float32)
+        om = None if refer_order_mask is None else np.ascontiguousarray(refer_order_mask, dtype=np.int32)
+        ns = 0 if ss is None else int(ss.shape[0])
+        nl = 0 if le is None else int(le.shape[0])
+        nr, rl = (0, 0) if rf is None else (int(rf.shape[0]), int(rf.shape[1]))
+        if text_hidden is None:
+            text_hidden = int(ss.shape[1]) if ss is not None else (int(le.shape[1]) if le is not None else 0)
+        H = self.cond_info().hidden_size
+        cap = max(ns + nl + nr, 1)
+        enc = np.empty((cap, H), np.float32)
+        mask = np.empty(cap, np.int32)
+        n = ctypes.c_int32(0)
+        st = self.lib.ace_mi_build_condition(self.ctx, _fptr(ss), ns, _fptr(le), nl, int(text_hidden), _fptr(rf),
+                                             _iptr(om), nr, rl, _fptr(enc), enc.nbytes, _iptr(mask), mask.nbytes,
+                                             ctypes.byref(n))
+        self._ensure_ok(st, "ace_mi_build_condition")
+        return enc[: n.value].copy(), mask[: n.value].copy()
 
     # -- MI355X extensions ---------------------------------------------------
     def vae_enc_out_len(self, n_samples: int) -> int:

@@ -39,6 +39,15 @@ def make_config(**overrides) -> dict:
 TINY_CONFIG = make_config(hidden_size=256, intermediate_size=512, num_hidden_layers=2, num_attention_heads=4,
                           num_key_value_heads=2, head_dim=128, sliding_window=16)
 
+# Condition-encoder keys (acestep_dit_config.cpp:69-73).  The released config values are not in the
+# reference tree; these are the Qwen3-Embedding-0.6B text width and a guess at the layer counts, used
+# only to size synthetic checkpoints.
+COND_KEYS = dict(text_hidden_dim=1024, num_lyric_encoder_hidden_layers=8, timbre_hidden_dim=64,
+                 num_timbre_encoder_hidden_layers=4, timbre_fix_frame=750)
+TINY_COND_CONFIG = make_config(**{k: v for k, v in TINY_CONFIG.items() if k != "layer_types"},
+                               text_hidden_dim=128, num_lyric_encoder_hidden_layers=2, timbre_hidden_dim=64,
+                               num_timbre_encoder_hidden_layers=2, timbre_fix_frame=8)
+
 
 def tensor_specs(cfg: dict) -> Iterator[Tuple[str, Tuple[int, ...], str]]:
     """(name, shape, kind) for every DiT decoder tensor; kind in {w, b, norm, table}."""
@@ -77,6 +86,36 @@ def tensor_specs(cfg: dict) -> Iterator[Tuple[str, Tuple[int, ...], str]]:
         yield p + "mlp.up_proj.weight", (I, H), "w"
         yield p + "mlp.down_proj.weight", (H, I), "w"
         yield p + "scale_shift_table", (1, 6, H), "table"
+    # condition encoders (acestep_dit_model.cpp:885-996), after the decoder so that adding them leaves
+    # the decoder's random draws unchanged
+    th = cfg.get("text_hidden_dim", 0)
+    if th:
+        yield "encoder.text_projector.weight", (H, th), "w"
+    for tag, n_key, in_dim in (("lyric", "num_lyric_encoder_hidden_layers", th or 1024),
+                               ("timbre", "num_timbre_encoder_hidden_layers",
+                                cfg.get("timbre_hidden_dim", 0) or cfg["audio_acoustic_hidden_dim"])):
+        n = cfg.get(n_key, 0)
+        if not n:
+            continue
+        p = f"encoder.{tag}_encoder."
+        yield p + "embed_tokens.weight", (H, in_dim), "w"
+        yield p + "embed_tokens.bias", (H,), "b"
+        yield p + "norm.weight", (H,), "norm"
+        if tag == "timbre":
+            yield p + "special_token", (1, 1, H), "table"
+        for i in range(n):
+            q = f"{p}layers.{i}."
+            yield q + "input_layernorm.weight", (H,), "norm"
+            yield q + "self_attn.q_proj.weight", (hq * D, H), "w"
+            yield q + "self_attn.k_proj.weight", (hkv * D, H), "w"
+            yield q + "self_attn.v_proj.weight", (hkv * D, H), "w"
+            yield q + "self_attn.o_proj.weight", (H, hq * D), "w"
+            yield q + "self_attn.q_norm.weight", (D,), "norm"
+            yield q + "self_attn.k_norm.weight", (D,), "norm"
+            yield q + "post_attention_layernorm.weight", (H,), "norm"
+            yield q + "mlp.gate_proj.weight", (I, H), "w"
+            yield q + "mlp.up_proj.weight", (I, H), "w"
+            yield q + "mlp.down_proj.weight", (H, I), "w"
 
 
 def _bf16_bits(x: np.ndarray) -> np.ndarray:

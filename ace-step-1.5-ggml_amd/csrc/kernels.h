@@ -88,6 +88,10 @@ void launch_to_act(ActType t, const float* in, int64_t n, bool silu, uint16_t* o
 void launch_rmsnorm_mod(ActType t, const float* x, int M, int H, const float* w, const float* scale,
                         const float* shift, int64_t mod_stride, int rows_per_item, float eps, uint16_t* out,
                         hipStream_t s, bool x3 = false);
+// out[r] = RMSNorm(x[r * row_step]) * w in f32 for r < rows (the condition encoders' final norm,
+// acestep_dit_model.cpp:1642-1644 / :1727-1729; row_step > 1 picks every item's first token).
+void launch_rmsnorm_f32(const float* x, int rows, int64_t row_step, int H, const float* w, float eps, float* out,
+                        hipStream_t s);
 // Per-head RMSNorm (+ NEOX RoPE) of the q/k sections and f16 re-layout for attention.
 struct PrepArgs {
     const float* src;

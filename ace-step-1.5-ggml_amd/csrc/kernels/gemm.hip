@@ -574,8 +574,15 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_q_kernel(GemmParams p) {
         // W(kt+2): waiting for its bytes also retires the older A(kt+1) DMA
         dequant_store<WQ>(wnext, lds0 + cur * STAGE + wrow_off, wh, wsw);
         stage_a(cur, min(kt + 2, nk - 1));
+        // keep the W(kt+3) loads behind the A(kt+2) DMA in issue order: the vmcnt the compiler
+        // places before the next iteration's dequant (waiting for those bytes) then also retires
+        // A(kt+2) before the barrier that ends that iteration publishes buffer `cur` again
+        asm volatile("" ::: "memory");
         wnext = load_wq<WQ>(qbase, sbase, min(kt + 3, nk - 1));
         mfma_half(a, b, TM / 2);
+        // the dequantized W rows are asm ds_writes the compiler does not count: retire them before
+        // the barrier that hands buffer `cur` to the other waves (gfx950 does not wait at s_barrier)
+        lds_wait_all();
         __builtin_amdgcn_s_barrier();
     }
     wait_vmcnt<0>();

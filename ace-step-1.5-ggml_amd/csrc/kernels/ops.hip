@@ -143,6 +143,42 @@ __global__ void __launch_bounds__(256) rmsnorm_mod_kernel(const float* __restric
     }
 }
 
+// f32 output variant for the condition encoders' final norm: ggml_rms_norm + ggml_mul by w
+template <int VPT>
+__global__ void __launch_bounds__(256) rmsnorm_f32_kernel(const float* __restrict__ x, int64_t row_step, int H,
+                                                          const float* __restrict__ w, float eps,
+                                                          float* __restrict__ out) {
+    const int m = blockIdx.x;
+    const float* xr = x + (int64_t)m * row_step * H;
+    __shared__ float red[4];
+    float4 v[VPT];
+    float ss = 0.f;
+#pragma unroll
+    for (int k = 0; k < VPT; ++k) {
+        const int i = (threadIdx.x + k * 256) * 4;
+        v[k] = i < H ? *(const float4*)(xr + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+        ss += v[k].x * v[k].x + v[k].y * v[k].y + v[k].z * v[k].z + v[k].w * v[k].w;
+    }
+    ss = wave_sum(ss);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+    __syncthreads();
+    const float tot = red[0] + red[1] + red[2] + red[3];
+    const float sc = 1.0f / sqrtf(tot / (float)H + eps);
+    float* orow = out + (int64_t)m * H;
+#pragma unroll
+    for (int k = 0; k < VPT; ++k) {
+        const int i = (threadIdx.x + k * 256) * 4;
+        if (i >= H) break;
+        const float4 wv = *(const float4*)(w + i);
+        float4 o;
+        o.x = __fmul_rn(__fmul_rn(v[k].x, sc), wv.x);
+        o.y = __fmul_rn(__fmul_rn(v[k].y, sc), wv.y);
+        o.z = __fmul_rn(__fmul_rn(v[k].z, sc), wv.z);
+        o.w = __fmul_rn(__fmul_rn(v[k].w, sc), wv.w);
+        *(float4*)(orow + i) = o;
+    }
+}
+
 // ------------------------------------------------------------ attention prep
 // QK-RMSNorm over head_dim (:1202-1203), NEOX RoPE (:1205-1210), the permute/cont copies
 // (:1212-1231) and the V transpose for the P.V MFMA: writes
@@ -430,6 +466,18 @@ void launch_rmsnorm_mod(ActType t, const float* x, int M, int H, const float* w,
         else ACEMI_RMS(false, 4, false);
     }
 #undef ACEMI_RMS
+    ACEMI_HIP(hipGetLastError());
+}
+
+void launch_rmsnorm_f32(const float* x, int rows, int64_t row_step, int H, const float* w, float eps, float* out,
+                        hipStream_t s) {
+    ACEMI_CHECK(H % 4 == 0 && H <= 4096 && rows >= 1 && row_step >= 1, "rmsnorm_f32: bad shape");
+    if (H <= 1024)
+        hipLaunchKernelGGL(rmsnorm_f32_kernel<1>, dim3(rows), dim3(256), 0, s, x, row_step, H, w, eps, out);
+    else if (H <= 2048)
+        hipLaunchKernelGGL(rmsnorm_f32_kernel<2>, dim3(rows), dim3(256), 0, s, x, row_step, H, w, eps, out);
+    else
+        hipLaunchKernelGGL(rmsnorm_f32_kernel<4>, dim3(rows), dim3(256), 0, s, x, row_step, H, w, eps, out);
     ACEMI_HIP(hipGetLastError());
 }
 

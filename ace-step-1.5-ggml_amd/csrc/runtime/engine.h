@@ -34,6 +34,21 @@ struct ForwardIO {
     bool reuse_cross = false;
 };
 
+// One condition-encoder pass for B items of n tokens each (forward_lyric_encoder /
+// forward_timbre_encoder, acestep_dit_model.cpp:1562-1739; the text projector of
+// ace_project_tokens_linear, acestep_ggml.cpp:1624-1678, is the enc == null case):
+//   x = in . proj^T (+ proj_b); x = block(x) for each layer; out = RMSNorm(x) * norm.
+struct EncodeIO {
+    const DevEncoder* enc = nullptr;  // blocks + final norm; null = projection only
+    const DevWeight* proj = nullptr;  // input projection [H][in_dim]
+    const float* proj_b = nullptr;    // [H] or null
+    const float* in = nullptr;        // [B][n][in_dim] f32 (device)
+    int B = 1, n = 0;
+    bool first_only = false;          // out [B][H] = token 0 of each item (timbre embedding)
+    float* out = nullptr;             // [B][n][H] or [B][H] f32 (device)
+    int max_layers = -1;              // ACE_GGML_{LYRIC,TIMBRE}_MAX_LAYERS
+};
+
 // Per-kernel-class timing, filled when profiling is enabled (hipEvents on the launch stream).
 struct KernelTimes {
     std::vector<std::string> names;
@@ -47,6 +62,7 @@ class DitEngine {
     ~DitEngine();
     DitModel& model() { return model_; }
     void forward(const ForwardIO& io, hipStream_t s);
+    void encode(const EncodeIO& io, hipStream_t s);
     // enable per-kernel-class event timing for subsequent forwards
     void set_profiling(bool on);
     const KernelTimes& times() const { return times_; }
@@ -80,6 +96,9 @@ class DitEngine {
     } cross_key_;
     Buf freq_, freq_act_, th_, th_act_, temb_t_, temb_r_, temb_act_, proj_, mods_, outmod_, cos_, sin_;
     int rope_np_ = -1;
+    Buf ein_, ecos_, esin_;  // encoder input activations, encoder RoPE table
+    int erope_n_ = -1;
+    void rope_table(int n, Buf& cs, Buf& sn);
     bool attn_split_ = true;  // ACE_MI_ATTN_FAST=1 -> single fp16 operands
     // profiling
     bool profiling_ = false;

@@ -165,6 +165,18 @@ struct Loader {
         }
         return out;
     }
+    bool has(const std::string& name) const { return gguf ? gg.has(name) : st.has(name); }
+    // (rows, cols) of a 2-D weight as stored (torch [out][in]; GGUF ne1 x ne0)
+    std::pair<int64_t, int64_t> shape2(const std::string& name) const {
+        if (gguf) {
+            const auto& t = gg.get(name);
+            if (t.ne_at(2) != 1 || t.ne_at(3) != 1) throw IoError("invalid 2d tensor shape in gguf: " + name);
+            return {t.ne_at(1), t.ne_at(0)};
+        }
+        const auto& t = st.get(name);
+        if (t.shape.size() != 2) throw IoError("invalid tensor shape for " + name);
+        return {t.shape[0], t.shape[1]};
+    }
     // conv weights as f32 values (proj_in [H][Cin][P], proj_out [H][A][P]): the GGUF path converts them
     // to F32 (load_conv1d/convtranspose1d_weight_as_linear_from_gguf, :602-718)
     Mat conv_f32(const std::string& name, int64_t d0, int64_t d1, int64_t d2) {
@@ -309,6 +321,20 @@ struct Loader {
         act = a.dtype == "F16" ? ActType::F16 : ActType::BF16;
         return upload<uint16_t>(a.u16.data(), a.u16.size() * 2);
     }
+    // mlp.gate_proj | mlp.up_proj as one [2I][H] weight, rows interleaved in groups of 16
+    // ([g0..15, u0..15, g16..31, ...]) for the SwiGLU epilogue
+    DevWeight gate_up(const std::string& p, int I, int H) {
+        const Mat wg = mat(p + "mlp.gate_proj.weight", I, H);
+        const Mat wu = mat(p + "mlp.up_proj.weight", I, H);
+        const Mat gu = concat_rows({&wg, &wu});
+        return finish(permute(
+            gu, 2LL * I, H,
+            [&](int64_t r) {
+                const int64_t grp = r / 32, w = r % 32;
+                return (w < 16 ? 0 : (int64_t)I) + grp * 16 + (w % 16);
+            },
+            [](int64_t col) { return col; }));
+    }
     // cast_f32 of a table loaded by load_tensor_3d_as_2d: dequant(quant(t)) when it is quantized
     std::vector<float> table(const std::string& name, int64_t rows, int64_t cols) {
         if (gguf) {  // load_tensor_3d_as_2d_from_gguf (:554-585): ne = (cols, rows, 1)
@@ -372,6 +398,14 @@ void load_config(const std::string& path, DitConfig& c) {
         if (o.has("sliding_window") && o.at("sliding_window").kind == Json::Number)
             c.sliding_window = (int)o.at("sliding_window").as_int();
         if (o.has("rope_theta")) c.rope_theta = (float)o.at("rope_theta").as_num();
+        auto opt_int = [&](const char* k, int& dst) {
+            if (o.has(k) && o.at(k).kind == Json::Number) dst = (int)o.at(k).as_int();
+        };
+        opt_int("text_hidden_dim", c.text_hidden_dim);
+        opt_int("num_lyric_encoder_hidden_layers", c.lyric_layers);
+        opt_int("timbre_hidden_dim", c.timbre_hidden_dim);
+        opt_int("num_timbre_encoder_hidden_layers", c.timbre_layers);
+        opt_int("timbre_fix_frame", c.timbre_fix_frame);
         const auto& lt = o.at("layer_types");
         if (lt.kind != Json::Array) throw IoError("missing layer_types");
         c.layer_types.clear();
@@ -515,19 +549,7 @@ void load_dit_model(const std::string& dir, DitModel& m, int& status_hint) {
                 ly.w_ckv = L.finish(Loader::concat_rows({&wk, &wv}));
             }
             ly.w_co = L.finish(L.mat(p2 + "cross_attn.o_proj.weight", H, qd));
-            {
-                const Mat wg = L.mat(p2 + "mlp.gate_proj.weight", I, H);
-                const Mat wu = L.mat(p2 + "mlp.up_proj.weight", I, H);
-                const Mat gu = Loader::concat_rows({&wg, &wu});
-                // rows interleaved in groups of 16: [g0..15, u0..15, g16..31, ...]
-                ly.w_gu = L.finish(Loader::permute(
-                    gu, 2LL * I, H,
-                    [&](int64_t r) {
-                        const int64_t grp = r / 32, w = r % 32;
-                        return (w < 16 ? 0 : (int64_t)I) + grp * 16 + (w % 16);
-                    },
-                    [](int64_t col) { return col; }));
-            }
+            ly.w_gu = L.gate_up(p2, I, H);
             ly.w_down = L.finish(L.mat(p2 + "mlp.down_proj.weight", H, I));
             {
                 auto v = L.table(p2 + "scale_shift_table", 6, H);
@@ -536,6 +558,52 @@ void load_dit_model(const std::string& dir, DitModel& m, int& status_hint) {
             ly.sliding = i < (int)c.layer_types.size() && c.layer_types[i] == "sliding_attention";
         }
         m.tables = L.upload<float>(tables.data(), tables.size() * 4);
+
+        // ---- condition encoders (optional; acestep_dit_model.cpp:885-996)
+        if (L.has("encoder.text_projector.weight")) {
+            const auto sh = L.shape2("encoder.text_projector.weight");
+            if (sh.first != H) throw IoError("invalid tensor shape for encoder.text_projector.weight");
+            m.text_proj = L.finish(L.mat("encoder.text_projector.weight", sh.first, sh.second));
+        }
+        auto load_encoder = [&](const std::string& pre, int n_layers, DevEncoder& e) {
+            if (L.has(pre + "embed_tokens.weight")) {
+                const auto sh = L.shape2(pre + "embed_tokens.weight");
+                e.embed = L.finish(L.mat(pre + "embed_tokens.weight", sh.first, sh.second));
+            }
+            if (L.has(pre + "embed_tokens.bias")) e.embed_b = L.vec_f32(pre + "embed_tokens.bias", H);
+            if (L.has(pre + "norm.weight")) e.norm = L.vec_f32(pre + "norm.weight", H);
+            e.layers.resize(std::max(0, n_layers));
+            if (n_layers > 0) {
+                const auto sh = L.shape2(pre + "layers.0.mlp.gate_proj.weight");
+                if (sh.second != H || sh.first <= 0 || sh.first % 128 != 0)
+                    throw Unsupported("encoder MLP width must be a multiple of 128: " + pre);
+                e.intermediate = (int)sh.first;
+            }
+            const int EI = e.intermediate;
+            for (int i = 0; i < n_layers; ++i) {  // EncoderLayer (:903-937 / :960-994)
+                const std::string p2 = pre + "layers." + std::to_string(i) + ".";
+                DevLayer& ly = e.layers[i];
+                ly.cross = false;
+                ly.self_norm = L.vec_f32(p2 + "input_layernorm.weight", H);
+                ly.mlp_norm = L.vec_f32(p2 + "post_attention_layernorm.weight", H);
+                ly.sq_norm = L.vec_f32(p2 + "self_attn.q_norm.weight", D);
+                ly.sk_norm = L.vec_f32(p2 + "self_attn.k_norm.weight", D);
+                const Mat wq = L.mat(p2 + "self_attn.q_proj.weight", qd, H);
+                const Mat wk = L.mat(p2 + "self_attn.k_proj.weight", kd, H);
+                const Mat wv = L.mat(p2 + "self_attn.v_proj.weight", kd, H);
+                ly.w_qkv = L.finish(Loader::concat_rows({&wq, &wk, &wv}));
+                ly.w_o = L.finish(L.mat(p2 + "self_attn.o_proj.weight", H, qd));
+                ly.w_gu = L.gate_up(p2, EI, H);
+                ly.w_down = L.finish(L.mat(p2 + "mlp.down_proj.weight", H, EI));
+                ly.sliding = i < (int)c.layer_types.size() && c.layer_types[i] == "sliding_attention";
+            }
+            e.act = e.layers.empty() ? ActType::BF16 : e.layers[0].w_qkv.act();
+            for (const DevLayer& ly : e.layers)
+                for (const DevWeight* w : {&ly.w_qkv, &ly.w_o, &ly.w_gu, &ly.w_down})
+                    if (w->act() != e.act) throw Unsupported("mixed encoder block weight types");
+        };
+        load_encoder("encoder.lyric_encoder.", c.lyric_layers, m.lyric);
+        load_encoder("encoder.timbre_encoder.", c.timbre_layers, m.timbre);
         m.act = m.layers.empty() ? m.cond_w.act() : m.layers[0].w_qkv.act();
         for (const DevLayer& ly : m.layers)
             for (const DevWeight* w : {&ly.w_qkv, &ly.w_o, &ly.w_cq, &ly.w_ckv, &ly.w_co, &ly.w_gu, &ly.w_down})

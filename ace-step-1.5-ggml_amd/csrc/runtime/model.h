@@ -25,7 +25,13 @@ struct DitConfig {
     int sliding_window = 0;
     bool use_sliding_window = false;
     std::vector<std::string> layer_types;
+    // condition encoders (acestep_dit_config.h:21-27; 0 = absent)
+    int text_hidden_dim = 0, lyric_layers = 0, timbre_hidden_dim = 0, timbre_layers = 0, timbre_fix_frame = 0;
     int ctx_dim() const { return in_channels - audio_dim; }
+    // input width of the lyric encoder / timbre encoder (forward_lyric_encoder :1572, forward_timbre_encoder
+    // :1659-1661)
+    int lyric_in_dim() const { return text_hidden_dim > 0 ? text_hidden_dim : 1024; }
+    int timbre_in_dim() const { return timbre_hidden_dim > 0 ? timbre_hidden_dim : (audio_dim > 0 ? audio_dim : 64); }
 };
 
 // A 2-D linear weight [rows = out][cols = in] in HBM: dense 16-bit (file dtype) or one of the
@@ -66,6 +72,20 @@ struct DevLayer {
     bool cross = true;  // Layer::use_cross_attention default
 };
 
+// A condition encoder (ace_dit::Model lyric_* / timbre_*, acestep_dit_model.h; loaded at
+// acestep_dit_model.cpp:889-996): input projection (+ bias), Qwen-style blocks without AdaLN stored in
+// DevLayer (self_norm = input_layernorm, mlp_norm = post_attention_layernorm, no cross-attention), and
+// an optional final RMSNorm weight.
+struct DevEncoder {
+    DevWeight embed;              // [H][in_dim] (embed_tokens.weight)
+    float* embed_b = nullptr;     // [H] or null
+    float* norm = nullptr;        // [H] or null
+    std::vector<DevLayer> layers;
+    int intermediate = 0;         // MLP width of the blocks (from mlp.gate_proj)
+    ActType act = ActType::BF16;  // activation type of the block GEMMs
+    bool has_embed() const { return embed.q != nullptr; }
+};
+
 // Timestep MLPs run as small-M GEMVs on dense 16-bit weights; when the checkpoint is quantized
 // online they hold bf16(dequant(q)) — the same values the dequant-fused GEMM feeds its MFMAs.
 struct DevTimestep {
@@ -93,6 +113,9 @@ struct DitModel {
     float* tables = nullptr;         // [layers][6][H]
     DevTimestep te[2];               // time_embed, time_embed_r
     std::vector<DevLayer> layers;
+    // condition encoders (optional tensors; acestep_dit_model.cpp:885-996)
+    DevWeight text_proj;             // encoder.text_projector.weight [H][text_hidden] (no bias)
+    DevEncoder lyric, timbre;
     std::vector<void*> allocs;
     size_t weight_bytes = 0;
 

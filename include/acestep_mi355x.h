@@ -140,6 +140,49 @@ ACE_GGML_API ace_ggml_status ace_mi_kernel_gemm_q(int32_t qtype, int32_t epi, in
 ACE_GGML_API ace_ggml_status ace_mi_bench_gemm_q(int32_t qtype, int32_t epi, int32_t variant, int32_t M, int32_t N,
                                                  int32_t K, int32_t iters, float* avg_ms);
 
+/* ---- condition encoders: the conditioning half of
+ * ace_generate_audio_style_lyric_timbre_impl (acestep_ggml.cpp:2324-2556) on the GPU.  Host buffers,
+ * blocking, like the reference's internal functions they expose. ---- */
+typedef struct ace_mi_cond_info {
+    int32_t hidden_size;         /* DiT hidden size = width of every condition state */
+    int32_t lyric_in_dim;        /* lyric encoder input width (config text_hidden_dim, else 1024) */
+    int32_t timbre_in_dim;       /* timbre encoder input width (timbre_hidden_dim, else audio dim, else 64) */
+    int32_t text_projector_in;   /* encoder.text_projector in-features (0 = not loaded) */
+    int32_t has_lyric_encoder;   /* lyric embed_tokens (or the text-projector fallback) loaded */
+    int32_t lyric_layers;
+    int32_t has_timbre_encoder;
+    int32_t timbre_layers;
+} ace_mi_cond_info;
+ACE_GGML_API ace_ggml_status ace_mi_cond_get_info(ace_ggml_context* ctx, ace_mi_cond_info* out);
+
+/* ace_project_tokens_linear with encoder.text_projector (acestep_ggml.cpp:1624-1678):
+ * states [n_tokens][in_dim] -> out [n_tokens][hidden_size]. */
+ACE_GGML_API ace_ggml_status ace_mi_text_project(ace_ggml_context* ctx, const float* states, int32_t n_tokens,
+                                                 int32_t in_dim, float* out, size_t out_size);
+/* ace_encode_lyric_condition / forward_lyric_encoder (acestep_ggml.cpp:1680-1727,
+ * acestep_dit_model.cpp:1562-1651): lyric token embeddings [n_tokens][lyric_in_dim] ->
+ * [n_tokens][hidden_size]; ACE_GGML_LYRIC_MAX_LAYERS honoured. */
+ACE_GGML_API ace_ggml_status ace_mi_lyric_encode(ace_ggml_context* ctx, const float* lyric_embeds, int32_t n_tokens,
+                                                 float* out, size_t out_size);
+/* ace_encode_timbre_condition / forward_timbre_encoder (acestep_ggml.cpp:1803-1899,
+ * acestep_dit_model.cpp:1653-1737): refer [n_refer][refer_len][timbre_in_dim] -> one token per
+ * reference, out [n_refer][hidden_size]; a non-zero order_mask entry is ACE_GGML_ERR_UNSUPPORTED. */
+ACE_GGML_API ace_ggml_status ace_mi_timbre_encode(ace_ggml_context* ctx, const float* refer,
+                                                  const int32_t* order_mask, int32_t n_refer, int32_t refer_len,
+                                                  float* out, size_t out_size);
+/* The encoder_hidden_states assembly of ace_generate_audio_style_lyric_timbre_impl
+ * (acestep_ggml.cpp:2414-2556): style states [n_style][text_hidden] (text-encoder output) through the
+ * text projector, lyric embeddings [n_lyric][text_hidden] through the lyric encoder (copy fallback),
+ * timbre references through the timbre encoder, packed lyric | timbre | style with
+ * ace_pack_sequences_single_batch (:1729-1801).  Writes out_enc [len][hidden_size] f32,
+ * out_mask [len] int32 and *out_len = len (sizes in bytes). */
+ACE_GGML_API ace_ggml_status ace_mi_build_condition(ace_ggml_context* ctx, const float* style_states,
+                                                    int32_t n_style, const float* lyric_embeds, int32_t n_lyric,
+                                                    int32_t text_hidden, const float* refer,
+                                                    const int32_t* refer_order_mask, int32_t n_refer,
+                                                    int32_t refer_len, float* out_enc, size_t out_enc_size,
+                                                    int32_t* out_mask, size_t out_mask_size, int32_t* out_len);
+
 #ifdef __cplusplus
 }
 #endif

@@ -38,6 +38,10 @@ class DitConfig:
     sliding_window: int = 0
     use_sliding_window: bool = False
     layer_types: list = field(default_factory=list)
+    text_hidden_dim: int = 0
+    num_lyric_encoder_hidden_layers: int = 0
+    timbre_hidden_dim: int = 0
+    num_timbre_encoder_hidden_layers: int = 0
 
     @staticmethod
     def load(path: str) -> "DitConfig":
@@ -59,6 +63,10 @@ class DitConfig:
             sliding_window=int(o.get("sliding_window", 0) or 0),
             use_sliding_window=bool(o.get("use_sliding_window", False)),
             layer_types=list(o["layer_types"]),
+            text_hidden_dim=int(o.get("text_hidden_dim", 0) or 0),
+            num_lyric_encoder_hidden_layers=int(o.get("num_lyric_encoder_hidden_layers", 0) or 0),
+            timbre_hidden_dim=int(o.get("timbre_hidden_dim", 0) or 0),
+            num_timbre_encoder_hidden_layers=int(o.get("num_timbre_encoder_hidden_layers", 0) or 0),
         )
 
 
@@ -264,6 +272,30 @@ class DitWeights:
             L["sliding"] = i < len(c.layer_types) and c.layer_types[i] == "sliding_attention"  # :1078-1080
             L["cross"] = True  # Layer::use_cross_attention default (acestep_dit_model.h:47)
             self.layers.append(L)
+
+        # condition encoders, all optional (:885-996); consumed by oracle/cond_oracle.py
+        self.text_proj = w2("encoder.text_projector.weight") if "encoder.text_projector.weight" in st else None
+        self.lyric = self._encoder(st, "encoder.lyric_encoder.", c.num_lyric_encoder_hidden_layers, w2, v1)
+        self.timbre = self._encoder(st, "encoder.timbre_encoder.", c.num_timbre_encoder_hidden_layers, w2, v1)
+
+    def _encoder(self, st, pre, n_layers, w2, v1):
+        """EncoderLayer stack of one condition encoder (:889-937 lyric, :941-994 timbre)."""
+        c = self.cfg
+        e = dict(embed=w2(pre + "embed_tokens.weight") if pre + "embed_tokens.weight" in st else None,
+                 embed_b=v1(pre + "embed_tokens.bias") if pre + "embed_tokens.bias" in st else None,
+                 norm=v1(pre + "norm.weight") if pre + "norm.weight" in st else None, layers=[])
+        for i in range(n_layers):
+            p = f"{pre}layers.{i}."
+            e["layers"].append(dict(
+                input_norm=v1(p + "input_layernorm.weight"),
+                post_norm=v1(p + "post_attention_layernorm.weight"),
+                self_attn=dict(q=w2(p + "self_attn.q_proj.weight"), k=w2(p + "self_attn.k_proj.weight"),
+                               v=w2(p + "self_attn.v_proj.weight"), o=w2(p + "self_attn.o_proj.weight"),
+                               q_norm=v1(p + "self_attn.q_norm.weight"), k_norm=v1(p + "self_attn.k_norm.weight")),
+                mlp=dict(gate=w2(p + "mlp.gate_proj.weight"), up=w2(p + "mlp.up_proj.weight"),
+                         down=w2(p + "mlp.down_proj.weight")),
+                sliding=i < len(c.layer_types) and c.layer_types[i] == "sliding_attention"))
+        return e
 
 
 # --------------------------------------------------------------------------

@@ -293,6 +293,17 @@ void launch_rmsnorm_mod(ActType t, const float* x, int M, int H, const float* w,
     }
 }
 
+void launch_rmsnorm_f32(const float* x, int rows, int64_t row_step, int H, const float* w, float eps, float* out,
+                        hipStream_t) {
+    for (int m = 0; m < rows; ++m) {
+        const float* xr = x + (int64_t)m * row_step * H;
+        double ss = 0;
+        for (int i = 0; i < H; ++i) ss += (double)xr[i] * xr[i];
+        const float sc = 1.0f / sqrtf((float)(ss / H) + eps);
+        for (int i = 0; i < H; ++i) out[(int64_t)m * H + i] = xr[i] * sc * w[i];
+    }
+}
+
 void launch_attn_prep(const PrepArgs& a, hipStream_t) {
     auto head = [&](bool isq, int b, int h) {
         const float* w = isq ? a.q_norm : a.k_norm;

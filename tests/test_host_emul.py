@@ -16,7 +16,7 @@ from conftest import ROOT
 
 CSRC = os.path.join(ROOT, "ace-step-1.5-ggml_amd", "csrc")
 CLANG = "/opt/rocm/llvm/bin/clang++"
-RUNTIME = ("json.cpp", "gguf.cpp", "quant.cpp", "model.cpp", "engine.cpp", "vae.cpp", "abi.cpp", "selftest.cpp")
+RUNTIME = ("json.cpp", "gguf.cpp", "quant.cpp", "model.cpp", "engine.cpp", "vae.cpp", "abi.cpp", "cond.cpp", "selftest.cpp")
 
 
 @pytest.fixture(scope="module")
@@ -211,4 +211,84 @@ def test_generation_loop_ex_ode_sde_cover_and_cross_cache(host_lib, tiny_ckpt):
                                 d_context_nc=p(c_nc) if cover is not None else 0,
                                 d_enc_nc=p(e_nc) if cover is not None else 0, cache_cross=cache)
         np.testing.assert_allclose(xt, ref_loop(sde, cover), rtol=1e-5, atol=1e-5, err_msg=str((sde, cover, cache)))
+    br.close()
+
+
+# ---------------------------------------------------------------- condition encoders
+@pytest.fixture(scope="module")
+def cond_ckpt():
+    from acestep_mi355x.synthetic import TINY_COND_CONFIG, write_checkpoint
+    d = tempfile.mkdtemp(prefix="acemi_hec_")
+    write_checkpoint(d, TINY_COND_CONFIG, seed=4, dtype="BF16")
+    return d
+
+
+def test_condition_encoders(host_lib, cond_ckpt):
+    """Lyric encoder, batched timbre encoder, text projector and the packed encoder_hidden_states of
+    ace_mi_build_condition against oracle/cond_oracle.py."""
+    from oracle import cond_oracle as co
+    from oracle.dit_oracle import DitWeights
+    W = DitWeights(cond_ckpt)
+    br = bridge(host_lib)
+    br.load_dit(cond_ckpt)
+    info = br.cond_info()
+    assert (info.hidden_size, info.lyric_in_dim, info.timbre_in_dim, info.text_projector_in) == (256, 128, 64, 128)
+    assert (info.lyric_layers, info.timbre_layers, info.has_lyric_encoder, info.has_timbre_encoder) == (2, 2, 1, 1)
+    rng = np.random.default_rng(8)
+    lyr = rng.standard_normal((45, 128)).astype(np.float32)
+    ref, floor = co.encode_with_floor(co.forward_lyric_encoder, W, lyr)
+    got = br.lyric_encode(lyr)
+    assert rel(got, ref) <= max(1e-3, 1.5 * floor), (rel(got, ref), floor)
+    refer = rng.standard_normal((3, 20, 64)).astype(np.float32)
+    tim = br.timbre_encode(refer)
+    for i in range(3):
+        r, f = co.encode_with_floor(co.forward_timbre_encoder, W, refer[i])
+        assert rel(tim[i], r) <= max(1e-3, 1.5 * f), (i, rel(tim[i], r), f)
+    sty = rng.standard_normal((17, 128)).astype(np.float32)
+    np.testing.assert_allclose(br.text_project(sty), co.project_tokens_linear(W, sty), rtol=1e-5, atol=1e-6)
+    enc, mask = br.build_condition(sty, lyr, refer)
+    eref, mref = co.build_condition(W, sty, lyr, refer, text_hidden=128)
+    assert enc.shape == (45 + 3 + 17, 256) and np.array_equal(mask, mref)
+    assert rel(enc, eref) <= max(1e-3, 1.5 * floor), rel(enc, eref)
+    br.close()
+
+
+def test_condition_encoder_layer_cap_and_fallbacks(host_lib, cond_ckpt, tiny_ckpt, monkeypatch):
+    from oracle import cond_oracle as co
+    from oracle.dit_oracle import DitWeights
+    W = DitWeights(cond_ckpt)
+    rng = np.random.default_rng(9)
+    lyr = rng.standard_normal((30, 128)).astype(np.float32)
+    monkeypatch.setenv("ACE_GGML_LYRIC_MAX_LAYERS", "1")
+    br = bridge(host_lib)
+    br.load_dit(cond_ckpt)
+    ref, floor = co.encode_with_floor(co.forward_lyric_encoder, W, lyr, max_layers=1)
+    got = br.lyric_encode(lyr)
+    assert rel(got, ref) <= max(1e-3, 1.5 * floor)
+    # order mask: multi-batch references are not supported (acestep_ggml.cpp:1832-1834)
+    import ctypes
+    refer = rng.standard_normal((2, 9, 64)).astype(np.float32)
+    with pytest.raises(RuntimeError, match="multi-batch refer_audio_order_mask is not supported"):
+        br.timbre_encode(refer, order_mask=np.array([0, 1], np.int32))
+    # lyric width != lyric encoder input: the copy fallback, widened to H (zero padded)
+    lyr2 = rng.standard_normal((6, 96)).astype(np.float32)
+    monkeypatch.setenv("ACE_GGML_ALLOW_TEXT_DIM_MISMATCH", "1")
+    enc, mask = br.build_condition(lyric_embeds=lyr2)
+    eref, _ = co.build_condition(W, lyric_embeds=lyr2, text_hidden=96, allow_text_mismatch=True)
+    np.testing.assert_array_equal(enc, eref)
+    monkeypatch.delenv("ACE_GGML_ALLOW_TEXT_DIM_MISMATCH")
+    with pytest.raises(RuntimeError, match="text encoder hidden size mismatch with dit"):
+        br.build_condition(lyric_embeds=lyr2)
+    br.close()
+    # a DiT checkpoint without encoder tensors
+    br = bridge(host_lib)
+    br.load_dit(tiny_ckpt)
+    assert br.cond_info().has_timbre_encoder == 0
+    with pytest.raises(RuntimeError, match="forward_lyric_encoder failed"):
+        br.lyric_encode(lyr)
+    with pytest.raises(RuntimeError, match="timbre encoder weights are not loaded"):
+        br.timbre_encode(refer)
+    fp = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+    out = np.zeros((30, 256), np.float32)
+    assert br.lib.ace_mi_text_project(br.ctx, fp(lyr), 30, 128, fp(out), out.nbytes) == 2
     br.close()
