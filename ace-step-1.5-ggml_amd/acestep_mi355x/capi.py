@@ -37,7 +37,9 @@ EXPORTED_SYMBOLS = (
     "ace_mi_vae_out_len", "ace_mi_vae_decode_device", "ace_ggml_vae_encode", "ace_mi_vae_enc_out_len",
     "ace_mi_vae_encode_device", "ace_mi_quantize", "ace_mi_dequantize", "ace_mi_kernel_gemm_q", "ace_mi_bench_gemm_q",
     "ace_mi_cond_get_info", "ace_mi_text_project", "ace_mi_lyric_encode", "ace_mi_timbre_encode",
-    "ace_mi_build_condition",
+    "ace_mi_build_condition", "ace_ggml_load_lm", "ace_ggml_load_text_encoder", "ace_ggml_text_encoder_forward",
+    "ace_ggml_text_encoder_forward_masked", "ace_ggml_text_encoder_forward_embeddings",
+    "ace_ggml_text_encoder_forward_layers",
 )
 
 # qtype codes of ace_mi_quantize & co. (names as parse_quant_type, acestep_dit_model.cpp:27-37)
@@ -152,6 +154,17 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.ace_mi_kernel_gemm_q.restype = ctypes.c_int
     lib.ace_mi_bench_gemm_q.argtypes = [i32, i32, i32, i32, i32, i32, i32, fp]
     lib.ace_mi_bench_gemm_q.restype = ctypes.c_int
+    for name in ("ace_ggml_load_lm", "ace_ggml_load_text_encoder"):
+        getattr(lib, name).argtypes = [vp, ctypes.c_char_p]
+        getattr(lib, name).restype = ctypes.c_int
+    lib.ace_ggml_text_encoder_forward.argtypes = [vp, ip, i32, fp, sz]
+    lib.ace_ggml_text_encoder_forward.restype = ctypes.c_int
+    lib.ace_ggml_text_encoder_forward_masked.argtypes = [vp, ip, ip, i32, fp, sz]
+    lib.ace_ggml_text_encoder_forward_masked.restype = ctypes.c_int
+    lib.ace_ggml_text_encoder_forward_embeddings.argtypes = [vp, ip, i32, fp, sz]
+    lib.ace_ggml_text_encoder_forward_embeddings.restype = ctypes.c_int
+    lib.ace_ggml_text_encoder_forward_layers.argtypes = [vp, ip, ip, i32, i32, i32, fp, sz]
+    lib.ace_ggml_text_encoder_forward_layers.restype = ctypes.c_int
     lib.ace_mi_cond_get_info.argtypes = [vp, ctypes.POINTER(AceMiCondInfo)]
     lib.ace_mi_cond_get_info.restype = ctypes.c_int
     lib.ace_mi_text_project.argtypes = [vp, fp, i32, i32, fp, sz]
@@ -269,6 +282,43 @@ class GGMLCAPIBridge:
         out = np.empty((n // self.hop_length, self.latent_channels), dtype=np.float32)
         st = self.lib.ace_ggml_vae_encode(self.ctx, _fptr(a), n, _fptr(out), out.nbytes)
         self._ensure_ok(st, "ace_ggml_vae_encode")
+        return out
+
+    # -- Qwen3 text encoder (acestep_ggml.h:41-94; the reference's ctypes callers are
+    #    acestep_ggml/tools/compare_text_encoder.py and run_style_lyric_pipeline.py) ----------------
+    def load_text_encoder(self, model_dir) -> None:
+        st = self.lib.ace_ggml_load_text_encoder(self.ctx, str(model_dir).encode("utf-8"))
+        self._ensure_ok(st, "ace_ggml_load_text_encoder")
+        with open(os.path.join(str(model_dir) if not str(model_dir).endswith(".gguf")
+                               else os.path.dirname(str(model_dir)), "config.json"), "r", encoding="utf-8") as f:
+            import json
+            self.text_hidden = int(json.load(f)["hidden_size"])
+
+    def text_encoder_forward(self, token_ids, attention_mask=None, n_layers: Optional[int] = None,
+                             apply_final_norm: bool = True) -> np.ndarray:
+        """Causal Qwen3 forward: ids [n] -> hidden states [n, hidden] (the _layers entry when n_layers is
+        given, _masked with a mask, the plain entry otherwise)."""
+        ids = np.ascontiguousarray(token_ids, dtype=np.int32)
+        am = None if attention_mask is None else np.ascontiguousarray(attention_mask, dtype=np.int32)
+        out = np.empty((ids.shape[0], self.text_hidden), np.float32)
+        if n_layers is not None:
+            st = self.lib.ace_ggml_text_encoder_forward_layers(self.ctx, _iptr(ids), _iptr(am), ids.shape[0],
+                                                               int(n_layers), 1 if apply_final_norm else 0,
+                                                               _fptr(out), out.nbytes)
+        elif am is not None:
+            st = self.lib.ace_ggml_text_encoder_forward_masked(self.ctx, _iptr(ids), _iptr(am), ids.shape[0],
+                                                               _fptr(out), out.nbytes)
+        else:
+            st = self.lib.ace_ggml_text_encoder_forward(self.ctx, _iptr(ids), ids.shape[0], _fptr(out), out.nbytes)
+        self._ensure_ok(st, "ace_ggml_text_encoder_forward")
+        return out
+
+    def text_encoder_embeddings(self, token_ids) -> np.ndarray:
+        ids = np.ascontiguousarray(token_ids, dtype=np.int32)
+        out = np.empty((ids.shape[0], self.text_hidden), np.float32)
+        st = self.lib.ace_ggml_text_encoder_forward_embeddings(self.ctx, _iptr(ids), ids.shape[0], _fptr(out),
+                                                               out.nbytes)
+        self._ensure_ok(st, "ace_ggml_text_encoder_forward_embeddings")
         return out
 
     # -- condition encoders (include/acestep_mi355x.h; acestep_ggml.cpp:1624-1899, :2414-2556) -------
@@ -427,7 +477,7 @@ def kernel_gemm(a_bits: np.ndarray, w_bits: np.ndarray, act_type: int = 0, epi: 
 
 def kernel_attention(q: np.ndarray, kv: np.ndarray, hq: int, hkv: int, window: int = 0,
                      kmask: Optional[np.ndarray] = None, scale: Optional[float] = None,
-                     split: bool = True) -> np.ndarray:
+                     split: bool = True, causal: bool = False) -> np.ndarray:
     """q [B][nq][hq*128] f32, kv [B][nk][2*hkv*128] f32 -> out [B][nq][hq*128] f32 (bf16-rounded)."""
     lib = load_library()
     q = np.ascontiguousarray(q, dtype=np.float32)
@@ -437,7 +487,8 @@ def kernel_attention(q: np.ndarray, kv: np.ndarray, hq: int, hkv: int, window: i
     km = None if kmask is None else np.ascontiguousarray(kmask, dtype=np.int32)
     out = np.empty_like(q)
     sc = float(scale) if scale is not None else 1.0 / np.sqrt(128.0)
-    st = lib.ace_mi_kernel_attention(B, hq, hkv, nq, nk, int(window), sc, 1 if split else 0, _fptr(q), _fptr(kv),
+    st = lib.ace_mi_kernel_attention(B, hq, hkv, nq, nk, int(window), sc, (1 if split else 0) | (2 if causal else 0),
+                                     _fptr(q), _fptr(kv),
                                      _iptr(km), _fptr(out))
     if st != ACE_GGML_OK:
         raise RuntimeError(f"ace_mi_kernel_attention failed (status={st})")

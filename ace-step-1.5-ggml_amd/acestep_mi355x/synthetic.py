@@ -133,15 +133,45 @@ def _encode(values: np.ndarray, dtype: str) -> bytes:
     raise ValueError(dtype)
 
 
+# Qwen3-Embedding-0.6B, the ACE-Step text encoder (config keys of qwen_config.cpp:52-61; tensor names of
+# qwen_model.cpp:425-467, no "model." prefix)
+TEXT_FULL_CONFIG = dict(vocab_size=151669, hidden_size=1024, num_hidden_layers=28, num_attention_heads=16,
+                        num_key_value_heads=8, intermediate_size=3072, head_dim=128, max_position_embeddings=32768,
+                        rms_norm_eps=1e-6, rope_theta=1000000.0)
+TEXT_TINY_CONFIG = dict(TEXT_FULL_CONFIG, vocab_size=1000, hidden_size=256, num_hidden_layers=2,
+                        num_attention_heads=4, num_key_value_heads=2, intermediate_size=512)
+
+
+def text_tensor_specs(cfg: dict) -> Iterator[Tuple[str, Tuple[int, ...], str]]:
+    H, I, D = cfg["hidden_size"], cfg["intermediate_size"], cfg["head_dim"]
+    hq, hkv = cfg["num_attention_heads"], cfg["num_key_value_heads"]
+    yield "embed_tokens.weight", (cfg["vocab_size"], H), "w"
+    yield "norm.weight", (H,), "norm"
+    for i in range(cfg["num_hidden_layers"]):
+        p = f"layers.{i}."
+        yield p + "input_layernorm.weight", (H,), "norm"
+        yield p + "post_attention_layernorm.weight", (H,), "norm"
+        yield p + "self_attn.q_proj.weight", (hq * D, H), "w"
+        yield p + "self_attn.k_proj.weight", (hkv * D, H), "w"
+        yield p + "self_attn.v_proj.weight", (hkv * D, H), "w"
+        yield p + "self_attn.o_proj.weight", (H, hq * D), "w"
+        yield p + "self_attn.q_norm.weight", (D,), "norm"
+        yield p + "self_attn.k_norm.weight", (D,), "norm"
+        yield p + "mlp.gate_proj.weight", (I, H), "w"
+        yield p + "mlp.up_proj.weight", (I, H), "w"
+        yield p + "mlp.down_proj.weight", (H, I), "w"
+
+
 def write_checkpoint(out_dir: str, cfg: dict, seed: int = 0, dtype: str = "BF16", std: float = 0.02,
-                     backend: str = "numpy") -> str:
+                     backend: str = "numpy", specs=None) -> str:
     """Write config.json + model.safetensors into out_dir; returns out_dir.
     backend "numpy" (default, used by the golden fixtures) or "torch" (multi-threaded, ~10x
-    faster for the 1.5 B-parameter benchmark checkpoint; different random values)."""
+    faster for the 1.5 B-parameter benchmark checkpoint; different random values).
+    specs: tensor list (default: the DiT's, tensor_specs(cfg); text_tensor_specs for Qwen3)."""
     os.makedirs(out_dir, exist_ok=True)
     with open(os.path.join(out_dir, "config.json"), "w", encoding="utf-8") as f:
         json.dump(cfg, f, indent=1)
-    specs = list(tensor_specs(cfg))
+    specs = list(tensor_specs(cfg) if specs is None else specs)
     esz = {"BF16": 2, "F16": 2, "F32": 4}[dtype]
     header: Dict[str, dict] = {}
     off = 0

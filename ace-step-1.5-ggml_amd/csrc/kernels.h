@@ -70,6 +70,7 @@ struct AttnArgs {
     int B, Hq, Hkv;
     int nq, nq_pad, nk, nk_pad;
     int window;  // >0: bidirectional sliding window |q-k| <= window
+    bool causal = false;  // key k > query q masked (Qwen3 text encoder)
     float scale;
     bool split = true;                 // hi/lo fp16 operands (see attention.hip)
     int64_t q_plane = 0, k_plane = 0, v_plane = 0;  // element offset of the lo planes
@@ -92,6 +93,9 @@ void launch_rmsnorm_mod(ActType t, const float* x, int M, int H, const float* w,
 // acestep_dit_model.cpp:1642-1644 / :1727-1729; row_step > 1 picks every item's first token).
 void launch_rmsnorm_f32(const float* x, int rows, int64_t row_step, int H, const float* w, float eps, float* out,
                         hipStream_t s);
+// out[t] = f32(table[ids[t]]) for t < n (ggml_get_rows + cast_f32, qwen_model.cpp:563-564):
+// table [rows][H] as bf16 (fmt 0), fp16 (1) or f32 (2) values.
+void launch_embed_rows(const void* table, int fmt, const int32_t* ids, int n, int H, float* out, hipStream_t s);
 // Per-head RMSNorm (+ NEOX RoPE) of the q/k sections and f16 re-layout for attention.
 struct PrepArgs {
     const float* src;

@@ -5,8 +5,9 @@
 // soft_max, V.attn, with GQA head h -> kv head h / n_rep
 // (repeat_kv_interleave :1118-1130) and the additive mask of
 // build_attention_mask (:1132-1173: key padding, bidirectional sliding window
-// |q-k| <= w).  Scores never touch HBM; the sliding layers visit only the
-// key tiles inside the window.
+// |q-k| <= w), plus the causal mask of the Qwen3 text encoder
+// (qwen_model.cpp:618-637).  Scores never touch HBM; the sliding layers visit
+// only the key tiles inside the window, causal blocks stop at their last query.
 //
 // Numerics: the reference runs attention in F32.  SPLIT=true (default) keeps
 // every operand as an fp16 pair x = hi + lo (hi = fp16(x), lo = fp16(x - hi))
@@ -118,6 +119,7 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
         klo = max(0, q0 - a.window);
         khi = min(a.nk, q0 + qpb - 1 + a.window + 1);
     }
+    if (a.causal) khi = min(khi, q0 + qpb);  // no key after the block's last query
     const int kt_begin = klo / KT;
     const int kt_end = (khi + KT - 1) / KT;
 
@@ -235,6 +237,7 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
             lds_wait_all();
         }
         const bool need_window = a.window > 0 && (k0 < qw0 + 31 - a.window || k0 + KT - 1 > qw0 + a.window);
+        const bool need_causal = a.causal && k0 + KT - 1 > qw0;
         float mloc = -INFINITY;
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
@@ -247,6 +250,7 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
                     const int d = qrow - (k0 + krel);
                     if (d > a.window || d < -a.window) x = -INFINITY;
                 }
+                if (need_causal && k0 + krel > qrow) x = -INFINITY;
                 s[t][r] = x;
                 mloc = fmaxf(mloc, x);
             }

@@ -179,6 +179,31 @@ __global__ void __launch_bounds__(256) rmsnorm_f32_kernel(const float* __restric
     }
 }
 
+// token-embedding gather: one workgroup per token, 4 values per thread per step
+template <int FMT>
+__global__ void __launch_bounds__(256) embed_rows_kernel(const void* __restrict__ table, const int32_t* __restrict__ ids,
+                                                         int H, float* __restrict__ out) {
+    const int t = blockIdx.x;
+    const int64_t row = ids[t];
+    float* o = out + (int64_t)t * H;
+    for (int i = threadIdx.x * 4; i < H; i += 256 * 4) {
+        float4 v;
+        if constexpr (FMT == 2) {
+            v = *(const float4*)((const float*)table + row * H + i);
+        } else {
+            const uint2 u = *(const uint2*)((const uint16_t*)table + row * H + i);
+            const uint16_t h[4] = {(uint16_t)(u.x & 0xffffu), (uint16_t)(u.x >> 16), (uint16_t)(u.y & 0xffffu),
+                                   (uint16_t)(u.y >> 16)};
+            float f[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                f[j] = FMT == 0 ? __uint_as_float((uint32_t)h[j] << 16) : (float)__builtin_bit_cast(_Float16, h[j]);
+            v = make_float4(f[0], f[1], f[2], f[3]);
+        }
+        *(float4*)(o + i) = v;
+    }
+}
+
 // ------------------------------------------------------------ attention prep
 // QK-RMSNorm over head_dim (:1202-1203), NEOX RoPE (:1205-1210), the permute/cont copies
 // (:1212-1231) and the V transpose for the P.V MFMA: writes
@@ -478,6 +503,17 @@ void launch_rmsnorm_f32(const float* x, int rows, int64_t row_step, int H, const
         hipLaunchKernelGGL(rmsnorm_f32_kernel<2>, dim3(rows), dim3(256), 0, s, x, row_step, H, w, eps, out);
     else
         hipLaunchKernelGGL(rmsnorm_f32_kernel<4>, dim3(rows), dim3(256), 0, s, x, row_step, H, w, eps, out);
+    ACEMI_HIP(hipGetLastError());
+}
+
+void launch_embed_rows(const void* table, int fmt, const int32_t* ids, int n, int H, float* out, hipStream_t s) {
+    ACEMI_CHECK(H % 4 == 0 && n >= 1 && table && ids, "embed_rows: bad arguments");
+    if (fmt == 0)
+        hipLaunchKernelGGL(embed_rows_kernel<0>, dim3(n), dim3(256), 0, s, table, ids, H, out);
+    else if (fmt == 1)
+        hipLaunchKernelGGL(embed_rows_kernel<1>, dim3(n), dim3(256), 0, s, table, ids, H, out);
+    else
+        hipLaunchKernelGGL(embed_rows_kernel<2>, dim3(n), dim3(256), 0, s, table, ids, H, out);
     ACEMI_HIP(hipGetLastError());
 }
 

@@ -51,6 +51,7 @@ void ace_ggml_destroy(ace_ggml_context* ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     ctx->dit.reset();
     ctx->vae.reset();
+    ctx->text.reset();
     if (ctx->d_vae) (void)hipFree(ctx->d_vae);
     if (ctx->d_in) (void)hipFree(ctx->d_in);
     if (ctx->d_v) (void)hipFree(ctx->d_v);

@@ -9,6 +9,7 @@
 
 #include "../../../include/acestep_mi355x.h"
 #include "engine.h"
+#include "text_encoder.h"
 #include "vae.h"
 
 struct ace_ggml_context {
@@ -20,6 +21,7 @@ struct ace_ggml_context {
     hipStream_t stream = nullptr;
     std::unique_ptr<acemi::DitEngine> dit;
     std::unique_ptr<acemi::VaeEngine> vae;
+    std::unique_ptr<acemi::TextEncoderEngine> text;  // ace_ggml_load_text_encoder / ace_ggml_load_lm
     void* d_vae = nullptr;  // host-ABI staging for ace_ggml_vae_decode
     size_t d_vae_bytes = 0;
     // host-ABI staging (device)

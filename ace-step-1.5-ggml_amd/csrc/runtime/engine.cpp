@@ -17,7 +17,7 @@ DitEngine::DitEngine(int device) : device_(device) {
 DitEngine::~DitEngine() {
     for (Buf* b : {&a0_, &x_, &act_, &attn_, &act2_, &qkv_, &qh_, &kh_, &vt_, &kbias_, &enc_act_, &encp_, &ckv_, &kc_,
                    &vc_, &kbias_c_, &freq_, &freq_act_, &th_, &th_act_, &temb_t_, &temb_r_, &temb_act_, &proj_,
-                   &mods_, &outmod_, &cos_, &sin_}) {
+                   &mods_, &outmod_, &cos_, &sin_, &ein_}) {
         if (b->p) (void)hipFree(b->p);
     }
     if (ev0_) (void)hipEventDestroy(ev0_);
@@ -484,7 +484,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
 void DitEngine::encode(const EncodeIO& io, hipStream_t s) {
     const DitModel& m = model_;
     const DitConfig& c = m.cfg;
-    const int H = c.hidden, D = c.head_dim;
+    const int H = c.hidden;
     const int B = io.B, n = io.n;
     ACEMI_CHECK(io.proj && io.proj->q, "encoder: input projection not loaded");
     ACEMI_CHECK(B >= 1 && n >= 1 && io.in && io.out, "encoder: bad arguments");
@@ -505,118 +505,22 @@ void DitEngine::encode(const EncodeIO& io, hipStream_t s) {
         return;
     }
     const DevEncoder& e = *io.enc;
-    const ActType at = e.act;
     int n_layers = (int)e.layers.size();
     if (io.max_layers >= 0) n_layers = std::min(n_layers, io.max_layers);
-    const int Npad = (int)round_up(n, 128);
-    const int qd = c.hq * D, kd = c.hkv * D;
-    const bool split = attn_split_;
-    const int64_t q_plane = (int64_t)B * c.hq * Npad * D;
-    const int64_t k_plane = (int64_t)B * c.hkv * Npad * D;
-    const int I = e.intermediate;
-    prepare_shape(B, n, 0);
-    ensure(act2_, (size_t)M * I * 2);
-    float* x = get<float>(x_);
-    uint16_t* act = get<uint16_t>(act_);
-    uint16_t* attn = get<uint16_t>(attn_);
-    uint16_t* act2 = get<uint16_t>(act2_);
-    float* qkv = get<float>(qkv_);
-    pe.c_f32 = x;
+    BlockShape sh;
+    sh.hidden = H;
+    sh.hq = c.hq;
+    sh.hkv = c.hkv;
+    sh.head_dim = c.head_dim;
+    sh.intermediate = e.intermediate;
+    sh.eps = c.eps;
+    sh.rope_theta = c.rope_theta;
+    sh.sliding_window = c.sliding_window;
+    pe.c_f32 = cond_.x(M, H);
     launch_gemm(ein, in_dim, io.proj->view(), (int)M, H, in_dim, pe, s);  // x = in W^T + b
-    if (erope_n_ != n) {
-        rope_table(n, ecos_, esin_);  // positions 0..n-1 of each item
-        erope_n_ = n;
-    }
-    launch_key_bias(nullptr, B, n, 1, n, Npad, get<float>(kbias_), s);  // all-ones token mask
-    const float scale = 1.0f / std::sqrt((float)D);
-    for (int li = 0; li < n_layers; ++li) {  // :1614-1640 / :1705-1725
-        const DevLayer& ly = e.layers[li];
-        launch_rmsnorm_mod(at, x, (int)M, H, ly.self_norm, nullptr, nullptr, 0, n, c.eps, act, s);
-        {
-            GemmEpilogue g;
-            g.kind = EPI_STORE_F32;
-            g.c_f32 = qkv;
-            g.ldc = qd + 2 * kd;
-            launch_gemm(act, H, ly.w_qkv.view(), (int)M, qd + 2 * kd, H, g, s);
-        }
-        {
-            PrepArgs pa{};
-            pa.src = qkv;
-            pa.ld = qd + 2 * kd;
-            pa.q_col = 0;
-            pa.k_col = qd;
-            pa.v_col = qd + kd;
-            pa.hq = c.hq;
-            pa.hkv = c.hkv;
-            pa.n_tok = n;
-            pa.n_pad = Npad;
-            pa.B = B;
-            pa.q_norm = ly.sq_norm;
-            pa.k_norm = ly.sk_norm;
-            pa.rope_cos = get<float>(ecos_);
-            pa.rope_sin = get<float>(esin_);
-            pa.eps = c.eps;
-            pa.qh = get<uint16_t>(qh_);
-            pa.kh = get<uint16_t>(kh_);
-            pa.vt = get<uint16_t>(vt_);
-            pa.q_plane = split ? q_plane : 0;
-            pa.k_plane = split ? k_plane : 0;
-            pa.v_plane = split ? k_plane : 0;
-            launch_attn_prep(pa, s);
-        }
-        {
-            AttnArgs aa{};
-            aa.q = get<uint16_t>(qh_);
-            aa.k = get<uint16_t>(kh_);
-            aa.vt = get<uint16_t>(vt_);
-            aa.kbias = get<float>(kbias_);
-            aa.out = attn;
-            aa.B = B;
-            aa.Hq = c.hq;
-            aa.Hkv = c.hkv;
-            aa.nq = n;
-            aa.nq_pad = Npad;
-            aa.nk = n;
-            aa.nk_pad = Npad;
-            aa.window = ly.sliding ? std::max(c.sliding_window, 0) : 0;
-            aa.scale = scale;
-            aa.split = split;
-            aa.q_plane = q_plane;
-            aa.k_plane = k_plane;
-            aa.v_plane = k_plane;
-            launch_attention(at, aa, s);
-        }
-        {
-            GemmEpilogue g;  // h = x + attn_out
-            g.kind = EPI_RESID;
-            g.c_f32 = x;
-            g.ldc = H;
-            launch_gemm(attn, qd, ly.w_o.view(), (int)M, H, qd, g, s);
-        }
-        launch_rmsnorm_mod(at, x, (int)M, H, ly.mlp_norm, nullptr, nullptr, 0, n, c.eps, act, s);
-        {
-            GemmEpilogue g;
-            g.kind = EPI_SWIGLU;
-            g.c_act = act2;
-            g.ldc = I;
-            launch_gemm(act, H, ly.w_gu.view(), (int)M, 2 * I, H, g, s);
-        }
-        {
-            GemmEpilogue g;  // x = h + down
-            g.kind = EPI_RESID;
-            g.c_f32 = x;
-            g.ldc = H;
-            launch_gemm(act2, I, ly.w_down.view(), (int)M, H, I, g, s);
-        }
-    }
-    const int rows = io.first_only ? B : (int)M;
-    const int64_t step = io.first_only ? n : 1;
-    if (e.norm) {
-        launch_rmsnorm_f32(x, rows, step, H, e.norm, c.eps, io.out, s);
-    } else {
-        ACEMI_HIP(hipMemcpy2DAsync(io.out, (size_t)H * 4, x, (size_t)step * H * 4, (size_t)H * 4, rows,
-                                   hipMemcpyDeviceToDevice, s));
-    }
+    // all-ones token mask (acestep_ggml.cpp:1692 / :1838), bidirectional
+    cond_.run(sh, e.layers, n_layers, e.act, B, n, nullptr, false, s);
+    cond_.finish(sh, e.norm, B, n, io.first_only, io.out, s);
 }
 
 void DitEngine::probe_gemm(int which, int M, int iters, hipStream_t s) {

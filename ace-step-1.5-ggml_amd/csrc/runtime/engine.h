@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "../kernels.h"
+#include "blocks.h"
 #include "model.h"
 
 namespace acemi {
@@ -96,8 +97,8 @@ class DitEngine {
     } cross_key_;
     Buf freq_, freq_act_, th_, th_act_, temb_t_, temb_r_, temb_act_, proj_, mods_, outmod_, cos_, sin_;
     int rope_np_ = -1;
-    Buf ein_, ecos_, esin_;  // encoder input activations, encoder RoPE table
-    int erope_n_ = -1;
+    Buf ein_;             // condition-encoder input activations
+    BlockRunner cond_;    // condition-encoder blocks (own workspace: the DiT buffers stay untouched)
     void rope_table(int n, Buf& cs, Buf& sn);
     bool attn_split_ = true;  // ACE_MI_ATTN_FAST=1 -> single fp16 operands
     // profiling

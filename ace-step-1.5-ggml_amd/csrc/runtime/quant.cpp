@@ -397,11 +397,13 @@ QType parse(const char* value) {
     return QNONE;
 }
 
-QType from_env() {
-    const QType t = parse(std::getenv("ACE_GGML_DIT_WEIGHT_QTYPE"));
+QType from_env(const char* primary_key) {
+    const QType t = parse(std::getenv(primary_key));
     if (t != QNONE) return t;
     return parse(std::getenv("ACE_GGML_WEIGHT_QTYPE"));
 }
+
+QType from_env() { return from_env("ACE_GGML_DIT_WEIGHT_QTYPE"); }
 
 const char* name(QType t) {
     switch (t) {

@@ -25,8 +25,10 @@ enum QType : int { QNONE = 0, Q8_0 = 1, Q4_K = 2, Q6_K = 3 };
 
 // parse_quant_type (acestep_dit_model.cpp:27-37): Q8/Q8_0, Q6/Q6_K, Q4/Q4_K/Q4_K_M (case-insensitive)
 QType parse(const char* s);
-// get_quant_type_from_env (:39-45)
+// get_quant_type_from_env (:39-45): ACE_GGML_DIT_WEIGHT_QTYPE, else ACE_GGML_WEIGHT_QTYPE
 QType from_env();
+// the same rule with another model-specific key first (qwen_model.cpp:38-44: ACE_GGML_QWEN_WEIGHT_QTYPE)
+QType from_env(const char* primary_key);
 const char* name(QType t);
 
 int block_values(QType t);       // 32 / 256 / 256

@@ -88,7 +88,7 @@ ace_ggml_status ace_mi_kernel_attention(int32_t B, int32_t Hq, int32_t Hkv, int3
         pq.B = B;
         pq.qh = dqh.as<uint16_t>();
         const int64_t qpl = (int64_t)B * Hq * nq_pad * D, kpl = (int64_t)B * Hkv * nk_pad * D;
-        pq.q_plane = split ? qpl : 0;
+        pq.q_plane = (split & 1) ? qpl : 0;
         launch_attn_prep(pq, nullptr);
         PrepArgs pk{};
         pk.src = dkv.as<float>();
@@ -103,8 +103,8 @@ ace_ggml_status ace_mi_kernel_attention(int32_t B, int32_t Hq, int32_t Hkv, int3
         pk.B = B;
         pk.kh = dkh.as<uint16_t>();
         pk.vt = dvt.as<uint16_t>();
-        pk.k_plane = split ? kpl : 0;
-        pk.v_plane = split ? kpl : 0;
+        pk.k_plane = (split & 1) ? kpl : 0;
+        pk.v_plane = (split & 1) ? kpl : 0;
         launch_attn_prep(pk, nullptr);
         launch_key_bias(kmask ? dm.as<int32_t>() : nullptr, B, nk, 1, nk, nk_pad, dkb.as<float>(), nullptr);
         AttnArgs a{};
@@ -122,7 +122,8 @@ ace_ggml_status ace_mi_kernel_attention(int32_t B, int32_t Hq, int32_t Hkv, int3
         a.nk_pad = nk_pad;
         a.window = window;
         a.scale = scale;
-        a.split = split != 0;
+        a.split = (split & 1) != 0;
+        a.causal = (split & 2) != 0;
         a.q_plane = qpl;
         a.k_plane = kpl;
         a.v_plane = kpl;

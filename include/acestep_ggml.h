@@ -17,6 +17,12 @@
  *   ace_ggml_vae_get_info                    acestep_ggml/cpp/acestep_ggml.h:45-49
  *   ace_ggml_vae_decode                      acestep_ggml/cpp/acestep_ggml.h:50-55
  *   ace_ggml_vae_encode                      acestep_ggml/cpp/acestep_ggml.h:56-61
+ *   ace_ggml_load_lm                         acestep_ggml/cpp/acestep_ggml.h:41
+ *   ace_ggml_load_text_encoder               acestep_ggml/cpp/acestep_ggml.h:42
+ *   ace_ggml_text_encoder_forward            acestep_ggml/cpp/acestep_ggml.h:63-68
+ *   ace_ggml_text_encoder_forward_masked     acestep_ggml/cpp/acestep_ggml.h:70-76
+ *   ace_ggml_text_encoder_forward_embeddings acestep_ggml/cpp/acestep_ggml.h:78-83
+ *   ace_ggml_text_encoder_forward_layers     acestep_ggml/cpp/acestep_ggml.h:86-94
  *
  * Semantics: host f32 row-major, time-major buffers; one sample
  * per call; the caller owns every buffer; blocking; one context is not
@@ -81,6 +87,25 @@ ACE_GGML_API ace_ggml_status ace_ggml_vae_decode(ace_ggml_context* ctx, const fl
  * (needs the encoder.* tensors of the VAE checkpoint). */
 ACE_GGML_API ace_ggml_status ace_ggml_vae_encode(ace_ggml_context* ctx, const float* audio, int32_t n_samples,
                                                  float* out, size_t out_size);
+
+/* Qwen3 text encoder.  Both loaders fill the same text-encoder slot
+ * (acestep_ggml.cpp:246-258); safetensors (ACE_GGML_QWEN_WEIGHT_QTYPE / ACE_GGML_WEIGHT_QTYPE online
+ * quantization) or GGUF (ACE_GGML_QWEN_GGUF, ACE_GGML_TEXT_ENCODER_GGUF, ACE_GGML_LM_GGUF, <dir>.gguf,
+ * <dir>/model.gguf).  Forwards are causal; out is [n_tokens][hidden_size] f32. */
+ACE_GGML_API ace_ggml_status ace_ggml_load_lm(ace_ggml_context* ctx, const char* model_dir);
+ACE_GGML_API ace_ggml_status ace_ggml_load_text_encoder(ace_ggml_context* ctx, const char* model_dir);
+ACE_GGML_API ace_ggml_status ace_ggml_text_encoder_forward(ace_ggml_context* ctx, const int32_t* token_ids,
+                                                           int32_t n_tokens, float* out, size_t out_size);
+ACE_GGML_API ace_ggml_status ace_ggml_text_encoder_forward_masked(ace_ggml_context* ctx, const int32_t* token_ids,
+                                                                  const int32_t* attention_mask, int32_t n_tokens,
+                                                                  float* out, size_t out_size);
+ACE_GGML_API ace_ggml_status ace_ggml_text_encoder_forward_embeddings(ace_ggml_context* ctx,
+                                                                      const int32_t* token_ids, int32_t n_tokens,
+                                                                      float* out, size_t out_size);
+ACE_GGML_API ace_ggml_status ace_ggml_text_encoder_forward_layers(ace_ggml_context* ctx, const int32_t* token_ids,
+                                                                  const int32_t* attention_mask, int32_t n_tokens,
+                                                                  int32_t n_layers, int32_t apply_final_norm,
+                                                                  float* out, size_t out_size);
 
 #ifdef __cplusplus
 }

@@ -99,8 +99,9 @@ ACE_GGML_API ace_ggml_status ace_mi_kernel_gemm(int32_t act_type, int32_t epi, i
                                                 const uint16_t* A, const uint16_t* W, const float* bias,
                                                 float* out_f32, uint16_t* out_u16);
 /* Attention core only (no norm/RoPE): q [B][nq][Hq*128] f32, kv [B][nk][2*Hkv*128] f32 (K then V),
- * kmask [B][nk] int32 or NULL, window > 0 = sliding |q-k| <= window, split 1 = hi/lo fp16 operands
- * (default engine mode), 0 = single fp16; out [B][nq][Hq*128] f32 (the kernel's bf16 output widened). */
+ * kmask [B][nk] int32 or NULL, window > 0 = sliding |q-k| <= window; `split` is a flag word: bit 0 =
+ * hi/lo fp16 operands (default engine mode; clear = single fp16), bit 1 = causal (key k > query q
+ * masked); out [B][nq][Hq*128] f32 (the kernel's bf16 output widened). */
 ACE_GGML_API ace_ggml_status ace_mi_kernel_attention(int32_t B, int32_t Hq, int32_t Hkv, int32_t nq, int32_t nk,
                                                      int32_t window, float scale, int32_t split, const float* q,
                                                      const float* kv, const int32_t* kmask, float* out);

@@ -366,12 +366,14 @@ def apply_rope_neox(x: np.ndarray, cos: np.ndarray, sin: np.ndarray) -> np.ndarr
     return np.concatenate([x0 * c - x1 * s, x0 * s + x1 * c], axis=-1).astype(np.float32)
 
 
-def build_key_bias(q_len, k_len, key_mask, sliding, window):
-    """build_attention_mask (:1132-1173) for causal=False as an additive f32 [q][k] mask,
-    or None when nothing is masked."""
-    if key_mask is None and not sliding:
+def build_key_bias(q_len, k_len, key_mask, sliding, window, causal=False):
+    """build_attention_mask (:1132-1173) as an additive f32 [q][k] mask, or None when nothing is
+    masked.  causal (the text encoder's mask, qwen_model.cpp:618-637): key k > query q masked."""
+    if key_mask is None and not sliding and not causal:
         return None
     allow = np.ones((q_len, k_len), dtype=bool)
+    if causal:
+        allow &= np.arange(k_len)[None, :] <= np.arange(q_len)[:, None]
     if sliding:
         qi = np.arange(q_len)[:, None]
         ki = np.arange(k_len)[None, :]
@@ -381,7 +383,7 @@ def build_key_bias(q_len, k_len, key_mask, sliding, window):
     return np.where(allow, np.float32(0.0), np.float32(-np.inf)).astype(np.float32)
 
 
-def attention(cfg: DitConfig, w: dict, xq, xkv, key_mask, sliding, window, rope):
+def attention(cfg: DitConfig, w: dict, xq, xkv, key_mask, sliding, window, rope, causal=False):
     """attention() (:1175-1259): projections (weight vec_dot rules), per-head QK-RMSNorm,
     NEOX RoPE, f32 softmax(QK^T/sqrt(D) + mask) V with GQA head h -> kv h // n_rep."""
     nh, nkv, D = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
@@ -396,7 +398,7 @@ def attention(cfg: DitConfig, w: dict, xq, xkv, key_mask, sliding, window, rope)
         q = apply_rope_neox(q, cos[:q_len], sin[:q_len])
         k = apply_rope_neox(k, cos[:k_len], sin[:k_len])
     scale = np.float32(1.0 / math.sqrt(D))
-    bias = build_key_bias(q_len, k_len, key_mask, sliding, window)
+    bias = build_key_bias(q_len, k_len, key_mask, sliding, window, causal)
     rep = nh // nkv
     out = np.empty((q_len, nh, D), dtype=np.float32)
     with np.errstate(invalid="ignore", over="ignore"):

@@ -214,6 +214,7 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t) {
                 for (int k = 0; k < a.nk_pad; ++k) {
                     double bias = a.kbias ? a.kbias[(int64_t)b * a.nk_pad + k] : (k < a.nk ? 0.0 : -INFINITY);
                     if (a.window > 0 && std::abs(q - k) > a.window) bias = -INFINITY;
+                    if (a.causal && k > q) bias = -INFINITY;
                     if (std::isinf(bias)) {
                         s[k] = -INFINITY;
                         continue;
@@ -302,6 +303,23 @@ void launch_rmsnorm_f32(const float* x, int rows, int64_t row_step, int H, const
         const float sc = 1.0f / sqrtf((float)(ss / H) + eps);
         for (int i = 0; i < H; ++i) out[(int64_t)m * H + i] = xr[i] * sc * w[i];
     }
+}
+
+void launch_embed_rows(const void* table, int fmt, const int32_t* ids, int n, int H, float* out, hipStream_t) {
+    for (int t = 0; t < n; ++t)
+        for (int i = 0; i < H; ++i) {
+            const int64_t k = (int64_t)ids[t] * H + i;
+            float v;
+            if (fmt == 2) {
+                v = ((const float*)table)[k];
+            } else if (fmt == 0) {
+                const uint32_t u = (uint32_t)((const uint16_t*)table)[k] << 16;
+                std::memcpy(&v, &u, 4);
+            } else {
+                v = f16f(((const uint16_t*)table)[k]);
+            }
+            out[(int64_t)t * H + i] = v;
+        }
 }
 
 void launch_attn_prep(const PrepArgs& a, hipStream_t) {

@@ -75,11 +75,13 @@ def engine_view(W):
             return g.GgmlWeight(g.round_bf16(x.values), "bf16")
         if isinstance(x, dict):
             return {k: fix(v) for k, v in x.items()}
+        if isinstance(x, list):
+            return [fix(v) for v in x]
         return x
 
     W2 = copy.deepcopy(W)
     for k, v in list(vars(W2).items()):
-        setattr(W2, k, [fix(L) for L in v] if k == "layers" else fix(v))
+        setattr(W2, k, fix(v))
     return W2
 
 

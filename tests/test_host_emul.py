@@ -16,7 +16,8 @@ from conftest import ROOT
 
 CSRC = os.path.join(ROOT, "ace-step-1.5-ggml_amd", "csrc")
 CLANG = "/opt/rocm/llvm/bin/clang++"
-RUNTIME = ("json.cpp", "gguf.cpp", "quant.cpp", "model.cpp", "engine.cpp", "vae.cpp", "abi.cpp", "cond.cpp", "selftest.cpp")
+RUNTIME = ("json.cpp", "gguf.cpp", "quant.cpp", "model.cpp", "blocks.cpp", "engine.cpp", "text_encoder.cpp", "vae.cpp", "abi.cpp",
+           "cond.cpp", "text.cpp", "selftest.cpp")
 
 
 @pytest.fixture(scope="module")
@@ -291,4 +292,66 @@ def test_condition_encoder_layer_cap_and_fallbacks(host_lib, cond_ckpt, tiny_ckp
     fp = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
     out = np.zeros((30, 256), np.float32)
     assert br.lib.ace_mi_text_project(br.ctx, fp(lyr), 30, 128, fp(out), out.nbytes) == 2
+    br.close()
+
+
+# ---------------------------------------------------------------- Qwen3 text encoder
+@pytest.fixture(scope="module")
+def text_ckpt():
+    from acestep_mi355x.synthetic import TEXT_TINY_CONFIG, text_tensor_specs, write_checkpoint
+    d = tempfile.mkdtemp(prefix="acemi_het_")
+    write_checkpoint(d, TEXT_TINY_CONFIG, seed=6, dtype="BF16", specs=text_tensor_specs(TEXT_TINY_CONFIG))
+    return d
+
+
+@pytest.mark.parametrize("qtype", [None, "q8_0"])
+def test_text_encoder_forward_entries(host_lib, text_ckpt, monkeypatch, qtype):
+    """ace_ggml_text_encoder_forward / _masked / _layers / _embeddings vs oracle/text_oracle.py
+    (causal attention, key mask, layer cap with and without the final norm)."""
+    from oracle import text_oracle as to
+    if qtype:
+        monkeypatch.setenv("ACE_GGML_QWEN_WEIGHT_QTYPE", qtype)
+    br = bridge(host_lib)
+    br.load_text_encoder(text_ckpt)
+    W = to.TextWeights(text_ckpt, qtype=qtype)
+    if qtype:
+        W = engine_view(W)
+    rng = np.random.default_rng(12)
+    ids = rng.integers(0, 1000, 37).astype(np.int32)
+    np.testing.assert_array_equal(br.text_encoder_embeddings(ids), to.forward_text_encoder_embeddings(W, ids))
+    ref, floor = to.forward_with_floor(W, ids)
+    got = br.text_encoder_forward(ids)
+    assert rel(got, ref) <= max(1e-3, 1.5 * floor), (rel(got, ref), floor)
+    mask = np.ones(37, np.int32)
+    mask[30:] = 0
+    ref, floor = to.forward_with_floor(W, ids, mask)
+    assert rel(br.text_encoder_forward(ids, mask), ref) <= max(1e-3, 1.5 * floor)
+    ref, floor = to.forward_with_floor(W, ids, None, 1, True)   # capped: no final norm
+    assert rel(br.text_encoder_forward(ids, None, n_layers=1), ref) <= max(1e-3, 1.5 * floor)
+    br.close()
+
+
+def test_text_encoder_causality_and_errors(host_lib, text_ckpt):
+    import ctypes
+    br = bridge(host_lib)
+    out = np.zeros((4, 256), np.float32)
+    ip = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+    fp = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+    ids = np.array([1, 2, 3, 4], np.int32)
+    assert br.lib.ace_ggml_text_encoder_forward(br.ctx, ip(ids), 4, fp(out), out.nbytes) == 1
+    assert br._last_error() == "text encoder not loaded"
+    assert br.lib.ace_ggml_load_text_encoder(br.ctx, b"/nonexistent") == 3
+    br.load_text_encoder(text_ckpt)
+    assert br.lib.ace_ggml_text_encoder_forward(br.ctx, ip(ids), 4, fp(out), out.nbytes - 4) == 2
+    assert br._last_error() == "output buffer too small"
+    assert br.lib.ace_ggml_text_encoder_forward(br.ctx, ip(ids), 0, fp(out), out.nbytes) == 2
+    bad = np.array([1, 2, 1000, 4], np.int32)
+    assert br.lib.ace_ggml_text_encoder_forward(br.ctx, ip(bad), 4, fp(out), out.nbytes) == 2
+    assert br._last_error() == "token id out of range"
+    # causal: a prefix's states do not depend on later tokens
+    rng = np.random.default_rng(13)
+    a = rng.integers(0, 1000, 20).astype(np.int32)
+    b = a.copy()
+    b[15:] = rng.integers(0, 1000, 5)
+    np.testing.assert_array_equal(br.text_encoder_forward(a)[:15], br.text_encoder_forward(b)[:15])
     br.close()
