@@ -39,7 +39,8 @@ EXPORTED_SYMBOLS = (
     "ace_mi_cond_get_info", "ace_mi_text_project", "ace_mi_lyric_encode", "ace_mi_timbre_encode",
     "ace_mi_build_condition", "ace_ggml_load_lm", "ace_ggml_load_text_encoder", "ace_ggml_text_encoder_forward",
     "ace_ggml_text_encoder_forward_masked", "ace_ggml_text_encoder_forward_embeddings",
-    "ace_ggml_text_encoder_forward_layers",
+    "ace_ggml_text_encoder_forward_layers", "ace_ggml_generate_audio_simple", "ace_ggml_generate_audio_style_lyric_simple",
+    "ace_ggml_generate_audio_style_lyric_timbre_simple", "ace_mi_reference_noise",
 )
 
 # qtype codes of ace_mi_quantize & co. (names as parse_quant_type, acestep_dit_model.cpp:27-37)
@@ -165,6 +166,15 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.ace_ggml_text_encoder_forward_embeddings.restype = ctypes.c_int
     lib.ace_ggml_text_encoder_forward_layers.argtypes = [vp, ip, ip, i32, i32, i32, fp, sz]
     lib.ace_ggml_text_encoder_forward_layers.restype = ctypes.c_int
+    lib.ace_ggml_generate_audio_simple.argtypes = [vp, ip, i32, i32, f32, i32, fp, sz, ip, ip]
+    lib.ace_ggml_generate_audio_simple.restype = ctypes.c_int
+    lib.ace_ggml_generate_audio_style_lyric_simple.argtypes = [vp, ip, i32, ip, i32, i32, f32, i32, fp, sz, ip, ip]
+    lib.ace_ggml_generate_audio_style_lyric_simple.restype = ctypes.c_int
+    lib.ace_ggml_generate_audio_style_lyric_timbre_simple.argtypes = [vp, ip, i32, ip, i32, fp, ip, i32, i32, i32, f32,
+                                                                      i32, fp, sz, ip, ip]
+    lib.ace_ggml_generate_audio_style_lyric_timbre_simple.restype = ctypes.c_int
+    lib.ace_mi_reference_noise.argtypes = [i32, i64, fp]
+    lib.ace_mi_reference_noise.restype = ctypes.c_int
     lib.ace_mi_cond_get_info.argtypes = [vp, ctypes.POINTER(AceMiCondInfo)]
     lib.ace_mi_cond_get_info.restype = ctypes.c_int
     lib.ace_mi_text_project.argtypes = [vp, fp, i32, i32, fp, sz]
@@ -320,6 +330,40 @@ class GGMLCAPIBridge:
                                                                out.nbytes)
         self._ensure_ok(st, "ace_ggml_text_encoder_forward_embeddings")
         return out
+
+    # -- end-to-end generation (acestep_ggml.h:110-152; reference caller:
+    #    acestep_ggml/tools/run_unified_prompt_style_lyric_timbre.py) ------------------------------------
+    def generate_audio(self, seq_len: int, shift: float = 3.0, seed: int = 0, token_ids=None, style_ids=None,
+                       lyric_ids=None, refer=None, refer_order_mask=None) -> np.ndarray:
+        """audio [samples, channels]: ace_ggml_generate_audio_simple when token_ids is given, else the
+        style/lyric(/timbre) entry."""
+        if self.audio_channels <= 0 or self.hop_length <= 0:
+            raise RuntimeError("VAE not initialized in ggml bridge")
+        out = np.empty((int(seq_len) * self.hop_length * self.audio_channels,), np.float32)
+        ns, nc = ctypes.c_int32(0), ctypes.c_int32(0)
+        arr = lambda a: None if a is None else np.ascontiguousarray(a, dtype=np.int32)
+        if token_ids is not None:
+            ids = arr(token_ids)
+            st = self.lib.ace_ggml_generate_audio_simple(self.ctx, _iptr(ids), len(ids), int(seq_len), float(shift),
+                                                         int(seed), _fptr(out), out.nbytes, ctypes.byref(ns),
+                                                         ctypes.byref(nc))
+        else:
+            si, li = arr(style_ids), arr(lyric_ids)
+            n_s = 0 if si is None else len(si)
+            n_l = 0 if li is None else len(li)
+            if refer is None:
+                st = self.lib.ace_ggml_generate_audio_style_lyric_simple(
+                    self.ctx, _iptr(si), n_s, _iptr(li), n_l, int(seq_len), float(shift), int(seed), _fptr(out),
+                    out.nbytes, ctypes.byref(ns), ctypes.byref(nc))
+            else:
+                rf = np.ascontiguousarray(refer, dtype=np.float32)
+                om = arr(refer_order_mask)
+                st = self.lib.ace_ggml_generate_audio_style_lyric_timbre_simple(
+                    self.ctx, _iptr(si), n_s, _iptr(li), n_l, _fptr(rf), _iptr(om), int(rf.shape[0]),
+                    int(rf.shape[1]), int(seq_len), float(shift), int(seed), _fptr(out), out.nbytes,
+                    ctypes.byref(ns), ctypes.byref(nc))
+        self._ensure_ok(st, "ace_ggml_generate_audio")
+        return out[: ns.value * nc.value].reshape(ns.value, nc.value)
 
     # -- condition encoders (include/acestep_mi355x.h; acestep_ggml.cpp:1624-1899, :2414-2556) -------
     def cond_info(self) -> AceMiCondInfo:
@@ -566,6 +610,14 @@ def bench_gemm_q(M: int, N: int, K: int, qtype: str, variant: int = -1, epi: int
     if st != ACE_GGML_OK:
         raise RuntimeError(f"ace_mi_bench_gemm_q failed (status={st})")
     return float(ms.value)
+
+
+def reference_noise(seed: int, n: int) -> np.ndarray:
+    """x_T of the reference generator (std::mt19937 + std::normal_distribution<float>), host code."""
+    out = np.empty(int(n), np.float32)
+    if load_library().ace_mi_reference_noise(int(seed), int(n), _fptr(out)) != ACE_GGML_OK:
+        raise RuntimeError("ace_mi_reference_noise failed")
+    return out
 
 
 def gemm_variant(variant: int) -> None:

@@ -45,7 +45,7 @@ TINY_CONFIG = make_config(hidden_size=256, intermediate_size=512, num_hidden_lay
 COND_KEYS = dict(text_hidden_dim=1024, num_lyric_encoder_hidden_layers=8, timbre_hidden_dim=64,
                  num_timbre_encoder_hidden_layers=4, timbre_fix_frame=750)
 TINY_COND_CONFIG = make_config(**{k: v for k, v in TINY_CONFIG.items() if k != "layer_types"},
-                               text_hidden_dim=128, num_lyric_encoder_hidden_layers=2, timbre_hidden_dim=64,
+                               text_hidden_dim=256, num_lyric_encoder_hidden_layers=2, timbre_hidden_dim=64,
                                num_timbre_encoder_hidden_layers=2, timbre_fix_frame=8)
 
 

@@ -23,6 +23,9 @@
  *   ace_ggml_text_encoder_forward_masked     acestep_ggml/cpp/acestep_ggml.h:70-76
  *   ace_ggml_text_encoder_forward_embeddings acestep_ggml/cpp/acestep_ggml.h:78-83
  *   ace_ggml_text_encoder_forward_layers     acestep_ggml/cpp/acestep_ggml.h:86-94
+ *   ace_ggml_generate_audio_simple           acestep_ggml/cpp/acestep_ggml.h:110-120
+ *   ace_ggml_generate_audio_style_lyric_simple         acestep_ggml/cpp/acestep_ggml.h:122-134
+ *   ace_ggml_generate_audio_style_lyric_timbre_simple  acestep_ggml/cpp/acestep_ggml.h:136-152
  *
  * Semantics: host f32 row-major, time-major buffers; one sample
  * per call; the caller owns every buffer; blocking; one context is not
@@ -106,6 +109,24 @@ ACE_GGML_API ace_ggml_status ace_ggml_text_encoder_forward_layers(ace_ggml_conte
                                                                   const int32_t* attention_mask, int32_t n_tokens,
                                                                   int32_t n_layers, int32_t apply_final_norm,
                                                                   float* out, size_t out_size);
+
+/* End-to-end text-to-audio (acestep_ggml.cpp:1901-2576): text encoder -> condition -> 8-step Euler
+ * sampler (turbo schedule nearest to `shift`, x_T from std::mt19937(seed)) -> VAE decode.  out_audio
+ * [samples][audio_channels] f32 with out_size >= seq_len * hop * channels * 4; the silence-latent
+ * context and the windowed decode honour the reference's ACE_GGML_* variables. */
+ACE_GGML_API ace_ggml_status ace_ggml_generate_audio_simple(ace_ggml_context* ctx, const int32_t* token_ids,
+                                                            int32_t n_tokens, int32_t seq_len, float shift,
+                                                            int32_t seed, float* out_audio, size_t out_size,
+                                                            int32_t* out_audio_samples, int32_t* out_audio_channels);
+ACE_GGML_API ace_ggml_status ace_ggml_generate_audio_style_lyric_simple(
+    ace_ggml_context* ctx, const int32_t* style_token_ids, int32_t n_style_tokens, const int32_t* lyric_token_ids,
+    int32_t n_lyric_tokens, int32_t seq_len, float shift, int32_t seed, float* out_audio, size_t out_size,
+    int32_t* out_audio_samples, int32_t* out_audio_channels);
+ACE_GGML_API ace_ggml_status ace_ggml_generate_audio_style_lyric_timbre_simple(
+    ace_ggml_context* ctx, const int32_t* style_token_ids, int32_t n_style_tokens, const int32_t* lyric_token_ids,
+    int32_t n_lyric_tokens, const float* refer_audio_acoustic_hidden_states, const int32_t* refer_audio_order_mask,
+    int32_t n_refer_audio, int32_t refer_audio_len, int32_t seq_len, float shift, int32_t seed, float* out_audio,
+    size_t out_size, int32_t* out_audio_samples, int32_t* out_audio_channels);
 
 #ifdef __cplusplus
 }

@@ -184,6 +184,10 @@ ACE_GGML_API ace_ggml_status ace_mi_build_condition(ace_ggml_context* ctx, const
                                                     int32_t refer_len, float* out_enc, size_t out_enc_size,
                                                     int32_t* out_mask, size_t out_mask_size, int32_t* out_len);
 
+/* The x_T stream of the reference generator (std::mt19937(seed) + std::normal_distribution<float>,
+ * acestep_ggml.cpp:2043-2048) as the generate entries draw it: n values into out (host). */
+ACE_GGML_API ace_ggml_status ace_mi_reference_noise(int32_t seed, int64_t n, float* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -33,10 +33,10 @@ def cond_weights():
 def test_condition_order_lyric_timbre_style(cond_weights):
     W = cond_weights
     rng = np.random.default_rng(1)
-    sty = rng.standard_normal((5, 128)).astype(np.float32)
-    lyr = rng.standard_normal((7, 128)).astype(np.float32)
+    sty = rng.standard_normal((5, 256)).astype(np.float32)
+    lyr = rng.standard_normal((7, 256)).astype(np.float32)
     refer = rng.standard_normal((2, 6, 64)).astype(np.float32)
-    enc, mask = co.build_condition(W, sty, lyr, refer, text_hidden=128)
+    enc, mask = co.build_condition(W, sty, lyr, refer, text_hidden=256)
     assert enc.shape == (14, 256) and mask.tolist() == [1] * 14
     np.testing.assert_array_equal(enc[:7], co.forward_lyric_encoder(W, lyr))
     np.testing.assert_array_equal(enc[7], co.forward_timbre_encoder(W, refer[0]))
@@ -60,9 +60,26 @@ def test_lyric_projection_falls_back_to_text_projector(cond_weights):
     import copy
     W = copy.copy(cond_weights)
     W.lyric = dict(cond_weights.lyric, embed=None, embed_b=None)
-    x = np.random.default_rng(3).standard_normal((4, 128)).astype(np.float32)
+    x = np.random.default_rng(3).standard_normal((4, 256)).astype(np.float32)
     y = co.forward_lyric_encoder(W, x)
     np.testing.assert_array_equal(y, co.encoder_blocks(W, W.lyric, co.project_tokens_linear(W, x)))
     W.text_proj = None
     with pytest.raises(co.EncoderFailed):
         co.forward_lyric_encoder(W, x)
+
+
+def test_reference_noise_restatement_matches_the_library_stream():
+    """oracle.pipeline_oracle.reference_noise (std::mt19937 + std::normal_distribution<float> restated)
+    equals the stream the generate entries draw (ace_mi_reference_noise: host code, no GPU)."""
+    from acestep_mi355x import capi
+    from oracle.pipeline_oracle import reference_noise
+    for seed in (0, 42, -7, 2 ** 31 - 1):
+        np.testing.assert_array_equal(capi.reference_noise(seed, 3001), reference_noise(seed, 3001))
+
+
+def test_shift_schedule_picks_the_nearest_turbo_table():
+    from oracle.pipeline_oracle import shift_schedule
+    assert shift_schedule(1.0)[1] == np.float32(0.875)
+    assert shift_schedule(2.4)[1] == np.float32(0.9333333333)
+    assert shift_schedule(2.5)[1] == np.float32(0.9333333333)   # tie d2 == d3 -> s2 (d2 <= d3 first)
+    assert shift_schedule(7.0)[7] == np.float32(0.3)

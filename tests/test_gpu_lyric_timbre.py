@@ -33,7 +33,7 @@ def cond_bridge(cond_ckpt):
 def test_lyric_encoder(cond_ckpt, cond_bridge, n):
     from oracle import cond_oracle as co
     from oracle.dit_oracle import DitWeights
-    x = np.random.default_rng(n).standard_normal((n, 128)).astype(np.float32)
+    x = np.random.default_rng(n).standard_normal((n, 256)).astype(np.float32)
     ref, floor = co.encode_with_floor(co.forward_lyric_encoder, DitWeights(cond_ckpt), x)
     check(cond_bridge.lyric_encode(x), ref, floor, f"lyric n={n}")
 
@@ -54,11 +54,11 @@ def test_build_condition(cond_ckpt, cond_bridge):
     from oracle.dit_oracle import DitWeights
     W = DitWeights(cond_ckpt)
     rng = np.random.default_rng(6)
-    sty = rng.standard_normal((20, 128)).astype(np.float32)
-    lyr = rng.standard_normal((60, 128)).astype(np.float32)
+    sty = rng.standard_normal((20, 256)).astype(np.float32)
+    lyr = rng.standard_normal((60, 256)).astype(np.float32)
     refer = rng.standard_normal((2, 40, 64)).astype(np.float32)
     enc, mask = cond_bridge.build_condition(sty, lyr, refer)
-    ref, mref = co.build_condition(W, sty, lyr, refer, text_hidden=128)
+    ref, mref = co.build_condition(W, sty, lyr, refer, text_hidden=256)
     _, floor = co.encode_with_floor(co.forward_lyric_encoder, W, lyr)
     assert np.array_equal(mask, mref)
     check(enc, ref, floor, "build_condition")

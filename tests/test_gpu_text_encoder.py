@@ -86,3 +86,41 @@ def test_text_encoder_prefix_causality(text_bridge):
     b = a.copy()
     b[140:] = rng.integers(0, 1000, 10)
     np.testing.assert_array_equal(text_bridge.text_encoder_forward(a)[:140], text_bridge.text_encoder_forward(b)[:140])
+
+
+def test_generate_entries_end_to_end(text_ckpt):
+    """ace_ggml_generate_audio_simple / _style_lyric_simple / _style_lyric_timbre_simple on the GPU vs
+    oracle/pipeline_oracle.py (same x_T: the reference's std::mt19937 stream).  8 Euler steps through
+    bf16 DiT forwards and a VAE decode amplify the per-forward floor; the bound is 2e-2 rel. L2."""
+    from acestep_mi355x.capi import GGMLCAPIBridge
+    from acestep_mi355x.synthetic import TINY_COND_CONFIG, VAE_TINY_CONFIG, write_checkpoint, write_vae_checkpoint
+    from oracle import pipeline_oracle as po
+    from oracle.dit_oracle import DitWeights
+    from oracle.text_oracle import TextWeights
+    from oracle.vae_oracle import VaeWeights
+    dd, vd = tempfile.mkdtemp(prefix="acemi_gg_"), tempfile.mkdtemp(prefix="acemi_ggv_")
+    write_checkpoint(dd, TINY_COND_CONFIG, seed=4, dtype="BF16")
+    write_vae_checkpoint(vd, VAE_TINY_CONFIG, seed=1)
+    br = GGMLCAPIBridge()
+    br.load_dit(dd)
+    br.load_vae(vd)
+    br.load_text_encoder(text_ckpt)
+    DW, VW, TW = DitWeights(dd), VaeWeights(vd), TextWeights(text_ckpt)
+    rng = np.random.default_rng(14)
+    style, lyric = rng.integers(0, 1000, 9), rng.integers(0, 1000, 12)
+    refer = rng.standard_normal((1, 10, 64)).astype(np.float32)
+    seq_len, hop = 150, br.hop_length   # > 128: chunked silence encode and windowed decode
+    for i, kw in enumerate([dict(token_ids=style), dict(style_ids=style, lyric_ids=lyric),
+                            dict(style_ids=style, lyric_ids=lyric, refer=refer)]):
+        got = br.generate_audio(seq_len, shift=3.0, seed=11 + i, **kw)
+        if "token_ids" in kw:
+            enc = po.forward_text_encoder_layers_for_simple(TW, style)
+            ref, _ = po.generate_from_encoder(DW, VW, enc, np.ones(len(enc), np.int32), seq_len, 3.0, 11 + i, hop, 2)
+        else:
+            ref, _ = po.generate_style_lyric_timbre(DW, VW, TW, kw.get("style_ids"), kw.get("lyric_ids"),
+                                                    kw.get("refer"), seq_len, 3.0, 11 + i, hop, 2)
+        n = min(len(ref), len(got))
+        l2 = float(np.linalg.norm(got[:n] - ref[:n]) / np.linalg.norm(ref[:n]))
+        print(f"generate case {i}: rel_l2={l2:.3e} samples got={len(got)} ref={len(ref)}")
+        assert abs(len(got) - len(ref)) <= hop and l2 < 2e-2, (i, l2)
+    br.close()

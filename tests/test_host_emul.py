@@ -17,7 +17,7 @@ from conftest import ROOT
 CSRC = os.path.join(ROOT, "ace-step-1.5-ggml_amd", "csrc")
 CLANG = "/opt/rocm/llvm/bin/clang++"
 RUNTIME = ("json.cpp", "gguf.cpp", "quant.cpp", "model.cpp", "blocks.cpp", "engine.cpp", "text_encoder.cpp", "vae.cpp", "abi.cpp",
-           "cond.cpp", "text.cpp", "selftest.cpp")
+           "cond.cpp", "text.cpp", "generate.cpp", "selftest.cpp")
 
 
 @pytest.fixture(scope="module")
@@ -233,10 +233,10 @@ def test_condition_encoders(host_lib, cond_ckpt):
     br = bridge(host_lib)
     br.load_dit(cond_ckpt)
     info = br.cond_info()
-    assert (info.hidden_size, info.lyric_in_dim, info.timbre_in_dim, info.text_projector_in) == (256, 128, 64, 128)
+    assert (info.hidden_size, info.lyric_in_dim, info.timbre_in_dim, info.text_projector_in) == (256, 256, 64, 256)
     assert (info.lyric_layers, info.timbre_layers, info.has_lyric_encoder, info.has_timbre_encoder) == (2, 2, 1, 1)
     rng = np.random.default_rng(8)
-    lyr = rng.standard_normal((45, 128)).astype(np.float32)
+    lyr = rng.standard_normal((45, 256)).astype(np.float32)
     ref, floor = co.encode_with_floor(co.forward_lyric_encoder, W, lyr)
     got = br.lyric_encode(lyr)
     assert rel(got, ref) <= max(1e-3, 1.5 * floor), (rel(got, ref), floor)
@@ -245,10 +245,10 @@ def test_condition_encoders(host_lib, cond_ckpt):
     for i in range(3):
         r, f = co.encode_with_floor(co.forward_timbre_encoder, W, refer[i])
         assert rel(tim[i], r) <= max(1e-3, 1.5 * f), (i, rel(tim[i], r), f)
-    sty = rng.standard_normal((17, 128)).astype(np.float32)
+    sty = rng.standard_normal((17, 256)).astype(np.float32)
     np.testing.assert_allclose(br.text_project(sty), co.project_tokens_linear(W, sty), rtol=1e-5, atol=1e-6)
     enc, mask = br.build_condition(sty, lyr, refer)
-    eref, mref = co.build_condition(W, sty, lyr, refer, text_hidden=128)
+    eref, mref = co.build_condition(W, sty, lyr, refer, text_hidden=256)
     assert enc.shape == (45 + 3 + 17, 256) and np.array_equal(mask, mref)
     assert rel(enc, eref) <= max(1e-3, 1.5 * floor), rel(enc, eref)
     br.close()
@@ -259,7 +259,7 @@ def test_condition_encoder_layer_cap_and_fallbacks(host_lib, cond_ckpt, tiny_ckp
     from oracle.dit_oracle import DitWeights
     W = DitWeights(cond_ckpt)
     rng = np.random.default_rng(9)
-    lyr = rng.standard_normal((30, 128)).astype(np.float32)
+    lyr = rng.standard_normal((30, 256)).astype(np.float32)
     monkeypatch.setenv("ACE_GGML_LYRIC_MAX_LAYERS", "1")
     br = bridge(host_lib)
     br.load_dit(cond_ckpt)
@@ -291,7 +291,7 @@ def test_condition_encoder_layer_cap_and_fallbacks(host_lib, cond_ckpt, tiny_ckp
         br.timbre_encode(refer)
     fp = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
     out = np.zeros((30, 256), np.float32)
-    assert br.lib.ace_mi_text_project(br.ctx, fp(lyr), 30, 128, fp(out), out.nbytes) == 2
+    assert br.lib.ace_mi_text_project(br.ctx, fp(lyr), 30, 256, fp(out), out.nbytes) == 2
     br.close()
 
 
@@ -354,4 +354,44 @@ def test_text_encoder_causality_and_errors(host_lib, text_ckpt):
     b = a.copy()
     b[15:] = rng.integers(0, 1000, 5)
     np.testing.assert_array_equal(br.text_encoder_forward(a)[:15], br.text_encoder_forward(b)[:15])
+    br.close()
+
+
+# ---------------------------------------------------------------- end-to-end generate entries
+def test_generate_entries_end_to_end(host_lib, cond_ckpt, text_ckpt):
+    """ace_ggml_generate_audio_simple / _style_lyric_simple / _style_lyric_timbre_simple (text encoder ->
+    condition -> silence context -> 8-step Euler loop -> windowed VAE decode) vs oracle/pipeline_oracle.py."""
+    from acestep_mi355x.synthetic import VAE_TINY_CONFIG, write_vae_checkpoint
+    from oracle import pipeline_oracle as po
+    from oracle.dit_oracle import DitWeights
+    from oracle.text_oracle import TextWeights
+    from oracle.vae_oracle import VaeWeights
+    vd = tempfile.mkdtemp(prefix="acemi_hegv_")
+    write_vae_checkpoint(vd, VAE_TINY_CONFIG, seed=1)
+    br = bridge(host_lib)
+    br.load_dit(cond_ckpt)
+    br.load_vae(vd)
+    br.load_text_encoder(text_ckpt)
+    DW, VW, TW = DitWeights(cond_ckpt), VaeWeights(vd), TextWeights(text_ckpt)
+    rng = np.random.default_rng(14)
+    style, lyric = rng.integers(0, 1000, 9), rng.integers(0, 1000, 12)
+    refer = rng.standard_normal((1, 10, 64)).astype(np.float32)
+    hop = br.hop_length
+    cases = [dict(token_ids=style), dict(style_ids=style, lyric_ids=lyric),
+             dict(style_ids=style, lyric_ids=lyric, refer=refer)]
+    for i, kw in enumerate(cases):
+        seq_len = 150 if i == 2 else 30   # > 128: chunked silence encode + windowed decode
+        got = br.generate_audio(seq_len, shift=3.0, seed=11 + i, **kw)
+        if "token_ids" in kw:
+            enc = po.forward_text_encoder_layers_for_simple(TW, style)
+            ref, _ = po.generate_from_encoder(DW, VW, enc, np.ones(len(enc), np.int32), seq_len, 3.0, 11 + i, hop, 2)
+        else:
+            ref, _ = po.generate_style_lyric_timbre(DW, VW, TW, kw.get("style_ids"), kw.get("lyric_ids"),
+                                                    kw.get("refer"), seq_len, 3.0, 11 + i, hop, 2)
+        if seq_len <= 128:  # one decode; tiny VAE strides (2, 3) make it <= seq_len * hop samples, rest zero
+            assert got.shape == (seq_len * hop, 2) and len(ref) <= seq_len * hop, (got.shape, ref.shape)
+            assert not got[len(ref):].any()
+        else:               # windowed: as many samples as the trimmed windows hold
+            assert got.shape == ref.shape, (got.shape, ref.shape)
+        assert rel(got[:len(ref)], ref) < 2e-2, (i, rel(got[:len(ref)], ref))
     br.close()
