@@ -116,7 +116,7 @@ void DitEngine::prepare_shape(int B, int Np, int L) {
 // NEOX RoPE table with the reference's own float arithmetic: ggml_rope_cache_init runs
 // theta = p; theta *= theta_scale per pair, theta_scale = powf(base, -2/n_dims), cos/sinf on the CPU
 // (acestep_dit_model.cpp:1205-1210).  Computed once per sequence length on the host.
-void DitEngine::rope_table(int n, Buf& cb, Buf& sb) {
+void DitEngine::rope_table(int n, Buf& cb, Buf& sb, hipStream_t s) {
     const DitConfig& c = model_.cfg;
     const int half = c.head_dim / 2;
     const float theta_scale = powf(c.rope_theta, -2.0f / (float)c.head_dim);
@@ -129,15 +129,17 @@ void DitEngine::rope_table(int n, Buf& cb, Buf& sb) {
             theta *= theta_scale;
         }
     }
+    // a forward still queued on `s` (a non-blocking stream) may read the old table: drain it first
+    ACEMI_HIP(hipStreamSynchronize(s));
     ensure(cb, cs.size() * 4);
     ensure(sb, sn.size() * 4);
     ACEMI_HIP(hipMemcpy(cb.p, cs.data(), cs.size() * 4, hipMemcpyHostToDevice));
     ACEMI_HIP(hipMemcpy(sb.p, sn.data(), sn.size() * 4, hipMemcpyHostToDevice));
 }
 
-void DitEngine::rope_for(int Np) {
+void DitEngine::rope_for(int Np, hipStream_t s) {
     if (rope_np_ == Np) return;
-    rope_table(Np, cos_, sin_);
+    rope_table(Np, cos_, sin_, s);
     rope_np_ = Np;
 }
 
@@ -160,7 +162,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
     ACEMI_CHECK(T >= 1, "seq_len must be > 0");
     ACEMI_CHECK(L == 0 || io.enc != nullptr, "encoder_hidden_states required when enc_len > 0");
     prepare_shape(B, Np, L);
-    rope_for(Np);
+    rope_for(Np, s);
 
     int n_layers = c.layers;
     if (io.max_layers > 0) n_layers = std::min(n_layers, io.max_layers);

@@ -82,7 +82,7 @@ class DitEngine {
         return static_cast<T*>(b.p);
     }
     void prepare_shape(int B, int Np, int L);
-    void rope_for(int Np);
+    void rope_for(int Np, hipStream_t s);
     void tic(hipStream_t s);
     void toc(const char* name, hipStream_t s);
 
@@ -99,7 +99,7 @@ class DitEngine {
     int rope_np_ = -1;
     Buf ein_;             // condition-encoder input activations
     BlockRunner cond_;    // condition-encoder blocks (own workspace: the DiT buffers stay untouched)
-    void rope_table(int n, Buf& cs, Buf& sn);
+    void rope_table(int n, Buf& cs, Buf& sn, hipStream_t s);
     bool attn_split_ = true;  // ACE_MI_ATTN_FAST=1 -> single fp16 operands
     // profiling
     bool profiling_ = false;
