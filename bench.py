@@ -174,6 +174,9 @@ def main():
                         "frac": round(ach / BF16_PEAK_TFLOPS, 4), "traffic": None,
                         "flops_per_launch": flops, "avg_launch_us": round(avg_s * 1e6, 2),
                         "shape_MNK": [M, 2 * info.intermediate_size, info.hidden_size]}
+            traffic = pmc_traffic(T, L, b_loc, args.qtype or "bf16")
+            if traffic is not None:
+                roofline["traffic"] = traffic
         lin = [p for p in prof if p[0].startswith("gemm_")]
         if lin:
             Np = (T + 1) // 2
@@ -235,6 +238,22 @@ def main():
     br.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def pmc_traffic(T, L, b_loc, weights):
+    """HBM bytes per launch of the gate|up GEMM from the committed PMC summary of the same workload
+    (tools/gpu_pmc.sh -> tools/pmc_summary.py -> profiles/pmc_traffic.json, whose "config" names
+    T / enc_len / batch_per_gpu / weights); None when no matching summary exists."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_traffic.json")
+    try:
+        with open(path, "r", encoding="utf-8") as f:
+            d = json.load(f)
+        c = d["config"]
+        if (c["latent_frames"], c["enc_len"], c["batch_per_gpu"], c["weights"]) != (T, L, b_loc, weights):
+            return None
+        return float(d["gate_up"]["hbm_bytes"])
+    except (OSError, KeyError, ValueError, TypeError):
+        return None
 
 
 def cpu_baseline(ckpt, T, L, qtype=None):
