@@ -323,6 +323,22 @@ class GGMLCAPIBridge:
         self._ensure_ok(st, "ace_ggml_text_encoder_forward")
         return out
 
+    # reference GGMLCAPIBridge names (scripts/run_non_ggml_real_case.py:255-281)
+    def text_forward_full(self, token_ids, hidden_dim: int) -> np.ndarray:
+        ids = np.ascontiguousarray(token_ids, dtype=np.int32)
+        out = np.empty((ids.shape[0] * int(hidden_dim),), np.float32)
+        st = self.lib.ace_ggml_text_encoder_forward(self.ctx, _iptr(ids), ids.shape[0], _fptr(out), out.nbytes)
+        self._ensure_ok(st, "ace_ggml_text_encoder_forward")
+        return out.reshape(ids.shape[0], int(hidden_dim))
+
+    def text_forward_embeddings(self, token_ids, hidden_dim: int) -> np.ndarray:
+        ids = np.ascontiguousarray(token_ids, dtype=np.int32)
+        out = np.empty((ids.shape[0] * int(hidden_dim),), np.float32)
+        st = self.lib.ace_ggml_text_encoder_forward_embeddings(self.ctx, _iptr(ids), ids.shape[0], _fptr(out),
+                                                               out.nbytes)
+        self._ensure_ok(st, "ace_ggml_text_encoder_forward_embeddings")
+        return out.reshape(ids.shape[0], int(hidden_dim))
+
     def text_encoder_embeddings(self, token_ids) -> np.ndarray:
         ids = np.ascontiguousarray(token_ids, dtype=np.int32)
         out = np.empty((ids.shape[0], self.text_hidden), np.float32)

@@ -180,3 +180,28 @@ def install_vae_backend(dit_handler: Any, bridge, chunk_size_default: int = 32, 
 
     dit_handler.tiled_decode = types.MethodType(tiled_decode_mi355x, dit_handler)
     setattr(dit_handler, "_ggml_vae_backend", "mi355x-capi")
+
+
+def install_text_encoder_backend(dit_handler: Any, bridge) -> None:
+    """`_install_ggml_text_encoder_backend` (scripts/run_non_ggml_real_case.py:406-428): route
+    `dit_handler.infer_text_embeddings` / `infer_lyric_embeddings` through the GPU text encoder
+    (ace_ggml_text_encoder_forward / _embeddings), one call per row as the reference does."""
+    import torch
+
+    hidden_dim = int(dit_handler.text_encoder.config.hidden_size)
+
+    def _rows(ids):
+        if not isinstance(ids, torch.Tensor):
+            ids = torch.tensor(ids, dtype=torch.long)
+        return ids.detach().cpu().numpy().astype(np.int32, copy=False)
+
+    def infer_text_embeddings_mi355x(self, text_token_idss):
+        out = np.stack([bridge.text_forward_full(r, hidden_dim) for r in _rows(text_token_idss)], axis=0)
+        return torch.from_numpy(out).to(self.device).to(self.dtype)
+
+    def infer_lyric_embeddings_mi355x(self, lyric_token_ids):
+        out = np.stack([bridge.text_forward_embeddings(r, hidden_dim) for r in _rows(lyric_token_ids)], axis=0)
+        return torch.from_numpy(out).to(self.device).to(self.dtype)
+
+    dit_handler.infer_text_embeddings = types.MethodType(infer_text_embeddings_mi355x, dit_handler)
+    dit_handler.infer_lyric_embeddings = types.MethodType(infer_lyric_embeddings_mi355x, dit_handler)

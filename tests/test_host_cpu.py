@@ -95,3 +95,28 @@ def test_synthetic_checkpoint_format():
             assert header[name]["shape"] == list(shape) and header[name]["dtype"] == "BF16"
         assert os.path.getsize(os.path.join(d, "model.safetensors")) == 8 + n + max(
             v["data_offsets"][1] for v in header.values())
+
+
+def test_text_encoder_hook_routes_rows_through_the_bridge():
+    """install_text_encoder_backend mirrors _install_ggml_text_encoder_backend
+    (scripts/run_non_ggml_real_case.py:406-428): one bridge call per row, stacked, moved to the
+    handler's device/dtype."""
+    calls = []
+
+    class TB:
+        def text_forward_full(self, ids, hidden):
+            calls.append(("full", ids.tolist(), hidden))
+            return np.tile(ids[:, None].astype(np.float32), (1, hidden))
+
+        def text_forward_embeddings(self, ids, hidden):
+            calls.append(("emb", ids.tolist(), hidden))
+            return -np.tile(ids[:, None].astype(np.float32), (1, hidden))
+
+    h = types.SimpleNamespace(text_encoder=types.SimpleNamespace(config=types.SimpleNamespace(hidden_size=8)),
+                              device="cpu", dtype=torch.bfloat16)
+    hook.install_text_encoder_backend(h, TB())
+    out = h.infer_text_embeddings(torch.tensor([[1, 2, 3], [4, 5, 6]]))
+    assert out.shape == (2, 3, 8) and out.dtype == torch.bfloat16 and float(out[1, 2, 0]) == 6.0
+    lyr = h.infer_lyric_embeddings([[7, 8]])
+    assert lyr.shape == (1, 2, 8) and float(lyr[0, 1, 3]) == -8.0
+    assert [c[0] for c in calls] == ["full", "full", "emb"] and calls[0][1:] == ([1, 2, 3], 8)
