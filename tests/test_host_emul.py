@@ -395,3 +395,66 @@ def test_generate_entries_end_to_end(host_lib, cond_ckpt, text_ckpt):
             assert got.shape == ref.shape, (got.shape, ref.shape)
         assert rel(got[:len(ref)], ref) < 2e-2, (i, rel(got[:len(ref)], ref))
     br.close()
+
+
+@pytest.mark.parametrize("quant", ["Q4", "F16"])
+def test_text_encoder_gguf(host_lib, text_ckpt, quant):
+    """model.gguf next to config.json (resolve_gguf_path, qwen_model.cpp:46-72): types kept, a
+    quantized embed_tokens table dequantized for get_rows."""
+    from acestep_mi355x.synthetic import write_gguf
+    from oracle import text_oracle as to
+    d = tempfile.mkdtemp(prefix="acemi_hetg_")
+    shutil.copy(os.path.join(text_ckpt, "config.json"), d)
+    path = write_gguf(os.path.join(text_ckpt, "model.safetensors"), os.path.join(d, "model.gguf"), quant=quant,
+                      arch="qwen3")
+    br = bridge(host_lib)
+    br.load_text_encoder(d)
+    W = engine_view(to.TextWeights(d, gguf=path))
+    ids = np.random.default_rng(15).integers(0, 1000, 25).astype(np.int32)
+    np.testing.assert_array_equal(br.text_encoder_embeddings(ids), to.forward_text_encoder_embeddings(W, ids))
+    ref, floor = to.forward_with_floor(W, ids)
+    assert rel(br.text_encoder_forward(ids), ref) <= max(1e-3, 1.5 * floor)
+    br.close()
+
+
+def test_generate_context_options(host_lib, cond_ckpt, text_ckpt, monkeypatch):
+    """ACE_GGML_SILENCE_LATENT_F32 (frames past the file repeat its last frame) and
+    ACE_GGML_USE_SILENCE_CONTEXT=0 (zero context) reach the sampler as the reference builds them."""
+    from acestep_mi355x.synthetic import VAE_TINY_CONFIG, write_vae_checkpoint
+    from oracle import pipeline_oracle as po
+    from oracle.dit_oracle import DitWeights, forward_dit
+    from oracle.text_oracle import TextWeights
+    from oracle.vae_oracle import VaeWeights, decode
+    vd = tempfile.mkdtemp(prefix="acemi_hegc_")
+    write_vae_checkpoint(vd, VAE_TINY_CONFIG, seed=1)
+    br = bridge(host_lib)
+    br.load_dit(cond_ckpt)
+    br.load_vae(vd)
+    br.load_text_encoder(text_ckpt)
+    DW, VW, TW = DitWeights(cond_ckpt), VaeWeights(vd), TextWeights(text_ckpt)
+    ids = np.random.default_rng(16).integers(0, 1000, 6)
+    enc = po.forward_text_encoder_layers_for_simple(TW, ids)
+    seq_len = 20
+    sil = np.random.default_rng(17).standard_normal((7, 64)).astype(np.float32)
+    f = os.path.join(vd, "silence.f32")
+    sil.tofile(f)
+
+    def run_oracle(ctx):
+        xt = po.reference_noise(5, seq_len * 64).reshape(seq_len, 64)
+        sched = po.shift_schedule(1.0)
+        for i, t in enumerate(sched):
+            v = forward_dit(DW, xt, ctx, enc, None, np.ones(len(enc), np.int32), seq_len, len(enc), t, t)
+            xt = (xt - v * (t if i + 1 == len(sched) else np.float32(t - sched[i + 1]))).astype(np.float32)
+        return decode(VW, xt)
+
+    monkeypatch.setenv("ACE_GGML_SILENCE_LATENT_F32", f)
+    got = br.generate_audio(seq_len, shift=1.0, seed=5, token_ids=ids)
+    ctx = np.ones((seq_len, 128), np.float32)
+    ctx[:, :64] = sil[np.minimum(np.arange(seq_len), 6)]
+    ref = run_oracle(ctx)
+    assert rel(got[:len(ref)], ref) < 2e-2
+    monkeypatch.setenv("ACE_GGML_USE_SILENCE_CONTEXT", "0")
+    got = br.generate_audio(seq_len, shift=1.0, seed=5, token_ids=ids)
+    ref = run_oracle(np.zeros((seq_len, 128), np.float32))
+    assert rel(got[:len(ref)], ref) < 2e-2
+    br.close()
