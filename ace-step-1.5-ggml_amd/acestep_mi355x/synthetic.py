@@ -208,13 +208,16 @@ def write_checkpoint(out_dir: str, cfg: dict, seed: int = 0, dtype: str = "BF16"
 
 
 def cached_checkpoint(cfg: dict, seed: int = 0, dtype: str = "BF16", root: str | None = None,
-                      backend: str = "numpy") -> str:
-    """Write the checkpoint once per (cfg, seed, dtype, backend) under a cache dir and reuse it."""
-    key = hashlib.sha1(json.dumps([cfg, seed, dtype, backend], sort_keys=True).encode()).hexdigest()[:16]
+                      backend: str = "numpy", kind: str = "dit") -> str:
+    """Write the checkpoint once per (cfg, seed, dtype, backend, kind) under a cache dir and reuse it.
+    kind "dit" (tensor_specs) or "text" (the Qwen3 text encoder, text_tensor_specs)."""
+    key_parts = [cfg, seed, dtype, backend] + ([kind] if kind != "dit" else [])
+    key = hashlib.sha1(json.dumps(key_parts, sort_keys=True).encode()).hexdigest()[:16]
     root = root or os.environ.get("ACE_MI_SYNTH_DIR") or os.path.join(tempfile.gettempdir(), "acestep_mi355x_synth")
     d = os.path.join(root, key)
     if not os.path.exists(os.path.join(d, "model.safetensors")):
-        write_checkpoint(d, cfg, seed=seed, dtype=dtype, backend=backend)
+        specs = text_tensor_specs(cfg) if kind == "text" else None
+        write_checkpoint(d, cfg, seed=seed, dtype=dtype, backend=backend, specs=specs)
     return d
 
 
