@@ -1,7 +1,8 @@
 """End-to-end text-to-audio timing on one MI355X: ace_ggml_generate_audio_style_lyric_simple with
 full-size synthetic weights (Qwen3-0.6B text encoder, 24-layer DiT with lyric/timbre encoders,
 Oobleck VAE), the reference's own end-to-end entry (acestep_ggml.cpp:2576) whose CPU timings are
-in SURVEY §8d (quant_eval summary: 17.3 s FP for the style+lyric pipeline on Apple arm64 CPU).
+in SURVEY §8d (quant_eval summary: 17.3 s FP for the style+lyric pipeline on an Apple arm64 CPU,
+sequence length not recorded).
 
 Usage: python tools/bench_generate.py [--seconds 10 240] [--runs 3]   (prints one JSON line per length)
 """
@@ -54,7 +55,7 @@ def main():
                           "infer_s_all": [round(x, 4) for x in times], "samples": int(audio.shape[0]),
                           "finite": bool(np.isfinite(audio).all()), "style_tokens": args.style_tokens,
                           "lyric_tokens": args.lyric_tokens, "weights": "synthetic bf16, real shapes",
-                          "reference_cpu_s": {"10 s FP (Apple arm64 CPU)": 17.303}}), flush=True)
+                          "reference_cpu_s": {"FP, Apple arm64 CPU, seq_len unknown (SURVEY 8d)": 17.303}}), flush=True)
     br.close()
 
 
