@@ -88,6 +88,13 @@ def gather_latents(x_local: torch.Tensor, global_batch: int, dst: int = 0) -> Op
     return out
 
 
+def _sync(t: torch.Tensor) -> None:
+    """Order torch's pending work on `t` before the library reads it (its own stream); host tensors
+    (the host-emulated library of the CPU tests) need nothing."""
+    if t.is_cuda:
+        torch.cuda.current_stream().synchronize()
+
+
 def euler_sample_local(bridge, cond: Conditioning, items: Sequence[int], schedule: Sequence[float],
                        stream: int = 0) -> torch.Tensor:
     """Run the ODE loop (acestep_ggml.cpp:2056-2086) for `items` on this rank's GPU through
@@ -100,7 +107,7 @@ def euler_sample_local(bridge, cond: Conditioning, items: Sequence[int], schedul
     mk = cond.mask.index_select(0, idx).contiguous() if cond.mask is not None else None
     B, T, _ = xt.shape
     L = enc.shape[1]
-    torch.cuda.current_stream().synchronize()
+    _sync(xt)
     bridge.dit_sample_device(B, T, L, xt.data_ptr(), ctx.data_ptr(), enc.data_ptr(),
                              mk.data_ptr() if mk is not None else 0, em.data_ptr() if em is not None else 0,
                              list(schedule), stream)
@@ -133,7 +140,7 @@ def generate_local(bridge, cond: Conditioning, items: Sequence[int], schedule: S
         noise = torch.randn((len(schedule) - 1, B, T, C), generator=g, device=dev, dtype=torch.float32)
     elif infer_method not in ("ode", "sde"):
         raise ValueError(infer_method)
-    torch.cuda.current_stream().synchronize()
+    _sync(xt)
     ptr = lambda t: t.data_ptr() if t is not None else 0
     bridge.dit_sample_ex_device(B, T, L, xt.data_ptr(), ptr(ctx), ptr(enc), ptr(mk), ptr(em), list(schedule),
                                 sde=infer_method == "sde", d_noise=ptr(noise), cover_steps=cover_steps,

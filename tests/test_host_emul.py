@@ -6,30 +6,19 @@ paths, the batched/sampler entries and the VAE decode/encode is wired as the ora
 the kernels themselves are checked by the -m gpu tests."""
 import os
 import shutil
-import subprocess
 import tempfile
 
 import numpy as np
 import pytest
 
-from conftest import ROOT
-
-CSRC = os.path.join(ROOT, "ace-step-1.5-ggml_amd", "csrc")
-CLANG = "/opt/rocm/llvm/bin/clang++"
-RUNTIME = ("json.cpp", "gguf.cpp", "quant.cpp", "model.cpp", "blocks.cpp", "engine.cpp", "text_encoder.cpp", "vae.cpp", "abi.cpp",
-           "cond.cpp", "text.cpp", "generate.cpp", "selftest.cpp")
+from hostlib import CLANG, build_host_lib
 
 
 @pytest.fixture(scope="module")
 def host_lib():
     if not os.path.exists(CLANG):
         pytest.skip("host clang++ not available")
-    out = os.path.join(tempfile.mkdtemp(prefix="acemi_hl_"), "libacestep_mi355x_host.so")
-    srcs = [os.path.join(CSRC, "runtime", f) for f in RUNTIME] + [os.path.join(ROOT, "tests", "host", "kernel_emul.cpp")]
-    subprocess.run([CLANG, "-std=c++17", "-O2", "-fPIC", "-shared", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
-                    "-I" + CSRC, "-ffp-contract=off", "-pthread", "-Wno-unused-result", "-Wl,-Bsymbolic", *srcs,
-                    "-o", out], check=True)
-    return out
+    return build_host_lib()
 
 
 @pytest.fixture(scope="module")
