@@ -62,6 +62,7 @@ class DitEngine {
     explicit DitEngine(int device);
     ~DitEngine();
     DitModel& model() { return model_; }
+    int device() const { return device_; }
     void forward(const ForwardIO& io, hipStream_t s);
     void encode(const EncodeIO& io, hipStream_t s);
     // enable per-kernel-class event timing for subsequent forwards

@@ -79,6 +79,7 @@ public:
     explicit VaeEngine(int device) : device_(device) {}
     ~VaeEngine();
     VaeModel& model() { return model_; }
+    int device() const { return device_; }
     // samples produced for n_frames latent frames (= n_frames * hop for even strides; PyTorch
     // ConvTranspose1d lengths for odd ones)
     int64_t out_len(int n_frames) const;
