@@ -197,8 +197,26 @@ void launch_gemm(ActType t, const uint16_t* A, int lda, const uint16_t* W, int l
     launch_gemm(A, lda, w, M, N, K, epi, s);
 }
 
+// Read the first and last element of the range the real kernel touches, so that an allocation smaller
+// than the kernel's footprint (padded rows, lo planes) is an AddressSanitizer report in the host runs.
+template <typename T>
+void touch(const T* p, int64_t n) {
+    if (n <= 0) return;
+    volatile T x = p[0];
+    x = p[n - 1];
+    (void)x;
+}
+
 void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t) {
     const int D = 128, rep = a.Hq / a.Hkv;
+    {  // attn_kernel footprint: Q rows up to nq_pad, K / V^T tiles up to nk_pad, both planes when split
+        const int64_t nq = (int64_t)a.B * a.Hq * a.nq_pad * D, nk = (int64_t)a.B * a.Hkv * a.nk_pad * D;
+        touch(a.q, a.split ? a.q_plane + nq : nq);
+        touch(a.k, a.split ? a.k_plane + nk : nk);
+        touch(a.vt, a.split ? a.v_plane + nk : nk);
+        if (a.kbias) touch(a.kbias, (int64_t)a.B * a.nk_pad);
+        touch(a.out, (int64_t)a.B * a.nq * a.Hq * D);
+    }
     std::vector<double> s((size_t)a.nk_pad), o((size_t)D);
     auto val = [&](const uint16_t* base, int64_t idx, int64_t plane) {
         double v = f16f(base[idx]);
