@@ -465,6 +465,7 @@ void launch_sde(float* xt, const float* v, const float* noise, int64_t n, float 
 // ---------------------------------------------------------------- VAE
 void launch_conv_gemm(const ConvGemmArgs& a, hipStream_t) {
     ACEMI_CHECK(a.Cin % 64 == 0 && a.N % 128 == 0 && a.M >= 1 && a.taps >= 1, "conv_gemm: unsupported shape");
+    touch(a.zero, 64);  // the kernel stages out-of-range rows from 64 zero halves
     const int K = a.taps * a.Cin;
     std::vector<float> row((size_t)K);
     for (int m = 0; m < a.M; ++m) {
