@@ -93,7 +93,7 @@ void DitEngine::prepare_shape(int B, int Np, int L) {
         const int64_t Me = (int64_t)B * L;
         ensure(enc_act_, Me * H * act);
         ensure(encp_, Me * H * act);
-        ensure(ckv_, Me * 2 * kd * 4);
+        ensure(ckv_, Me * c.layers * 2 * kd * 4);  // all layers' cross k|v (one GEMM)
         const void* kc_old = kc_.p;
         const void* vc_old = vc_.p;
         ensure(kc_, (size_t)2 * c.layers * B * c.hkv * Lpad * D * 2);
@@ -240,18 +240,32 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
         e.ldc = H;
         launch_gemm(enc_act, H, m.cond_w.view(), (int)Me, H, H, e, s);
         toc("gemm_condition", s);
-        for (int li = 0; li < n_layers; ++li) {
-            const DevLayer& ly = m.layers[li];
+        // one GEMM for every layer's cross k|v when the weights are fused: ckv [Me][n_layers*2kd]
+        const bool fused = m.w_ckv_all.q != nullptr;
+        const int ld_ckv = fused ? n_layers * 2 * kd : 2 * kd;
+        if (fused) {
             GemmEpilogue ek;
             ek.kind = EPI_STORE_F32;
             ek.c_f32 = get<float>(ckv_);
-            ek.ldc = 2 * kd;
+            ek.ldc = ld_ckv;
             tic(s);
-            launch_gemm(encp, H, ly.w_ckv.view(), (int)Me, 2 * kd, H, ek, s);
+            launch_gemm(encp, H, m.w_ckv_all.view(), (int)Me, ld_ckv, H, ek, s);  // first n_layers layers
             toc("gemm_cross_kv", s);
+        }
+        for (int li = 0; li < n_layers; ++li) {
+            const DevLayer& ly = m.layers[li];
+            if (!fused) {
+                GemmEpilogue ek;
+                ek.kind = EPI_STORE_F32;
+                ek.c_f32 = get<float>(ckv_);
+                ek.ldc = 2 * kd;
+                tic(s);
+                launch_gemm(encp, H, ly.w_ckv.view(), (int)Me, 2 * kd, H, ek, s);
+                toc("gemm_cross_kv", s);
+            }
             PrepArgs pa{};
-            pa.src = get<float>(ckv_);
-            pa.ld = 2 * kd;
+            pa.src = get<float>(ckv_) + (fused ? (size_t)li * 2 * kd : 0);
+            pa.ld = ld_ckv;
             pa.q_col = -1;
             pa.k_col = 0;
             pa.v_col = kd;

@@ -176,6 +176,7 @@ void load_dit_model(const std::string& dir, DitModel& m, int& status_hint) {
             m.te[e].act = a1;
         }
         std::vector<float> tables((size_t)c.layers * 6 * H);
+        std::vector<Mat> ckv(c.layers);  // cross k|v rows per layer, uploaded as one matrix below
         m.layers.resize(c.layers);
         for (int i = 0; i < c.layers; ++i) {
             const std::string p2 = "decoder.layers." + std::to_string(i) + ".";
@@ -198,7 +199,7 @@ void load_dit_model(const std::string& dir, DitModel& m, int& status_hint) {
             {
                 const Mat wk = L.mat(p2 + "cross_attn.k_proj.weight", kd, H);
                 const Mat wv = L.mat(p2 + "cross_attn.v_proj.weight", kd, H);
-                ly.w_ckv = L.finish(Loader::concat_rows({&wk, &wv}));
+                ckv[i] = Loader::concat_rows({&wk, &wv});
             }
             ly.w_co = L.finish(L.mat(p2 + "cross_attn.o_proj.weight", H, qd));
             ly.w_gu = L.gate_up(p2, I, H);
@@ -210,6 +211,36 @@ void load_dit_model(const std::string& dir, DitModel& m, int& status_hint) {
             ly.sliding = i < (int)c.layer_types.size() && c.layer_types[i] == "sliding_attention";
         }
         m.tables = L.upload<float>(tables.data(), tables.size() * 4);
+        // every layer's cross k|v in one [layers*2kd][H] matrix when they share a type (always, except a
+        // GGUF file mixing types across layers): the encoder-side projections become one GEMM with
+        // N = layers*2kd instead of `layers` GEMMs of M = L rows that fill a quarter of the GPU
+        bool one_type = true;
+        for (int i = 1; i < c.layers; ++i)
+            one_type = one_type && ckv[i].dtype == ckv[0].dtype && ckv[i].qt == ckv[0].qt;
+        if (one_type && c.layers > 0) {
+            std::vector<const Mat*> parts;
+            for (const Mat& x : ckv) parts.push_back(&x);
+            m.w_ckv_all = L.finish(Loader::concat_rows(parts));
+            for (int i = 0; i < c.layers; ++i) {
+                DevWeight v = m.w_ckv_all;
+                v.rows = 2 * kd;
+                const int64_t r0 = (int64_t)i * 2 * kd;
+                const quant::QType q = v.fmt == WF_Q8_0 ? quant::Q8_0
+                                       : v.fmt == WF_Q4_K ? quant::Q4_K
+                                       : v.fmt == WF_Q6_K ? quant::Q6_K
+                                                          : quant::QNONE;
+                if (q == quant::QNONE) {
+                    v.q = static_cast<char*>(v.q) + r0 * v.cols * 2;
+                } else {
+                    v.q = static_cast<char*>(v.q) + quant::q_plane_bytes(q, r0, v.cols);
+                    v.s = v.s + quant::s_plane_floats(q, r0, v.cols);
+                }
+                m.layers[i].w_ckv = v;
+            }
+        } else {
+            for (int i = 0; i < c.layers; ++i) m.layers[i].w_ckv = L.finish(ckv[i]);
+        }
+        ckv.clear();
 
         // ---- condition encoders (optional; acestep_dit_model.cpp:885-996)
         if (L.has("encoder.text_projector.weight")) {

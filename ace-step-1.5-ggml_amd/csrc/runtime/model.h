@@ -106,6 +106,8 @@ struct DitModel {
     float* proj_in_b = nullptr;
     DevWeight proj_out_w;            // [P*audio][H], row o + k*audio
     float* proj_out_b = nullptr;
+    DevWeight w_ckv_all;             // [layers * 2*hkv*D][H]: every layer's cross k|v rows in one matrix
+                                     // (one GEMM per forward); DevLayer::w_ckv are views into it
     DevWeight cond_w;                // [H][H]
     float* cond_b = nullptr;
     float* norm_out = nullptr;

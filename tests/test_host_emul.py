@@ -447,3 +447,17 @@ def test_generate_context_options(host_lib, cond_ckpt, text_ckpt, monkeypatch):
     ref = run_oracle(np.zeros((seq_len, 128), np.float32))
     assert rel(got[:len(ref)], ref) < 2e-2
     br.close()
+
+
+def test_dit_forward_layer_cap_with_fused_cross_kv(host_lib, tiny_ckpt, monkeypatch):
+    """ACE_GGML_DIT_MAX_LAYERS=1: the fused cross-k|v GEMM covers only the first layer's rows (ld of the
+    k|v buffer = n_layers * 2kd), then the cache is reused by a full-depth forward of the sampler."""
+    from oracle.dit_oracle import DitWeights, forward_with_floor
+    monkeypatch.setenv("ACE_GGML_DIT_MAX_LAYERS", "1")
+    br = bridge(host_lib)
+    br.load_dit(tiny_ckpt)
+    h, c, e = inputs(19, 40, 11)
+    got = br.dit_forward_tfirst(h, c, e, None, None, 0.9, 0.9)
+    ref, floor = forward_with_floor(DitWeights(tiny_ckpt), h, c, e, None, None, 40, 11, 0.9, 0.9, max_layers=1)
+    assert rel(got, ref) <= max(1e-3, 1.5 * floor), (rel(got, ref), floor)
+    br.close()
