@@ -323,6 +323,11 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(GemmParams p) {
             wait_vmcnt<0>();
         }
         __builtin_amdgcn_s_barrier();
+        // The first half of the tile's MFMAs normally issues before the barrier (overlapping the wait).
+        // For the plain-store epilogues the register allocator then rotates that half's accumulators
+        // through VGPRs every iteration (48 v_accvgpr copies per 32 MFMAs in the 128x128 ISA, 96 per 64
+        // in 256x128; none for the other epilogues), so those instances issue every MFMA after it.
+        constexpr int I_EARLY = (EPI == EPI_STORE_F32 || EPI == EPI_STORE_ACT) ? 0 : TM / 2;
         for (int kt = 0; kt < nk; ++kt) {
             const int cur = kt & 1;
             uint4 a[TM][2], b[TN][2];
@@ -330,7 +335,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(GemmParams p) {
 #pragma unroll
             for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-                for (int i = 0; i < TM / 2; ++i)
+                for (int i = 0; i < I_EARLY; ++i)
 #pragma unroll
                     for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<F16>(a[i][kk], b[j][kk], acc[i][j]);
             __builtin_amdgcn_s_barrier();  // every wave has its fragments of tile kt: buffer `cur` is free
@@ -339,7 +344,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(GemmParams p) {
 #pragma unroll
             for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-                for (int i = TM / 2; i < TM; ++i)
+                for (int i = I_EARLY; i < TM; ++i)
 #pragma unroll
                     for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<F16>(a[i][kk], b[j][kk], acc[i][j]);
             if (kt + 1 < nk) {

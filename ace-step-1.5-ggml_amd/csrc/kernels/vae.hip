@@ -148,7 +148,7 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(ConvGemmArgs p) {
     };
 
     // PIPE-1 schedule of the DiT GEMM (gemm.hip): fragments read up front, raw barrier frees the
-    // buffer, tile kt+2 staged during the second half, counted vmcnt retires kt+1.
+    // buffer, tile kt+2 staged while the MFMAs run, counted vmcnt retires kt+1.
     stage(0, 0);
     if (nk > 1) {
         stage(1, 1);
@@ -157,14 +157,16 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(ConvGemmArgs p) {
         wait_vmcnt<0>();
     }
     __builtin_amdgcn_s_barrier();
+    // every MFMA after the barrier: issuing half of them before it makes the register allocator
+    // rotate those accumulators through VGPRs each iteration (48 v_accvgpr copies per 32 MFMAs)
     for (int kt = 0; kt < nk; ++kt) {
         const int cur = kt & 1;
         uint4 a[TM][2], b[TN][2];
         read_frags(cur, a, b);
-        mma(a, b, 0);
         __builtin_amdgcn_s_barrier();
         const bool more = kt + 2 < nk;
         if (more) stage(cur, kt + 2);
+        mma(a, b, 0);
         mma(a, b, TM / 2);
         if (kt + 1 < nk) {
             if (more)
