@@ -259,6 +259,9 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
         const float m_new = fmaxf(m_run, mloc);
         const float m_use = ((m_new == -INFINITY) ? 0.f : m_new) - PSCALE_LOG2;
         const float alpha = __builtin_amdgcn_exp2f(m_run - PSCALE_LOG2 - m_use);
+        // alpha is exp2(0) = 1 for every row whose running max did not move; once the maxima settle
+        // (after the first few key tiles) whole waves skip the O rescale below
+        const bool rescale = __ballot(m_new != m_run) != 0;
         m_run = m_new;
         float lsum = 0.f;
         uint4 pf[4], pfl[4];
@@ -288,11 +291,13 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
                 }
             }
         }
-        l_run = l_run * alpha + lsum;
+        l_run = (rescale ? l_run * alpha : l_run) + lsum;  // O and l always scaled together
+        if (rescale) {
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt)
+            for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+                for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+        }
 
         // ---- O^T += V^T . P^T ; SPLIT: Vh.Ph + Vh.Pl + Vl.Ph
 #pragma unroll
