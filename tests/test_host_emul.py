@@ -461,3 +461,23 @@ def test_dit_forward_layer_cap_with_fused_cross_kv(host_lib, tiny_ckpt, monkeypa
     ref, floor = forward_with_floor(DitWeights(tiny_ckpt), h, c, e, None, None, 40, 11, 0.9, 0.9, max_layers=1)
     assert rel(got, ref) <= max(1e-3, 1.5 * floor), (rel(got, ref), floor)
     br.close()
+
+
+def test_eval_quant_tool_on_tiny_models(host_lib, cond_ckpt, text_ckpt):
+    """tools/eval_quant.py (the reference's FP-vs-quantized acceptance metrics) end to end on the tiny
+    models: identical FP runs give zero error, Q8_0 stays close, Q4_K further away."""
+    import importlib.util
+    from acestep_mi355x.synthetic import VAE_TINY_CONFIG, write_vae_checkpoint
+    spec = importlib.util.spec_from_file_location("eval_quant", os.path.join(os.path.dirname(__file__), "..", "tools",
+                                                                             "eval_quant.py"))
+    eq = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(eq)
+    vd = tempfile.mkdtemp(prefix="acemi_heq_")
+    write_vae_checkpoint(vd, VAE_TINY_CONFIG, seed=1)
+    rows = eq.run(cond_ckpt, vd, text_ckpt, 0.8, ["q8_0", "q4_k"], style_tokens=5, lyric_tokens=7, lib=host_lib,
+                  vocab=1000)
+    r8, r4 = rows[1], rows[2]
+    assert r8["cosine"] > 0.99 and r8["snr_db"] > 20, r8
+    assert r4["rmse"] > r8["rmse"], (r4, r8)
+    m = eq.metrics(np.ones((300, 2)), np.ones((300, 2)))
+    assert m["mae"] == 0 and m["lsd"] == 0 and m["cosine"] == pytest.approx(1.0)
