@@ -4,7 +4,8 @@
 #   2. GEMM micro-bench, dense and dequant-fused (tools/gemm_bench.py)
 #   3. bench.py line + rocprofv3 --kernel-trace --stats of the same command (tools/gpu_bench.sh)
 #   4. HBM traffic from counter-only PMC passes (tools/gpu_pmc.sh)
-#   5. bench.py with Q8_0 weights, end-to-end generate timing (tools/bench_generate.py)
+#   5. bench.py with Q8_0 weights, end-to-end generate timing (tools/bench_generate.py), FP-vs-quantized
+#      end-to-end quality (tools/eval_quant.py)
 # Outputs under gpurun_out/; copy the summaries to be kept into profiles/.
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
@@ -27,4 +28,7 @@ if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 900 python tools/bench_generate.py --seconds 10 240 --runs 2 > gpurun_out/bench_generate.json \
     2> gpurun_out/bench_generate.err
 rc=$?; echo "bench_generate rc=$rc" >> gpurun_out/bench_generate.err
+if [ $rc -ne 0 ]; then exit $rc; fi
+timeout -k 10 900 python tools/eval_quant.py --seconds 10 > gpurun_out/eval_quant.json 2> gpurun_out/eval_quant.err
+rc=$?; echo "eval_quant rc=$rc" >> gpurun_out/eval_quant.err
 exit $rc
