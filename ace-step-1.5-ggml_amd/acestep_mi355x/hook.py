@@ -61,16 +61,16 @@ def dit_forward_torch(bridge, hidden_states, timestep, timestep_r, attention_mas
     enc_len = int(enc.shape[1])
     if dev.type == "cuda":
         out = torch.empty((bsz, seq_len, audio), dtype=torch.float32, device=dev)
-        stream = torch.cuda.current_stream(dev).cuda_stream
-        for b0 in range(0, bsz, MAX_BATCH_PER_CALL):
-            b1 = min(bsz, b0 + MAX_BATCH_PER_CALL)
-            n = b1 - b0
-            bridge.dit_forward_batched_device(
-                n, seq_len, enc_len, x[b0:b1].data_ptr(), ctx[b0:b1].data_ptr(),
-                enc[b0:b1].data_ptr() if enc_len > 0 else 0,
-                am[b0:b1].data_ptr() if am is not None else 0,
-                eam[b0:b1].data_ptr() if eam is not None else 0,
-                t[b0:b1].data_ptr(), r[b0:b1].data_ptr(), out[b0:b1].data_ptr(), stream)
+        with _OrderedCall(bridge, dev) as stream:
+            for b0 in range(0, bsz, MAX_BATCH_PER_CALL):
+                b1 = min(bsz, b0 + MAX_BATCH_PER_CALL)
+                n = b1 - b0
+                bridge.dit_forward_batched_device(
+                    n, seq_len, enc_len, x[b0:b1].data_ptr(), ctx[b0:b1].data_ptr(),
+                    enc[b0:b1].data_ptr() if enc_len > 0 else 0,
+                    am[b0:b1].data_ptr() if am is not None else 0,
+                    eam[b0:b1].data_ptr() if eam is not None else 0,
+                    t[b0:b1].data_ptr(), r[b0:b1].data_ptr(), out[b0:b1].data_ptr(), stream)
         return out.to(hidden_states.dtype)
     # host tensors: reference host-pointer ABI, one item per call (compute still on the GPU)
     out_np = np.empty((bsz, seq_len, audio), dtype=np.float32)
@@ -134,6 +134,30 @@ def _tile_plan(T: int, chunk_size: int, overlap: int):
     return plan
 
 
+class _OrderedCall:
+    """Order one library call on device tensors against torch's current stream.  A non-default torch
+    stream is handed to the library, so both sides run in stream order.  torch's legacy default stream
+    has handle 0, which the C-ABI reads as "the context's own stream" (a non-blocking stream,
+    include/acestep_mi355x.h): then torch's pending work is drained before the call and the library's
+    stream after it, so neither side reads a buffer the other is still writing."""
+
+    def __init__(self, bridge, dev):
+        import torch
+        self.bridge = bridge
+        self.torch_stream = torch.cuda.current_stream(dev)
+        self.stream = self.torch_stream.cuda_stream
+
+    def __enter__(self):
+        if self.stream == 0:
+            self.torch_stream.synchronize()
+        return self.stream
+
+    def __exit__(self, *exc):
+        if self.stream == 0:
+            self.bridge.synchronize()
+        return False
+
+
 def vae_decode_torch(bridge, latents_bct, chunk_size: int, overlap: int):
     """latents [B, C, T] (ROCm tensor) -> audio [B, channels, samples] on the same device, decoding
     each window with ace_mi_vae_decode_device on torch's current stream (no host round trip).
@@ -141,7 +165,6 @@ def vae_decode_torch(bridge, latents_bct, chunk_size: int, overlap: int):
     import torch
     B, C, T = latents_bct.shape
     dev = latents_bct.device
-    stream = torch.cuda.current_stream(dev).cuda_stream
     lat = latents_bct.detach().to(torch.float32)
     outs = []
     plan = [(0, T, 0, T)] if T <= chunk_size else _tile_plan(T, chunk_size, overlap)
@@ -151,7 +174,8 @@ def vae_decode_torch(bridge, latents_bct, chunk_size: int, overlap: int):
             win = lat[b, :, ws:we].transpose(0, 1).contiguous()        # [frames, C]
             n = we - ws
             wav = torch.empty((bridge.vae_out_len(n), bridge.audio_channels), dtype=torch.float32, device=dev)
-            bridge.vae_decode_device(win.data_ptr(), n, wav.data_ptr(), stream)
+            with _OrderedCall(bridge, dev) as stream:
+                bridge.vae_decode_device(win.data_ptr(), n, wav.data_ptr(), stream)
             up = float(wav.shape[0]) / float(max(1, n))
             ts = int(round((cs - ws) * up))
             te = int(round((we - ce) * up))

@@ -383,9 +383,12 @@ __device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) {
     return __builtin_bit_cast(uint32_t, v);
 }
 
+// A compiler-visible LDS store, not inline asm: the hazard recognizer does not cover an asm
+// ds_write_b128's data VGPRs, and on gfx950 the VALU overwrote them before the DS unit had read the
+// last lanes (lanes 48-63 of the dequantized W rows came out wrong on the GPU).
 __device__ __forceinline__ void ds_write_b128_v(uint32_t addr, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-    u32x4 v = {a, b, c, d};
-    asm volatile("ds_write_b128 %0, %1" : : "v"(addr), "v"(v) : "memory");
+    typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+    *(lds_u32x4*)(uintptr_t)addr = u32x4{a, b, c, d};
 }
 
 // Weight bytes are plain (compiler-tracked) loads issued one k-tile ahead; the loop consumes them
@@ -574,19 +577,28 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_q_kernel(GemmParams p) {
         const int cur = kt & 1;
         uint4 a[TM][2], b[TN][2];
         read_frags_asm(cur, a, b);
-        mfma_half(a, b, 0);
+        // Every MFMA of the tile issues after this barrier (the dequant VALU work interleaves with them).
         __builtin_amdgcn_s_barrier();  // every wave holds its fragments of tile kt: buffer `cur` is free
+        asm volatile("" ::: "memory");  // the LDS stores below stay after the barrier
         // W(kt+2): waiting for its bytes also retires the older A(kt+1) DMA
         dequant_store<WQ>(wnext, lds0 + cur * STAGE + wrow_off, wh, wsw);
+        // Every wave's ds_writes retire before any wave issues its LDS-DMA: measured on gfx950, an LDS
+        // DMA issued while ds_write_b128s of the workgroup are still in flight corrupts lanes 48-63 of
+        // those writes (random W elements of rows 24-31 of every 32, on some launches).  A per-wave
+        // lgkmcnt(0) cleared the 4-wave tiles but not the 8-wave 256x256 one; lgkmcnt(0) + barrier
+        // cleared all (tools/diag_gemm_q.py stress: 0 bad launches of 20 per variant and format).
+        lds_wait_all();
+        __builtin_amdgcn_s_barrier();
         stage_a(cur, min(kt + 2, nk - 1));
         // keep the W(kt+3) loads behind the A(kt+2) DMA in issue order: the vmcnt the compiler
         // places before the next iteration's dequant (waiting for those bytes) then also retires
         // A(kt+2) before the barrier that ends that iteration publishes buffer `cur` again
         asm volatile("" ::: "memory");
         wnext = load_wq<WQ>(qbase, sbase, min(kt + 3, nk - 1));
+        mfma_half(a, b, 0);
         mfma_half(a, b, TM / 2);
-        // the dequantized W rows are asm ds_writes the compiler does not count: retire them before
-        // the barrier that hands buffer `cur` to the other waves (gfx950 does not wait at s_barrier)
+        // retire this wave's LDS traffic before the barrier that hands buffer `cur` to the other waves
+        // (gfx950 does not wait at s_barrier)
         lds_wait_all();
         __builtin_amdgcn_s_barrier();
     }

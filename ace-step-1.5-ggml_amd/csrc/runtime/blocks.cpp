@@ -29,6 +29,9 @@ void BlockRunner::ensure(Buf& b, size_t bytes) {
     const size_t alloc = (bytes + 255) & ~size_t(255);
     ACEMI_HIP(hipMalloc(&b.p, alloc));
     ACEMI_HIP(hipMemset(b.p, 0, alloc));
+    // hipMemset runs on the legacy null stream, which does not order against the library's
+    // non-blocking streams: finish it before any kernel can write the new buffer
+    ACEMI_HIP(hipDeviceSynchronize());
     b.bytes = alloc;
 }
 
@@ -73,6 +76,7 @@ void BlockRunner::run(const BlockShape& sh, const std::vector<DevLayer>& layers,
         ensure(sin_, sn.size() * 4);
         ACEMI_HIP(hipMemcpy(cos_.p, cs.data(), cs.size() * 4, hipMemcpyHostToDevice));
         ACEMI_HIP(hipMemcpy(sin_.p, sn.data(), sn.size() * 4, hipMemcpyHostToDevice));
+        ACEMI_HIP(hipDeviceSynchronize());  // null-stream copy: done before any stream reads it
         rope_n_ = n;
         rope_theta_ = sh.rope_theta;
     }

@@ -73,7 +73,10 @@ inline void bind_device(ace_ggml_context* ctx) {
 
 inline void ensure_dev(void*& p, size_t& have, size_t need) {
     if (have >= need) return;
-    if (p) ACEMI_HIP(hipFree(p));
+    if (p) {
+        ACEMI_HIP(hipDeviceSynchronize());  // in-flight work may still use the old staging buffer
+        ACEMI_HIP(hipFree(p));
+    }
     p = nullptr;
     have = 0;
     ACEMI_HIP(hipMalloc(&p, need));

@@ -36,6 +36,9 @@ void DitEngine::ensure(Buf& b, size_t bytes) {
     const size_t alloc = (bytes + 255) & ~size_t(255);
     ACEMI_HIP(hipMalloc(&b.p, alloc));
     ACEMI_HIP(hipMemset(b.p, 0, alloc));
+    // hipMemset runs on the legacy null stream, which does not order against the library's
+    // non-blocking streams: finish it before any kernel can write the new buffer
+    ACEMI_HIP(hipDeviceSynchronize());
     b.bytes = alloc;
 }
 
@@ -135,6 +138,7 @@ void DitEngine::rope_table(int n, Buf& cb, Buf& sb, hipStream_t s) {
     ensure(sb, sn.size() * 4);
     ACEMI_HIP(hipMemcpy(cb.p, cs.data(), cs.size() * 4, hipMemcpyHostToDevice));
     ACEMI_HIP(hipMemcpy(sb.p, sn.data(), sn.size() * 4, hipMemcpyHostToDevice));
+    ACEMI_HIP(hipDeviceSynchronize());  // null-stream copy: done before any stream reads it
 }
 
 void DitEngine::rope_for(int Np, hipStream_t s) {

@@ -71,6 +71,7 @@ struct Loader {
         ACEMI_HIP(hipMalloc(&d, bytes));
         allocs.push_back(d);
         ACEMI_HIP(hipMemcpy(d, host, bytes, hipMemcpyHostToDevice));
+        ACEMI_HIP(hipDeviceSynchronize());  // null-stream copy: done before any stream reads it
         weight_bytes += bytes;
         return static_cast<T*>(d);
     }

@@ -30,6 +30,7 @@ struct VaeLoader {
         ACEMI_HIP(hipMalloc(&d, bytes));
         m.allocs.push_back(d);
         ACEMI_HIP(hipMemcpy(d, host, bytes, hipMemcpyHostToDevice));
+        ACEMI_HIP(hipDeviceSynchronize());  // null-stream copy: done before any stream reads it
         m.weight_bytes += bytes;
         return static_cast<T*>(d);
     }
@@ -294,6 +295,9 @@ void VaeEngine::ensure(Buf& b, size_t bytes) {
     const size_t alloc = (bytes + 255) & ~size_t(255);
     ACEMI_HIP(hipMalloc(&b.p, alloc));
     ACEMI_HIP(hipMemset(b.p, 0, alloc));
+    // hipMemset runs on the legacy null stream, which does not order against the library's
+    // non-blocking streams: finish it before any kernel can write the new buffer
+    ACEMI_HIP(hipDeviceSynchronize());
     b.bytes = alloc;
 }
 

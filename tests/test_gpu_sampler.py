@@ -31,6 +31,10 @@ def test_generation_loop_ex_on_gpu(tiny_bridge):
             elif sde:
                 tn = np.float32(sched[i + 1])
                 ref = tn * noise[i] + (np.float32(1) - tn) * (ref - v * np.float32(t))
-            else:
-                ref = ref - v * np.float32(t - sched[i + 1])
-        np.testing.assert_allclose(xt.cpu().numpy(), ref, rtol=1e-4, atol=1e-4)
+            else:  # dt in f32, as the reference C loop computes it (acestep_ggml.cpp:2056-2086)
+                ref = ref - v * (np.float32(t) - np.float32(sched[i + 1]))
+        # same per-step forwards; only the f32 order of the Euler / re-noise arithmetic may differ, and
+        # bf16 activation rounding amplifies such 1-ulp differences over the steps (test_gpu_forward.py)
+        got = xt.cpu().numpy()
+        l2 = float(np.linalg.norm(got - ref) / np.linalg.norm(ref))
+        assert l2 < 1e-5, (sde, l2, float(np.abs(got - ref).max()))
