@@ -14,4 +14,4 @@ for ctr in FETCH_SIZE WRITE_SIZE; do
     echo "pmc $ctr rc=$rc" >> "gpurun_out/pmc/$ctr.log"
     if [ $rc -ne 0 ]; then exit $rc; fi
 done
-python tools/pmc_summary.py gpurun_out/pmc > gpurun_out/pmc/summary.json
+python tools/pmc_summary.py gpurun_out/pmc gpurun_out/pmc/FETCH_SIZE.log > gpurun_out/pmc/summary.json

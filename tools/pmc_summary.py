@@ -25,7 +25,7 @@ def read_counter(root, name):
     return per_kernel
 
 
-def main(root):
+def main(root, bench_json=None):
     fetch = read_counter(root, "FETCH_SIZE")
     write = read_counter(root, "WRITE_SIZE")
     out = {"unit": "bytes per launch", "fetch_correction": 2.0, "kernels": {}}
@@ -40,8 +40,13 @@ def main(root):
     gu = [k for k in out["kernels"] if pat.search(k)]
     if gu:
         out["gate_up"] = {"kernel": gu[0], **out["kernels"][gu[0]]}
+    if bench_json:  # the workload these passes ran (bench.py matches it before using the bytes)
+        with open(bench_json, "r", encoding="utf-8") as f:
+            line = [ln for ln in f if ln.startswith("{")][-1]
+        c = json.loads(line)["config"]
+        out["config"] = {k: c[k] for k in ("latent_frames", "enc_len", "batch_per_gpu", "weights")}
     json.dump(out, sys.stdout, indent=1)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc")
+    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc", sys.argv[2] if len(sys.argv) > 2 else None)
