@@ -32,7 +32,7 @@ EXPORTED_SYMBOLS = (
     "ace_mi_create_on_device", "ace_mi_dit_get_info", "ace_mi_dit_forward_batched", "ace_mi_dit_sample",
     "ace_mi_dit_sample_ex",
     "ace_mi_profile_enable", "ace_mi_profile_reset", "ace_mi_profile_get", "ace_mi_probe_gemm",
-    "ace_mi_synchronize", "ace_mi_kernel_gemm", "ace_mi_kernel_attention", "ace_mi_bench_gemm",
+    "ace_mi_synchronize", "ace_mi_kernel_gemm", "ace_mi_kernel_attention", "ace_mi_bench_attention", "ace_mi_bench_gemm",
     "ace_mi_gemm_variant", "ace_ggml_load_vae", "ace_ggml_vae_get_info", "ace_ggml_vae_decode",
     "ace_mi_vae_out_len", "ace_mi_vae_decode_device", "ace_ggml_vae_encode", "ace_mi_vae_enc_out_len",
     "ace_mi_vae_encode_device", "ace_mi_quantize", "ace_mi_dequantize", "ace_mi_kernel_gemm_q", "ace_mi_bench_gemm_q",
@@ -127,6 +127,8 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.ace_mi_kernel_attention.argtypes = [i32, i32, i32, i32, i32, i32, f32, i32, fp, fp, ip, fp]
     lib.ace_mi_kernel_attention.restype = ctypes.c_int
     lib.ace_mi_bench_gemm.argtypes = [i32, i32, i32, i32, i32, i32, i32, fp]
+    lib.ace_mi_bench_attention.argtypes = [i32, i32, i32, i32, i32, i32, i32, i32, fp]
+    lib.ace_mi_bench_attention.restype = ctypes.c_int
     lib.ace_mi_bench_gemm.restype = ctypes.c_int
     lib.ace_mi_gemm_variant.argtypes = [i32]
     lib.ace_mi_gemm_variant.restype = ctypes.c_int
@@ -553,6 +555,18 @@ def kernel_attention(q: np.ndarray, kv: np.ndarray, hq: int, hkv: int, window: i
     if st != ACE_GGML_OK:
         raise RuntimeError(f"ace_mi_kernel_attention failed (status={st})")
     return out
+
+
+def bench_attention(B: int, hq: int, hkv: int, nq: int, nk: int, window: int = 0, split: bool = True,
+                    causal: bool = False, masked: bool = False, iters: int = 20) -> float:
+    """Average ms per launch of the engine's attention kernel on pseudo-random operands (GPU)."""
+    lib = load_library()
+    ms = ctypes.c_float(0.0)
+    flags = (1 if split else 0) | (2 if causal else 0) | (4 if masked else 0)
+    st = lib.ace_mi_bench_attention(B, hq, hkv, nq, nk, int(window), flags, iters, ctypes.byref(ms))
+    if st != ACE_GGML_OK:
+        raise RuntimeError(f"ace_mi_bench_attention failed (status={st})")
+    return float(ms.value)
 
 
 def bench_gemm(M: int, N: int, K: int, variant: int = -1, epi: int = 0, act_type: int = 0, iters: int = 20) -> float:

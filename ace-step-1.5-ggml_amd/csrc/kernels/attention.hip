@@ -17,8 +17,11 @@
 // almost never relative to the F32 reference.  SPLIT=false is the plain fp16
 // fast path (ACE_MI_ATTN_FAST=1).  P is formed as exp2(s - m + 12) (scaled by
 // 2^12 so its lo part stays a normal fp16; O and l carry the same factor).
-// Online softmax in f32 (exp2 domain).  A row whose keys are all masked
-// yields 0/0 = NaN exactly like ggml's soft_max of an all -inf row.
+// Online softmax in f32 (exp2 domain) with a lazy running max: O and l are
+// rescaled only when a row's max grows by more than 2^RESCALE_LOG2 (P then
+// stays below 2^15, inside fp16), which after the first tiles is almost never.
+// A row whose keys are all masked yields 0/0 = NaN exactly like ggml's
+// soft_max of an all -inf row.
 //
 // Structure: one workgroup = 4 waves = (batch item, kv head, 128 query rows
 // spread over the n_rep q heads sharing that kv head), so each K/V tile is
@@ -28,8 +31,15 @@
 // S^T accumulator registers are, after f16 packing, directly the B operand of
 // O^T = V^T . P^T (the k order inside a 16-key step is permuted; V^T is stored
 // with the matching permutation by the prep kernel), so P never goes through
-// LDS and the per-row rescale factor is lane-local.  K/V^T tiles arrive by
-// global_load_lds into a double-buffered, XOR-swizzled LDS image.
+// LDS and the per-row rescale factor is lane-local.
+//
+// Software pipeline (one wave per SIMD, so the wave itself must overlap its
+// VALU softmax with its MFMAs): iteration i issues the MFMAs of S(i+1) while
+// it turns S(i) into P(i) (exp2, row sums, fp16 hi/lo packing), then the
+// MFMAs of O += V(i) P(i) while it scales and masks S(i+1) and takes its row
+// max.  K and V^T tiles arrive by global_load_lds into two 2-slot rings in
+// LDS: K(i+2) and V(i+1) are requested at the top of iteration i (their
+// slots were last read in iteration i-1) and land by its closing barrier.
 #include "../kernels.h"
 #include "lds_asm.h"
 
@@ -45,25 +55,56 @@ constexpr int KT = 64;                    // keys per tile
 constexpr int K_BYTES = KT * D * 2;       // 16 KiB
 constexpr int V_BYTES = D * KT * 2;       // 16 KiB
 constexpr float PSCALE_LOG2 = 12.0f;
+constexpr float RESCALE_LOG2 = 3.0f;      // P <= 2^(12+3) = 32768 < fp16 max
 
+// LDS rings.  K slot: [key bias (64 f32) | K hi | K lo]; V slot: [V^T hi | V^T lo].  All fragment
+// reads of the K ring use a 16-bit immediate offset from a per-lane address; the V ring has its own
+// base register (it starts past 64 KiB).
 template <bool SPLIT>
-struct Stage {
-    static constexpr int K_HI = 0;
-    static constexpr int K_LO = K_BYTES;
-    static constexpr int V_HI = SPLIT ? 2 * K_BYTES : K_BYTES;
-    static constexpr int V_LO = V_HI + V_BYTES;
-    static constexpr int KB = SPLIT ? 2 * (K_BYTES + V_BYTES) : K_BYTES + V_BYTES;
-    static constexpr int BYTES = KB + KT * 4;
+struct Ring {
+    static constexpr int KB = 0;
+    static constexpr int K_HI = KT * 4;
+    static constexpr int K_LO = K_HI + K_BYTES;
+    static constexpr int KS = K_HI + (SPLIT ? 2 : 1) * K_BYTES;  // one K slot
+    static constexpr int V_LO = V_BYTES;
+    static constexpr int VS = (SPLIT ? 2 : 1) * V_BYTES;          // one V slot
+    static constexpr int V0 = 2 * KS;                              // V ring start
+    static constexpr int BYTES = 2 * KS + 2 * VS;
+    static_assert(KS + K_LO + 32 * 256 + 255 < 65536, "K reads need 16-bit offsets");
+    static_assert(VS + V_LO + 3 * 32 * 128 + 127 < 65536, "V reads need 16-bit offsets");
 };
 
-__device__ __forceinline__ f32x16 mfma32(const uint4& a, const uint4& b, f32x16 c) {
+typedef u32x4_t frag;  // 8 fp16 of one MFMA operand
+
+__device__ __forceinline__ f32x16 mfma32(const frag& a, const frag& b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0,
                                                   0, 0);
+}
+
+template <int OFF>
+__device__ __forceinline__ frag lds_frag(uint32_t addr) {
+    frag v;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
+    return v;
+}
+
+// Wait for this wave's LDS reads and tie the fragments to the wait (guide §5.7 item 1, form ii): their
+// consumers stay below it, while independent VALU / MFMA work may still be scheduled across it.
+template <int N>
+__device__ __forceinline__ void lds_wait_tie(frag (&r)[N]) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < N; ++j) asm volatile("" : "+v"(r[j]));
 }
 
 __device__ __forceinline__ uint32_t pack_f16x2(float a, float b) {
     _Float16 ha = (_Float16)a, hb = (_Float16)b;
     return (uint32_t)__builtin_bit_cast(uint16_t, ha) | ((uint32_t)__builtin_bit_cast(uint16_t, hb) << 16);
+}
+
+__device__ __forceinline__ uint32_t pack_f16x2_lo(float a, float b) {
+    const _Float16 ha = (_Float16)a, hb = (_Float16)b;
+    return pack_f16x2(a - (float)ha, b - (float)hb);
 }
 
 __device__ __forceinline__ uint16_t f32_to_bf16_rne(float f) {
@@ -83,19 +124,26 @@ __device__ __forceinline__ uint16_t to_act(float f) {
     }
 }
 
-__device__ __forceinline__ uint32_t pack_f16x2_lo(float a, float b) {
-    const _Float16 ha = (_Float16)a, hb = (_Float16)b;
-    return pack_f16x2(a - (float)ha, b - (float)hb);
+// f(std::integral_constant<int, I>) for I = B..E-1 (compile-time LDS offsets inside the body)
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
 }
 
-template <bool F16OUT, bool SPLIT>
+// key index (within a 64-key tile) of accumulator element r of 32-key half t, for lane half h:
+// the 32x32 C/D map puts rows (= keys of S^T) at 8*(r/4) + 4*h + r%4
+__device__ __forceinline__ constexpr int key_of(int t, int r) { return 32 * t + (r & 3) + 8 * (r >> 2); }
+
+template <bool F16OUT, bool SPLIT, bool KBIAS>
 __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
-    using ST = Stage<SPLIT>;
-    constexpr int STAGE = ST::BYTES;
+    using RG = Ring<SPLIT>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const int wid = tid >> 6;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int h = lane >> 5;     // lane half
     const int lq = lane & 31;
 
@@ -113,7 +161,7 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
     const int qw0 = q0 + (wid % waves_per_head) * 32;  // this wave's first row
     const int qrow = qw0 + lq;
 
-    // ---- key tile range
+    // ---- key tile range of the block
     int klo = 0, khi = a.nk;
     if (a.window > 0) {
         klo = max(0, q0 - a.window);
@@ -121,24 +169,34 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
     }
     if (a.causal) khi = min(khi, q0 + qpb);  // no key after the block's last query
     const int kt_begin = klo / KT;
-    const int kt_end = (khi + KT - 1) / KT;
+    const int n = max(0, (khi + KT - 1) / KT - kt_begin);
+
+    // ---- this lane's valid absolute key range [lo_abs, hi_abs): padding, window, causal
+    int lo_abs = 0, hi_abs = a.nk;
+    if (a.window > 0) {
+        lo_abs = max(lo_abs, qrow - a.window);
+        hi_abs = min(hi_abs, qrow + a.window + 1);
+    }
+    if (a.causal) hi_abs = min(hi_abs, qrow + 1);
+    lo_abs -= 4 * h;  // compared against the lane-independent part of the key index
+    hi_abs -= 4 * h;
 
     // ---- Q fragments (B operand of S^T = K Q^T): Q[q][16ks + 8h + j]
     const uint16_t* qptr = a.q + (((int64_t)b * a.Hq + head) * a.nq_pad + qrow) * D + 8 * h;
-    uint4 qf[8], qfl[8];
+    frag qf[8], qfl[8];
 #pragma unroll
-    for (int ks = 0; ks < 8; ++ks) qf[ks] = *(const uint4*)(qptr + 16 * ks);
+    for (int ks = 0; ks < 8; ++ks) qf[ks] = *(const frag*)(qptr + 16 * ks);
     if constexpr (SPLIT) {
 #pragma unroll
-        for (int ks = 0; ks < 8; ++ks) qfl[ks] = *(const uint4*)(qptr + a.q_plane + 16 * ks);
+        for (int ks = 0; ks < 8; ++ks) qfl[ks] = *(const frag*)(qptr + a.q_plane + 16 * ks);
     }
 
     const uint16_t* kbase = a.k + ((int64_t)b * a.Hkv + kvh) * a.nk_pad * D;
     const uint16_t* vbase = a.vt + ((int64_t)b * a.Hkv + kvh) * D * a.nk_pad;
-    const float* kb = a.kbias ? a.kbias + (int64_t)b * a.nk_pad : nullptr;
+    const float* kb = KBIAS ? a.kbias + (int64_t)b * a.nk_pad : nullptr;
 
-    auto stage = [&](int buf, int kt) {
-        char* base = smem + buf * STAGE;
+    auto stage_k = [&](int slot, int kt) {
+        char* base = smem + slot * RG::KS;
         const int k0 = kt * KT;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {  // K: 16 instr of 4 rows
@@ -146,186 +204,226 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
             const int row = 4 * g + (lane >> 4);
             const int ch = (lane & 15) ^ (row & 15);
             const uint16_t* src = kbase + (int64_t)(k0 + row) * D + ch * 8;
-            __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(base + ST::K_HI + g * 1024), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(base + RG::K_HI + g * 1024), 16, 0, 0);
             if constexpr (SPLIT)
-                __builtin_amdgcn_global_load_lds((const void*)(src + a.k_plane), (lds_void*)(base + ST::K_LO + g * 1024),
+                __builtin_amdgcn_global_load_lds((const void*)(src + a.k_plane), (lds_void*)(base + RG::K_LO + g * 1024),
                                                  16, 0, 0);
         }
+        if constexpr (KBIAS) {
+            if (wid == 0)
+                __builtin_amdgcn_global_load_lds((const void*)(kb + k0 + lane), (lds_void*)(base + RG::KB), 4, 0, 0);
+        }
+    };
+    auto stage_v = [&](int slot, int kt) {
+        char* base = smem + RG::V0 + slot * RG::VS;
+        const int k0 = kt * KT;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {  // V^T: 16 instr of 8 d-rows
             const int g = wid + 4 * j;
             const int d = 8 * g + (lane >> 3);
             const int ch = (lane & 7) ^ ((d >> 1) & 7);
             const uint16_t* src = vbase + (int64_t)d * a.nk_pad + k0 + ch * 8;
-            __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(base + ST::V_HI + g * 1024), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(base + g * 1024), 16, 0, 0);
             if constexpr (SPLIT)
-                __builtin_amdgcn_global_load_lds((const void*)(src + a.v_plane), (lds_void*)(base + ST::V_LO + g * 1024),
+                __builtin_amdgcn_global_load_lds((const void*)(src + a.v_plane), (lds_void*)(base + RG::V_LO + g * 1024),
                                                  16, 0, 0);
-        }
-        if (kb && wid == 0) {
-            __builtin_amdgcn_global_load_lds((const void*)(kb + k0 + lane), (lds_void*)(base + ST::KB), 4, 0, 0);
         }
     };
 
+    // Per-lane LDS read addresses.  K rows are 256 B with 16-B chunk c stored at c ^ (key & 15); the
+    // fragment chunk of k-step ks is 2*ks + h, so its physical chunk is (2*ks) ^ cK (cK lane constant).
+    // V^T rows are 128 B with chunk c at c ^ ((d >> 1) & 7): chunk of key-step g is (2*g) ^ cV.
+    const int cK = h ^ (lq & 15);
+    const int cV = h ^ ((lq >> 1) & 7);
+    const uint32_t smem_l = lds_addr(smem);
+    uint32_t kaddr[8], vaddr[4];
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) kaddr[ks] = smem_l + RG::K_HI + lq * 256 + (((2 * ks) ^ cK) << 4);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) vaddr[g] = smem_l + RG::V0 + lq * 128 + (((2 * g) ^ cV) << 4);
+    const uint32_t kbaddr = smem_l + RG::KB + 16 * h;
+
+    // S^T(tile in K slot SLOT) -> s (two 32-key halves); SPLIT: Kh.Qh + Kh.Ql + Kl.Qh
+    auto s_tile = [&](auto slot_c, f32x16 (&s)[2]) {
+        constexpr int SLOT = decltype(slot_c)::value;
+        static_for<0, 2>([&](auto t_c) {
+            constexpr int t = decltype(t_c)::value;
+            frag kf[SPLIT ? 16 : 8];  // hi frags, then lo frags
+#pragma unroll
+            for (int ks = 0; ks < 8; ++ks) kf[ks] = lds_frag<SLOT * RG::KS + t * 32 * 256>(kaddr[ks]);
+            if constexpr (SPLIT) {
+#pragma unroll
+                for (int ks = 0; ks < 8; ++ks)
+                    kf[8 + ks] = lds_frag<SLOT * RG::KS + t * 32 * 256 + RG::K_LO - RG::K_HI>(kaddr[ks]);
+            }
+            lds_wait_tie(kf);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s[t][r] = 0.f;
+#pragma unroll
+            for (int ks = 0; ks < 8; ++ks) {
+                s[t] = mfma32(kf[ks], qf[ks], s[t]);
+                if constexpr (SPLIT) {
+                    s[t] = mfma32(kf[ks], qfl[ks], s[t]);
+                    s[t] = mfma32(kf[8 + ks], qf[ks], s[t]);
+                }
+            }
+        });
+    };
+
     const float c_log2 = a.scale * 1.4426950408889634f;
-    float m_run = -INFINITY;
+    // scale + mask S of the tile at relative index i (its key bias in K slot SLOT) in place; returns
+    // the lane's max over its 32 keys (combined across the two lane halves by the caller)
+    auto prep = [&](auto slot_c, f32x16 (&s)[2], int i) -> float {
+        constexpr int SLOT = decltype(slot_c)::value;
+        const int k0 = (kt_begin + i) * KT;
+        const int lo = lo_abs - k0, hi = hi_abs - k0;
+        frag kbv[8];  // key bias of element r of half t: kbv[4t + r/4][r%4]
+        if constexpr (KBIAS) {
+            static_for<0, 8>([&](auto j_c) {
+                constexpr int j = decltype(j_c)::value;  // (t, g4) = (j / 4, j % 4): keys 32t + 8g4 + 4h + 0..3
+                kbv[j] = lds_frag<SLOT * RG::KS + (32 * (j / 4) + 8 * (j % 4)) * 4>(kbaddr);
+            });
+            lds_wait_tie(kbv);
+        }
+        float mloc = -INFINITY;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                float x = s[t][r] * c_log2;
+                if constexpr (KBIAS) x += __uint_as_float(kbv[4 * t + (r >> 2)][r & 3]);
+                const int kr = key_of(t, r);
+                x = (kr >= lo && kr < hi) ? x : -INFINITY;
+                s[t][r] = x;
+                mloc = fmaxf(mloc, x);
+            }
+        }
+        return fmaxf(mloc, __shfl_xor(mloc, 32));
+    };
+
+    float m_run = -INFINITY;   // running reference max (exp2 domain) of this lane's query
     float l_run = 0.f;
+    float alpha = 1.f;         // pending rescale of O and l (applied before the next P.V)
+    bool rescale = false;      // wave-uniform
     f32x16 o[4];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
 
-    if (kt_begin < kt_end) {
-        stage(0, kt_begin);
+    // new tile max -> lazy update of the running max; sets (alpha, rescale) for the caller
+    auto update_max = [&](float mloc) {
+        const bool move = mloc > m_run + RESCALE_LOG2;
+        alpha = move ? __builtin_amdgcn_exp2f(m_run - mloc) : 1.f;
+        m_run = move ? mloc : m_run;
+        rescale = __builtin_amdgcn_ballot_w64(move) != 0;
+    };
+
+    f32x16 s_cur[2], s_nxt[2];
+    if (n > 0) {
+        stage_k(0, kt_begin);
+        stage_v(0, kt_begin);
+        if (n > 1) stage_k(1, kt_begin + 1);
+        wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        s_tile(std::integral_constant<int, 0>{}, s_cur);
+        update_max(prep(std::integral_constant<int, 0>{}, s_cur, 0));
+        __builtin_amdgcn_s_barrier();  // every wave has read K slot 0: iteration 0 restages it
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
 
-    // Per-lane LDS read addressing.  K rows are 256 B with 16-B chunk c stored at c ^ (key & 15); the
-    // fragment chunk of k-step ks is 2*ks + h, so its physical chunk is (2*ks) ^ cK (cK lane constant).
-    // V^T rows are 128 B with chunk c at c ^ ((d >> 1) & 7): chunk of key-step g is (2*g) ^ cV.
-    const int cK = h ^ (lq & 15);
-    const int cV = h ^ ((lq >> 1) & 7);
-    const uint32_t smem_l = lds_addr(smem);
+    // one pipeline iteration for relative tile i (its K slot and V slot are SLOT = i & 1)
+    auto iter = [&](auto slot_c, int i) {
+        constexpr int SLOT = decltype(slot_c)::value;
+        constexpr int NXT = SLOT ^ 1;
+        const bool more = i + 1 < n;
+        if (i + 2 < n) stage_k(SLOT, kt_begin + i + 2);
+        if (more) stage_v(NXT, kt_begin + i + 1);
 
-    for (int kt = kt_begin; kt < kt_end; ++kt) {
-        const int cur = (kt - kt_begin) & 1;
-        if (kt + 1 < kt_end) stage(cur ^ 1, kt + 1);
-        const uint32_t st = smem_l + cur * STAGE;
-        const int k0 = kt * KT;
-
-        // ---- S^T = K . Q^T (two 32-key tiles); SPLIT: Kh.Qh + Kh.Ql + Kl.Qh
-        f32x16 s[2];
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) s[t][r] = 0.f;
-            const uint32_t rowk = st + ST::K_HI + (32 * t + lq) * 256;
-            uint4 kf[8], kfl[8];
-#pragma unroll
-            for (int ks = 0; ks < 8; ++ks) kf[ks] = ds_read_b128_v(rowk + (((2 * ks) ^ cK) << 4));
-            if constexpr (SPLIT) {
-#pragma unroll
-                for (int ks = 0; ks < 8; ++ks)
-                    kfl[ks] = ds_read_b128_v(rowk + (ST::K_LO - ST::K_HI) + (((2 * ks) ^ cK) << 4));
-            }
-            lds_wait_all();
-#pragma unroll
-            for (int ks = 0; ks < 8; ++ks) {
-                s[t] = mfma32(kf[ks], qf[ks], s[t]);
-                if constexpr (SPLIT) {
-                    s[t] = mfma32(kf[ks], qfl[ks], s[t]);
-                    s[t] = mfma32(kfl[ks], qf[ks], s[t]);
-                }
-            }
-        }
-
-        // ---- scale, mask, online softmax (this lane: query qrow, 32 of the 64 keys)
-        float kbv[2][16];
-        if (kb) {
-#pragma unroll
-            for (int t = 0; t < 2; ++t)
-#pragma unroll
-                for (int g4 = 0; g4 < 4; ++g4) {
-                    const uint4 v = ds_read_b128_v(st + ST::KB + (32 * t + 8 * g4 + 4 * h) * 4);
-                    kbv[t][4 * g4 + 0] = __uint_as_float(v.x);
-                    kbv[t][4 * g4 + 1] = __uint_as_float(v.y);
-                    kbv[t][4 * g4 + 2] = __uint_as_float(v.z);
-                    kbv[t][4 * g4 + 3] = __uint_as_float(v.w);
-                }
-            lds_wait_all();
-        }
-        const bool need_window = a.window > 0 && (k0 < qw0 + 31 - a.window || k0 + KT - 1 > qw0 + a.window);
-        const bool need_causal = a.causal && k0 + KT - 1 > qw0;
-        float mloc = -INFINITY;
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int krel = 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h;
-                float x = s[t][r] * c_log2;
-                if (kb) x += kbv[t][r];
-                if (need_window) {
-                    const int d = qrow - (k0 + krel);
-                    if (d > a.window || d < -a.window) x = -INFINITY;
-                }
-                if (need_causal && k0 + krel > qrow) x = -INFINITY;
-                s[t][r] = x;
-                mloc = fmaxf(mloc, x);
-            }
-        }
-        mloc = fmaxf(mloc, __shfl_xor(mloc, 32));
-        const float m_new = fmaxf(m_run, mloc);
-        const float m_use = ((m_new == -INFINITY) ? 0.f : m_new) - PSCALE_LOG2;
-        const float alpha = __builtin_amdgcn_exp2f(m_run - PSCALE_LOG2 - m_use);
-        // alpha is exp2(0) = 1 for every row whose running max did not move; once the maxima settle
-        // (after the first few key tiles) whole waves skip the O rescale below
-        const bool rescale = __ballot(m_new != m_run) != 0;
-        m_run = m_new;
-        float lsum = 0.f;
-        uint4 pf[4], pfl[4];
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float pr = __builtin_amdgcn_exp2f(s[t][r] - m_use);
-                s[t][r] = pr;
-                lsum += pr;
-            }
-#pragma unroll
-            for (int ss = 0; ss < 2; ++ss) {
-                uint4 f;
-                f.x = pack_f16x2(s[t][8 * ss + 0], s[t][8 * ss + 1]);
-                f.y = pack_f16x2(s[t][8 * ss + 2], s[t][8 * ss + 3]);
-                f.z = pack_f16x2(s[t][8 * ss + 4], s[t][8 * ss + 5]);
-                f.w = pack_f16x2(s[t][8 * ss + 6], s[t][8 * ss + 7]);
-                pf[2 * t + ss] = f;
-                if constexpr (SPLIT) {
-                    uint4 fl;
-                    fl.x = pack_f16x2_lo(s[t][8 * ss + 0], s[t][8 * ss + 1]);
-                    fl.y = pack_f16x2_lo(s[t][8 * ss + 2], s[t][8 * ss + 3]);
-                    fl.z = pack_f16x2_lo(s[t][8 * ss + 4], s[t][8 * ss + 5]);
-                    fl.w = pack_f16x2_lo(s[t][8 * ss + 6], s[t][8 * ss + 7]);
-                    pfl[2 * t + ss] = fl;
-                }
-            }
-        }
-        l_run = (rescale ? l_run * alpha : l_run) + lsum;  // O and l always scaled together
+        // pending rescale of O / l for tile i (rare: its max moved by more than 2^RESCALE_LOG2)
         if (rescale) {
 #pragma unroll
             for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
         }
+        l_run *= alpha;
 
-        // ---- O^T += V^T . P^T ; SPLIT: Vh.Ph + Vh.Pl + Vl.Ph
+        // S(i+1) from K slot NXT (on the last tile: a discarded product of the slot's stale but
+        // finite contents, which keeps this block branch-free) || P(i) = exp2(S(i) - m + 12)
+        s_tile(std::integral_constant<int, NXT>{}, s_nxt);
+        const float m_use = ((m_run == -INFINITY) ? 0.f : m_run) - PSCALE_LOG2;
+        float lsum = 0.f;
+        frag pf[4], pfl[4];
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-            const uint32_t rowv = st + ST::V_HI + (32 * dt + lq) * 128;
-            uint4 vf[4], vfl[4];
+        for (int t = 0; t < 2; ++t) {
 #pragma unroll
-            for (int g = 0; g < 4; ++g) vf[g] = ds_read_b128_v(rowv + (((2 * g) ^ cV) << 4));
-            if constexpr (SPLIT) {
-#pragma unroll
-                for (int g = 0; g < 4; ++g)
-                    vfl[g] = ds_read_b128_v(rowv + (ST::V_LO - ST::V_HI) + (((2 * g) ^ cV) << 4));
+            for (int r = 0; r < 16; ++r) {
+                const float pr = __builtin_amdgcn_exp2f(s_cur[t][r] - m_use);
+                s_cur[t][r] = pr;
+                lsum += pr;
             }
-            lds_wait_all();
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                o[dt] = mfma32(vf[g], pf[g], o[dt]);
+            for (int ss = 0; ss < 2; ++ss) {
+                frag f;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) f[j] = pack_f16x2(s_cur[t][8 * ss + 2 * j], s_cur[t][8 * ss + 2 * j + 1]);
+                pf[2 * t + ss] = f;
                 if constexpr (SPLIT) {
-                    o[dt] = mfma32(vf[g], pfl[g], o[dt]);
-                    o[dt] = mfma32(vfl[g], pf[g], o[dt]);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        f[j] = pack_f16x2_lo(s_cur[t][8 * ss + 2 * j], s_cur[t][8 * ss + 2 * j + 1]);
+                    pfl[2 * t + ss] = f;
                 }
             }
         }
-        if (kt + 1 < kt_end) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile kt+1 landed (issued a whole tile ago)
-            __builtin_amdgcn_s_barrier();                     // ... for every wave; buffer `cur` released
+        l_run += lsum;
+
+        // O^T += V^T(i) . P^T(i) ; SPLIT: Vh.Ph + Vh.Pl + Vl.Ph  ||  scale / mask / max of S(i+1)
+        static_for<0, 2>([&](auto dp_c) {  // two 32-row d-tiles per LDS round trip
+            constexpr int dp = 2 * decltype(dp_c)::value;
+            frag vf[SPLIT ? 16 : 8];  // [u][g] hi, then lo
+            static_for<0, 2>([&](auto u_c) {
+                constexpr int u = decltype(u_c)::value;
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    vf[4 * u + g] = lds_frag<SLOT * RG::VS + (dp + u) * 32 * 128>(vaddr[g]);
+                    if constexpr (SPLIT)
+                        vf[8 + 4 * u + g] = lds_frag<SLOT * RG::VS + (dp + u) * 32 * 128 + RG::V_LO>(vaddr[g]);
+                }
+            });
+            lds_wait_tie(vf);
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    o[dp + u] = mfma32(vf[4 * u + g], pf[g], o[dp + u]);
+                    if constexpr (SPLIT) {
+                        o[dp + u] = mfma32(vf[4 * u + g], pfl[g], o[dp + u]);
+                        o[dp + u] = mfma32(vf[8 + 4 * u + g], pf[g], o[dp + u]);
+                    }
+                }
+        });
+        const float mnx = prep(std::integral_constant<int, NXT>{}, s_nxt, i + 1);
+        if (more) {
+            update_max(mnx);
+        } else {
+            alpha = 1.f;
+            rescale = false;
         }
+#pragma unroll
+        for (int t = 0; t < 2; ++t) s_cur[t] = s_nxt[t];
+        if (more) {
+            wait_vmcnt<0>();                   // K(i+2), V(i+1) landed (requested at the top)
+            __builtin_amdgcn_s_barrier();      // ... for every wave; K slot NXT / V slot SLOT released
+        }
+    };
+
+    int i = 0;
+    for (; i + 1 < n; i += 2) {
+        iter(std::integral_constant<int, 0>{}, i);
+        iter(std::integral_constant<int, 1>{}, i + 1);
     }
+    if (i < n) iter(std::integral_constant<int, 0>{}, i);
 
     // ---- normalise and store O[q][head*128 + d]
     const float l = l_run + __shfl_xor(l_run, 32);
@@ -348,6 +446,15 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
     }
 }
 
+template <bool F16OUT, bool SPLIT>
+void launch_t(const AttnArgs& a, dim3 grid, hipStream_t s) {
+    const size_t lds = Ring<SPLIT>::BYTES;
+    if (a.kbias)
+        hipLaunchKernelGGL((attn_kernel<F16OUT, SPLIT, true>), grid, dim3(256), lds, s, a);
+    else
+        hipLaunchKernelGGL((attn_kernel<F16OUT, SPLIT, false>), grid, dim3(256), lds, s, a);
+}
+
 }  // namespace
 
 void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s) {
@@ -361,17 +468,15 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s) {
     const dim3 grid(a.B * a.Hkv * n_qt);
     if (a.split) {
         ACEMI_CHECK(a.q_plane > 0 && a.k_plane > 0 && a.v_plane > 0, "attention: split mode needs lo planes");
-        const size_t lds = 2 * Stage<true>::BYTES;
         if (out_t == ActType::F16)
-            hipLaunchKernelGGL((attn_kernel<true, true>), grid, dim3(256), lds, s, a);
+            launch_t<true, true>(a, grid, s);
         else
-            hipLaunchKernelGGL((attn_kernel<false, true>), grid, dim3(256), lds, s, a);
+            launch_t<false, true>(a, grid, s);
     } else {
-        const size_t lds = 2 * Stage<false>::BYTES;
         if (out_t == ActType::F16)
-            hipLaunchKernelGGL((attn_kernel<true, false>), grid, dim3(256), lds, s, a);
+            launch_t<true, false>(a, grid, s);
         else
-            hipLaunchKernelGGL((attn_kernel<false, false>), grid, dim3(256), lds, s, a);
+            launch_t<false, false>(a, grid, s);
     }
     ACEMI_HIP(hipGetLastError());
 }

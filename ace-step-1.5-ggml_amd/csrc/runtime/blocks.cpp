@@ -127,7 +127,7 @@ void BlockRunner::run(const BlockShape& sh, const std::vector<DevLayer>& layers,
             aa.q = get<uint16_t>(qh_);
             aa.k = get<uint16_t>(kh_);
             aa.vt = get<uint16_t>(vt_);
-            aa.kbias = get<float>(kbias_);
+            aa.kbias = key_mask ? get<float>(kbias_) : nullptr;  // padding keys are masked in-kernel
             aa.out = attn;
             aa.B = B;
             aa.Hq = sh.hq;

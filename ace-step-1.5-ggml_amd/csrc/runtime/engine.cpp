@@ -349,7 +349,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
             aa.q = get<uint16_t>(qh_);
             aa.k = get<uint16_t>(kh_);
             aa.vt = get<uint16_t>(vt_);
-            aa.kbias = get<float>(kbias_);
+            aa.kbias = io.mask ? get<float>(kbias_) : nullptr;  // padding keys are masked in-kernel
             aa.out = attn;
             aa.B = B;
             aa.Hq = c.hq;
@@ -421,7 +421,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
                 aa.q = get<uint16_t>(qh_);
                 aa.k = get<uint16_t>(kc_) + (size_t)li * B * c.hkv * Lpad * D;
                 aa.vt = get<uint16_t>(vc_) + (size_t)li * B * c.hkv * D * Lpad;
-                aa.kbias = get<float>(kbias_c_);
+                aa.kbias = io.enc_mask ? get<float>(kbias_c_) : nullptr;
                 aa.out = attn;
                 aa.B = B;
                 aa.Hq = c.hq;

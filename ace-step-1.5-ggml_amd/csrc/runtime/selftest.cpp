@@ -60,21 +60,30 @@ ace_ggml_status ace_mi_kernel_gemm(int32_t act_type, int32_t epi, int32_t M, int
     return ACE_GGML_OK;
 }
 
-ace_ggml_status ace_mi_kernel_attention(int32_t B, int32_t Hq, int32_t Hkv, int32_t nq, int32_t nk, int32_t window,
-                                        float scale, int32_t split, const float* q, const float* kv,
-                                        const int32_t* kmask, float* out) {
-    using namespace acemi;
-    if (B <= 0 || Hq <= 0 || Hkv <= 0 || nq <= 0 || nk <= 0 || !q || !kv || !out) return ACE_GGML_ERR_INVALID_ARG;
-    try {
+}  // extern "C"
+
+namespace {
+// Device operands of one attention launch, prepared from host f32 q [B][nq][Hq*128] and kv
+// [B][nk][2*Hkv*128] through the engine's own prep kernel (hi/lo planes, V^T, key bias).
+struct AttnSetup {
+    DevMem dq, dkv, dm, dqh, dkh, dvt, dkb, dout;
+    acemi::AttnArgs a{};
+    size_t nqf;
+    AttnSetup(int B, int Hq, int Hkv, int nq, int nk, int window, float scale, int flags, const float* q,
+              const float* kv, const int32_t* kmask)
+        : dq((size_t)B * nq * Hq * 128 * 4), dkv((size_t)B * nk * 2 * Hkv * 128 * 4), dm((size_t)B * nk * 4),
+          dqh((size_t)2 * B * Hq * acemi::round_up(nq, 128) * 128 * 2), dkh((size_t)2 * B * Hkv * acemi::round_up(nk, 128) * 128 * 2),
+          dvt((size_t)2 * B * Hkv * 128 * acemi::round_up(nk, 128) * 2), dkb((size_t)B * acemi::round_up(nk, 128) * 4),
+          dout((size_t)B * nq * Hq * 128 * 2) {
+        using namespace acemi;
         const int D = 128;
         const int nq_pad = (int)round_up(nq, 128), nk_pad = (int)round_up(nk, 128);
-        const size_t nqf = (size_t)B * nq * Hq * D, nkvf = (size_t)B * nk * 2 * Hkv * D;
-        DevMem dq(nqf * 4), dkv(nkvf * 4), dm((size_t)B * nk * 4), dqh((size_t)2 * B * Hq * nq_pad * D * 2),
-            dkh((size_t)2 * B * Hkv * nk_pad * D * 2), dvt((size_t)2 * B * Hkv * D * nk_pad * 2), dkb((size_t)B * nk_pad * 4),
-            dout(nqf * 2);
+        nqf = (size_t)B * nq * Hq * D;
+        const size_t nkvf = (size_t)B * nk * 2 * Hkv * D;
         ACEMI_HIP(hipMemcpy(dq.p, q, nqf * 4, hipMemcpyHostToDevice));
         ACEMI_HIP(hipMemcpy(dkv.p, kv, nkvf * 4, hipMemcpyHostToDevice));
         if (kmask) ACEMI_HIP(hipMemcpy(dm.p, kmask, (size_t)B * nk * 4, hipMemcpyHostToDevice));
+        const bool split = (flags & 1) != 0;
         PrepArgs pq{};
         pq.src = dq.as<float>();
         pq.ld = Hq * D;
@@ -88,7 +97,7 @@ ace_ggml_status ace_mi_kernel_attention(int32_t B, int32_t Hq, int32_t Hkv, int3
         pq.B = B;
         pq.qh = dqh.as<uint16_t>();
         const int64_t qpl = (int64_t)B * Hq * nq_pad * D, kpl = (int64_t)B * Hkv * nk_pad * D;
-        pq.q_plane = (split & 1) ? qpl : 0;
+        pq.q_plane = split ? qpl : 0;
         launch_attn_prep(pq, nullptr);
         PrepArgs pk{};
         pk.src = dkv.as<float>();
@@ -103,15 +112,14 @@ ace_ggml_status ace_mi_kernel_attention(int32_t B, int32_t Hq, int32_t Hkv, int3
         pk.B = B;
         pk.kh = dkh.as<uint16_t>();
         pk.vt = dvt.as<uint16_t>();
-        pk.k_plane = (split & 1) ? kpl : 0;
-        pk.v_plane = (split & 1) ? kpl : 0;
+        pk.k_plane = split ? kpl : 0;
+        pk.v_plane = split ? kpl : 0;
         launch_attn_prep(pk, nullptr);
         launch_key_bias(kmask ? dm.as<int32_t>() : nullptr, B, nk, 1, nk, nk_pad, dkb.as<float>(), nullptr);
-        AttnArgs a{};
         a.q = dqh.as<uint16_t>();
         a.k = dkh.as<uint16_t>();
         a.vt = dvt.as<uint16_t>();
-        a.kbias = dkb.as<float>();
+        a.kbias = kmask ? dkb.as<float>() : nullptr;
         a.out = dout.as<uint16_t>();
         a.B = B;
         a.Hq = Hq;
@@ -122,16 +130,30 @@ ace_ggml_status ace_mi_kernel_attention(int32_t B, int32_t Hq, int32_t Hkv, int3
         a.nk_pad = nk_pad;
         a.window = window;
         a.scale = scale;
-        a.split = (split & 1) != 0;
-        a.causal = (split & 2) != 0;
+        a.split = split;
+        a.causal = (flags & 2) != 0;
         a.q_plane = qpl;
         a.k_plane = kpl;
         a.v_plane = kpl;
-        launch_attention(ActType::BF16, a, nullptr);
         ACEMI_HIP(hipDeviceSynchronize());
-        std::vector<uint16_t> h(nqf);
-        ACEMI_HIP(hipMemcpy(h.data(), dout.p, nqf * 2, hipMemcpyDeviceToHost));
-        for (size_t i = 0; i < nqf; ++i) {
+    }
+};
+}  // namespace
+
+extern "C" {
+
+ace_ggml_status ace_mi_kernel_attention(int32_t B, int32_t Hq, int32_t Hkv, int32_t nq, int32_t nk, int32_t window,
+                                        float scale, int32_t split, const float* q, const float* kv,
+                                        const int32_t* kmask, float* out) {
+    using namespace acemi;
+    if (B <= 0 || Hq <= 0 || Hkv <= 0 || nq <= 0 || nk <= 0 || !q || !kv || !out) return ACE_GGML_ERR_INVALID_ARG;
+    try {
+        AttnSetup st(B, Hq, Hkv, nq, nk, window, scale, split, q, kv, kmask);
+        launch_attention(ActType::BF16, st.a, nullptr);
+        ACEMI_HIP(hipDeviceSynchronize());
+        std::vector<uint16_t> h(st.nqf);
+        ACEMI_HIP(hipMemcpy(h.data(), st.dout.p, st.nqf * 2, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < st.nqf; ++i) {
             const uint32_t u = (uint32_t)h[i] << 16;
             std::memcpy(&out[i], &u, 4);
         }
@@ -141,6 +163,52 @@ ace_ggml_status ace_mi_kernel_attention(int32_t B, int32_t Hq, int32_t Hkv, int3
     }
     return ACE_GGML_OK;
 }
+
+// Attention micro-benchmark: pseudo-random N(0,1)-like q / kv (fixed seed), average ms per launch over
+// `iters` launches timed with hipEvents.  flags: bit 0 split (hi/lo) operands, bit 1 causal,
+// bit 2 a key-padding mask (every 7th key masked).
+ace_ggml_status ace_mi_bench_attention(int32_t B, int32_t Hq, int32_t Hkv, int32_t nq, int32_t nk, int32_t window,
+                                       int32_t flags, int32_t iters, float* avg_ms) {
+    using namespace acemi;
+    if (B <= 0 || Hq <= 0 || Hkv <= 0 || nq <= 0 || nk <= 0 || iters <= 0 || !avg_ms) return ACE_GGML_ERR_INVALID_ARG;
+    try {
+        std::vector<float> q((size_t)B * nq * Hq * 128), kv((size_t)B * nk * 2 * Hkv * 128);
+        std::vector<int32_t> km((size_t)B * nk);
+        uint32_t r = 2024u;
+        auto rnd = [&]() {  // sum of 4 uniforms, centred: roughly N(0, 1/3)
+            float acc = 0.f;
+            for (int j = 0; j < 4; ++j) {
+                r = r * 1664525u + 1013904223u;
+                acc += (float)(r >> 8) * (1.0f / 16777216.0f);
+            }
+            return acc - 2.0f;
+        };
+        for (auto& v : q) v = 2.0f * rnd();
+        for (auto& v : kv) v = rnd();
+        for (size_t i = 0; i < km.size(); ++i) km[i] = (i % 7) != 6;
+        AttnSetup st(B, Hq, Hkv, nq, nk, window, 1.0f / std::sqrt(128.0f), flags & 3, q.data(), kv.data(),
+                     (flags & 4) ? km.data() : nullptr);
+        hipEvent_t e0, e1;
+        ACEMI_HIP(hipEventCreate(&e0));
+        ACEMI_HIP(hipEventCreate(&e1));
+        for (int i = 0; i < 2; ++i) launch_attention(ActType::BF16, st.a, nullptr);
+        ACEMI_HIP(hipEventRecord(e0, nullptr));
+        for (int i = 0; i < iters; ++i) launch_attention(ActType::BF16, st.a, nullptr);
+        ACEMI_HIP(hipEventRecord(e1, nullptr));
+        ACEMI_HIP(hipEventSynchronize(e1));
+        float ms = 0.f;
+        ACEMI_HIP(hipEventElapsedTime(&ms, e0, e1));
+        *avg_ms = ms / (float)iters;
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+    } catch (const std::exception& ex) {
+        std::fprintf(stderr, "ace_mi_bench_attention: %s\n", ex.what());
+        return ACE_GGML_ERR;
+    }
+    return ACE_GGML_OK;
+}
+
+
 
 }  // extern "C"
 

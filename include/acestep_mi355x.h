@@ -106,6 +106,12 @@ ACE_GGML_API ace_ggml_status ace_mi_kernel_attention(int32_t B, int32_t Hq, int3
                                                      int32_t window, float scale, int32_t split, const float* q,
                                                      const float* kv, const int32_t* kmask, float* out);
 
+/* Attention micro-benchmark on pseudo-random device operands (fixed seed): average ms per launch (HIP
+ * events) of the engine's attention kernel; flags bit 0 = hi/lo operands, bit 1 = causal, bit 2 = a
+ * key-padding mask (every 7th key masked). */
+ACE_GGML_API ace_ggml_status ace_mi_bench_attention(int32_t B, int32_t Hq, int32_t Hkv, int32_t nq, int32_t nk,
+                                                    int32_t window, int32_t flags, int32_t iters, float* avg_ms);
+
 /* GEMM micro-benchmark on random device operands: average ms per launch (HIP events) of the
  * engine's GEMM for act_type (0 bf16, 1 fp16), epilogue `epi` (0 f32 store, 2 gated residual,
  * 4 SwiGLU), kernel `variant` (-1 automatic, 0..3 forced). */
