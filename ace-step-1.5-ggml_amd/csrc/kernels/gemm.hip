@@ -616,7 +616,8 @@ void launch_cfg(const GemmParams& p, hipStream_t s) {
     hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, F16, EPI, PIPE>), grid, block, 0, s, p);
 }
 
-// variant: 0 = 128x128 PIPE0, 1 = 128x128 PIPE1, 2 = 256x256 PIPE1 (8 waves 2x4), 3 = 256x128 PIPE1
+// variant: 0 = 128x128 PIPE0, 1 = 128x128 PIPE1, 2 = 256x256 PIPE1 (8 waves 2x4), 3 = 256x128 PIPE1,
+// 4 = 192x128 PIPE1, 5 = 192x256 PIPE1 (8 waves 2x4)
 template <bool F16, int EPI>
 void launch_variant(int variant, const GemmParams& p, hipStream_t s) {
     switch (variant) {
@@ -624,6 +625,8 @@ void launch_variant(int variant, const GemmParams& p, hipStream_t s) {
         case 1: launch_cfg<128, 128, 2, 2, F16, EPI, 1>(p, s); break;
         case 2: launch_cfg<256, 256, 2, 4, F16, EPI, 1>(p, s); break;
         case 3: launch_cfg<256, 128, 2, 2, F16, EPI, 1>(p, s); break;
+        case 4: launch_cfg<192, 128, 2, 2, F16, EPI, 1>(p, s); break;
+        case 5: launch_cfg<192, 256, 2, 4, F16, EPI, 1>(p, s); break;
         default: throw std::runtime_error("gemm: bad variant");
     }
 }
@@ -655,6 +658,8 @@ void launch_q_variant(int variant, const GemmParams& p, hipStream_t s) {
         case 1: launch_q_cfg<128, 128, 2, 2, EPI, WQ>(p, s); break;
         case 2: launch_q_cfg<256, 256, 2, 4, EPI, WQ>(p, s); break;
         case 3: launch_q_cfg<256, 128, 2, 2, EPI, WQ>(p, s); break;
+        case 4: launch_q_cfg<192, 128, 2, 2, EPI, WQ>(p, s); break;
+        case 5: launch_q_cfg<192, 256, 2, 4, EPI, WQ>(p, s); break;
         default: throw std::runtime_error("gemm: bad variant");
     }
 }
@@ -677,21 +682,26 @@ int g_forced_variant = -1;
 // Tile choice: measured kernel ceiling (random bf16 operands, MI355X: v1 ~950, v2 ~1120 TFLOP/s at
 // large shapes) times the wave-quantization efficiency of the grid over 256 CUs (v1: 2 blocks/CU,
 // 64 KiB LDS each; v2: 1 block/CU, 128 KiB) and the M-edge utilisation.
-double predicted_tflops(int variant, int M, int N) {
-    const int bm = variant == 2 ? 256 : 128, bn = variant == 2 ? 256 : 128;
-    const double ceiling = variant == 2 ? 1120.0 : 950.0;
-    const int slots = variant == 2 ? 256 : 512;
-    const int64_t tiles = (int64_t)((M + bm - 1) / bm) * (N / bn);
-    const double waves = (double)tiles / slots;
-    const double eff = waves / std::ceil(waves);
-    const double medge = (double)M / (double)(((M + bm - 1) / bm) * bm);
-    return ceiling * eff * medge;
-}
+// Tile choice from the measured table (tools/gemm_bench.py on MI355X, profiles/r01_gemm_bench.log): at
+// M = 3000 the 192-row tiles make 16 exact M blocks, so 192x128 fills the chip in whole rounds where
+// 128x128 leaves a half round (qkv: 512 vs 768 tiles, 1036 vs 854 TFLOP/s; gate|up 1536 tiles, 900 vs
+// 827); with only N = 2048 (256 tiles) the 128x128 tile's two blocks per CU win (down 779 vs 684).
+// Dequant-fused: 192x256 (one block per CU, the dequant VALU spread over 8 waves) leads where it
+// gives at least one tile per CU (gate|up 655 vs 525, qkv 709 vs 502), else 192x128 (down 506 vs 437).
+double m_edge(int M, int bm) { return (double)M / (double)(((M + bm - 1) / bm) * bm); }
 
-int pick_variant(int M, int N) {
+int pick_variant(int M, int N, bool quant) {
     if (g_forced_variant >= 0) return g_forced_variant;
-    if (N % 256 != 0) return 1;
-    return predicted_tflops(2, M, N) > predicted_tflops(1, M, N) ? 2 : 1;
+    const int64_t mb192 = (M + 191) / 192;
+    const bool edge_ok = m_edge(M, 192) >= m_edge(M, 128) - 0.02;
+    if (quant) {
+        if (N % 256 == 0 && edge_ok && mb192 * (N / 256) >= 256) return 5;
+        if (edge_ok && mb192 * (N / 128) >= 256) return 4;
+        return 1;
+    }
+    if (N % 256 == 0 && M >= 8192) return 2;
+    if (edge_ok && mb192 * (N / 128) >= 384) return 4;
+    return 1;
 }
 
 }  // namespace
@@ -702,7 +712,7 @@ void launch_gemm(const uint16_t* A, int lda, const WeightView& W, int M, int N, 
     ACEMI_CHECK(lda % 8 == 0, "gemm: leading dims must be multiples of 8");
     ACEMI_CHECK(W.q != nullptr, "gemm: null weight");
     GemmParams p{A, (const uint16_t*)W.q, W.q, W.s, lda, W.ld, M, N, K, epi};
-    const int v = pick_variant(M, N);
+    const int v = pick_variant(M, N, weight_quantized(W.fmt));
     switch (W.fmt) {
         case WF_BF16:
         case WF_F16:

@@ -153,13 +153,13 @@ def test_attention_split_handles_small_values():
     assert mism < 0.02, mism
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("M,N,K", [(1, 256, 64), (300, 512, 128), (1000, 768, 2048), (513, 256, 6144)])
 def test_gemm_all_variants(variant, M, N, K):
-    """Every GEMM kernel variant (128x128 / 256x256 / 256x128, both pipelines), incl. M edges and
-    K = 1, 2 and many tiles (pipeline prologue/epilogue paths)."""
+    """Every GEMM kernel variant (128x128 / 256x256 / 256x128 / 192x128 / 192x256, both pipelines),
+    incl. M edges and K = 1, 2 and many tiles (pipeline prologue/epilogue paths)."""
     capi = _capi()
-    if N % 256 and variant == 2:
+    if N % 256 and variant in (2, 5):
         pytest.skip("256-wide tiles need N % 256 == 0")
     rng = np.random.default_rng(variant * 7 + M)
     a = _bits(rng.standard_normal((M, K)).astype(np.float32), 0)
