@@ -561,11 +561,11 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_q_kernel(GemmParams p) {
     lds_wait_all();
     __builtin_amdgcn_s_barrier();
 
-    auto mfma_half = [&](const uint4 (&a)[TM][2], const uint4 (&b)[TN][2], int i0) {
+    auto mfma_all = [&](const uint4 (&a)[TM][2], const uint4 (&b)[TN][2]) {
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-            for (int i = i0; i < i0 + TM / 2; ++i)
+            for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<false>(a[i][kk], b[j][kk], acc[i][j]);
     };
@@ -595,8 +595,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_q_kernel(GemmParams p) {
         // A(kt+2) before the barrier that ends that iteration publishes buffer `cur` again
         asm volatile("" ::: "memory");
         wnext = load_wq<WQ>(qbase, sbase, min(kt + 3, nk - 1));
-        mfma_half(a, b, 0);
-        mfma_half(a, b, TM / 2);
+        mfma_all(a, b);
         // retire this wave's LDS traffic before the barrier that hands buffer `cur` to the other waves
         // (gfx950 does not wait at s_barrier)
         lds_wait_all();
@@ -617,7 +616,7 @@ void launch_cfg(const GemmParams& p, hipStream_t s) {
 }
 
 // variant: 0 = 128x128 PIPE0, 1 = 128x128 PIPE1, 2 = 256x256 PIPE1 (8 waves 2x4), 3 = 256x128 PIPE1,
-// 4 = 192x128 PIPE1, 5 = 192x256 PIPE1 (8 waves 2x4)
+// 4 = 192x128 PIPE1, 5 = 192x256 PIPE1 (8 waves 2x4), 6 = 192x64 PIPE1 (dense only), 7 = 96x128 PIPE1
 template <bool F16, int EPI>
 void launch_variant(int variant, const GemmParams& p, hipStream_t s) {
     switch (variant) {
@@ -627,6 +626,8 @@ void launch_variant(int variant, const GemmParams& p, hipStream_t s) {
         case 3: launch_cfg<256, 128, 2, 2, F16, EPI, 1>(p, s); break;
         case 4: launch_cfg<192, 128, 2, 2, F16, EPI, 1>(p, s); break;
         case 5: launch_cfg<192, 256, 2, 4, F16, EPI, 1>(p, s); break;
+        case 6: launch_cfg<192, 64, 2, 2, F16, EPI, 1>(p, s); break;
+        case 7: launch_cfg<96, 128, 2, 2, F16, EPI, 1>(p, s); break;
         default: throw std::runtime_error("gemm: bad variant");
     }
 }
@@ -660,6 +661,7 @@ void launch_q_variant(int variant, const GemmParams& p, hipStream_t s) {
         case 3: launch_q_cfg<256, 128, 2, 2, EPI, WQ>(p, s); break;
         case 4: launch_q_cfg<192, 128, 2, 2, EPI, WQ>(p, s); break;
         case 5: launch_q_cfg<192, 256, 2, 4, EPI, WQ>(p, s); break;
+        case 7: launch_q_cfg<96, 128, 2, 2, EPI, WQ>(p, s); break;
         default: throw std::runtime_error("gemm: bad variant");
     }
 }
@@ -688,6 +690,8 @@ int g_forced_variant = -1;
 // 827); with only N = 2048 (256 tiles) the 128x128 tile's two blocks per CU win (down 779 vs 684).
 // Dequant-fused: 192x256 (one block per CU, the dequant VALU spread over 8 waves) leads where it
 // gives at least one tile per CU (gate|up 655 vs 525, qkv 709 vs 502), else 192x128 (down 506 vs 437).
+// Dense N = 2048 at M = 3000: 96x128 makes 512 tiles, exactly two blocks per CU (down 857 vs 775,
+// o / cross 662 vs 569).
 double m_edge(int M, int bm) { return (double)M / (double)(((M + bm - 1) / bm) * bm); }
 
 int pick_variant(int M, int N, bool quant) {
@@ -696,11 +700,12 @@ int pick_variant(int M, int N, bool quant) {
     const bool edge_ok = m_edge(M, 192) >= m_edge(M, 128) - 0.02;
     if (quant) {
         if (N % 256 == 0 && edge_ok && mb192 * (N / 256) >= 256) return 5;
-        if (edge_ok && mb192 * (N / 128) >= 256) return 4;
+        if (m_edge(M, 96) >= m_edge(M, 128) - 0.02) return 7;  // down 590 vs 493, o / cross 474 vs 396
         return 1;
     }
     if (N % 256 == 0 && M >= 8192) return 2;
     if (edge_ok && mb192 * (N / 128) >= 384) return 4;
+    if (m_edge(M, 96) >= m_edge(M, 128) - 0.02) return 7;  // N = 2048: 512 tiles, two per CU
     return 1;
 }
 

@@ -236,38 +236,58 @@ __global__ void __launch_bounds__(256) attn_prep_kernel(PrepArgs a) {
         uint16_t* base = isq ? a.qh + ((int64_t)b * a.hq + head) * a.n_pad * 128
                              : a.kh + ((int64_t)b * a.hkv + head) * a.n_pad * 128;
         const int64_t plane = isq ? a.q_plane : a.k_plane;
-        const float w0 = w ? w[lane] : 1.f, w1 = w ? w[lane + 64] : 1.f;
-        for (int tok = wid; tok < 64; tok += 4) {
-            const int n = n0 + tok;
-            float r0 = 0.f, r1 = 0.f;
+        // lane: token sub = lane / 16 of the wave's group of 4, dims d..d+3 and d+64..d+67 (the NEOX
+        // rotation pairs d with d+64 inside the lane); 16-byte loads, 8-byte f16 stores
+        const int sub = lane >> 4;
+        const int d = (lane & 15) * 4;
+        const float4 one = make_float4(1.f, 1.f, 1.f, 1.f);
+        const float4 w0 = w ? *(const float4*)(w + d) : one, w1 = w ? *(const float4*)(w + 64 + d) : one;
+        auto pk4 = [](float p, float q, float r, float t) {
+            return make_uint2((uint32_t)f32_to_f16(p) | ((uint32_t)f32_to_f16(q) << 16),
+                              (uint32_t)f32_to_f16(r) | ((uint32_t)f32_to_f16(t) << 16));
+        };
+        auto lo = [](float v) { return v - (float)__builtin_bit_cast(_Float16, f32_to_f16(v)); };
+#pragma unroll
+        for (int t0 = wid * 4; t0 < 64; t0 += 16) {  // 4 groups of 4 tokens per wave, loads hoisted
+            const int n = n0 + t0 + sub;
+            float4 x0 = make_float4(0.f, 0.f, 0.f, 0.f), x1 = x0;
             if (n < a.n_tok) {
                 const float* row = a.src + ((int64_t)b * a.n_tok + n) * a.ld + col;
-                const float x0 = row[lane];
-                const float x1 = row[lane + 64];
-                float y0 = x0, y1 = x1;
-                if (w) {  // null weight: plain copy (kernel self-test entry)
-                    const float ss = wave_sum(x0 * x0 + x1 * x1);
-                    const float sc = 1.0f / sqrtf(ss / 128.0f + a.eps);
-                    y0 = __fmul_rn(__fmul_rn(x0, sc), w0);
-                    y1 = __fmul_rn(__fmul_rn(x1, sc), w1);
+                x0 = *(const float4*)(row + d);
+                x1 = *(const float4*)(row + 64 + d);
+            }
+            float y[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+            if (w) {  // null weight: plain copy (kernel self-test entry)
+                float ss = 0.f;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) ss += y[j] * y[j];
+#pragma unroll
+                for (int o = 8; o >= 1; o >>= 1) ss += __shfl_xor(ss, o);  // the token's 16 lanes
+                const float sc = 1.0f / sqrtf(ss / 128.0f + a.eps);
+                const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+                for (int j = 0; j < 8; ++j) y[j] = __fmul_rn(__fmul_rn(y[j], sc), wv[j]);
+            }
+            float r[8];
+            if (a.rope_cos && n < a.n_tok) {
+                const float4 c4 = *(const float4*)(a.rope_cos + (int64_t)n * 64 + d);
+                const float4 s4 = *(const float4*)(a.rope_sin + (int64_t)n * 64 + d);
+                const float c[4] = {c4.x, c4.y, c4.z, c4.w}, sn[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    r[j] = __fsub_rn(__fmul_rn(y[j], c[j]), __fmul_rn(y[4 + j], sn[j]));
+                    r[4 + j] = __fadd_rn(__fmul_rn(y[j], sn[j]), __fmul_rn(y[4 + j], c[j]));
                 }
-                if (a.rope_cos) {
-                    const float c = a.rope_cos[(int64_t)n * 64 + lane];
-                    const float s = a.rope_sin[(int64_t)n * 64 + lane];
-                    r0 = __fsub_rn(__fmul_rn(y0, c), __fmul_rn(y1, s));
-                    r1 = __fadd_rn(__fmul_rn(y0, s), __fmul_rn(y1, c));
-                } else {
-                    r0 = y0;
-                    r1 = y1;
-                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) r[j] = y[j];
             }
             uint16_t* dst = base + (int64_t)n * 128;
-            const uint16_t h0 = f32_to_f16(r0), h1 = f32_to_f16(r1);
-            dst[lane] = h0;
-            dst[lane + 64] = h1;
+            *(uint2*)(dst + d) = pk4(r[0], r[1], r[2], r[3]);
+            *(uint2*)(dst + 64 + d) = pk4(r[4], r[5], r[6], r[7]);
             if (plane > 0) {
-                dst[plane + lane] = f32_to_f16(r0 - (float)__builtin_bit_cast(_Float16, h0));
-                dst[plane + lane + 64] = f32_to_f16(r1 - (float)__builtin_bit_cast(_Float16, h1));
+                *(uint2*)(dst + plane + d) = pk4(lo(r[0]), lo(r[1]), lo(r[2]), lo(r[3]));
+                *(uint2*)(dst + plane + 64 + d) = pk4(lo(r[4]), lo(r[5]), lo(r[6]), lo(r[7]));
             }
         }
         return;

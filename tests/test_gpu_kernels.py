@@ -153,7 +153,7 @@ def test_attention_split_handles_small_values():
     assert mism < 0.02, mism
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("M,N,K", [(1, 256, 64), (300, 512, 128), (1000, 768, 2048), (513, 256, 6144)])
 def test_gemm_all_variants(variant, M, N, K):
     """Every GEMM kernel variant (128x128 / 256x256 / 256x128 / 192x128 / 192x256, both pipelines),

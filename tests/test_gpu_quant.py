@@ -29,7 +29,7 @@ def _q_ref(a_bits, w_blocks, qtype):
 
 
 @pytest.mark.parametrize("qtype", ["q8_0", "q4_k", "q6_k"])
-@pytest.mark.parametrize("variant", [-1, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [-1, 1, 2, 3, 4, 5, 7])
 @pytest.mark.parametrize("M,N,K", [(1, 256, 256), (300, 512, 512), (1000, 256, 2048), (129, 768, 6144)])
 def test_gemm_q_matches_dequantized_product(qtype, variant, M, N, K):
     capi = _capi()

@@ -24,7 +24,7 @@ def main():
     for qtype in ("q8_0", "q4_k", "q6_k"):
         blocks = capi.quantize(w, qtype)
         want = g.round_bf16(DEQ[qtype](blocks)).astype(np.float32)  # [N][K]
-        for variant in (1, 2, 3, 4, 5):
+        for variant in (1, 2, 3, 4, 5, 7):
             prev = None
             for rep in range(3):
                 got = capi.kernel_gemm_q(a, blocks, qtype, epi=0, variant=variant).T  # [N][K]
@@ -65,7 +65,7 @@ def stress(reps=20):
     for qtype in ("q4_k", "q6_k", "q8_0"):
         blocks = capi.quantize(w, qtype)
         ref, scale = _q_ref(a, blocks, qtype)
-        for variant in (1, 2, 3, 4, 5):
+        for variant in (1, 2, 3, 4, 5, 7):
             nbad = 0
             worst = 0.0
             for _ in range(reps):
