@@ -74,7 +74,12 @@ struct AttnArgs {
     float scale;
     bool split = true;                 // hi/lo fp16 operands (see attention.hip)
     int64_t q_plane = 0, k_plane = 0, v_plane = 0;  // element offset of the lo planes
+    // Optional f32 workspace of attn_part_floats(): with it, a grid too small to fill the chip in
+    // whole rounds splits every block's key range in two and merges the halves in a second kernel.
+    float* part = nullptr;
+    int ksplit = 1;  // set by launch_attention
 };
+size_t attn_part_floats(int B, int nq, int Hq);
 void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s);
 
 // ------------------------------------------------------------ elementwise

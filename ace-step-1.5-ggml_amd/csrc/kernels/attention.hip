@@ -40,6 +40,8 @@
 // max.  K and V^T tiles arrive by global_load_lds into two 2-slot rings in
 // LDS: K(i+2) and V(i+1) are requested at the top of iteration i (their
 // slots were last read in iteration i-1) and land by its closing barrier.
+#include <algorithm>
+
 #include "../kernels.h"
 #include "lds_asm.h"
 
@@ -102,11 +104,6 @@ __device__ __forceinline__ uint32_t pack_f16x2(float a, float b) {
     return (uint32_t)__builtin_bit_cast(uint16_t, ha) | ((uint32_t)__builtin_bit_cast(uint16_t, hb) << 16);
 }
 
-__device__ __forceinline__ uint32_t pack_f16x2_lo(float a, float b) {
-    const _Float16 ha = (_Float16)a, hb = (_Float16)b;
-    return pack_f16x2(a - (float)ha, b - (float)hb);
-}
-
 __device__ __forceinline__ uint16_t f32_to_bf16_rne(float f) {
     uint32_t u = __float_as_uint(f);
     if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 64u);
@@ -151,6 +148,8 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
     const int qpb = 128 / rep;   // query rows per head in this block
     const int n_qt = (a.nq + qpb - 1) / qpb;
     int bid = blockIdx.x;
+    const int split = bid % a.ksplit;  // key-range part of this block (AttnArgs::part)
+    bid /= a.ksplit;
     const int qt = bid % n_qt;
     bid /= n_qt;
     const int kvh = bid % a.Hkv;
@@ -168,8 +167,10 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
         khi = min(a.nk, q0 + qpb - 1 + a.window + 1);
     }
     if (a.causal) khi = min(khi, q0 + qpb);  // no key after the block's last query
-    const int kt_begin = klo / KT;
-    const int n = max(0, (khi + KT - 1) / KT - kt_begin);
+    const int n_all = max(0, (khi + KT - 1) / KT - klo / KT);
+    const int chunk = (n_all + a.ksplit - 1) / a.ksplit;
+    const int kt_begin = klo / KT + split * chunk;
+    const int n = max(0, min(chunk, n_all - split * chunk));
 
     // ---- this lane's valid absolute key range [lo_abs, hi_abs): padding, window, causal
     int lo_abs = 0, hi_abs = a.nk;
@@ -285,19 +286,31 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
             });
             lds_wait_tie(kbv);
         }
-        float mloc = -INFINITY;
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 float x = s[t][r] * c_log2;
                 if constexpr (KBIAS) x += __uint_as_float(kbv[4 * t + (r >> 2)][r & 3]);
-                const int kr = key_of(t, r);
-                x = (kr >= lo && kr < hi) ? x : -INFINITY;
                 s[t][r] = x;
-                mloc = fmaxf(mloc, x);
             }
         }
+        // padding / window / causal bounds: only tiles that cross a bound for some lane of the wave
+        // (key_of spans 0..59 before the lane-half offset, already folded into lo / hi)
+        if (__builtin_amdgcn_ballot_w64(lo > 0 || hi < 60) != 0) {
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int kr = key_of(t, r);
+                    s[t][r] = (kr >= lo && kr < hi) ? s[t][r] : -INFINITY;
+                }
+        }
+        float mloc = -INFINITY;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) mloc = fmaxf(mloc, s[t][r]);
         return fmaxf(mloc, __shfl_xor(mloc, 32));
     };
 
@@ -364,16 +377,22 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
             }
 #pragma unroll
             for (int ss = 0; ss < 2; ++ss) {
-                frag f;
+                frag f, fl;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) f[j] = pack_f16x2(s_cur[t][8 * ss + 2 * j], s_cur[t][8 * ss + 2 * j + 1]);
-                pf[2 * t + ss] = f;
-                if constexpr (SPLIT) {
-#pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        f[j] = pack_f16x2_lo(s_cur[t][8 * ss + 2 * j], s_cur[t][8 * ss + 2 * j + 1]);
-                    pfl[2 * t + ss] = f;
+                for (int j = 0; j < 4; ++j) {
+                    const float p0 = s_cur[t][8 * ss + 2 * j], p1 = s_cur[t][8 * ss + 2 * j + 1];
+                    if constexpr (SPLIT) {
+                        // hi = fp16 toward zero (one v_cvt_pkrtz per pair); p - hi is exact in f32 and
+                        // its fp16 lo keeps the pair at ~22 bits, as with round-to-nearest
+                        const auto h2 = __builtin_amdgcn_cvt_pkrtz(p0, p1);
+                        f[j] = __builtin_bit_cast(uint32_t, h2);
+                        fl[j] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(p0 - (float)h2[0], p1 - (float)h2[1]));
+                    } else {
+                        f[j] = pack_f16x2(p0, p1);
+                    }
                 }
+                pf[2 * t + ss] = f;
+                if constexpr (SPLIT) pfl[2 * t + ss] = fl;
             }
         }
         l_run += lsum;
@@ -425,8 +444,24 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
     }
     if (i < n) iter(std::integral_constant<int, 0>{}, i);
 
-    // ---- normalise and store O[q][head*128 + d]
     const float l = l_run + __shfl_xor(l_run, 32);
+    if (a.ksplit > 1) {  // unnormalised partial O, running max and sum for attn_merge_kernel
+        if (qrow < a.nq) {
+            const int64_t row = ((int64_t)split * a.B + b) * a.nq + qrow;
+            float* po = a.part + row * (a.Hq * D) + head * D;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int g4 = 0; g4 < 4; ++g4)
+                    *(float4*)(po + 32 * dt + 8 * g4 + 4 * h) =
+                        make_float4(o[dt][4 * g4 + 0], o[dt][4 * g4 + 1], o[dt][4 * g4 + 2], o[dt][4 * g4 + 3]);
+            if (h == 0)
+                *(float2*)(a.part + (int64_t)a.ksplit * a.B * a.nq * a.Hq * D + (row * a.Hq + head) * 2) =
+                    make_float2(m_run, l);
+        }
+        return;
+    }
+    // ---- normalise and store O[q][head*128 + d]
     const float inv = 1.0f / l;
     if (qrow < a.nq) {
         uint16_t* op = a.out + ((int64_t)b * a.nq + qrow) * (a.Hq * D) + head * D;
@@ -444,6 +479,33 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
             }
         }
     }
+}
+
+// Combine the key-range parts of one (item, query, head) row per wave: M = max m_k, weights
+// 2^(m_k - M) (0 for a part whose keys were all masked), out = sum w_k O_k / sum w_k l_k; a row with
+// no unmasked key at all stays 0/0 = NaN as in ggml.
+template <bool F16OUT>
+__global__ void __launch_bounds__(256) attn_merge_kernel(AttnArgs a) {
+    const int64_t rows = (int64_t)a.B * a.nq * a.Hq;
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= rows) return;
+    const int lane = threadIdx.x & 63;
+    const float* ml = a.part + (int64_t)a.ksplit * rows * D;
+    float M = -INFINITY;
+    for (int k = 0; k < a.ksplit; ++k) M = fmaxf(M, ml[(k * rows + r) * 2]);
+    float o0 = 0.f, o1 = 0.f, l = 0.f;
+    for (int k = 0; k < a.ksplit; ++k) {
+        const float mk = ml[(k * rows + r) * 2];
+        const float w = mk == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(mk - M);
+        const float2 ov = *(const float2*)(a.part + (k * rows + r) * D + 2 * lane);
+        o0 += w * ov.x;
+        o1 += w * ov.y;
+        l += w * ml[(k * rows + r) * 2 + 1];
+    }
+    const float inv = 1.0f / l;
+    // row r = (b * nq + q) * Hq + head: out[b][q][head*128 + d] is contiguous in r * 128 + d
+    *(uint32_t*)(a.out + r * D + 2 * lane) =
+        (uint32_t)to_act<F16OUT>(o0 * inv) | ((uint32_t)to_act<F16OUT>(o1 * inv) << 16);
 }
 
 template <bool F16OUT, bool SPLIT>
@@ -465,20 +527,51 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s) {
     const int qpb = 128 / rep;
     const int n_qt = (a.nq + qpb - 1) / qpb;
     ACEMI_CHECK(a.nq_pad >= n_qt * qpb, "attention: nq_pad too small");
-    const dim3 grid(a.B * a.Hkv * n_qt);
+    AttnArgs b = a;
+    b.ksplit = 1;
+    {
+        // a grid of fewer than ~1.6 rounds over the CUs idles a third of the chip in its last
+        // round: split each block's key range in two (B = 1 at 240 s: 376 blocks -> 752)
+        static int n_cu = 0;
+        if (n_cu == 0) {
+            int dev = 0;
+            ACEMI_HIP(hipGetDevice(&dev));
+            ACEMI_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+        }
+        const int64_t blocks = (int64_t)a.B * a.Hkv * n_qt;
+        const int span = a.window > 0 ? std::min(a.nk, qpb + 2 * a.window) : a.nk;
+        // (measured: full 240 s 317 -> 262 us incl. the merge; at 8 key tiles or fewer -- cross attention,
+        // sliding windows -- the extra prologue and merge cost more than the round saves)
+        if (a.part && blocks * 10 < (int64_t)n_cu * 16 && (span + KT - 1) / KT >= 16) b.ksplit = 2;
+    }
+    const dim3 grid(a.B * a.Hkv * n_qt * b.ksplit);
     if (a.split) {
         ACEMI_CHECK(a.q_plane > 0 && a.k_plane > 0 && a.v_plane > 0, "attention: split mode needs lo planes");
         if (out_t == ActType::F16)
-            launch_t<true, true>(a, grid, s);
+            launch_t<true, true>(b, grid, s);
         else
-            launch_t<false, true>(a, grid, s);
+            launch_t<false, true>(b, grid, s);
     } else {
         if (out_t == ActType::F16)
-            launch_t<true, false>(a, grid, s);
+            launch_t<true, false>(b, grid, s);
         else
-            launch_t<false, false>(a, grid, s);
+            launch_t<false, false>(b, grid, s);
     }
     ACEMI_HIP(hipGetLastError());
+    if (b.ksplit > 1) {
+        const int64_t rows = (int64_t)a.B * a.nq * a.Hq;
+        const dim3 mgrid((unsigned)((rows + 3) / 4));
+        if (out_t == ActType::F16)
+            hipLaunchKernelGGL(attn_merge_kernel<true>, mgrid, dim3(256), 0, s, b);
+        else
+            hipLaunchKernelGGL(attn_merge_kernel<false>, mgrid, dim3(256), 0, s, b);
+        ACEMI_HIP(hipGetLastError());
+    }
+}
+
+size_t attn_part_floats(int B, int nq, int Hq) {
+    const size_t rows = (size_t)B * nq * Hq;
+    return 2 * rows * (D + 2);
 }
 
 }  // namespace acemi

@@ -16,7 +16,7 @@ DitEngine::DitEngine(int device) : device_(device) {
 
 DitEngine::~DitEngine() {
     for (Buf* b : {&a0_, &x_, &act_, &attn_, &act2_, &qkv_, &qh_, &kh_, &vt_, &kbias_, &enc_act_, &encp_, &ckv_, &kc_,
-                   &vc_, &kbias_c_, &freq_, &freq_act_, &th_, &th_act_, &temb_t_, &temb_r_, &temb_act_, &proj_,
+                   &vc_, &kbias_c_, &attn_part_, &freq_, &freq_act_, &th_, &th_act_, &temb_t_, &temb_r_, &temb_act_, &proj_,
                    &mods_, &outmod_, &cos_, &sin_, &ein_}) {
         if (b->p) (void)hipFree(b->p);
     }
@@ -91,6 +91,7 @@ void DitEngine::prepare_shape(int B, int Np, int L) {
     ensure(kh_, (size_t)2 * B * c.hkv * Npad * D * 2);
     ensure(vt_, (size_t)2 * B * c.hkv * D * Npad * 2);
     ensure(kbias_, (size_t)B * Npad * 4);
+    ensure(attn_part_, attn_part_floats(B, (int)Np, c.hq) * 4);
     if (L > 0) {
         const int64_t Lpad = round_up(L, 64);
         const int64_t Me = (int64_t)B * L;
@@ -350,6 +351,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
             aa.k = get<uint16_t>(kh_);
             aa.vt = get<uint16_t>(vt_);
             aa.kbias = io.mask ? get<float>(kbias_) : nullptr;  // padding keys are masked in-kernel
+            aa.part = get<float>(attn_part_);
             aa.out = attn;
             aa.B = B;
             aa.Hq = c.hq;
@@ -422,6 +424,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
                 aa.k = get<uint16_t>(kc_) + (size_t)li * B * c.hkv * Lpad * D;
                 aa.vt = get<uint16_t>(vc_) + (size_t)li * B * c.hkv * D * Lpad;
                 aa.kbias = io.enc_mask ? get<float>(kbias_c_) : nullptr;
+                aa.part = get<float>(attn_part_);
                 aa.out = attn;
                 aa.B = B;
                 aa.Hq = c.hq;

@@ -91,6 +91,7 @@ class DitEngine {
     DitModel model_;
     // workspace
     Buf a0_, x_, act_, attn_, act2_, qkv_, qh_, kh_, vt_, kbias_, enc_act_, encp_, ckv_, kc_, vc_, kbias_c_;
+    Buf attn_part_;  // key-range split partials of the attention kernel (AttnArgs::part)
     struct CrossKey {  // what kc_/vc_ currently hold (ForwardIO::reuse_cross)
         bool valid = false;
         int B = 0, L = 0, layers = 0;

@@ -66,7 +66,7 @@ namespace {
 // Device operands of one attention launch, prepared from host f32 q [B][nq][Hq*128] and kv
 // [B][nk][2*Hkv*128] through the engine's own prep kernel (hi/lo planes, V^T, key bias).
 struct AttnSetup {
-    DevMem dq, dkv, dm, dqh, dkh, dvt, dkb, dout;
+    DevMem dq, dkv, dm, dqh, dkh, dvt, dkb, dout, dpart;
     acemi::AttnArgs a{};
     size_t nqf;
     AttnSetup(int B, int Hq, int Hkv, int nq, int nk, int window, float scale, int flags, const float* q,
@@ -74,7 +74,7 @@ struct AttnSetup {
         : dq((size_t)B * nq * Hq * 128 * 4), dkv((size_t)B * nk * 2 * Hkv * 128 * 4), dm((size_t)B * nk * 4),
           dqh((size_t)2 * B * Hq * acemi::round_up(nq, 128) * 128 * 2), dkh((size_t)2 * B * Hkv * acemi::round_up(nk, 128) * 128 * 2),
           dvt((size_t)2 * B * Hkv * 128 * acemi::round_up(nk, 128) * 2), dkb((size_t)B * acemi::round_up(nk, 128) * 4),
-          dout((size_t)B * nq * Hq * 128 * 2) {
+          dout((size_t)B * nq * Hq * 128 * 2), dpart(acemi::attn_part_floats(B, nq, Hq) * 4) {
         using namespace acemi;
         const int D = 128;
         const int nq_pad = (int)round_up(nq, 128), nk_pad = (int)round_up(nk, 128);
@@ -121,6 +121,7 @@ struct AttnSetup {
         a.vt = dvt.as<uint16_t>();
         a.kbias = kmask ? dkb.as<float>() : nullptr;
         a.out = dout.as<uint16_t>();
+        a.part = dpart.as<float>();
         a.B = B;
         a.Hq = Hq;
         a.Hkv = Hkv;

@@ -207,6 +207,8 @@ void touch(const T* p, int64_t n) {
     (void)x;
 }
 
+size_t attn_part_floats(int B, int nq, int Hq) { return 2 * (size_t)B * nq * Hq * (128 + 2); }
+
 void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t) {
     const int D = 128, rep = a.Hq / a.Hkv;
     {  // attn_kernel footprint: Q rows up to nq_pad, K / V^T tiles up to nk_pad, both planes when split
