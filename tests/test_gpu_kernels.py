@@ -102,6 +102,8 @@ def _attn_ref(q, kv, hq, hkv, window, kmask, scale, rnd=round_f16):
     (2, 16, 8, 300, 77, 0, True),
     (1, 2, 2, 130, 130, 128, True),
     (1, 4, 1, 97, 500, 0, False),
+    (1, 2, 1, 1100, 1100, 0, False),   # >= 16 key tiles on a small grid: two-way key split + merge
+    (1, 2, 1, 150, 1500, 0, True),
 ])
 @pytest.mark.parametrize("split", [True, False])
 def test_attention_vs_fp64(B, hq, hkv, nq, nk, window, masked, split):
@@ -135,6 +137,11 @@ def test_attention_fully_masked_row_is_nan(split):
     q = np.ones((1, 8, 128), np.float32)
     kv = np.ones((1, 8, 256), np.float32)
     got = _capi().kernel_attention(q, kv, 1, 1, window=0, kmask=np.zeros((1, 8), np.int32), split=split)
+    assert np.isnan(got).all()
+    # same through the key-split path (every part fully masked -> merge 0/0)
+    q = np.ones((1, 8, 128), np.float32)
+    kv = np.ones((1, 1100, 256), np.float32)
+    got = _capi().kernel_attention(q, kv, 1, 1, window=0, kmask=np.zeros((1, 1100), np.int32), split=split)
     assert np.isnan(got).all()
 
 
@@ -180,3 +187,17 @@ def test_gemm_all_variants(variant, M, N, K):
     u = ref.reshape(M, N // 32, 2, 16)[:, :, 1, :].reshape(M, N // 2)
     sw = (g / (1 + np.exp(-g))) * u
     np.testing.assert_allclose(_vals(got_sw, 0), sw, rtol=2.0 ** -8, atol=1e-4)
+
+
+def test_attention_key_split_with_one_part_fully_masked():
+    """Key split: the first part sees only masked keys (m = -inf, l = 0) and must get weight 0."""
+    rng = np.random.default_rng(77)
+    B, hq, hkv, nq, nk = 1, 2, 1, 100, 1500
+    q = rng.standard_normal((B, nq, hq * 128)).astype(np.float32) * 2.0
+    kv = rng.standard_normal((B, nk, 2 * hkv * 128)).astype(np.float32) * 0.3
+    kmask = np.ones((B, nk), np.int32)
+    kmask[:, :1000] = 0
+    scale = 1.0 / np.sqrt(128.0)
+    got = _capi().kernel_attention(q, kv, hq, hkv, window=0, kmask=kmask, scale=scale, split=True)
+    ref = _attn_ref(q, kv, hq, hkv, 0, kmask, scale, rnd=lambda x: np.asarray(x, np.float32))
+    assert np.all(np.abs(got - ref) <= 2.0 ** -8 * np.abs(ref) + 1e-5)
