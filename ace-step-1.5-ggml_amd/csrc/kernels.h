@@ -161,12 +161,17 @@ struct ConvGemmArgs {
     uint16_t* S_out = nullptr;
     const float* snake_ea = nullptr;
     const float* snake_eb = nullptr;
+    // independent sequences in one launch (windows of the tiled decode): the M rows split into
+    // `items` equal runs; S is [items][T_in][Cin], X / S_out are [items][T_out][Cout]
+    int items = 1;
 };
 void launch_conv_gemm(const ConvGemmArgs& a, hipStream_t s);
 void launch_to_f16(const float* x, int64_t n, uint16_t* y, hipStream_t s);
 // x [rows][C] f32 -> y [rows][Cpad] fp16, channels >= C zero
 void launch_pack_f16(const float* x, int64_t rows, int C, int Cpad, uint16_t* y, hipStream_t s);
 // out[t][o] = sum_k sum_c W[o][k][c] * S[t + k - 3][c]   (kernel 7, pad 3, no bias), f32 out
-void launch_conv_out(const uint16_t* S, int T, int C, const uint16_t* W, int out_ch, float* out, hipStream_t s);
+// (items sequences of T rows each: S [items][T][C], out [items][T][out_ch])
+void launch_conv_out(const uint16_t* S, int T, int C, const uint16_t* W, int out_ch, float* out, hipStream_t s,
+                     int items = 1);
 
 }  // namespace acemi

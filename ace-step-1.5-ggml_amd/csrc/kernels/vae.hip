@@ -32,11 +32,15 @@ __device__ __forceinline__ uint16_t f32_to_f16(float f) {
     return __builtin_bit_cast(uint16_t, h);
 }
 
-// snake_forward (:682-692) with ea = exp(alpha), eb = exp(beta) precomputed on the host (expf)
+// snake_forward (:682-692) with ea = exp(alpha), eb = exp(beta) precomputed on the host (expf).
+// The hardware sine (v_sin_f32) and a reciprocal-multiply divide: the epilogue runs this for every
+// output element, and the IEEE sinf / division sequences cost ~50 VALU instructions per element --
+// more than the tile's MFMAs at 128 channels.  Their results differ from libm's by ~1e-6 relative,
+// far below the fp16 rounding of the next conv's operand that follows.
 __device__ __forceinline__ float snake_f(float x, float ea, float eb) {
-    float s = sinf(__fmul_rn(ea, x));
+    float s = __sinf(__fmul_rn(ea, x));
     s = __fmul_rn(s, s);
-    s = __fdiv_rn(s, eb);
+    s = __fdividef(s, eb);
     return __fadd_rn(x, s);
 }
 
@@ -85,13 +89,19 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(ConvGemmArgs p) {
     const int K = p.taps * p.Cin;
 
     // per-lane staging rows (fixed) and swizzled 16-byte chunk
+    const int Mi = p.M / p.items;  // rows per sequence
     int srow[G_PER_WAVE];
     int schunk[G_PER_WAVE];
+    int sml[G_PER_WAVE];           // row within its sequence (A rows)
+    int64_t sbase[G_PER_WAVE];     // first input row of its sequence
 #pragma unroll
     for (int j = 0; j < G_PER_WAVE; ++j) {
         const int row = (wid + NW * j) * 8 + (lane >> 3);
         srow[j] = row;
         schunk[j] = (lane & 7) ^ swz(row);
+        const int m = m0 + row, item = m / Mi;
+        sml[j] = m - item * Mi;
+        sbase[j] = (int64_t)item * p.T_in;
     }
     auto stage = [&](int buf, int kt) {
         char* base = smem + buf * STAGE;
@@ -105,8 +115,8 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(ConvGemmArgs p) {
             const uint16_t* src;
             if (row < BM) {
                 const int m = m0 + row;
-                const int t = m * istr + shift;
-                src = (m < p.M && t >= 0 && t < p.T_in) ? p.S + (int64_t)t * p.Cin + c0 + schunk[j] * 8
+                const int t = sml[j] * istr + shift;
+                src = (m < p.M && t >= 0 && t < p.T_in) ? p.S + (sbase[j] + t) * p.Cin + c0 + schunk[j] * 8
                                                         : p.zero + schunk[j] * 8;
             } else {
                 src = p.W + (int64_t)(n0 + row - BM) * K + kt * BK + schunk[j] * 8;
@@ -185,6 +195,8 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(ConvGemmArgs p) {
         for (int r = 0; r < 4; ++r) {
             const int m = m0 + wm0 + i * 16 + crow + r;
             if (m >= p.M) continue;
+            const int item = m / Mi, ml = m - item * Mi;
+            const int64_t obase = (int64_t)item * p.T_out;
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
                 const int n = n0 + wn0 + j * 16 + ccol;
@@ -192,15 +204,15 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(ConvGemmArgs p) {
                 if (p.up > 1) {
                     const int rr = n / p.Cout;
                     co = n - rr * p.Cout;
-                    u = m * p.up + rr - p.crop;
+                    u = ml * p.up + rr - p.crop;
                 } else {
                     co = n;
-                    u = m;
+                    u = ml;
                 }
                 if (u < 0 || u >= p.T_out) continue;
                 float v = acc[i][j][r];
                 if (p.bias) v = __fadd_rn(v, p.bias[co]);
-                const int64_t o = (int64_t)u * p.Cout + co;
+                const int64_t o = (obase + u) * p.Cout + co;
                 if (p.resid) v = __fadd_rn(p.X[o], v);
                 if (p.store_x) p.X[o] = v;
                 if (p.S_out) p.S_out[o] = f32_to_f16(p.snake_ea ? snake_f(v, p.snake_ea[co], p.snake_eb[co]) : v);
@@ -230,15 +242,19 @@ __global__ void pack_f16_kernel(const float* __restrict__ x, int64_t rows, int C
 // fp16 products.
 template <int OUT>
 __global__ void __launch_bounds__(256) conv_out_kernel(const uint16_t* __restrict__ S, int T, int C,
-                                                       const uint16_t* __restrict__ W, float* __restrict__ out) {
+                                                       const uint16_t* __restrict__ W, float* __restrict__ out,
+                                                       int items) {
     extern __shared__ float wsh[];  // [7][C][OUT] as f32
     for (int i = threadIdx.x; i < 7 * C * OUT; i += blockDim.x) {
         const int o = i % OUT, c = (i / OUT) % C, k = i / (OUT * C);
         wsh[i] = (float)__builtin_bit_cast(_Float16, W[((int64_t)o * 7 + k) * C + c]);
     }
     __syncthreads();
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= T) return;
+    const int tg = blockIdx.x * blockDim.x + threadIdx.x;  // row over all sequences
+    if (tg >= T * items) return;
+    const int item = tg / T, t = tg - item * T;
+    S += (int64_t)item * T * C;
+    out += (int64_t)item * T * OUT;
     float acc[OUT];
 #pragma unroll
     for (int o = 0; o < OUT; ++o) acc[o] = 0.f;
@@ -274,6 +290,7 @@ void launch_conv_gemm(const ConvGemmArgs& a, hipStream_t s) {
     ACEMI_CHECK(a.up <= 1 || a.N == a.up * a.Cout, "conv_gemm: transposed conv needs N = stride * Cout");
     ACEMI_CHECK(a.up > 1 || a.N == a.Cout, "conv_gemm: N must equal Cout");
     ACEMI_CHECK(!(a.resid || a.store_x) || a.X, "conv_gemm: null X");
+    ACEMI_CHECK(a.items >= 1 && a.M % a.items == 0, "conv_gemm: rows must split evenly into the sequences");
     const int nbm = (a.M + 127) / 128, nbn = a.N / 128;
     hipLaunchKernelGGL(conv_gemm_kernel, dim3(nbm * nbn), dim3(256), 0, s, a);
     ACEMI_HIP(hipGetLastError());
@@ -292,15 +309,17 @@ void launch_pack_f16(const float* x, int64_t rows, int C, int Cpad, uint16_t* y,
     ACEMI_HIP(hipGetLastError());
 }
 
-void launch_conv_out(const uint16_t* S, int T, int C, const uint16_t* W, int out_ch, float* out, hipStream_t s) {
+void launch_conv_out(const uint16_t* S, int T, int C, const uint16_t* W, int out_ch, float* out, hipStream_t s,
+                     int items) {
     ACEMI_CHECK(C % 8 == 0, "conv_out: channels must be a multiple of 8");
+    ACEMI_CHECK(items >= 1 && (int64_t)T * items < (1LL << 31), "conv_out: bad sequence count");
     const size_t shm = (size_t)7 * C * out_ch * 4;
     ACEMI_CHECK(shm <= 64 * 1024, "conv_out: weights do not fit LDS");
-    const dim3 grid((T + 255) / 256);
+    const dim3 grid((unsigned)(((int64_t)T * items + 255) / 256));
     if (out_ch == 1)
-        hipLaunchKernelGGL(conv_out_kernel<1>, grid, dim3(256), shm, s, S, T, C, W, out);
+        hipLaunchKernelGGL(conv_out_kernel<1>, grid, dim3(256), shm, s, S, T, C, W, out, items);
     else if (out_ch == 2)
-        hipLaunchKernelGGL(conv_out_kernel<2>, grid, dim3(256), shm, s, S, T, C, W, out);
+        hipLaunchKernelGGL(conv_out_kernel<2>, grid, dim3(256), shm, s, S, T, C, W, out, items);
     else
         throw std::runtime_error("conv_out: audio_channels must be 1 or 2");
     ACEMI_HIP(hipGetLastError());

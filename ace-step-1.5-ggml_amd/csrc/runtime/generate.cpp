@@ -186,30 +186,66 @@ ace_ggml_status generate_from_encoder(ace_ggml_context* ctx, const float* enc, c
             overlap = 0;
             stride = chunk;
         }
-        double up = -1.0;
-        size_t pos = 0;
+        // The windows (reference order) decode in batches: consecutive windows of equal length share
+        // every conv launch (VaeEngine::decode items), so the narrow early stages of a 128-frame
+        // window fill the chip.  Each window's output is the reference's zero-filled
+        // wf * hop_length buffer holding the decoder's out_len(wf) samples, trimmed as there.
+        struct Win {
+            int32_t core0, core1, w0, w1;
+        };
+        std::vector<Win> wins;
         for (int32_t core0 = 0; core0 < seq_len; core0 += stride) {
             const int32_t core1 = std::min(core0 + stride, seq_len);
-            const int32_t w0 = std::max(0, core0 - overlap), w1 = std::min(seq_len, core1 + overlap);
-            const int32_t wf = w1 - w0;
-            std::vector<float> audio((size_t)wf * hop_length * cs, 0.0f);
-            st = ace_ggml_vae_decode(ctx, &xt[(size_t)w0 * audio_dim], wf, audio.data(), audio.size() * sizeof(float));
-            if (st != ACE_GGML_OK) return st;
-            const size_t decoded = audio.size() / cs;
-            if (up <= 0.0 && wf > 0) up = (double)decoded / (double)wf;
-            const double trim = up > 0.0 ? up : (double)hop_length;
-            int32_t ts = (int32_t)std::llround((double)(core0 - w0) * trim);
-            int32_t te = (int32_t)std::llround((double)(w1 - core1) * trim);
-            ts = std::max(0, std::min(ts, (int32_t)decoded));
-            te = std::max(0, std::min(te, (int32_t)decoded));
-            int32_t end = (int32_t)decoded - te;
-            if (end < ts) end = ts;
-            size_t core = (size_t)(end - ts);
-            if (core > 0 && pos < cap_samples) {
-                core = std::min(core, cap_samples - pos);
-                std::copy(&audio[(size_t)ts * cs], &audio[(size_t)ts * cs] + core * cs, out_audio + pos * cs);
-                pos += core;
+            wins.push_back({core0, core1, std::max(0, core0 - overlap), std::min(seq_len, core1 + overlap)});
+        }
+        const int32_t max_batch = std::max<int32_t>(1, nonneg_env("ACE_MI_VAE_WINDOW_BATCH", 16));
+        double up = -1.0;
+        size_t pos = 0;
+        try {
+            bind_device(ctx);
+            hipStream_t s = ctx->stream;
+            for (size_t g0 = 0; g0 < wins.size();) {
+                const int32_t wf = wins[g0].w1 - wins[g0].w0;
+                size_t g1 = g0 + 1;
+                while (g1 < wins.size() && (int32_t)(g1 - g0) < max_batch && wins[g1].w1 - wins[g1].w0 == wf) ++g1;
+                const int nb = (int)(g1 - g0);
+                const int64_t dec_len = ctx->vae->out_len(wf);
+                const size_t lat_n = (size_t)wf * audio_dim, aud_n = (size_t)dec_len * cs;
+                std::vector<float> lat((size_t)nb * lat_n);
+                for (int b = 0; b < nb; ++b)
+                    std::copy(&xt[(size_t)wins[g0 + b].w0 * audio_dim], &xt[(size_t)wins[g0 + b].w0 * audio_dim] + lat_n,
+                              &lat[(size_t)b * lat_n]);
+                DevMem d_lat(lat.size() * 4), d_aud((size_t)nb * aud_n * 4);
+                ACEMI_HIP(hipMemcpyAsync(d_lat.p, lat.data(), lat.size() * 4, hipMemcpyHostToDevice, s));
+                ctx->vae->decode(d_lat.as<float>(), wf, d_aud.as<float>(), s, nb);
+                std::vector<float> dec((size_t)nb * aud_n);
+                ACEMI_HIP(hipMemcpyAsync(dec.data(), d_aud.p, dec.size() * 4, hipMemcpyDeviceToHost, s));
+                ACEMI_HIP(hipStreamSynchronize(s));
+                for (int b = 0; b < nb; ++b) {
+                    const Win& w = wins[g0 + b];
+                    std::vector<float> audio((size_t)wf * hop_length * cs, 0.0f);
+                    std::copy(&dec[(size_t)b * aud_n], &dec[(size_t)b * aud_n] + std::min(aud_n, audio.size()),
+                              audio.begin());
+                    const size_t decoded = audio.size() / cs;
+                    if (up <= 0.0 && wf > 0) up = (double)decoded / (double)wf;
+                    const double trim = up > 0.0 ? up : (double)hop_length;
+                    int32_t ts = (int32_t)std::llround((double)(w.core0 - w.w0) * trim);
+                    int32_t te = (int32_t)std::llround((double)(w.w1 - w.core1) * trim);
+                    ts = std::max(0, std::min(ts, (int32_t)decoded));
+                    te = std::max(0, std::min(te, (int32_t)decoded));
+                    int32_t end = (int32_t)decoded - te;
+                    if (end < ts) end = ts;
+                    size_t core = (size_t)(end - ts);
+                    if (core > 0 && pos < cap_samples) {
+                        core = std::min(core, cap_samples - pos);
+                        std::copy(&audio[(size_t)ts * cs], &audio[(size_t)ts * cs] + core * cs, out_audio + pos * cs);
+                        pos += core;
+                    }
+                }
+                g0 = g1;
             }
+        } catch (const std::exception& e) {
+            return set_error(ctx, ACE_GGML_ERR, std::string("graph compute failed: ") + e.what());
         }
         produced = (int32_t)pos;
     } else {

@@ -343,6 +343,8 @@ void VaeEngine::run_conv(const VaeConv& c, const uint16_t* S, int T_in, int T_ou
     a.resid = resid ? 1 : 0;
     a.store_x = store ? 1 : 0;
     a.S_out = S_out;
+    a.items = items_;
+    a.M *= items_;
     if (next) {
         a.snake_ea = next->ea;
         a.snake_eb = next->eb;
@@ -368,21 +370,23 @@ int64_t conv_len(int64_t L, const VaeConv& c) {  // ggml_conv_1d output length
 }
 }  // namespace
 
-void VaeEngine::decode(const float* d_latents, int n_frames, float* d_out, hipStream_t s) {
+void VaeEngine::decode(const float* d_latents, int n_frames, float* d_out, hipStream_t s, int items) {
     const VaeModel& m = model_;
     ACEMI_CHECK(n_frames >= 1, "vae decode: n_frames must be > 0");
+    ACEMI_CHECK(items >= 1, "vae decode: items must be > 0");
     // buffer sizes: the largest (length x channels) over the stages
     int64_t L = n_frames, maxe = (int64_t)n_frames * m.conv1.cout;
     for (const auto& b : m.blocks) {
         L = convt_len(L, b.ct);
         maxe = std::max(maxe, L * b.ct.cout);
     }
-    ACEMI_CHECK(L < (1LL << 31), "vae decode: sequence too long");
+    ACEMI_CHECK(L * items < (1LL << 31), "vae decode: sequence too long");
+    maxe *= items;
     ensure(x_, (size_t)maxe * 4);
     ensure(sa_, (size_t)maxe * 2);
     ensure(sb_, (size_t)maxe * 2);
     ensure(sc_, (size_t)maxe * 2);
-    ensure(lat_, (size_t)n_frames * m.conv1.cin * 2);
+    ensure(lat_, (size_t)items * n_frames * m.conv1.cin * 2);
     ensure(zero_, 4096);  // >= 64 fp16 zeros (hipMemset in ensure())
 
     float* X = static_cast<float*>(x_.p);
@@ -391,7 +395,8 @@ void VaeEngine::decode(const float* d_latents, int n_frames, float* d_out, hipSt
     uint16_t* Sc = static_cast<uint16_t*>(sc_.p);
 
     // latents -> fp16 (ggml im2col of decoder.conv1's input)
-    launch_to_f16(d_latents, (int64_t)n_frames * m.conv1.cin, static_cast<uint16_t*>(lat_.p), s);
+    launch_to_f16(d_latents, (int64_t)items * n_frames * m.conv1.cin, static_cast<uint16_t*>(lat_.p), s);
+    items_ = items;
     const VaeSnake* first = m.blocks.empty() ? &m.snake1 : &m.blocks[0].s1;
     // decoder.conv1 -> X, Sa = snake(next)(X)
     run_conv(m.conv1, static_cast<const uint16_t*>(lat_.p), n_frames, n_frames, X, false, true, Sa, first, s);
@@ -408,7 +413,8 @@ void VaeEngine::decode(const float* d_latents, int n_frames, float* d_out, hipSt
         }
     }
     // decoder.snake1 (applied into Sa) -> decoder.conv2
-    launch_conv_out(Sa, (int)L, m.conv2.cin, m.conv2.w, m.conv2.cout, d_out, s);
+    items_ = 1;
+    launch_conv_out(Sa, (int)L, m.conv2.cin, m.conv2.w, m.conv2.cout, d_out, s, items);
 }
 
 int64_t VaeEngine::enc_out_len(int n_samples) const {
@@ -423,6 +429,7 @@ void VaeEngine::encode(const float* d_audio, int n_samples, float* d_out, hipStr
     const VaeModel& m = model_;
     ACEMI_CHECK(m.has_encoder, "vae encoder weights not loaded");
     ACEMI_CHECK(n_samples >= 1, "vae encode: n_samples must be > 0");
+    items_ = 1;
     int64_t L = conv_len(n_samples, m.enc_conv1);
     int64_t maxe = (int64_t)n_samples * m.enc_conv1.cin;  // padded input
     maxe = std::max(maxe, L * m.enc_conv1.cout);

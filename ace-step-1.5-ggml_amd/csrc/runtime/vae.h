@@ -84,7 +84,9 @@ public:
     // ConvTranspose1d lengths for odd ones)
     int64_t out_len(int n_frames) const;
     // latents [n_frames][latent_channels] f32 -> out [out_len][audio_channels] f32, device pointers
-    void decode(const float* d_latents, int n_frames, float* d_out, hipStream_t s);
+    // `items` windows of n_frames each in one pass: d_latents [items][n_frames][C], d_out
+    // [items][out_len(n_frames)][audio_channels] (the windows of a tiled decode share every launch)
+    void decode(const float* d_latents, int n_frames, float* d_out, hipStream_t s, int items = 1);
     // latent frames produced by encode (ggml_conv_1d output lengths of the strided convs)
     int64_t enc_out_len(int n_samples) const;
     // audio [n_samples][audio_channels] f32 -> latent mean [enc_out_len][latent_channels] f32
@@ -99,6 +101,7 @@ private:
     int device_;
     VaeModel model_;
     Buf x_, sa_, sb_, sc_, lat_, zero_;
+    int items_ = 1;  // sequences per conv launch during decode (ConvGemmArgs::items)
     void run_conv(const VaeConv& c, const uint16_t* S, int T_in, int T_out, float* X, bool resid, bool store,
                   uint16_t* S_out, const VaeSnake* next, hipStream_t s);
     void run_res(const VaeRes& r, int L, float* X, uint16_t* Sin, uint16_t* Stmp, uint16_t* Snext_out,

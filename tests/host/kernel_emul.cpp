@@ -468,13 +468,18 @@ void launch_sde(float* xt, const float* v, const float* noise, int64_t n, float 
 void launch_conv_gemm(const ConvGemmArgs& a, hipStream_t) {
     ACEMI_CHECK(a.Cin % 64 == 0 && a.N % 128 == 0 && a.M >= 1 && a.taps >= 1, "conv_gemm: unsupported shape");
     touch(a.zero, 64);  // the kernel stages out-of-range rows from 64 zero halves
+    ACEMI_CHECK(a.items >= 1 && a.M % a.items == 0, "conv_gemm: rows must split evenly into the sequences");
     const int K = a.taps * a.Cin;
+    const int Mi = a.M / a.items;
     std::vector<float> row((size_t)K);
-    for (int m = 0; m < a.M; ++m) {
+    for (int mg = 0; mg < a.M; ++mg) {
+        const int item = mg / Mi, m = mg - item * Mi;
+        const uint16_t* S = a.S + (int64_t)item * a.T_in * a.Cin;
+        const int64_t obase = (int64_t)item * a.T_out;
         for (int tap = 0; tap < a.taps; ++tap) {
             const int t = m * a.in_stride + tap * a.dil - a.pad;
             for (int c = 0; c < a.Cin; ++c)
-                row[(size_t)tap * a.Cin + c] = (t >= 0 && t < a.T_in) ? f16f(a.S[(int64_t)t * a.Cin + c]) : 0.f;
+                row[(size_t)tap * a.Cin + c] = (t >= 0 && t < a.T_in) ? f16f(S[(int64_t)t * a.Cin + c]) : 0.f;
         }
         for (int n = 0; n < a.N; ++n) {
             double s = 0;
@@ -492,7 +497,7 @@ void launch_conv_gemm(const ConvGemmArgs& a, hipStream_t) {
             if (u < 0 || u >= a.T_out) continue;
             float v = (float)s;
             if (a.bias) v += a.bias[co];
-            const int64_t o = (int64_t)u * a.Cout + co;
+            const int64_t o = (obase + u) * a.Cout + co;
             if (a.resid) v = a.X[o] + v;
             if (a.store_x) a.X[o] = v;
             if (a.S_out) {
@@ -516,17 +521,23 @@ void launch_pack_f16(const float* x, int64_t rows, int C, int Cpad, uint16_t* y,
         for (int c = 0; c < Cpad; ++c) y[r * Cpad + c] = c < C ? to_f16(x[r * C + c]) : (uint16_t)0;
 }
 
-void launch_conv_out(const uint16_t* S, int T, int C, const uint16_t* W, int out_ch, float* out, hipStream_t) {
-    for (int t = 0; t < T; ++t)
-        for (int o = 0; o < out_ch; ++o) {
-            double s = 0;
-            for (int k = 0; k < 7; ++k) {
-                const int ti = t + k - 3;
-                if (ti < 0 || ti >= T) continue;
-                for (int c = 0; c < C; ++c) s += (double)f16f(S[(int64_t)ti * C + c]) * f16f(W[((int64_t)o * 7 + k) * C + c]);
+void launch_conv_out(const uint16_t* S0, int T, int C, const uint16_t* W, int out_ch, float* out0, hipStream_t,
+                     int items) {
+    for (int item = 0; item < items; ++item) {
+        const uint16_t* S = S0 + (int64_t)item * T * C;
+        float* out = out0 + (int64_t)item * T * out_ch;
+        for (int t = 0; t < T; ++t)
+            for (int o = 0; o < out_ch; ++o) {
+                double s = 0;
+                for (int k = 0; k < 7; ++k) {
+                    const int ti = t + k - 3;
+                    if (ti < 0 || ti >= T) continue;
+                    for (int c = 0; c < C; ++c)
+                        s += (double)f16f(S[(int64_t)ti * C + c]) * f16f(W[((int64_t)o * 7 + k) * C + c]);
+                }
+                out[(int64_t)t * out_ch + o] = (float)s;
             }
-            out[(int64_t)t * out_ch + o] = (float)s;
-        }
+    }
 }
 
 }  // namespace acemi

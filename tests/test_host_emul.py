@@ -369,7 +369,9 @@ def test_generate_entries_end_to_end(host_lib, cond_ckpt, text_ckpt):
     cases = [dict(token_ids=style), dict(style_ids=style, lyric_ids=lyric),
              dict(style_ids=style, lyric_ids=lyric, refer=refer)]
     for i, kw in enumerate(cases):
-        seq_len = 150 if i == 2 else 30   # > 128: chunked silence encode + windowed decode
+        # > 128: chunked silence encode + windowed decode (300: three equal 128-frame windows decoded
+        # as one batch, then the 96- and 76-frame edge windows)
+        seq_len = 300 if i == 2 else 30
         got = br.generate_audio(seq_len, shift=3.0, seed=11 + i, **kw)
         if "token_ids" in kw:
             enc = po.forward_text_encoder_layers_for_simple(TW, style)
