@@ -37,10 +37,10 @@ __device__ __forceinline__ uint16_t f32_to_f16(float f) {
 // output element, and the IEEE sinf / division sequences cost ~50 VALU instructions per element --
 // more than the tile's MFMAs at 128 channels.  Their results differ from libm's by ~1e-6 relative,
 // far below the fp16 rounding of the next conv's operand that follows.
-__device__ __forceinline__ float snake_f(float x, float ea, float eb) {
+__device__ __forceinline__ float snake_f(float x, float ea, float rcp_eb) {
     float s = __sinf(__fmul_rn(ea, x));
     s = __fmul_rn(s, s);
-    s = __fdividef(s, eb);
+    s = __fmul_rn(s, rcp_eb);  // / e^beta as a multiply by the (1-ulp) hardware reciprocal
     return __fadd_rn(x, s);
 }
 
@@ -188,7 +188,20 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(ConvGemmArgs p) {
     }
 
     // epilogue: (m, n) -> output time u and channel co; bias, residual, store, next Snake
+    // A thread's TN output columns are fixed, so their channel, transposed-conv phase, bias and Snake
+    // parameters are loaded once (not per element); the sequence split is one division per row.
     const int ccol = lane & 15, crow = (lane >> 4) * 4;
+    int co_j[TN], rr_j[TN];
+    float bias_j[TN], ea_j[TN], reb_j[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn0 + j * 16 + ccol;
+        rr_j[j] = p.up > 1 ? n / p.Cout : 0;
+        co_j[j] = n - rr_j[j] * p.Cout;
+        bias_j[j] = p.bias ? p.bias[co_j[j]] : 0.f;
+        ea_j[j] = p.snake_ea ? p.snake_ea[co_j[j]] : 0.f;
+        reb_j[j] = p.snake_eb ? __builtin_amdgcn_rcpf(p.snake_eb[co_j[j]]) : 0.f;
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
@@ -199,23 +212,15 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(ConvGemmArgs p) {
             const int64_t obase = (int64_t)item * p.T_out;
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
-                const int n = n0 + wn0 + j * 16 + ccol;
-                int u, co;
-                if (p.up > 1) {
-                    const int rr = n / p.Cout;
-                    co = n - rr * p.Cout;
-                    u = ml * p.up + rr - p.crop;
-                } else {
-                    co = n;
-                    u = ml;
-                }
+                const int co = co_j[j];
+                const int u = p.up > 1 ? ml * p.up + rr_j[j] - p.crop : ml;
                 if (u < 0 || u >= p.T_out) continue;
                 float v = acc[i][j][r];
-                if (p.bias) v = __fadd_rn(v, p.bias[co]);
+                if (p.bias) v = __fadd_rn(v, bias_j[j]);
                 const int64_t o = (obase + u) * p.Cout + co;
                 if (p.resid) v = __fadd_rn(p.X[o], v);
                 if (p.store_x) p.X[o] = v;
-                if (p.S_out) p.S_out[o] = f32_to_f16(p.snake_ea ? snake_f(v, p.snake_ea[co], p.snake_eb[co]) : v);
+                if (p.S_out) p.S_out[o] = f32_to_f16(p.snake_ea ? snake_f(v, ea_j[j], reb_j[j]) : v);
             }
         }
     }
