@@ -139,6 +139,45 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
     const int M = p.M;
     const int ccol = lane & 15;
     const int crow = (lane >> 4) * 4;
+    if constexpr (EPI == EPI_RESID_GATED || EPI == EPI_RESID) {
+        // Residual read-modify-write: every old x (and gate) value is loaded before the first store.
+        // Interleaved, the compiler cannot move a load of x above an earlier store to x (same pointer),
+        // so each element paid a full memory round trip in sequence.
+        float xo[TM][4][TN], gt[TM][4][TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = mw + i * 16 + crow + r;
+                const bool ok = m < M;
+                const int item = EPI == EPI_RESID_GATED ? m / e.rows_per_item : 0;
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const int n = nw + j * 16 + ccol;
+                    xo[i][r][j] = ok ? e.c_f32[(int64_t)m * e.ldc + n] : 0.f;
+                    if constexpr (EPI == EPI_RESID_GATED) gt[i][r][j] = ok ? e.gate[(int64_t)item * e.gate_stride + n] : 0.f;
+                }
+            }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = mw + i * 16 + crow + r;
+                if (m >= M) continue;
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const int n = nw + j * 16 + ccol;
+                    float v = acc[i][j][r];
+                    if constexpr (EPI == EPI_RESID_GATED) v = __fmul_rn(v, gt[i][r][j]);
+                    e.c_f32[(int64_t)m * e.ldc + n] = __fadd_rn(xo[i][r][j], v);
+                }
+            }
+        return;
+    }
+    float bias_j[TN];  // a thread's columns are fixed: their bias is loaded once, before any store
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+        bias_j[j] = ((EPI == EPI_STORE_F32 || EPI == EPI_STORE_ACT) && e.bias) ? e.bias[nw + j * 16 + ccol] : 0.f;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
@@ -159,19 +198,11 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
                     const int n = nw + j * 16 + ccol;
                     float v = acc[i][j][r];
                     if constexpr (EPI == EPI_STORE_F32) {
-                        if (e.bias) v = v + e.bias[n];
+                        if (e.bias) v = v + bias_j[j];
                         e.c_f32[(int64_t)m * e.ldc + n] = v;
                     } else if constexpr (EPI == EPI_STORE_ACT) {
-                        if (e.bias) v = v + e.bias[n];
+                        if (e.bias) v = v + bias_j[j];
                         e.c_act[(int64_t)m * e.ldc + n] = to_act<F16>(v);
-                    } else if constexpr (EPI == EPI_RESID_GATED) {
-                        const int item = m / e.rows_per_item;
-                        float* xp = e.c_f32 + (int64_t)m * e.ldc + n;
-                        const float gated = __fmul_rn(v, e.gate[(int64_t)item * e.gate_stride + n]);
-                        *xp = __fadd_rn(*xp, gated);
-                    } else if constexpr (EPI == EPI_RESID) {
-                        float* xp = e.c_f32 + (int64_t)m * e.ldc + n;
-                        *xp = __fadd_rn(*xp, v);
                     } else if constexpr (EPI == EPI_PROJ_OUT) {
                         const int item = m / e.rows_per_item;
                         const int pp = m - item * e.rows_per_item;

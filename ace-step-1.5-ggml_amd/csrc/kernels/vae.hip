@@ -202,23 +202,38 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(ConvGemmArgs p) {
         ea_j[j] = p.snake_ea ? p.snake_ea[co_j[j]] : 0.f;
         reb_j[j] = p.snake_eb ? __builtin_amdgcn_rcpf(p.snake_eb[co_j[j]]) : 0.f;
     }
+    // (sequence, row within it) of each accumulator row; the residual's old values are all loaded
+    // before the first store (interleaved, every load waited for the store before it)
+    int it_r[TM][4], ml_r[TM][4];
+    float xo[TM][4][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int m = m0 + wm0 + i * 16 + crow + r;
+            it_r[i][r] = m < p.M ? m / Mi : -1;
+            ml_r[i][r] = m - it_r[i][r] * Mi;
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int u = p.up > 1 ? ml_r[i][r] * p.up + rr_j[j] - p.crop : ml_r[i][r];
+                const bool ok = it_r[i][r] >= 0 && u >= 0 && u < p.T_out;
+                xo[i][r][j] = (ok && p.resid) ? p.X[((int64_t)it_r[i][r] * p.T_out + u) * p.Cout + co_j[j]] : 0.f;
+            }
+        }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int m = m0 + wm0 + i * 16 + crow + r;
-            if (m >= p.M) continue;
-            const int item = m / Mi, ml = m - item * Mi;
-            const int64_t obase = (int64_t)item * p.T_out;
+            if (it_r[i][r] < 0) continue;
+            const int64_t obase = (int64_t)it_r[i][r] * p.T_out;
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
-                const int co = co_j[j];
-                const int u = p.up > 1 ? ml * p.up + rr_j[j] - p.crop : ml;
+                const int u = p.up > 1 ? ml_r[i][r] * p.up + rr_j[j] - p.crop : ml_r[i][r];
                 if (u < 0 || u >= p.T_out) continue;
+                const int64_t o = (obase + u) * p.Cout + co_j[j];
                 float v = acc[i][j][r];
                 if (p.bias) v = __fadd_rn(v, bias_j[j]);
-                const int64_t o = (obase + u) * p.Cout + co;
-                if (p.resid) v = __fadd_rn(p.X[o], v);
+                if (p.resid) v = __fadd_rn(xo[i][r][j], v);
                 if (p.store_x) p.X[o] = v;
                 if (p.S_out) p.S_out[o] = f32_to_f16(p.snake_ea ? snake_f(v, ea_j[j], reb_j[j]) : v);
             }
