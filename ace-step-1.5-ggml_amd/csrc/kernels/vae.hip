@@ -202,38 +202,37 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(ConvGemmArgs p) {
         ea_j[j] = p.snake_ea ? p.snake_ea[co_j[j]] : 0.f;
         reb_j[j] = p.snake_eb ? __builtin_amdgcn_rcpf(p.snake_eb[co_j[j]]) : 0.f;
     }
-    // (sequence, row within it) of each accumulator row; the residual's old values are all loaded
-    // before the first store (interleaved, every load waited for the store before it)
-    int it_r[TM][4], ml_r[TM][4];
-    float xo[TM][4][TN];
+    // Per 16-row group i: (sequence, row within it) of its 4 rows, then the residual's 16 old values
+    // loaded before the group's first store (interleaved, every load waited for the store before it;
+    // a whole-tile preload held 64 more registers and halved the occupancy).
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < TM; ++i) {
+        int it_r[4], ml_r[4];
+        float xo[4][TN];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int m = m0 + wm0 + i * 16 + crow + r;
-            it_r[i][r] = m < p.M ? m / Mi : -1;
-            ml_r[i][r] = m - it_r[i][r] * Mi;
+            it_r[r] = m < p.M ? m / Mi : -1;
+            ml_r[r] = m - it_r[r] * Mi;
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
-                const int u = p.up > 1 ? ml_r[i][r] * p.up + rr_j[j] - p.crop : ml_r[i][r];
-                const bool ok = it_r[i][r] >= 0 && u >= 0 && u < p.T_out;
-                xo[i][r][j] = (ok && p.resid) ? p.X[((int64_t)it_r[i][r] * p.T_out + u) * p.Cout + co_j[j]] : 0.f;
+                const int u = p.up > 1 ? ml_r[r] * p.up + rr_j[j] - p.crop : ml_r[r];
+                const bool ok = it_r[r] >= 0 && u >= 0 && u < p.T_out;
+                xo[r][j] = (ok && p.resid) ? p.X[((int64_t)it_r[r] * p.T_out + u) * p.Cout + co_j[j]] : 0.f;
             }
         }
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-#pragma unroll
         for (int r = 0; r < 4; ++r) {
-            if (it_r[i][r] < 0) continue;
-            const int64_t obase = (int64_t)it_r[i][r] * p.T_out;
+            if (it_r[r] < 0) continue;
+            const int64_t obase = (int64_t)it_r[r] * p.T_out;
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
-                const int u = p.up > 1 ? ml_r[i][r] * p.up + rr_j[j] - p.crop : ml_r[i][r];
+                const int u = p.up > 1 ? ml_r[r] * p.up + rr_j[j] - p.crop : ml_r[r];
                 if (u < 0 || u >= p.T_out) continue;
                 const int64_t o = (obase + u) * p.Cout + co_j[j];
                 float v = acc[i][j][r];
                 if (p.bias) v = __fadd_rn(v, bias_j[j]);
-                if (p.resid) v = __fadd_rn(xo[i][r][j], v);
+                if (p.resid) v = __fadd_rn(xo[r][j], v);
                 if (p.store_x) p.X[o] = v;
                 if (p.S_out) p.S_out[o] = f32_to_f16(p.snake_ea ? snake_f(v, ea_j[j], reb_j[j]) : v);
             }
