@@ -316,7 +316,7 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
 
     float m_run = -INFINITY;   // running reference max (exp2 domain) of this lane's query
     float l_run = 0.f;
-    float alpha = 1.f;         // pending rescale of O and l (applied before the next P.V)
+    float alpha = 1.f;         // rescale of O and l for the latest max move
     bool rescale = false;      // wave-uniform
     f32x16 o[4];
 #pragma unroll
@@ -332,6 +332,18 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
         rescale = __builtin_amdgcn_ballot_w64(move) != 0;
     };
 
+    // rescale O and l to a moved running max (rare: a max grew by more than 2^RESCALE_LOG2); done right
+    // after the P.V that precedes the move, so the accumulators are touched only on that branch
+    auto apply_rescale = [&]() {
+        if (rescale) {
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+            l_run *= alpha;
+        }
+    };
+
     f32x16 s_cur[2], s_nxt[2];
     if (n > 0) {
         stage_k(0, kt_begin);
@@ -341,6 +353,7 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
         __builtin_amdgcn_s_barrier();
         s_tile(std::integral_constant<int, 0>{}, s_cur);
         update_max(prep(std::integral_constant<int, 0>{}, s_cur, 0));
+        apply_rescale();
         __builtin_amdgcn_s_barrier();  // every wave has read K slot 0: iteration 0 restages it
     }
 
@@ -351,15 +364,6 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
         const bool more = i + 1 < n;
         if (i + 2 < n) stage_k(SLOT, kt_begin + i + 2);
         if (more) stage_v(NXT, kt_begin + i + 1);
-
-        // pending rescale of O / l for tile i (rare: its max moved by more than 2^RESCALE_LOG2)
-        if (rescale) {
-#pragma unroll
-            for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
-        }
-        l_run *= alpha;
 
         // S(i+1) from K slot NXT (on the last tile: a discarded product of the slot's stale but
         // finite contents, which keeps this block branch-free) || P(i) = exp2(S(i) - m + 12)
@@ -425,9 +429,7 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
         const float mnx = prep(std::integral_constant<int, NXT>{}, s_nxt, i + 1);
         if (more) {
             update_max(mnx);
-        } else {
-            alpha = 1.f;
-            rescale = false;
+            apply_rescale();
         }
 #pragma unroll
         for (int t = 0; t < 2; ++t) s_cur[t] = s_nxt[t];
