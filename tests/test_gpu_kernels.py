@@ -160,6 +160,29 @@ def test_attention_split_handles_small_values():
     assert mism < 0.02, mism
 
 
+@pytest.mark.parametrize("nk", [700, 1100])
+@pytest.mark.parametrize("split", [True, False])
+def test_attention_running_max_moves_mid_sequence(nk, split):
+    """Scores that keep growing along the keys (and one spike on an odd tile) move the running max by
+    more than the lazy-rescale threshold on many tiles: the tile loop leaves, rescales O and l, and
+    resumes on even and odd tiles alike."""
+    rng = np.random.default_rng(nk + split)
+    hq, hkv, nq = 2, 1, 96
+    q = rng.standard_normal((1, nq, hq * 128)).astype(np.float32)
+    kv = rng.standard_normal((1, nk, 2 * hkv * 128)).astype(np.float32) * 0.3
+    ramp = np.linspace(0.2, 20.0, nk).astype(np.float32)
+    kv[0, :, :128] *= ramp[:, None]
+    kv[0, 64 * 5 + 17, :128] = 4.0 * q[0, :, :128].mean(axis=0)  # spike in tile 5
+    scale = 1.0 / np.sqrt(128.0)
+    got = _capi().kernel_attention(q, kv, hq, hkv, window=0, kmask=None, scale=scale, split=split)
+    if split:
+        ref = _attn_ref(q, kv, hq, hkv, 0, None, scale, rnd=lambda x: np.asarray(x, np.float32))
+        assert np.all(np.abs(got - ref) <= 2.0 ** -8 * np.abs(ref) + 1e-5)
+    else:
+        ref = _attn_ref(q, kv, hq, hkv, 0, None, scale)
+        assert np.all(np.abs(got - ref) <= 2.0 ** -8 * np.abs(ref) + 2e-3)
+
+
 @pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("M,N,K", [(1, 256, 64), (300, 512, 128), (1000, 768, 2048), (513, 256, 6144)])
 def test_gemm_all_variants(variant, M, N, K):

@@ -19,8 +19,11 @@ CASES = [  # name, B, hq, hkv, nq, nk, window, masked
 
 
 def main():
+    only = os.environ.get("ATTN_CASE")  # e.g. "self_full 240s" (split mode only) for a PMC pass
     for name, B, hq, hkv, nq, nk, win, masked in CASES:
-        for split in (True, False):
+        if only and name != only:
+            continue
+        for split in ((True,) if only else (True, False)):
             ms = capi.bench_attention(B, hq, hkv, nq, nk, win, split=split, masked=masked, iters=10)
             nk_eff = min(nk, 2 * win + 1) if win else nk
             flop = 4.0 * B * nq * nk_eff * 128 * hq
