@@ -220,7 +220,6 @@ __device__ __forceinline__ int vperm(int k) {
 // grid: (n_pad/64 token tiles, nq + nk + nv head slots, B).  Slot < nq: one q head; < nq+nk: one k
 // head; else the V^T transpose of one kv head.  One workgroup = 64 tokens of one head.
 __global__ void __launch_bounds__(256) attn_prep_kernel(PrepArgs a) {
-    __shared__ float vs[64][129];
     const int b = blockIdx.z;
     const int n0 = blockIdx.x * 64;
     const int lane = threadIdx.x & 63;
@@ -293,37 +292,36 @@ __global__ void __launch_bounds__(256) attn_prep_kernel(PrepArgs a) {
         return;
     }
     if (a.v_col < 0) return;
+    // V^T without an LDS round trip: lane = one d, a wave = 64 consecutive d (each token's row is
+    // one coalesced 256-B load), 16 tokens per group -> two 16-B f16 stores per plane, in the
+    // attention kernel's permuted key order
     const int hk = slot - nq - nk;
-    for (int i = threadIdx.x; i < 64 * 32; i += 256) {
-        const int tok = i >> 5;
-        const int d4 = (i & 31) * 4;
-        const int n = n0 + tok;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (n < a.n_tok) v = *(const float4*)(a.src + ((int64_t)b * a.n_tok + n) * a.ld + a.v_col + hk * 128 + d4);
-        vs[tok][d4 + 0] = v.x;
-        vs[tok][d4 + 1] = v.y;
-        vs[tok][d4 + 2] = v.z;
-        vs[tok][d4 + 3] = v.w;
-    }
-    __syncthreads();
-    const int d = threadIdx.x >> 1;
-    const int half = threadIdx.x & 1;
-    uint16_t* dst = a.vt + (((int64_t)b * a.hkv + hk) * 128 + d) * a.n_pad + n0 + half * 32;
+    const int d = (wid & 1) * 64 + lane;
+    const float* vsrc = a.src + (int64_t)b * a.n_tok * a.ld + a.v_col + hk * 128 + d;
+    uint16_t* vdst = a.vt + (((int64_t)b * a.hkv + hk) * 128 + d) * a.n_pad;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        uint32_t wv[4], wl[4];
+    for (int grp = 0; grp < 2; ++grp) {
+        const int g0 = n0 + (wid >> 1) * 32 + grp * 16;
+        float v[16];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int p0 = half * 32 + c * 8 + 2 * j;
-            const float v0 = vs[vperm(p0)][d];
-            const float v1 = vs[vperm(p0 + 1)][d];
-            const uint16_t h0 = f32_to_f16(v0), h1 = f32_to_f16(v1);
-            wv[j] = (uint32_t)h0 | ((uint32_t)h1 << 16);
-            wl[j] = (uint32_t)f32_to_f16(v0 - (float)__builtin_bit_cast(_Float16, h0)) |
-                    ((uint32_t)f32_to_f16(v1 - (float)__builtin_bit_cast(_Float16, h1)) << 16);
+        for (int k = 0; k < 16; ++k) {
+            const int n = g0 + vperm(k);
+            v[k] = n < a.n_tok ? vsrc[(int64_t)n * a.ld] : 0.f;
         }
-        *(uint4*)(dst + c * 8) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
-        if (a.v_plane > 0) *(uint4*)(dst + a.v_plane + c * 8) = make_uint4(wl[0], wl[1], wl[2], wl[3]);
+        uint32_t wv[8], wl[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const uint16_t h0 = f32_to_f16(v[2 * j]), h1 = f32_to_f16(v[2 * j + 1]);
+            wv[j] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+            wl[j] = (uint32_t)f32_to_f16(v[2 * j] - (float)__builtin_bit_cast(_Float16, h0)) |
+                    ((uint32_t)f32_to_f16(v[2 * j + 1] - (float)__builtin_bit_cast(_Float16, h1)) << 16);
+        }
+        *(uint4*)(vdst + g0) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+        *(uint4*)(vdst + g0 + 8) = make_uint4(wv[4], wv[5], wv[6], wv[7]);
+        if (a.v_plane > 0) {
+            *(uint4*)(vdst + a.v_plane + g0) = make_uint4(wl[0], wl[1], wl[2], wl[3]);
+            *(uint4*)(vdst + a.v_plane + g0 + 8) = make_uint4(wl[4], wl[5], wl[6], wl[7]);
+        }
     }
 }
 
