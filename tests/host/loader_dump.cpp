@@ -40,7 +40,7 @@ namespace acemi {  // kernels are not linked: the engines are never run here
 void launch_conv_gemm(const ConvGemmArgs&, hipStream_t) {}
 void launch_to_f16(const float*, int64_t, uint16_t*, hipStream_t) {}
 void launch_pack_f16(const float*, int64_t, int, int, uint16_t*, hipStream_t) {}
-void launch_conv_out(const uint16_t*, int, int, const uint16_t*, int, float*, hipStream_t) {}
+void launch_conv_out(const uint16_t*, int, int, const uint16_t*, int, float*, hipStream_t, int) {}
 }  // namespace acemi
 
 namespace {
