@@ -192,6 +192,30 @@ def test_full_width_two_layers_240s(monkeypatch):
 
 
 @pytest.mark.slow
+def test_full_width_two_layers_600s(monkeypatch):
+    """The largest BASELINE config's sequence (C5: 600 s, T = 15000 frames, N = 7500 tokens, L = 512)
+    at full width, first 2 layers (one sliding, one full), vs the oracle: 118 key tiles per
+    block, so the full layer runs the two-way key split with the merge kernel."""
+    from acestep_mi355x.capi import GGMLCAPIBridge
+    from acestep_mi355x.synthetic import cached_checkpoint, make_config
+    from oracle.dit_oracle import DitWeights, forward_with_floor
+    cfg = make_config(num_hidden_layers=2)
+    d = cached_checkpoint(cfg, seed=0, backend="torch")
+    monkeypatch.setenv("ACE_GGML_DIT_MAX_LAYERS", "2")
+    br = GGMLCAPIBridge()
+    br.load_dit(d)
+    rng = np.random.default_rng(600)
+    T, L = 15000, 512
+    h = rng.standard_normal((T, 64)).astype(np.float32)
+    c = np.concatenate([rng.standard_normal((T, 64)), np.ones((T, 64))], axis=1).astype(np.float32)
+    e = rng.standard_normal((L, 2048)).astype(np.float32)
+    got = br.dit_forward_tfirst(h, c, e, None, None, 0.5, 0.5)
+    br.close()
+    ref, floor = forward_with_floor(DitWeights(d), h, c, e, None, None, T, L, 0.5, 0.5, max_layers=2)
+    check(got, ref, floor, "full-width 2-layer 600s")
+
+
+@pytest.mark.slow
 def test_full_model_24_layers_20s():
     """The complete 24-layer DiT (synthetic weights, real shapes) at 20 s of audio
     (T = 500 frames, N = 250 tokens, L = 256) vs the oracle: the error budget over full depth."""
