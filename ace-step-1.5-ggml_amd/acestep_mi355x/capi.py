@@ -515,8 +515,9 @@ class GGMLCAPIBridge:
 
 # ---- kernel self-test wrappers (GPU parity tests) ----------------------------
 def kernel_gemm(a_bits: np.ndarray, w_bits: np.ndarray, act_type: int = 0, epi: int = 0,
-                bias: Optional[np.ndarray] = None) -> np.ndarray:
-    """a_bits [M][K], w_bits [N][K] uint16 words; epi 0 -> f32 [M][N], epi 4 -> uint16 [M][N/2]."""
+                bias: Optional[np.ndarray] = None, x: Optional[np.ndarray] = None) -> np.ndarray:
+    """a_bits [M][K], w_bits [N][K] uint16 words; epi 0 -> f32 [M][N], epi 4 -> uint16 [M][N/2];
+    epi 3 / 2 -> f32 x + C (* gate) with x [M][N] f32 and, for epi 2, the gate [N] passed as `bias`."""
     lib = load_library()
     a = np.ascontiguousarray(a_bits, dtype=np.uint16)
     w = np.ascontiguousarray(w_bits, dtype=np.uint16)
@@ -524,7 +525,11 @@ def kernel_gemm(a_bits: np.ndarray, w_bits: np.ndarray, act_type: int = 0, epi: 
     N = w.shape[0]
     u16p = ctypes.POINTER(ctypes.c_uint16)
     b = None if bias is None else np.ascontiguousarray(bias, dtype=np.float32)
-    if epi == 0:
+    if epi in (2, 3):
+        out = np.array(x, dtype=np.float32, order="C", copy=True)
+        st = lib.ace_mi_kernel_gemm(act_type, epi, M, N, K, a.ctypes.data_as(u16p), w.ctypes.data_as(u16p),
+                                    _fptr(b), _fptr(out), None)
+    elif epi == 0:
         out = np.empty((M, N), dtype=np.float32)
         st = lib.ace_mi_kernel_gemm(act_type, epi, M, N, K, a.ctypes.data_as(u16p), w.ctypes.data_as(u16p),
                                     _fptr(b), _fptr(out), None)

@@ -133,45 +133,56 @@ __device__ __forceinline__ void block_tile(const GemmParams& p, int& m0, int& n0
 
 // Fused epilogue of one wave's TM x TN grid of 16x16 accumulators at (mw, nw).
 // C/D map of 16x16x32: col = lane & 15, row = (lane >> 4) * 4 + r.
-template <int TM, int TN, bool F16, int EPI>
+template <int TM, int TN, bool F16, int EPI, int NW>
 __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[TM][TN], int mw, int nw, int lane) {
     const GemmEpilogue& e = p.e;
     const int M = p.M;
     const int ccol = lane & 15;
     const int crow = (lane >> 4) * 4;
     if constexpr (EPI == EPI_RESID_GATED || EPI == EPI_RESID) {
-        // Residual read-modify-write: every old x (and gate) value is loaded before the first store.
-        // Interleaved, the compiler cannot move a load of x above an earlier store to x (same pointer),
-        // so each element paid a full memory round trip in sequence.
-        float xo[TM][4][TN], gt[TM][4][TN];
+        // Residual read-modify-write: the old x (and gate) values of a chunk of GI 16-row groups are all
+        // loaded before the chunk's first store.  Interleaved, the compiler cannot move a load of x above
+        // an earlier store to x (same pointer), so each element paid a full memory round trip in
+        // sequence.  A whole-tile preload fits the 512-register budget of the 4-wave tiles; the 8-wave
+        // tiles (256 registers, accumulators included) preload 64 values per chunk instead of spilling.
+        constexpr int PER_I = 4 * TN * (EPI == EPI_RESID_GATED ? 2 : 1);
+        constexpr int GI0 = (NW >= 8 ? 64 : 1024) / PER_I;
+        constexpr int GI = GI0 < 1 ? 1 : (GI0 > TM ? TM : GI0);
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+        for (int i0 = 0; i0 < TM; i0 += GI) {
+            float xo[GI][4][TN], gt[GI][4][TN];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int m = mw + i * 16 + crow + r;
-                const bool ok = m < M;
-                const int item = EPI == EPI_RESID_GATED ? m / e.rows_per_item : 0;
+            for (int ii = 0; ii < GI; ++ii)
 #pragma unroll
-                for (int j = 0; j < TN; ++j) {
-                    const int n = nw + j * 16 + ccol;
-                    xo[i][r][j] = ok ? e.c_f32[(int64_t)m * e.ldc + n] : 0.f;
-                    if constexpr (EPI == EPI_RESID_GATED) gt[i][r][j] = ok ? e.gate[(int64_t)item * e.gate_stride + n] : 0.f;
+                for (int r = 0; r < 4; ++r) {
+                    const int m = mw + (i0 + ii) * 16 + crow + r;
+                    const bool ok = i0 + ii < TM && m < M;
+                    const int item = EPI == EPI_RESID_GATED ? m / e.rows_per_item : 0;
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) {
+                        const int n = nw + j * 16 + ccol;
+                        xo[ii][r][j] = ok ? e.c_f32[(int64_t)m * e.ldc + n] : 0.f;
+                        if constexpr (EPI == EPI_RESID_GATED)
+                            gt[ii][r][j] = ok ? e.gate[(int64_t)item * e.gate_stride + n] : 0.f;
+                    }
+                }
+#pragma unroll
+            for (int ii = 0; ii < GI; ++ii) {
+                if (i0 + ii >= TM) break;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int m = mw + (i0 + ii) * 16 + crow + r;
+                    if (m >= M) continue;
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) {
+                        const int n = nw + j * 16 + ccol;
+                        float v = acc[i0 + ii][j][r];
+                        if constexpr (EPI == EPI_RESID_GATED) v = __fmul_rn(v, gt[ii][r][j]);
+                        e.c_f32[(int64_t)m * e.ldc + n] = __fadd_rn(xo[ii][r][j], v);
+                    }
                 }
             }
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int m = mw + i * 16 + crow + r;
-                if (m >= M) continue;
-#pragma unroll
-                for (int j = 0; j < TN; ++j) {
-                    const int n = nw + j * 16 + ccol;
-                    float v = acc[i][j][r];
-                    if constexpr (EPI == EPI_RESID_GATED) v = __fmul_rn(v, gt[i][r][j]);
-                    e.c_f32[(int64_t)m * e.ldc + n] = __fadd_rn(xo[i][r][j], v);
-                }
-            }
+        }
         return;
     }
     float bias_j[TN];  // a thread's columns are fixed: their bias is loaded once, before any store
@@ -388,7 +399,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(GemmParams p) {
         }
     }
 
-    gemm_epilogue<TM, TN, F16, EPI>(p, acc, m0 + wm0, n0 + wn0, lane);
+    gemm_epilogue<TM, TN, F16, EPI, NW>(p, acc, m0 + wm0, n0 + wn0, lane);
 }
 
 
@@ -634,7 +645,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_q_kernel(GemmParams p) {
     }
     wait_vmcnt<0>();
 
-    gemm_epilogue<TM, TN, false, EPI>(p, acc, m0 + wm0, n0 + wn0, lane);
+    gemm_epilogue<TM, TN, false, EPI, NW>(p, acc, m0 + wm0, n0 + wn0, lane);
 }
 
 template <int BM, int BN, int WM, int WN, bool F16, int EPI, int PIPE>

@@ -29,8 +29,11 @@ ace_ggml_status ace_mi_kernel_gemm(int32_t act_type, int32_t epi, int32_t M, int
                                    const uint16_t* W, const float* bias, float* out_f32, uint16_t* out_u16) {
     using namespace acemi;
     if (!A || !W || M <= 0 || N % 128 != 0 || K % 64 != 0) return ACE_GGML_ERR_INVALID_ARG;
-    if (epi != EPI_STORE_F32 && epi != EPI_SWIGLU) return ACE_GGML_ERR_UNSUPPORTED;
-    if ((epi == EPI_STORE_F32 && !out_f32) || (epi == EPI_SWIGLU && !out_u16)) return ACE_GGML_ERR_INVALID_ARG;
+    const bool resid = epi == EPI_RESID || epi == EPI_RESID_GATED;
+    if (epi != EPI_STORE_F32 && epi != EPI_SWIGLU && !resid) return ACE_GGML_ERR_UNSUPPORTED;
+    if (((epi == EPI_STORE_F32 || resid) && !out_f32) || (epi == EPI_SWIGLU && !out_u16))
+        return ACE_GGML_ERR_INVALID_ARG;
+    if (epi == EPI_RESID_GATED && !bias) return ACE_GGML_ERR_INVALID_ARG;
     try {
         DevMem dA((size_t)M * K * 2), dW((size_t)N * K * 2), dB((size_t)N * 4), dC((size_t)M * N * 4);
         ACEMI_HIP(hipMemcpy(dA.p, A, (size_t)M * K * 2, hipMemcpyHostToDevice));
@@ -38,8 +41,15 @@ ace_ggml_status ace_mi_kernel_gemm(int32_t act_type, int32_t epi, int32_t M, int
         if (bias) ACEMI_HIP(hipMemcpy(dB.p, bias, (size_t)N * 4, hipMemcpyHostToDevice));
         GemmEpilogue e;
         e.kind = epi;
-        e.bias = bias ? dB.as<float>() : nullptr;
-        if (epi == EPI_STORE_F32) {
+        e.bias = bias && !resid ? dB.as<float>() : nullptr;
+        if (resid) {  // out_f32 holds x on entry: x += acc (* gate[n], the gate passed as `bias`)
+            ACEMI_HIP(hipMemcpy(dC.p, out_f32, (size_t)M * N * 4, hipMemcpyHostToDevice));
+            e.c_f32 = dC.as<float>();
+            e.ldc = N;
+            e.gate = epi == EPI_RESID_GATED ? dB.as<float>() : nullptr;
+            e.gate_stride = 0;
+            e.rows_per_item = M;
+        } else if (epi == EPI_STORE_F32) {
             e.c_f32 = dC.as<float>();
             e.ldc = N;
         } else {
@@ -49,7 +59,7 @@ ace_ggml_status ace_mi_kernel_gemm(int32_t act_type, int32_t epi, int32_t M, int
         launch_gemm(act_type == 1 ? ActType::F16 : ActType::BF16, dA.as<uint16_t>(), K, dW.as<uint16_t>(), K, M, N,
                     K, e, nullptr);
         ACEMI_HIP(hipDeviceSynchronize());
-        if (epi == EPI_STORE_F32)
+        if (epi == EPI_STORE_F32 || resid)
             ACEMI_HIP(hipMemcpy(out_f32, dC.p, (size_t)M * N * 4, hipMemcpyDeviceToHost));
         else
             ACEMI_HIP(hipMemcpy(out_u16, dC.p, (size_t)M * (N / 2) * 2, hipMemcpyDeviceToHost));

@@ -94,7 +94,9 @@ ACE_GGML_API ace_ggml_status ace_mi_synchronize(ace_ggml_context* ctx);
 /* ---- kernel self-test entries (blocking, host buffers; used by the -m gpu parity tests) ----
  * GEMM: C = A[M][K] . W[N][K]^T with A, W raw 16-bit words of act_type (0 bf16, 1 fp16).
  * epi 0: out_f32[M][N] = C (+ bias[N] if bias != NULL);
- * epi 4: SwiGLU on 16-column interleaved gate|up weights, out_u16[M][N/2] raw act words. */
+ * epi 4: SwiGLU on 16-column interleaved gate|up weights, out_u16[M][N/2] raw act words;
+ * epi 3 / 2: residual update in place, out_f32[M][N] holds x on entry: x += C (epi 3) or
+ * x += C * gate[N] (epi 2, the gate passed in `bias`). */
 ACE_GGML_API ace_ggml_status ace_mi_kernel_gemm(int32_t act_type, int32_t epi, int32_t M, int32_t N, int32_t K,
                                                 const uint16_t* A, const uint16_t* W, const float* bias,
                                                 float* out_f32, uint16_t* out_u16);

@@ -212,6 +212,33 @@ def test_gemm_all_variants(variant, M, N, K):
     np.testing.assert_allclose(_vals(got_sw, 0), sw, rtol=2.0 ** -8, atol=1e-4)
 
 
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("epi", [2, 3])
+@pytest.mark.parametrize("M,N,K", [(300, 512, 128), (1000, 768, 2048), (9001, 512, 256)])
+def test_gemm_residual_epilogues(variant, epi, M, N, K):
+    """x += A.W^T (* gate[n]) in place (the o / cross-o / down projections), every tile incl. the 8-wave
+    ones whose epilogue preloads x in chunks of 16-row groups, with M edges."""
+    capi = _capi()
+    if N % 256 and variant in (2, 5):
+        pytest.skip("256-wide tiles need N % 256 == 0")
+    rng = np.random.default_rng(variant * 13 + epi + M)
+    a = _bits(rng.standard_normal((M, K)).astype(np.float32), 0)
+    w = _bits((rng.standard_normal((N, K)) * 0.05).astype(np.float32), 0)
+    x = rng.standard_normal((M, N)).astype(np.float32)
+    gate = rng.standard_normal(N).astype(np.float32) if epi == 2 else None
+    capi.gemm_variant(variant)
+    try:
+        got = capi.kernel_gemm(a, w, act_type=0, epi=epi, bias=gate, x=x)
+    finally:
+        capi.gemm_variant(-1)
+    av, wv = _vals(a, 0).astype(np.float64), _vals(w, 0).astype(np.float64)
+    acc = av @ wv.T
+    scale = np.abs(av) @ np.abs(wv).T
+    g = gate.astype(np.float64) if epi == 2 else np.ones(N)
+    ref = x.astype(np.float64) + acc * g
+    assert np.all(np.abs(got - ref) <= (2e-6 * scale + 1e-6) * np.abs(g) + 2e-7 * np.abs(ref))
+
+
 def test_attention_key_split_with_one_part_fully_masked():
     """Key split: the first part sees only masked keys (m = -inf, l = 0) and must get weight 0."""
     rng = np.random.default_rng(77)
