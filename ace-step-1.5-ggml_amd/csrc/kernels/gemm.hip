@@ -658,7 +658,8 @@ void launch_cfg(const GemmParams& p, hipStream_t s) {
 }
 
 // variant: 0 = 128x128 PIPE0, 1 = 128x128 PIPE1, 2 = 256x256 PIPE1 (8 waves 2x4), 3 = 256x128 PIPE1,
-// 4 = 192x128 PIPE1, 5 = 192x256 PIPE1 (8 waves 2x4), 6 = 192x64 PIPE1 (dense only), 7 = 96x128 PIPE1
+// 4 = 192x128 PIPE1, 5 = 192x256 PIPE1 (8 waves 2x4), 6 = 192x64 PIPE1 (dense only), 7 = 96x128 PIPE1,
+// 8 = 64x128 PIPE1, 9 = 64x64 PIPE1 (8, 9 dense only: short sequences)
 template <bool F16, int EPI>
 void launch_variant(int variant, const GemmParams& p, hipStream_t s) {
     switch (variant) {
@@ -670,6 +671,8 @@ void launch_variant(int variant, const GemmParams& p, hipStream_t s) {
         case 5: launch_cfg<192, 256, 2, 4, F16, EPI, 1>(p, s); break;
         case 6: launch_cfg<192, 64, 2, 2, F16, EPI, 1>(p, s); break;
         case 7: launch_cfg<96, 128, 2, 2, F16, EPI, 1>(p, s); break;
+        case 8: launch_cfg<64, 128, 2, 2, F16, EPI, 1>(p, s); break;
+        case 9: launch_cfg<64, 64, 2, 2, F16, EPI, 1>(p, s); break;
         default: throw std::runtime_error("gemm: bad variant");
     }
 }
@@ -747,6 +750,11 @@ int pick_variant(int M, int N, bool quant) {
     }
     if (N % 256 == 0 && M >= 8192) return 2;
     if (edge_ok && mb192 * (N / 128) >= 384) return 4;
+    // short sequences (60 s: M = 750): too few 96-row tiles to cover the CUs -> 64-row tiles, and
+    // 64x64 when even those leave CUs idle (M = 750: N = 2048 projections 273-337 -> 364-453 TFLOP/s,
+    // qkv 519 -> 567, tools/gemm_small_m.py)
+    const int64_t mb96 = (M + 95) / 96, mb64 = (M + 63) / 64;
+    if (mb96 * (N / 128) <= 256) return mb64 * (N / 128) >= 256 ? 8 : 9;
     if (m_edge(M, 96) >= m_edge(M, 128) - 0.02) return 7;  // N = 2048: 512 tiles, two per CU
     return 1;
 }

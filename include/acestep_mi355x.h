@@ -116,7 +116,7 @@ ACE_GGML_API ace_ggml_status ace_mi_bench_attention(int32_t B, int32_t Hq, int32
 
 /* GEMM micro-benchmark on random device operands: average ms per launch (HIP events) of the
  * engine's GEMM for act_type (0 bf16, 1 fp16), epilogue `epi` (0 f32 store, 2 gated residual,
- * 4 SwiGLU), kernel `variant` (-1 automatic, 0..7 forced: 128x128 two pipelines, 256x256, 256x128, 192x128, 192x256, 192x64, 96x128). */
+ * 4 SwiGLU), kernel `variant` (-1 automatic, 0..9 forced: 128x128 two pipelines, 256x256, 256x128, 192x128, 192x256, 192x64, 96x128, 64x128, 64x64). */
 ACE_GGML_API ace_ggml_status ace_mi_bench_gemm(int32_t act_type, int32_t epi, int32_t variant, int32_t M, int32_t N,
                                                int32_t K, int32_t iters, float* avg_ms);
 /* Force the GEMM kernel variant of all later launches in this process (-1 = automatic). */
@@ -141,7 +141,7 @@ ACE_GGML_API int64_t ace_mi_quantize(int32_t qtype, const float* src, int64_t ro
 ACE_GGML_API ace_ggml_status ace_mi_dequantize(int32_t qtype, const uint8_t* src, int64_t rows, int64_t cols,
                                                float* dst);
 /* Dequant-fused GEMM on ggml block rows W [N][K]: out = A . bf16(dequant(W))^T (+ bias), A bf16 [M][K];
- * epi 0 (f32 store) or 4 (SwiGLU, bf16 out [M][N/2]); variant -1 automatic, 0..7 forced (6 dense only). */
+ * epi 0 (f32 store) or 4 (SwiGLU, bf16 out [M][N/2]); variant -1 automatic, 0..7 forced (6 dense only; 8, 9 are dense-only tiles). */
 ACE_GGML_API ace_ggml_status ace_mi_kernel_gemm_q(int32_t qtype, int32_t epi, int32_t variant, int32_t M, int32_t N,
                                                   int32_t K, const uint16_t* A, const uint8_t* W_blocks,
                                                   const float* bias, float* out_f32, uint16_t* out_u16);
