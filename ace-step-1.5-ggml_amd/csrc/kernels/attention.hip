@@ -486,28 +486,29 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
 // Combine the key-range parts of one (item, query, head) row per wave: M = max m_k, weights
 // 2^(m_k - M) (0 for a part whose keys were all masked), out = sum w_k O_k / sum w_k l_k; a row with
 // no unmasked key at all stays 0/0 = NaN as in ggml.
+// Two key-split parts per row (the only split launch_attention makes): half a wave per row, 16-byte
+// partial reads, every load issued before the first use.
 template <bool F16OUT>
 __global__ void __launch_bounds__(256) attn_merge_kernel(AttnArgs a) {
     const int64_t rows = (int64_t)a.B * a.nq * a.Hq;
-    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t r = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
     if (r >= rows) return;
-    const int lane = threadIdx.x & 63;
-    const float* ml = a.part + (int64_t)a.ksplit * rows * D;
-    float M = -INFINITY;
-    for (int k = 0; k < a.ksplit; ++k) M = fmaxf(M, ml[(k * rows + r) * 2]);
-    float o0 = 0.f, o1 = 0.f, l = 0.f;
-    for (int k = 0; k < a.ksplit; ++k) {
-        const float mk = ml[(k * rows + r) * 2];
-        const float w = mk == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(mk - M);
-        const float2 ov = *(const float2*)(a.part + (k * rows + r) * D + 2 * lane);
-        o0 += w * ov.x;
-        o1 += w * ov.y;
-        l += w * ml[(k * rows + r) * 2 + 1];
-    }
-    const float inv = 1.0f / l;
+    const int d = (threadIdx.x & 31) * 4;
+    const float* ml = a.part + 2 * rows * D;
+    const float2 ml0 = *(const float2*)(ml + r * 2);
+    const float2 ml1 = *(const float2*)(ml + (rows + r) * 2);
+    const float4 o0 = *(const float4*)(a.part + r * D + d);
+    const float4 o1 = *(const float4*)(a.part + (rows + r) * D + d);
+    const float M = fmaxf(ml0.x, ml1.x);
+    const float w0 = ml0.x == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(ml0.x - M);
+    const float w1 = ml1.x == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(ml1.x - M);
+    const float inv = 1.0f / (w0 * ml0.y + w1 * ml1.y);
+    const float v[4] = {(w0 * o0.x + w1 * o1.x) * inv, (w0 * o0.y + w1 * o1.y) * inv,
+                        (w0 * o0.z + w1 * o1.z) * inv, (w0 * o0.w + w1 * o1.w) * inv};
     // row r = (b * nq + q) * Hq + head: out[b][q][head*128 + d] is contiguous in r * 128 + d
-    *(uint32_t*)(a.out + r * D + 2 * lane) =
-        (uint32_t)to_act<F16OUT>(o0 * inv) | ((uint32_t)to_act<F16OUT>(o1 * inv) << 16);
+    *(uint2*)(a.out + r * D + d) =
+        make_uint2((uint32_t)to_act<F16OUT>(v[0]) | ((uint32_t)to_act<F16OUT>(v[1]) << 16),
+                   (uint32_t)to_act<F16OUT>(v[2]) | ((uint32_t)to_act<F16OUT>(v[3]) << 16));
 }
 
 template <bool F16OUT, bool SPLIT>
@@ -562,7 +563,8 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s) {
     ACEMI_HIP(hipGetLastError());
     if (b.ksplit > 1) {
         const int64_t rows = (int64_t)a.B * a.nq * a.Hq;
-        const dim3 mgrid((unsigned)((rows + 3) / 4));
+        ACEMI_CHECK(b.ksplit == 2, "attention: the merge handles two key-split parts");
+        const dim3 mgrid((unsigned)((rows + 7) / 8));
         if (out_t == ActType::F16)
             hipLaunchKernelGGL(attn_merge_kernel<true>, mgrid, dim3(256), 0, s, b);
         else
