@@ -144,18 +144,36 @@ class _OrderedCall:
     def __init__(self, bridge, dev):
         import torch
         self.bridge = bridge
-        self.torch_stream = torch.cuda.current_stream(dev)
-        self.stream = self.torch_stream.cuda_stream
+        # host tensors (the host-emulated library of the CPU tests) are ordered by program order
+        self.torch_stream = torch.cuda.current_stream(dev) if torch.device(dev).type == "cuda" else None
+        self.stream = self.torch_stream.cuda_stream if self.torch_stream is not None else 0
 
     def __enter__(self):
-        if self.stream == 0:
+        if self.torch_stream is not None and self.stream == 0:
             self.torch_stream.synchronize()
         return self.stream
 
     def __exit__(self, *exc):
-        if self.stream == 0:
+        if self.torch_stream is not None and self.stream == 0:
             self.bridge.synchronize()
         return False
+
+
+def _trim(bridge, n: int, cs: int, ce: int, ws: int, we: int):
+    """(samples of a window of n frames, leading trim, trailing trim) of the reference tiled decode."""
+    total = bridge.vae_out_len(n)
+    up = float(total) / float(max(1, n))
+    return total, int(round((cs - ws) * up)), int(round((we - ce) * up))
+
+
+def tiled_out_len(bridge, T: int, chunk_size: int, overlap: int) -> int:
+    """Samples per item that vae_decode_torch returns for T latent frames (no decode)."""
+    plan = [(0, T, 0, T)] if T <= chunk_size else _tile_plan(T, chunk_size, overlap)
+    n = 0
+    for cs, ce, ws, we in plan:
+        total, ts, te = _trim(bridge, we - ws, cs, ce, ws, we)
+        n += (total - te if te > 0 else total) - ts
+    return n
 
 
 def vae_decode_torch(bridge, latents_bct, chunk_size: int, overlap: int):
@@ -173,12 +191,10 @@ def vae_decode_torch(bridge, latents_bct, chunk_size: int, overlap: int):
         for cs, ce, ws, we in plan:
             win = lat[b, :, ws:we].transpose(0, 1).contiguous()        # [frames, C]
             n = we - ws
-            wav = torch.empty((bridge.vae_out_len(n), bridge.audio_channels), dtype=torch.float32, device=dev)
+            total, ts, te = _trim(bridge, n, cs, ce, ws, we)
+            wav = torch.empty((total, bridge.audio_channels), dtype=torch.float32, device=dev)
             with _OrderedCall(bridge, dev) as stream:
                 bridge.vae_decode_device(win.data_ptr(), n, wav.data_ptr(), stream)
-            up = float(wav.shape[0]) / float(max(1, n))
-            ts = int(round((cs - ws) * up))
-            te = int(round((we - ce) * up))
             parts.append(wav[ts:wav.shape[0] - te if te > 0 else wav.shape[0]])
         outs.append(torch.cat(parts, dim=0).transpose(0, 1))            # [channels, samples]
     return torch.stack(outs, dim=0)

@@ -70,7 +70,9 @@ def broadcast_conditioning(cond: Optional[Conditioning], shapes: dict, device, s
 
 
 def gather_latents(x_local: torch.Tensor, global_batch: int, dst: int = 0) -> Optional[torch.Tensor]:
-    """Collect every rank's [b_local][T][C] shard into [B][T][C] (item order restored) on `dst`."""
+    """Collect every rank's [b_local][...] shard into [B][...] (item order restored) on `dst`: final
+    latents [b][T][C], or decoded audio [b][channels][samples] (every item of one request has the same
+    shape).  One `gather` of ceil(B/W) items per rank."""
     rank, world = dist_info()
     if world == 1:
         return x_local
@@ -115,15 +117,31 @@ def euler_sample_local(bridge, cond: Conditioning, items: Sequence[int], schedul
     return xt
 
 
+def sde_noise(n_draws: int, global_batch: int, T: int, C: int, seed: Optional[int], device) -> torch.Tensor:
+    """SDE re-noise draws [n_draws][B_global][T][C] for the WHOLE batch from one generator, so every item
+    gets its own independent stream (as generate.py:187 draws one (bsz, T, C) normal per step) and a
+    rank selects its items' slices: the result does not depend on the world size.  Drawn on the CPU
+    (the same stream on every rank and backend) and moved to `device`.  seed None -> a fresh
+    nondeterministic seed (every rank must then be given an explicit seed to agree)."""
+    g = torch.Generator()
+    if seed is None:
+        g.seed()
+    else:
+        g.manual_seed(int(seed))
+    return torch.randn((n_draws, global_batch, T, C), generator=g, dtype=torch.float32).to(device)
+
+
 def generate_local(bridge, cond: Conditioning, items: Sequence[int], schedule: Sequence[float],
                    infer_method: str = "ode", seed: Optional[int] = None, cover_steps: int = -1,
                    cond_non_cover: Optional[Conditioning] = None, cache_cross: bool = True,
                    stream: int = 0) -> torch.Tensor:
     """The reference generation loop (acestep/mlx_dit/generate.py:143-199) for this rank's `items`
     through `ace_mi_dit_sample_ex`: ODE or SDE stepping, the audio-cover switch to non-cover
-    conditions at `cover_steps`, and the cross-attention cache.  SDE re-noise draws come from a
-    torch generator seeded with `seed` on the device (the MLX draws cannot be reproduced)."""
+    conditions from step `cover_steps` on, and the cross-attention cache.  SDE re-noise draws come
+    from `sde_noise` (one generator for the global batch; the MLX draws cannot be reproduced)."""
     dev = cond.noise.device
+    if len(items) == 0:  # more ranks than items: this rank idles (and still joins the gather)
+        return cond.noise[:0].clone()
     idx = torch.tensor(list(items), dtype=torch.long, device=dev)
     sel = lambda t: t.index_select(0, idx).contiguous() if t is not None else None
     xt = sel(cond.noise)
@@ -134,10 +152,7 @@ def generate_local(bridge, cond: Conditioning, items: Sequence[int], schedule: S
     L = enc.shape[1]
     noise = None
     if infer_method == "sde" and len(schedule) > 1:
-        g = torch.Generator(device=dev)
-        if seed is not None:
-            g.manual_seed(int(seed))
-        noise = torch.randn((len(schedule) - 1, B, T, C), generator=g, device=dev, dtype=torch.float32)
+        noise = sde_noise(len(schedule) - 1, cond.noise.shape[0], T, C, seed, dev).index_select(1, idx).contiguous()
     elif infer_method not in ("ode", "sde"):
         raise ValueError(infer_method)
     _sync(xt)
@@ -148,3 +163,27 @@ def generate_local(bridge, cond: Conditioning, items: Sequence[int], schedule: S
                                 stream=stream)
     bridge.synchronize()
     return xt
+
+
+def decode_local(bridge, x0_local: torch.Tensor, chunk_size: int = 32, overlap: int = 8) -> torch.Tensor:
+    """VAE-decode this rank's final latents x0 [b][T][C] -> audio [b][channels][samples] on its own GPU,
+    with the reference's windowed plan (run_non_ggml_real_case.py:550-659, chunk 32 / overlap 8
+    defaults :889-890) through ace_mi_vae_decode_device (the 600 s pipeline decodes on
+    every rank, then gathers audio)."""
+    from .hook import tiled_out_len, vae_decode_torch
+    if x0_local.shape[0] == 0:
+        return x0_local.new_empty((0, bridge.audio_channels, tiled_out_len(bridge, x0_local.shape[1], chunk_size, overlap)))
+    return vae_decode_torch(bridge, x0_local.transpose(1, 2), chunk_size, overlap)
+
+
+def generate_and_decode(bridge, cond: Conditioning, global_batch: int, schedule: Sequence[float],
+                        infer_method: str = "ode", seed: Optional[int] = None, chunk_size: int = 32,
+                        overlap: int = 8, dst: int = 0) -> Optional[torch.Tensor]:
+    """Full batch-sharded pipeline of BASELINE configs[4] on this rank: its items' DiT sampling loop, its
+    items' VAE decode, then the audio of every item gathered to `dst` in item order
+    ([B][channels][samples] there, None elsewhere).  No collective inside either loop."""
+    rank, world = dist_info()
+    items = shard_indices(global_batch, world, rank)
+    x0 = generate_local(bridge, cond, items, schedule, infer_method=infer_method, seed=seed)
+    audio = decode_local(bridge, x0, chunk_size, overlap)
+    return gather_latents(audio.contiguous(), global_batch, dst=dst)

@@ -256,11 +256,16 @@ ace_ggml_status run_sampler(ace_ggml_context* ctx, int32_t batch, float* d_xt, c
         io.enc_mask = d_enc_mask;
         io.out = ctx->d_v;
         io.max_layers = max_layers_env();
+        bool switched = false;
         for (int i = 0; i < n_steps; ++i) {
             bool fresh = (i == 0);
-            if (i == cover_steps && (d_enc_nc || d_context_nc)) {  // switch to the non-cover conditions
-                if (d_enc_nc) io.enc = d_enc_nc;
+            // generate.py:160: `step_idx >= cover_steps and enc_hs_nc is not None` -> non-cover
+            // conditions from that step on (a negative cover_steps switches at step 0, a value
+            // >= n_steps or a NULL d_enc_nc never switches); the context follows when given
+            if (!switched && d_enc_nc && i >= cover_steps) {
+                io.enc = d_enc_nc;
                 if (d_context_nc) io.context = d_context_nc;
+                switched = true;
                 fresh = true;
             }
             io.reuse_cross = cache_cross && !fresh;

@@ -43,6 +43,15 @@ struct StTensor {
         for (auto d : shape) n *= d;
         return n;
     }
+    // bytes per element of the dtypes the loaders read; 0 for any other dtype (left to the caller,
+    // which raises Unsupported for it)
+    size_t elem_size() const {
+        if (dtype == "F32" || dtype == "I32") return 4;
+        if (dtype == "BF16" || dtype == "F16" || dtype == "I16") return 2;
+        if (dtype == "I8" || dtype == "U8") return 1;
+        if (dtype == "F64" || dtype == "I64") return 8;
+        return 0;
+    }
 };
 
 struct StFile {
@@ -54,6 +63,9 @@ struct StFile {
         path = p;
         std::ifstream in(p, std::ios::binary);
         if (!in) throw IoError("failed to open " + p);
+        in.seekg(0, std::ios::end);
+        const uint64_t file_size = static_cast<uint64_t>(in.tellg());
+        in.seekg(0, std::ios::beg);
         uint64_t hlen = 0;
         unsigned char b8[8];
         if (!in.read(reinterpret_cast<char*>(b8), 8)) throw IoError("failed to read header size");
@@ -76,8 +88,19 @@ struct StFile {
             for (const auto& d : kv.second.at("shape").arr) t.shape.push_back(d.as_int());
             const auto& off = kv.second.at("data_offsets").arr;
             if (off.size() != 2) throw IoError("data_offsets invalid");
-            t.begin = static_cast<uint64_t>(off[0].as_int());
-            t.end = static_cast<uint64_t>(off[1].as_int());
+            const int64_t b = off[0].as_int(), e = off[1].as_int();
+            // the reference sizes every read from the shape and rejects a mismatch
+            // (safetensors.cpp TensorInfo::nbytes / read_tensor); reject it here, at open, so no
+            // later read or conversion can run past the tensor's bytes
+            if (b < 0 || e < b) throw IoError("invalid data_offsets for tensor: " + kv.first);
+            t.begin = static_cast<uint64_t>(b);
+            t.end = static_cast<uint64_t>(e);
+            if (data_offset + t.end > file_size) throw IoError("tensor data out of file bounds: " + kv.first);
+            for (auto d : t.shape)
+                if (d < 0) throw IoError("invalid shape for tensor: " + kv.first);
+            const size_t es = t.elem_size();
+            if (es != 0 && static_cast<uint64_t>(t.numel()) * es != t.end - t.begin)
+                throw IoError("tensor byte size mismatch: " + kv.first);
             tensors[kv.first] = t;
         }
     }

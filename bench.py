@@ -114,6 +114,7 @@ def main():
     xt = cond.noise.index_select(0, idx).contiguous()
     ctx = cond.context.index_select(0, idx).contiguous()
     enc = cond.enc.index_select(0, idx).contiguous()
+    torch.cuda.synchronize()  # the library runs on its own stream: inputs complete before the warmup reads them
     sched = shifted_linear_schedule(args.sample_steps, 3.0)
     stream = torch.cuda.current_stream().cuda_stream
 

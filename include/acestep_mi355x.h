@@ -63,8 +63,10 @@ ACE_GGML_API ace_ggml_status ace_mi_dit_sample(ace_ggml_context* ctx, int32_t ba
                                                const float* schedule, int32_t n_steps, void* stream);
 /* The Python/MLX generation loop (acestep/mlx_dit/generate.py:143-199) on the device: ODE (sde = 0)
  * or SDE (sde = 1: x0 = xt - v*t; xt = t_next*noise_i + (1 - t_next)*x0 with caller noise
- * d_noise [n_steps-1][batch][seq_len][audio]); from step `cover_steps` on, the non-cover conditions
- * d_context_nc / d_enc_nc (either may be NULL) replace d_context / d_enc; cache_cross = 1 reuses the
+ * d_noise [n_steps-1][batch][seq_len][audio]); when d_enc_nc is non-NULL, every step i >= cover_steps
+ * runs on the non-cover conditions (generate.py:160): d_enc_nc replaces d_enc and d_context_nc (if
+ * non-NULL) replaces d_context.  d_enc_nc = NULL or cover_steps >= n_steps: no switch; a negative
+ * cover_steps switches at step 0.  cache_cross = 1 reuses the
  * encoder-side tensors (condition embedder + every layer's cross K/V) between steps with the same
  * conditions, as MLXCrossAttentionCache (use_cache=True) does.  Last step: x0 = xt - v*t. */
 ACE_GGML_API ace_ggml_status ace_mi_dit_sample_ex(ace_ggml_context* ctx, int32_t batch, float* d_xt,

@@ -4,7 +4,7 @@
 // smaller than what a launch touches, a loader that reads past a tensor, or a bad offset in the ABI
 // staging shows up as a sanitizer report instead of a GPU memory fault.
 //
-// usage: asan_driver <dit_cond_dir> <vae_dir> <text_dir> <dit_gguf_dir>
+// usage: asan_driver <dit_cond_dir> <vae_dir> <text_dir> <dit_gguf_dir> [<malformed_dit_dir>...]
 #include <cstdio>
 #include <cstdlib>
 #include <random>
@@ -139,6 +139,14 @@ int main(int argc, char** argv) {
                                     out.size() * 4) == ACE_GGML_OK);
         unsetenv("ACE_GGML_DIT_WEIGHT_QTYPE");
         ace_ggml_destroy(c2);
+    }
+    // malformed safetensors headers (short data_offsets, end < begin, past the end of the file): the
+    // loader must refuse them with IO before any read runs past a tensor's bytes
+    for (int i = 5; i < argc; ++i) {
+        ace_ggml_context* c3 = nullptr;
+        EXPECT(ace_ggml_create(nullptr, &c3) == ACE_GGML_OK);
+        EXPECT(ace_ggml_load_dit(c3, argv[i]) == ACE_GGML_ERR_IO);
+        ace_ggml_destroy(c3);
     }
     std::printf("asan_driver: %d failures\n", failures);
     return failures == 0 ? 0 : 1;
