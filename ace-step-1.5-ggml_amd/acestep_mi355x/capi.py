@@ -544,8 +544,9 @@ def kernel_gemm(a_bits: np.ndarray, w_bits: np.ndarray, act_type: int = 0, epi: 
 
 def kernel_attention(q: np.ndarray, kv: np.ndarray, hq: int, hkv: int, window: int = 0,
                      kmask: Optional[np.ndarray] = None, scale: Optional[float] = None,
-                     split: bool = True, causal: bool = False) -> np.ndarray:
-    """q [B][nq][hq*128] f32, kv [B][nk][2*hkv*128] f32 -> out [B][nq][hq*128] f32 (bf16-rounded)."""
+                     split: bool = True, causal: bool = False, pv_split: bool = False) -> np.ndarray:
+    """q [B][nq][hq*128] f32, kv [B][nk][2*hkv*128] f32 -> out [B][nq][hq*128] f32 (bf16-rounded).
+    split: hi/lo fp16 Q.K; pv_split: hi/lo fp16 P.V too (both = the fully f32-faithful mode)."""
     lib = load_library()
     q = np.ascontiguousarray(q, dtype=np.float32)
     kv = np.ascontiguousarray(kv, dtype=np.float32)
@@ -554,8 +555,8 @@ def kernel_attention(q: np.ndarray, kv: np.ndarray, hq: int, hkv: int, window: i
     km = None if kmask is None else np.ascontiguousarray(kmask, dtype=np.int32)
     out = np.empty_like(q)
     sc = float(scale) if scale is not None else 1.0 / np.sqrt(128.0)
-    st = lib.ace_mi_kernel_attention(B, hq, hkv, nq, nk, int(window), sc, (1 if split else 0) | (2 if causal else 0),
-                                     _fptr(q), _fptr(kv),
+    st = lib.ace_mi_kernel_attention(B, hq, hkv, nq, nk, int(window), sc, (1 if split else 0) | (2 if causal else 0)
+                                     | (8 if pv_split else 0), _fptr(q), _fptr(kv),
                                      _iptr(km), _fptr(out))
     if st != ACE_GGML_OK:
         raise RuntimeError(f"ace_mi_kernel_attention failed (status={st})")
@@ -563,11 +564,11 @@ def kernel_attention(q: np.ndarray, kv: np.ndarray, hq: int, hkv: int, window: i
 
 
 def bench_attention(B: int, hq: int, hkv: int, nq: int, nk: int, window: int = 0, split: bool = True,
-                    causal: bool = False, masked: bool = False, iters: int = 20) -> float:
+                    causal: bool = False, masked: bool = False, iters: int = 20, pv_split: bool = False) -> float:
     """Average ms per launch of the engine's attention kernel on pseudo-random operands (GPU)."""
     lib = load_library()
     ms = ctypes.c_float(0.0)
-    flags = (1 if split else 0) | (2 if causal else 0) | (4 if masked else 0)
+    flags = (1 if split else 0) | (2 if causal else 0) | (4 if masked else 0) | (8 if pv_split else 0)
     st = lib.ace_mi_bench_attention(B, hq, hkv, nq, nk, int(window), flags, iters, ctypes.byref(ms))
     if st != ACE_GGML_OK:
         raise RuntimeError(f"ace_mi_bench_attention failed (status={st})")

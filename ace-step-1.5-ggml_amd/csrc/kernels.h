@@ -2,9 +2,31 @@
 // allocation, no synchronisation: safe to capture into a hipGraph).
 #pragma once
 
+#include <cstdlib>
+#include <stdexcept>
+#include <string>
+
 #include "common.h"
 
 namespace acemi {
+
+// Per-head RMSNorm (+ NEOX RoPE) of the q/k sections and f16 re-layout for attention.
+struct PrepArgs {
+    const float* src;
+    int ld;
+    int q_col, k_col, v_col;  // -1: section absent
+    int hq, hkv;
+    int n_tok, n_pad, B;
+    const float* q_norm;
+    const float* k_norm;
+    const float* rope_cos;  // [n_tok][64] or null
+    const float* rope_sin;
+    float eps;
+    uint16_t* qh;
+    uint16_t* kh;
+    uint16_t* vt;
+    int64_t q_plane = 0, k_plane = 0, v_plane = 0;  // >0: also write lo = f16(x - f16(x)) planes
+};
 
 // ---------------------------------------------------------------- GEMM
 // C[M][N] = A[M][K] . W[N][K]^T   (A, W: 16-bit act type, f32 accumulate)
@@ -16,6 +38,10 @@ enum GemmEpiKind : int {
     EPI_RESID = 3,          // c_f32[m*ldc+n] += acc
     EPI_SWIGLU = 4,         // columns interleaved [g0..15,u0..15,g16..]: c_act[m*ldc + n'] = act(silu(g)*u)
     EPI_PROJ_OUT = 5,       // c_f32[b][2p+k][c] = acc[m=(b,p)][n = c + k*out_ch] + bias[c], cropped to T
+    EPI_QKV_PREP = 6,       // attn_prep fused: column tile n0/128 = one head of [q heads | k heads | v heads]
+                            // (sections present per prep.q_col / k_col / v_col >= 0), written straight into
+                            // the attention layouts of `prep` (QK-RMSNorm, RoPE, fp16 hi/lo, V^T); 128-wide
+                            // column tiles only, no bias
 };
 
 struct GemmEpilogue {
@@ -30,6 +56,7 @@ struct GemmEpilogue {
     int out_T = 0;        // EPI_PROJ_OUT: frames per item
     int out_ch = 0;       // EPI_PROJ_OUT: channels (64)
     int patch = 2;        // EPI_PROJ_OUT
+    PrepArgs prep{};      // EPI_QKV_PREP (src / ld unused)
 };
 
 // Weight operand.  Dense: 16-bit [N][ld] in the activation type.  Quantized (ggml block formats
@@ -72,14 +99,32 @@ struct AttnArgs {
     int window;  // >0: bidirectional sliding window |q-k| <= window
     bool causal = false;  // key k > query q masked (Qwen3 text encoder)
     float scale;
-    bool split = true;                 // hi/lo fp16 operands (see attention.hip)
+    bool split = true;                 // hi/lo fp16 Q.K operands (see attention.hip)
+    bool pv_split = false;             // hi/lo fp16 P.V operands too (needs split)
     int64_t q_plane = 0, k_plane = 0, v_plane = 0;  // element offset of the lo planes
     // Optional f32 workspace of attn_part_floats(): with it, a grid too small to fill the chip in
     // whole rounds splits every block's key range in two and merges the halves in a second kernel.
     float* part = nullptr;
     int ksplit = 1;  // set by launch_attention
+    int xcd_order = 1;  // set by launch_attention: XCD-aware block order
 };
 size_t attn_part_floats(int B, int nq, int Hq);
+// Operand precision of the attention MFMAs: FP16 = single fp16 operands (two workgroups per CU),
+// SPLIT = hi/lo fp16 Q.K (three MFMAs per product) with fp16 P.V, F32 = hi/lo fp16 for both products
+// (~22-bit operands, the f32-faithful mode).  ACE_MI_ATTN_PRECISION=fp16|split|f32 overrides `dflt`;
+// the legacy ACE_MI_ATTN_FAST=1 means fp16.
+enum class AttnPrecision { FP16, SPLIT, F32 };
+inline AttnPrecision attn_precision_from_env(AttnPrecision dflt) {
+    const char* f = std::getenv("ACE_MI_ATTN_FAST");
+    if (f && f[0] && f[0] != '0') return AttnPrecision::FP16;
+    const char* e = std::getenv("ACE_MI_ATTN_PRECISION");
+    if (!e || !e[0]) return dflt;
+    const std::string v(e);
+    if (v == "fp16") return AttnPrecision::FP16;
+    if (v == "split") return AttnPrecision::SPLIT;
+    if (v == "f32") return AttnPrecision::F32;
+    throw std::runtime_error("ACE_MI_ATTN_PRECISION must be fp16, split or f32");
+}
 void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s);
 
 // ------------------------------------------------------------ elementwise
@@ -101,23 +146,6 @@ void launch_rmsnorm_f32(const float* x, int rows, int64_t row_step, int H, const
 // out[t] = f32(table[ids[t]]) for t < n (ggml_get_rows + cast_f32, qwen_model.cpp:563-564):
 // table [rows][H] as bf16 (fmt 0), fp16 (1) or f32 (2) values.
 void launch_embed_rows(const void* table, int fmt, const int32_t* ids, int n, int H, float* out, hipStream_t s);
-// Per-head RMSNorm (+ NEOX RoPE) of the q/k sections and f16 re-layout for attention.
-struct PrepArgs {
-    const float* src;
-    int ld;
-    int q_col, k_col, v_col;  // -1: section absent
-    int hq, hkv;
-    int n_tok, n_pad, B;
-    const float* q_norm;
-    const float* k_norm;
-    const float* rope_cos;  // [n_tok][64] or null
-    const float* rope_sin;
-    float eps;
-    uint16_t* qh;
-    uint16_t* kh;
-    uint16_t* vt;
-    int64_t q_plane = 0, k_plane = 0, v_plane = 0;  // >0: also write lo = f16(x - f16(x)) planes
-};
 void launch_attn_prep(const PrepArgs& a, hipStream_t s);
 // kbias[b][k] = (k < nk && pooled mask) ? 0 : -inf ; mask [B][nk*patch-ish frames] or null.
 void launch_key_bias(const int32_t* mask, int B, int frames, int patch, int nk, int nk_pad, float* kbias,

@@ -10,12 +10,14 @@
 // only the key tiles inside the window, causal blocks stop at their last query.
 //
 // Numerics: the reference runs attention in F32.  SPLIT=true (default) keeps
-// every operand as an fp16 pair x = hi + lo (hi = fp16(x), lo = fp16(x - hi))
-// and forms each product as hi*hi + hi*lo + lo*hi with three
-// v_mfma_f32_32x32x16_f16 (f32 accumulate) -> ~22-bit operands, so the bf16
-// rounding of the attention output (the o_proj vec_dot conversion) flips
-// almost never relative to the F32 reference.  SPLIT=false is the plain fp16
-// fast path (ACE_MI_ATTN_FAST=1).  P is formed as exp2(s - m + 12) (scaled by
+// Q and K as fp16 pairs x = hi + lo (hi = fp16(x), lo = fp16(x - hi)) and forms
+// each score as hi*hi + hi*lo + lo*hi with three v_mfma_f32_32x32x16_f16 (f32
+// accumulate) -> ~22-bit operands: a score error moves exp() and is not
+// averaged out.  P.V runs on single fp16 operands (P rounded to nearest, V hi)
+// unless PVS (AttnArgs::pv_split, ACE_MI_ATTN_PV_SPLIT=1) asks for the same
+// three-product form there too: its errors are independent per key and
+// average over the row.  SPLIT=false is the plain fp16 fast path
+// (ACE_MI_ATTN_FAST=1).  P is formed as exp2(s - m + 12) (scaled by
 // 2^12 so its lo part stays a normal fp16; O and l carry the same factor).
 // Online softmax in f32 (exp2 domain) with a lazy running max: O and l are
 // rescaled only when a row's max grows by more than 2^RESCALE_LOG2 (P then
@@ -41,6 +43,9 @@
 // LDS: K(i+2) and V(i+1) are requested at the top of iteration i (their
 // slots were last read in iteration i-1) and land by its closing barrier.
 #include <algorithm>
+#include <cstdlib>
+#include <stdexcept>
+#include <string>
 
 #include "../kernels.h"
 #include "lds_asm.h"
@@ -62,14 +67,14 @@ constexpr float RESCALE_LOG2 = 3.0f;      // P <= 2^(12+3) = 32768 < fp16 max
 // LDS rings.  K slot: [key bias (64 f32) | K hi | K lo]; V slot: [V^T hi | V^T lo].  All fragment
 // reads of the K ring use a 16-bit immediate offset from a per-lane address; the V ring has its own
 // base register (it starts past 64 KiB).
-template <bool SPLIT>
+template <bool SPLIT, bool PVS>
 struct Ring {
     static constexpr int KB = 0;
     static constexpr int K_HI = KT * 4;
     static constexpr int K_LO = K_HI + K_BYTES;
     static constexpr int KS = K_HI + (SPLIT ? 2 : 1) * K_BYTES;  // one K slot
     static constexpr int V_LO = V_BYTES;
-    static constexpr int VS = (SPLIT ? 2 : 1) * V_BYTES;          // one V slot
+    static constexpr int VS = (PVS ? 2 : 1) * V_BYTES;            // one V slot
     static constexpr int V0 = 2 * KS;                              // V ring start
     static constexpr int BYTES = 2 * KS + 2 * VS;
     static_assert(KS + K_LO + 32 * 256 + 255 < 65536, "K reads need 16-bit offsets");
@@ -134,9 +139,12 @@ __device__ __forceinline__ void static_for(F&& f) {
 // the 32x32 C/D map puts rows (= keys of S^T) at 8*(r/4) + 4*h + r%4
 __device__ __forceinline__ constexpr int key_of(int t, int r) { return 32 * t + (r & 3) + 8 * (r >> 2); }
 
-template <bool F16OUT, bool SPLIT, bool KBIAS>
-__global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
-    using RG = Ring<SPLIT>;
+// OCC = workgroups per CU the register allocation targets (2: <= 256 registers per lane; the
+// single-fp16 ring of 66 KiB lets two workgroups share a CU's LDS)
+template <bool F16OUT, bool SPLIT, bool PVS, bool KBIAS, int OCC>
+__global__ void __launch_bounds__(256, OCC) attn_kernel(AttnArgs a) {
+    static_assert(SPLIT || !PVS, "hi/lo P.V needs hi/lo operands");
+    using RG = Ring<SPLIT, PVS>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -147,7 +155,14 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
     const int rep = a.Hq / a.Hkv;
     const int qpb = 128 / rep;   // query rows per head in this block
     const int n_qt = (a.nq + qpb - 1) / qpb;
-    int bid = blockIdx.x;
+    // XCD-aware order: the hardware deals blocks round-robin over the 8 XCDs (block j -> XCD j % 8), so
+    // logical block L = (j % 8) * per + j / 8 gives each XCD one contiguous run of logical blocks, i.e.
+    // the blocks of one (item, kv head) -- whose K / V^T tiles they all stream -- share one XCD's L2
+    // (at B = 1 with 8 kv heads: one kv head per XCD).  Up to 7 trailing hardware blocks are empty.
+    const int n_blocks = a.B * a.Hkv * n_qt * a.ksplit;
+    const int per = (n_blocks + 7) >> 3;
+    int bid = a.xcd_order ? (blockIdx.x & 7) * per + (blockIdx.x >> 3) : blockIdx.x;
+    if (bid >= n_blocks) return;
     const int split = bid % a.ksplit;  // key-range part of this block (AttnArgs::part)
     bid /= a.ksplit;
     const int qt = bid % n_qt;
@@ -225,7 +240,7 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
             const int ch = (lane & 7) ^ ((d >> 1) & 7);
             const uint16_t* src = vbase + (int64_t)d * a.nk_pad + k0 + ch * 8;
             __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(base + g * 1024), 16, 0, 0);
-            if constexpr (SPLIT)
+            if constexpr (PVS)
                 __builtin_amdgcn_global_load_lds((const void*)(src + a.v_plane), (lds_void*)(base + RG::V_LO + g * 1024),
                                                  16, 0, 0);
         }
@@ -385,32 +400,32 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const float p0 = s_cur[t][8 * ss + 2 * j], p1 = s_cur[t][8 * ss + 2 * j + 1];
-                    if constexpr (SPLIT) {
+                    if constexpr (PVS) {
                         // hi = fp16 toward zero (one v_cvt_pkrtz per pair); p - hi is exact in f32 and
                         // its fp16 lo keeps the pair at ~22 bits, as with round-to-nearest
                         const auto h2 = __builtin_amdgcn_cvt_pkrtz(p0, p1);
                         f[j] = __builtin_bit_cast(uint32_t, h2);
                         fl[j] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(p0 - (float)h2[0], p1 - (float)h2[1]));
                     } else {
-                        f[j] = pack_f16x2(p0, p1);
+                        f[j] = pack_f16x2(p0, p1);  // v_cvt_pk_f16_f32, round to nearest
                     }
                 }
                 pf[2 * t + ss] = f;
-                if constexpr (SPLIT) pfl[2 * t + ss] = fl;
+                if constexpr (PVS) pfl[2 * t + ss] = fl;
             }
         }
         l_run += lsum;
 
-        // O^T += V^T(i) . P^T(i) ; SPLIT: Vh.Ph + Vh.Pl + Vl.Ph  ||  scale / mask / max of S(i+1)
+        // O^T += V^T(i) . P^T(i) ; PVS: Vh.Ph + Vh.Pl + Vl.Ph  ||  scale / mask / max of S(i+1)
         static_for<0, 2>([&](auto dp_c) {  // two 32-row d-tiles per LDS round trip
             constexpr int dp = 2 * decltype(dp_c)::value;
-            frag vf[SPLIT ? 16 : 8];  // [u][g] hi, then lo
+            frag vf[PVS ? 16 : 8];  // [u][g] hi, then lo
             static_for<0, 2>([&](auto u_c) {
                 constexpr int u = decltype(u_c)::value;
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
                     vf[4 * u + g] = lds_frag<SLOT * RG::VS + (dp + u) * 32 * 128>(vaddr[g]);
-                    if constexpr (SPLIT)
+                    if constexpr (PVS)
                         vf[8 + 4 * u + g] = lds_frag<SLOT * RG::VS + (dp + u) * 32 * 128 + RG::V_LO>(vaddr[g]);
                 }
             });
@@ -420,7 +435,7 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
                     o[dp + u] = mfma32(vf[4 * u + g], pf[g], o[dp + u]);
-                    if constexpr (SPLIT) {
+                    if constexpr (PVS) {
                         o[dp + u] = mfma32(vf[4 * u + g], pfl[g], o[dp + u]);
                         o[dp + u] = mfma32(vf[8 + 4 * u + g], pf[g], o[dp + u]);
                     }
@@ -511,13 +526,25 @@ __global__ void __launch_bounds__(256) attn_merge_kernel(AttnArgs a) {
                    (uint32_t)to_act<F16OUT>(v[2]) | ((uint32_t)to_act<F16OUT>(v[3]) << 16));
 }
 
-template <bool F16OUT, bool SPLIT>
+template <bool F16OUT, bool SPLIT, bool PVS>
 void launch_t(const AttnArgs& a, dim3 grid, hipStream_t s) {
-    const size_t lds = Ring<SPLIT>::BYTES;
+    const size_t lds = Ring<SPLIT, PVS>::BYTES;
+    static int occ = 0;  // ACE_MI_ATTN_OCC=1: one workgroup per CU for the single-fp16 kernel too (A/B)
+    if (occ == 0) {
+        const char* e = std::getenv("ACE_MI_ATTN_OCC");
+        occ = (e && e[0] == '1') ? 1 : 2;
+    }
+    if (!SPLIT && occ == 2) {
+        if (a.kbias)
+            hipLaunchKernelGGL((attn_kernel<F16OUT, SPLIT, PVS, true, 2>), grid, dim3(256), lds, s, a);
+        else
+            hipLaunchKernelGGL((attn_kernel<F16OUT, SPLIT, PVS, false, 2>), grid, dim3(256), lds, s, a);
+        return;
+    }
     if (a.kbias)
-        hipLaunchKernelGGL((attn_kernel<F16OUT, SPLIT, true>), grid, dim3(256), lds, s, a);
+        hipLaunchKernelGGL((attn_kernel<F16OUT, SPLIT, PVS, true, 1>), grid, dim3(256), lds, s, a);
     else
-        hipLaunchKernelGGL((attn_kernel<F16OUT, SPLIT, false>), grid, dim3(256), lds, s, a);
+        hipLaunchKernelGGL((attn_kernel<F16OUT, SPLIT, PVS, false, 1>), grid, dim3(256), lds, s, a);
 }
 
 }  // namespace
@@ -533,6 +560,14 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s) {
     AttnArgs b = a;
     b.ksplit = 1;
     {
+        static int xcd = -1;  // ACE_MI_ATTN_XCD_ORDER=0: plain block order (A/B measurements)
+        if (xcd < 0) {
+            const char* e = std::getenv("ACE_MI_ATTN_XCD_ORDER");
+            xcd = (e && e[0] == '0') ? 0 : 1;
+        }
+        b.xcd_order = xcd;
+    }
+    {
         // a grid of fewer than ~1.6 rounds over the CUs idles a third of the chip in its last
         // round: split each block's key range in two (B = 1 at 240 s: 376 blocks -> 752)
         static int n_cu = 0;
@@ -545,20 +580,28 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s) {
         const int span = a.window > 0 ? std::min(a.nk, qpb + 2 * a.window) : a.nk;
         // (measured: full 240 s 317 -> 262 us incl. the merge; at 8 key tiles or fewer -- cross attention,
         // sliding windows -- the extra prologue and merge cost more than the round saves)
-        if (a.part && blocks * 10 < (int64_t)n_cu * 16 && (span + KT - 1) / KT >= 16) b.ksplit = 2;
+        static int mode = -1;  // ACE_MI_ATTN_KSPLIT=1 never / 2 always (where a workspace exists) / auto
+        if (mode < 0) {
+            const char* e = std::getenv("ACE_MI_ATTN_KSPLIT");
+            mode = (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 0;
+        }
+        // blocks resident per CU: two for the single-fp16 kernel (66 KiB ring), one for the hi/lo ones
+        const int per_cu = a.split ? 1 : 2;
+        const bool want = blocks * 10 < (int64_t)n_cu * per_cu * 16 && (span + KT - 1) / KT >= 16;
+        if (a.part && (mode == 2 || (mode == 0 && want))) b.ksplit = 2;
     }
-    const dim3 grid(a.B * a.Hkv * n_qt * b.ksplit);
+    const dim3 grid(8 * ((a.B * a.Hkv * n_qt * b.ksplit + 7) / 8));  // XCD-aware order, see attn_kernel
+    const bool f16 = out_t == ActType::F16;
     if (a.split) {
-        ACEMI_CHECK(a.q_plane > 0 && a.k_plane > 0 && a.v_plane > 0, "attention: split mode needs lo planes");
-        if (out_t == ActType::F16)
-            launch_t<true, true>(b, grid, s);
-        else
-            launch_t<false, true>(b, grid, s);
+        ACEMI_CHECK(a.q_plane > 0 && a.k_plane > 0, "attention: split mode needs lo planes");
+        if (a.pv_split) {
+            ACEMI_CHECK(a.v_plane > 0, "attention: hi/lo P.V needs the V lo plane");
+            f16 ? launch_t<true, true, true>(b, grid, s) : launch_t<false, true, true>(b, grid, s);
+        } else {
+            f16 ? launch_t<true, true, false>(b, grid, s) : launch_t<false, true, false>(b, grid, s);
+        }
     } else {
-        if (out_t == ActType::F16)
-            launch_t<true, false>(b, grid, s);
-        else
-            launch_t<false, false>(b, grid, s);
+        f16 ? launch_t<true, false, false>(b, grid, s) : launch_t<false, false, false>(b, grid, s);
     }
     ACEMI_HIP(hipGetLastError());
     if (b.ksplit > 1) {

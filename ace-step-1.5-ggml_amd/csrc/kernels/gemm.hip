@@ -19,6 +19,7 @@
 #include <cmath>
 
 #include "../kernels.h"
+#include "prep_math.h"
 
 namespace acemi {
 namespace {
@@ -230,6 +231,102 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
     }
 }
 
+// EPI_QKV_PREP: the block's BM x 128 f32 accumulator tile (one head of the [q | k | v] projection) goes
+// through LDS in row chunks (rows 144 floats apart: the 16x4 accumulator writes are conflict-free) and is
+// written straight into the attention operand layouts with attn_prep's arithmetic (prep_math.h): 16
+// lanes per token for q / k (QK-RMSNorm, RoPE, fp16 hi/lo), one lane per (d, 16-key group) for V^T.
+// This removes the f32 [M][4096] round trip through HBM and the separate prep launch.
+template <int BM, int NW, int TM, int TN, int SMEM>
+__device__ __forceinline__ void qkv_prep_tile(const GemmParams& p, f32x4 (&acc)[TM][TN], int m0, int n0, int wm0,
+                                              int wn0, int tid, char* smem) {
+    constexpr int LD = 144;
+    constexpr int CH = (BM * LD * 4 <= SMEM) ? BM : ((BM / 2) * LD * 4 <= SMEM ? BM / 2 : BM / 4);
+    static_assert(CH * LD * 4 <= SMEM && BM % CH == 0 && CH % 16 == 0, "qkv prep chunking");
+    constexpr int NT = NW * 64;
+    const PrepArgs& a = p.e.prep;
+    float* tile = reinterpret_cast<float*>(smem);
+    const int lane = tid & 63;
+    const int ccol = lane & 15, crow = (lane >> 4) * 4;
+    const int nq = a.q_col >= 0 ? a.hq : 0;
+    const int nk = a.k_col >= 0 ? a.hkv : 0;
+    const int hd = n0 >> 7;
+    for (int c0 = 0; c0 < BM; c0 += CH) {
+        const int mc0 = m0 + c0;
+        if (mc0 >= p.M) break;
+        __syncthreads();  // the main loop's (or the previous chunk's) LDS readers are done
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int rb = wm0 + i * 16 - c0;
+            if (rb < 0 || rb >= CH) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) tile[(rb + crow + r) * LD + wn0 + j * 16 + ccol] = acc[i][j][r];
+        }
+        __syncthreads();
+        const int rows = min(CH, p.M - mc0);
+        if (hd < nq + nk) {
+            const bool isq = hd < nq;
+            const int head = isq ? hd : hd - nq;
+            const float* w = isq ? a.q_norm : a.k_norm;
+            uint16_t* base = isq ? a.qh + (int64_t)head * a.n_pad * 128 : a.kh + (int64_t)head * a.n_pad * 128;
+            const int64_t bstride = (int64_t)(isq ? a.hq : a.hkv) * a.n_pad * 128;
+            const int64_t plane = isq ? a.q_plane : a.k_plane;
+            const int d = (tid & 15) * 4;
+            for (int t = tid >> 4; t < rows; t += NT / 16) {
+                const int m = mc0 + t;
+                const int b = m / a.n_tok, n = m - b * a.n_tok;
+                const float4 x0 = *(const float4*)(tile + t * LD + d), x1 = *(const float4*)(tile + t * LD + 64 + d);
+                float y[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+                prep::head_row(y, w, d, a.eps, a.rope_cos ? a.rope_cos + (int64_t)n * 64 + d : nullptr,
+                               a.rope_cos ? a.rope_sin + (int64_t)n * 64 + d : nullptr,
+                               base + b * bstride + (int64_t)n * 128, plane);
+            }
+        } else {
+            // V^T: groups of 16 keys of one item; a group cut by the chunk edge is written key by key
+            // (its other keys belong to the neighbouring chunk or tile), padding keys as zeros, and the
+            // tile holding an item's last token also zero-fills the item's groups up to n_pad
+            const int hk = hd - nq - nk;
+            const int d = tid & 127;
+            const int b_lo = mc0 / a.n_tok, b_hi = (mc0 + rows - 1) / a.n_tok;
+            for (int b = b_lo; b <= b_hi; ++b) {
+                const int n_lo = max(0, mc0 - b * a.n_tok), n_hi = min(a.n_tok, mc0 + rows - b * a.n_tok);
+                uint16_t* vdst = a.vt + (((int64_t)b * a.hkv + hk) * 128 + d) * a.n_pad;
+                const int g_end = n_hi == a.n_tok ? a.n_pad / 16 : ((n_hi - 1) >> 4) + 1;
+                for (int g = (n_lo >> 4) + (tid >> 7); g < g_end; g += NT / 128) {
+                    const int g0 = g * 16;
+                    float v[16];
+                    uint32_t have = 0;
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) {
+                        const int n = g0 + prep::vperm(k);
+                        const bool mine = n >= n_lo && n < n_hi;
+                        v[k] = mine ? tile[(b * a.n_tok + n - mc0) * LD + d] : 0.f;
+                        have |= (mine || n >= a.n_tok) ? (1u << k) : 0u;
+                    }
+                    uint32_t wv[8], wl[8];
+                    prep::v_words(v, wv, wl);
+                    if (have == 0xffffu) {
+                        *(uint4*)(vdst + g0) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+                        *(uint4*)(vdst + g0 + 8) = make_uint4(wv[4], wv[5], wv[6], wv[7]);
+                        if (a.v_plane > 0) {
+                            *(uint4*)(vdst + a.v_plane + g0) = make_uint4(wl[0], wl[1], wl[2], wl[3]);
+                            *(uint4*)(vdst + a.v_plane + g0 + 8) = make_uint4(wl[4], wl[5], wl[6], wl[7]);
+                        }
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < 16; ++k) {
+                            if (!((have >> k) & 1u)) continue;
+                            vdst[g0 + k] = (uint16_t)(wv[k >> 1] >> (16 * (k & 1)));
+                            if (a.v_plane > 0) vdst[a.v_plane + g0 + k] = (uint16_t)(wl[k >> 1] >> (16 * (k & 1)));
+                        }
+                    }
+                }
+            }
+        }
+    }
+}
+
 // PIPE 0: stage(t+1) ; compute(t) ; vmcnt(0) ; __syncthreads        (2 LDS buffers)
 // PIPE 1: compute first half of tile t from registers read up front, release the LDS buffer with
 //         a raw s_barrier, stage tile t+2 into it, compute the second half, then a COUNTED
@@ -399,7 +496,10 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(GemmParams p) {
         }
     }
 
-    gemm_epilogue<TM, TN, F16, EPI, NW>(p, acc, m0 + wm0, n0 + wn0, lane);
+    if constexpr (EPI == EPI_QKV_PREP)
+        qkv_prep_tile<BM, NW, TM, TN, 2 * STAGE>(p, acc, m0, n0, wm0, wn0, tid, smem);
+    else
+        gemm_epilogue<TM, TN, F16, EPI, NW>(p, acc, m0 + wm0, n0 + wn0, lane);
 }
 
 
@@ -645,7 +745,10 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_q_kernel(GemmParams p) {
     }
     wait_vmcnt<0>();
 
-    gemm_epilogue<TM, TN, false, EPI, NW>(p, acc, m0 + wm0, n0 + wn0, lane);
+    if constexpr (EPI == EPI_QKV_PREP)
+        qkv_prep_tile<BM, NW, TM, TN, 2 * STAGE>(p, acc, m0, n0, wm0, wn0, tid, smem);
+    else
+        gemm_epilogue<TM, TN, false, EPI, NW>(p, acc, m0 + wm0, n0 + wn0, lane);
 }
 
 template <int BM, int BN, int WM, int WN, bool F16, int EPI, int PIPE>
@@ -654,7 +757,10 @@ void launch_cfg(const GemmParams& p, hipStream_t s) {
     const int nbn = p.N / BN;
     const dim3 grid(nbm * nbn);
     const dim3 block(WM * WN * 64);
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, F16, EPI, PIPE>), grid, block, 0, s, p);
+    if constexpr (EPI == EPI_QKV_PREP && BN != 128)
+        throw std::runtime_error("gemm: the fused attention prep needs 128-wide column tiles");
+    else
+        hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, F16, EPI, PIPE>), grid, block, 0, s, p);
 }
 
 // variant: 0 = 128x128 PIPE0, 1 = 128x128 PIPE1, 2 = 256x256 PIPE1 (8 waves 2x4), 3 = 256x128 PIPE1,
@@ -686,6 +792,7 @@ void dispatch_epi(int variant, const GemmParams& p, hipStream_t s) {
         case EPI_RESID: launch_variant<F16, EPI_RESID>(variant, p, s); break;
         case EPI_SWIGLU: launch_variant<F16, EPI_SWIGLU>(variant, p, s); break;
         case EPI_PROJ_OUT: launch_variant<F16, EPI_PROJ_OUT>(variant, p, s); break;
+        case EPI_QKV_PREP: launch_variant<F16, EPI_QKV_PREP>(variant, p, s); break;
         default: throw std::runtime_error("gemm: bad epilogue kind");
     }
 }
@@ -694,7 +801,10 @@ template <int BM, int BN, int WM, int WN, int EPI, int WQ>
 void launch_q_cfg(const GemmParams& p, hipStream_t s) {
     const int nbm = (p.M + BM - 1) / BM;
     const int nbn = p.N / BN;
-    hipLaunchKernelGGL((gemm_q_kernel<BM, BN, WM, WN, EPI, WQ>), dim3(nbm * nbn), dim3(WM * WN * 64), 0, s, p);
+    if constexpr (EPI == EPI_QKV_PREP && BN != 128)
+        throw std::runtime_error("gemm: the fused attention prep needs 128-wide column tiles");
+    else
+        hipLaunchKernelGGL((gemm_q_kernel<BM, BN, WM, WN, EPI, WQ>), dim3(nbm * nbn), dim3(WM * WN * 64), 0, s, p);
 }
 
 template <int EPI, int WQ>
@@ -720,6 +830,7 @@ void dispatch_q_epi(int variant, const GemmParams& p, hipStream_t s) {
         case EPI_RESID: launch_q_variant<EPI_RESID, WQ>(variant, p, s); break;
         case EPI_SWIGLU: launch_q_variant<EPI_SWIGLU, WQ>(variant, p, s); break;
         case EPI_PROJ_OUT: launch_q_variant<EPI_PROJ_OUT, WQ>(variant, p, s); break;
+        case EPI_QKV_PREP: launch_q_variant<EPI_QKV_PREP, WQ>(variant, p, s); break;
         default: throw std::runtime_error("gemm: bad epilogue kind");
     }
 }
@@ -767,7 +878,15 @@ void launch_gemm(const uint16_t* A, int lda, const WeightView& W, int M, int N, 
     ACEMI_CHECK(lda % 8 == 0, "gemm: leading dims must be multiples of 8");
     ACEMI_CHECK(W.q != nullptr, "gemm: null weight");
     GemmParams p{A, (const uint16_t*)W.q, W.q, W.s, lda, W.ld, M, N, K, epi};
-    const int v = pick_variant(M, N, weight_quantized(W.fmt));
+    int v = pick_variant(M, N, weight_quantized(W.fmt));
+    if (epi.kind == EPI_QKV_PREP) {  // 128-wide column tiles: one head per tile
+        ACEMI_CHECK(epi.bias == nullptr && epi.prep.n_tok > 0 && M % epi.prep.n_tok == 0,
+                    "gemm: fused attention prep needs no bias and whole items");
+        ACEMI_CHECK(N == 128 * ((epi.prep.q_col >= 0 ? epi.prep.hq : 0) + (epi.prep.k_col >= 0 ? epi.prep.hkv : 0) +
+                                (epi.prep.v_col >= 0 ? epi.prep.hkv : 0)),
+                    "gemm: fused attention prep column count");
+        v = v == 2 ? 3 : v == 5 ? 4 : v == 6 ? 1 : v == 9 ? 8 : v;
+    }
     switch (W.fmt) {
         case WF_BF16:
         case WF_F16:

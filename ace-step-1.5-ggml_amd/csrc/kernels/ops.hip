@@ -1,6 +1,7 @@
 // Memory-bound kernels around the DiT GEMMs and attention (gfx950).
 // Each kernel cites the ggml graph nodes of ace_dit::forward_dit it fuses.
 #include "../kernels.h"
+#include "prep_math.h"
 
 namespace acemi {
 namespace {
@@ -210,12 +211,7 @@ __global__ void __launch_bounds__(256) embed_rows_kernel(const void* __restrict_
 //   qh [B][hq][n_pad][128], kh [B][hkv][n_pad][128]  (f16, rows >= n_tok zero)
 //   vt [B][hkv][128][n_pad] (f16, key position permuted inside each 16-group: positions
 //      4..7 <-> 8..11, the k order of the attention kernel's P^T operand)
-__device__ __forceinline__ int vperm(int k) {
-    const int w = k & 15;
-    const int g = w >> 2;
-    const int gp = (g == 1) ? 2 : (g == 2 ? 1 : g);
-    return (k & ~15) | (gp << 2) | (w & 3);
-}
+// (per-token math and the key order: prep_math.h, shared with the QKV GEMM's fused epilogue)
 
 // grid: (n_pad/64 token tiles, nq + nk + nv head slots, B).  Slot < nq: one q head; < nq+nk: one k
 // head; else the V^T transpose of one kv head.  One workgroup = 64 tokens of one head.
@@ -235,19 +231,12 @@ __global__ void __launch_bounds__(256) attn_prep_kernel(PrepArgs a) {
         uint16_t* base = isq ? a.qh + ((int64_t)b * a.hq + head) * a.n_pad * 128
                              : a.kh + ((int64_t)b * a.hkv + head) * a.n_pad * 128;
         const int64_t plane = isq ? a.q_plane : a.k_plane;
-        // lane: token sub = lane / 16 of the wave's group of 4, dims d..d+3 and d+64..d+67 (the NEOX
-        // rotation pairs d with d+64 inside the lane); 16-byte loads, 8-byte f16 stores
+        // lane: token sub = lane / 16 of the wave's group of 4, dims d..d+3 and d+64..d+67; 16-byte
+        // loads, 8-byte f16 stores; rows >= n_tok are written as zeros
         const int sub = lane >> 4;
         const int d = (lane & 15) * 4;
-        const float4 one = make_float4(1.f, 1.f, 1.f, 1.f);
-        const float4 w0 = w ? *(const float4*)(w + d) : one, w1 = w ? *(const float4*)(w + 64 + d) : one;
-        auto pk4 = [](float p, float q, float r, float t) {
-            return make_uint2((uint32_t)f32_to_f16(p) | ((uint32_t)f32_to_f16(q) << 16),
-                              (uint32_t)f32_to_f16(r) | ((uint32_t)f32_to_f16(t) << 16));
-        };
-        auto lo = [](float v) { return v - (float)__builtin_bit_cast(_Float16, f32_to_f16(v)); };
 #pragma unroll
-        for (int t0 = wid * 4; t0 < 64; t0 += 16) {  // 4 groups of 4 tokens per wave, loads hoisted
+        for (int t0 = wid * 4; t0 < 64; t0 += 16) {  // 4 groups of 4 tokens per wave
             const int n = n0 + t0 + sub;
             float4 x0 = make_float4(0.f, 0.f, 0.f, 0.f), x1 = x0;
             if (n < a.n_tok) {
@@ -256,38 +245,9 @@ __global__ void __launch_bounds__(256) attn_prep_kernel(PrepArgs a) {
                 x1 = *(const float4*)(row + 64 + d);
             }
             float y[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-            if (w) {  // null weight: plain copy (kernel self-test entry)
-                float ss = 0.f;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) ss += y[j] * y[j];
-#pragma unroll
-                for (int o = 8; o >= 1; o >>= 1) ss += __shfl_xor(ss, o);  // the token's 16 lanes
-                const float sc = 1.0f / sqrtf(ss / 128.0f + a.eps);
-                const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-#pragma unroll
-                for (int j = 0; j < 8; ++j) y[j] = __fmul_rn(__fmul_rn(y[j], sc), wv[j]);
-            }
-            float r[8];
-            if (a.rope_cos && n < a.n_tok) {
-                const float4 c4 = *(const float4*)(a.rope_cos + (int64_t)n * 64 + d);
-                const float4 s4 = *(const float4*)(a.rope_sin + (int64_t)n * 64 + d);
-                const float c[4] = {c4.x, c4.y, c4.z, c4.w}, sn[4] = {s4.x, s4.y, s4.z, s4.w};
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    r[j] = __fsub_rn(__fmul_rn(y[j], c[j]), __fmul_rn(y[4 + j], sn[j]));
-                    r[4 + j] = __fadd_rn(__fmul_rn(y[j], sn[j]), __fmul_rn(y[4 + j], c[j]));
-                }
-            } else {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) r[j] = y[j];
-            }
-            uint16_t* dst = base + (int64_t)n * 128;
-            *(uint2*)(dst + d) = pk4(r[0], r[1], r[2], r[3]);
-            *(uint2*)(dst + 64 + d) = pk4(r[4], r[5], r[6], r[7]);
-            if (plane > 0) {
-                *(uint2*)(dst + plane + d) = pk4(lo(r[0]), lo(r[1]), lo(r[2]), lo(r[3]));
-                *(uint2*)(dst + plane + 64 + d) = pk4(lo(r[4]), lo(r[5]), lo(r[6]), lo(r[7]));
-            }
+            const bool rope = a.rope_cos && n < a.n_tok;
+            prep::head_row(y, w, d, a.eps, rope ? a.rope_cos + (int64_t)n * 64 + d : nullptr,
+                           rope ? a.rope_sin + (int64_t)n * 64 + d : nullptr, base + (int64_t)n * 128, plane);
         }
         return;
     }
@@ -305,17 +265,11 @@ __global__ void __launch_bounds__(256) attn_prep_kernel(PrepArgs a) {
         float v[16];
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
-            const int n = g0 + vperm(k);
+            const int n = g0 + prep::vperm(k);
             v[k] = n < a.n_tok ? vsrc[(int64_t)n * a.ld] : 0.f;
         }
         uint32_t wv[8], wl[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const uint16_t h0 = f32_to_f16(v[2 * j]), h1 = f32_to_f16(v[2 * j + 1]);
-            wv[j] = (uint32_t)h0 | ((uint32_t)h1 << 16);
-            wl[j] = (uint32_t)f32_to_f16(v[2 * j] - (float)__builtin_bit_cast(_Float16, h0)) |
-                    ((uint32_t)f32_to_f16(v[2 * j + 1] - (float)__builtin_bit_cast(_Float16, h1)) << 16);
-        }
+        prep::v_words(v, wv, wl);
         *(uint4*)(vdst + g0) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
         *(uint4*)(vdst + g0 + 8) = make_uint4(wv[4], wv[5], wv[6], wv[7]);
         if (a.v_plane > 0) {

@@ -1,0 +1,85 @@
+// Per-token attention operand preparation shared by attn_prep_kernel (ops.hip) and the QKV GEMM's fused
+// epilogue (gemm.hip, EPI_QKV_PREP), so both produce the same bits:
+//   q/k heads: per-head RMSNorm over D = 128 with the q_norm / k_norm weights, then NEOX RoPE
+//              (acestep_dit_model.cpp:1198-1210), fp16 hi (+ lo = fp16(x - hi)) rows [b][head][n][128];
+//   v heads:   V^T [b][kvh][d][n] in the attention kernel's key order (vperm inside groups of 16).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace acemi {
+namespace prep {
+
+__device__ __forceinline__ uint16_t f16_bits(float f) {
+    _Float16 h = (_Float16)f;
+    return __builtin_bit_cast(uint16_t, h);
+}
+__device__ __forceinline__ float f16_lo(float v) { return v - (float)__builtin_bit_cast(_Float16, f16_bits(v)); }
+__device__ __forceinline__ uint2 pk4(float p, float q, float r, float t) {
+    return make_uint2((uint32_t)f16_bits(p) | ((uint32_t)f16_bits(q) << 16),
+                      (uint32_t)f16_bits(r) | ((uint32_t)f16_bits(t) << 16));
+}
+
+// Key order of V^T inside a group of 16: the attention kernel's P^T registers hold keys
+// (r & 3) + 8 * (r >> 2) + 4 * half, so the 4-key sub-groups 1 and 2 trade places.
+__device__ __forceinline__ int vperm(int k) {
+    const int w = k & 15;
+    const int g = w >> 2;
+    const int gp = (g == 1) ? 2 : (g == 2 ? 1 : g);
+    return (k & ~15) | (gp << 2) | (w & 3);
+}
+
+// One token's head row, 16 lanes per token (lane & 15 = d / 4): y[0..3] = dims d..d+3, y[4..7] = dims
+// 64+d..64+d+3 (the NEOX rotation pairs d with d+64 inside the lane).  w: norm weights or null (plain
+// copy); cs / sn: the position's RoPE row (+ d) or null.  Writes fp16 hi into dst[0..127] and, when
+// plane > 0, lo into dst[plane..].
+__device__ __forceinline__ void head_row(float (&y)[8], const float* w, int d, float eps, const float* cs,
+                                         const float* sn, uint16_t* dst, int64_t plane) {
+    if (w) {
+        const float4 w0 = *(const float4*)(w + d), w1 = *(const float4*)(w + 64 + d);
+        float ss = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ss += y[j] * y[j];
+#pragma unroll
+        for (int o = 8; o >= 1; o >>= 1) ss += __shfl_xor(ss, o);  // the token's 16 lanes
+        const float sc = 1.0f / sqrtf(ss / 128.0f + eps);
+        const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[j] = __fmul_rn(__fmul_rn(y[j], sc), wv[j]);
+    }
+    float r[8];
+    if (cs) {
+        const float4 c4 = *(const float4*)cs, s4 = *(const float4*)sn;
+        const float c[4] = {c4.x, c4.y, c4.z, c4.w}, s[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            r[j] = __fsub_rn(__fmul_rn(y[j], c[j]), __fmul_rn(y[4 + j], s[j]));
+            r[4 + j] = __fadd_rn(__fmul_rn(y[j], s[j]), __fmul_rn(y[4 + j], c[j]));
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] = y[j];
+    }
+    *(uint2*)(dst + d) = pk4(r[0], r[1], r[2], r[3]);
+    *(uint2*)(dst + 64 + d) = pk4(r[4], r[5], r[6], r[7]);
+    if (plane > 0) {
+        *(uint2*)(dst + plane + d) = pk4(f16_lo(r[0]), f16_lo(r[1]), f16_lo(r[2]), f16_lo(r[3]));
+        *(uint2*)(dst + plane + 64 + d) = pk4(f16_lo(r[4]), f16_lo(r[5]), f16_lo(r[6]), f16_lo(r[7]));
+    }
+}
+
+// 16 values of one V^T row segment (keys g0 + vperm(k), k = 0..15) as fp16 hi / lo words.
+__device__ __forceinline__ void v_words(const float (&v)[16], uint32_t (&wv)[8], uint32_t (&wl)[8]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const uint16_t h0 = f16_bits(v[2 * j]), h1 = f16_bits(v[2 * j + 1]);
+        wv[j] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+        wl[j] = (uint32_t)f16_bits(v[2 * j] - (float)__builtin_bit_cast(_Float16, h0)) |
+                ((uint32_t)f16_bits(v[2 * j + 1] - (float)__builtin_bit_cast(_Float16, h1)) << 16);
+    }
+}
+
+}  // namespace prep
+}  // namespace acemi

@@ -8,8 +8,10 @@
 namespace acemi {
 
 BlockRunner::BlockRunner() {
-    const char* f = std::getenv("ACE_MI_ATTN_FAST");
-    split_ = !(f && f[0] && f[0] != '0');
+    // the condition / text encoders (once per request) keep the f32-faithful default
+    const AttnPrecision prec = attn_precision_from_env(AttnPrecision::F32);
+    split_ = prec != AttnPrecision::FP16;
+    pv_split_ = prec == AttnPrecision::F32;
 }
 
 BlockRunner::~BlockRunner() {
@@ -119,7 +121,7 @@ void BlockRunner::run(const BlockShape& sh, const std::vector<DevLayer>& layers,
             pa.vt = get<uint16_t>(vt_);
             pa.q_plane = split_ ? q_plane : 0;
             pa.k_plane = split_ ? k_plane : 0;
-            pa.v_plane = split_ ? k_plane : 0;
+            pa.v_plane = pv_split_ ? k_plane : 0;
             launch_attn_prep(pa, s);
         }
         {
@@ -140,6 +142,7 @@ void BlockRunner::run(const BlockShape& sh, const std::vector<DevLayer>& layers,
             aa.causal = causal;
             aa.scale = scale;
             aa.split = split_;
+            aa.pv_split = pv_split_;
             aa.q_plane = q_plane;
             aa.k_plane = k_plane;
             aa.v_plane = k_plane;

@@ -49,7 +49,8 @@ class BlockRunner {
     Buf x_, act_, attn_, act2_, qkv_, qh_, kh_, vt_, kbias_, cos_, sin_;
     int rope_n_ = -1;
     float rope_theta_ = 0.f;
-    bool split_ = true;  // ACE_MI_ATTN_FAST=1 -> single fp16 attention operands
+    bool split_ = true;  // hi/lo fp16 Q.K operands (ACE_MI_ATTN_PRECISION)
+    bool pv_split_ = true;  // hi/lo fp16 P.V operands too
 };
 
 }  // namespace acemi

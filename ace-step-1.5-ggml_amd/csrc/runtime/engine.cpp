@@ -10,8 +10,11 @@
 namespace acemi {
 
 DitEngine::DitEngine(int device) : device_(device) {
-    const char* f = std::getenv("ACE_MI_ATTN_FAST");
-    attn_split_ = !(f && f[0] && f[0] != '0');
+    // DiT: single fp16 operands by default (parity at full width equals the f32-faithful modes,
+    // DESIGN.md "Parity"); the condition / text encoders keep the f32-faithful default
+    const AttnPrecision prec = attn_precision_from_env(AttnPrecision::FP16);
+    attn_split_ = prec != AttnPrecision::FP16;
+    attn_pv_split_ = prec == AttnPrecision::F32;
 }
 
 DitEngine::~DitEngine() {
@@ -284,7 +287,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
             pa.kh = get<uint16_t>(kc_) + (size_t)li * B * c.hkv * Lpad * D;
             pa.vt = get<uint16_t>(vc_) + (size_t)li * B * c.hkv * D * Lpad;
             pa.k_plane = split ? kc_plane : 0;
-            pa.v_plane = split ? kc_plane : 0;
+            pa.v_plane = attn_pv_split_ ? kc_plane : 0;
             tic(s);
             launch_attn_prep(pa, s);
             toc("attn_prep", s);
@@ -340,7 +343,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
             pa.vt = get<uint16_t>(vt_);
             pa.q_plane = split ? q_plane : 0;
             pa.k_plane = split ? k_plane : 0;
-            pa.v_plane = split ? k_plane : 0;
+            pa.v_plane = attn_pv_split_ ? k_plane : 0;
             tic(s);
             launch_attn_prep(pa, s);
             toc("attn_prep", s);
@@ -364,6 +367,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
             if (ly.sliding && c.sliding_window <= 0) aa.window = 0;
             aa.scale = scale;
             aa.split = split;
+            aa.pv_split = attn_pv_split_;
             aa.q_plane = q_plane;
             aa.k_plane = k_plane;
             aa.v_plane = k_plane;
@@ -436,6 +440,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
                 aa.window = 0;
                 aa.scale = scale;
                 aa.split = split;
+                aa.pv_split = attn_pv_split_;
                 aa.q_plane = q_plane;
                 aa.k_plane = kc_plane;
                 aa.v_plane = kc_plane;

@@ -102,7 +102,8 @@ class DitEngine {
     Buf ein_;             // condition-encoder input activations
     BlockRunner cond_;    // condition-encoder blocks (own workspace: the DiT buffers stay untouched)
     void rope_table(int n, Buf& cs, Buf& sn, hipStream_t s);
-    bool attn_split_ = true;  // ACE_MI_ATTN_FAST=1 -> single fp16 operands
+    bool attn_split_ = false;  // hi/lo fp16 Q.K operands (ACE_MI_ATTN_PRECISION)
+    bool attn_pv_split_ = false;  // hi/lo fp16 P.V operands too
     // profiling
     bool profiling_ = false;
     hipEvent_t ev0_ = nullptr, ev1_ = nullptr;

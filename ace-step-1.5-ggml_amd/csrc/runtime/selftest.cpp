@@ -143,6 +143,7 @@ struct AttnSetup {
         a.scale = scale;
         a.split = split;
         a.causal = (flags & 2) != 0;
+        a.pv_split = split && (flags & 8) != 0;
         a.q_plane = qpl;
         a.k_plane = kpl;
         a.v_plane = kpl;
@@ -176,7 +177,7 @@ ace_ggml_status ace_mi_kernel_attention(int32_t B, int32_t Hq, int32_t Hkv, int3
 }
 
 // Attention micro-benchmark: pseudo-random N(0,1)-like q / kv (fixed seed), average ms per launch over
-// `iters` launches timed with hipEvents.  flags: bit 0 split (hi/lo) operands, bit 1 causal,
+// `iters` launches timed with hipEvents.  flags: bit 0 split (hi/lo) operands, bit 1 causal, bit 3 hi/lo P.V,
 // bit 2 a key-padding mask (every 7th key masked).
 ace_ggml_status ace_mi_bench_attention(int32_t B, int32_t Hq, int32_t Hkv, int32_t nq, int32_t nk, int32_t window,
                                        int32_t flags, int32_t iters, float* avg_ms) {
@@ -197,7 +198,7 @@ ace_ggml_status ace_mi_bench_attention(int32_t B, int32_t Hq, int32_t Hkv, int32
         for (auto& v : q) v = 2.0f * rnd();
         for (auto& v : kv) v = rnd();
         for (size_t i = 0; i < km.size(); ++i) km[i] = (i % 7) != 6;
-        AttnSetup st(B, Hq, Hkv, nq, nk, window, 1.0f / std::sqrt(128.0f), flags & 3, q.data(), kv.data(),
+        AttnSetup st(B, Hq, Hkv, nq, nk, window, 1.0f / std::sqrt(128.0f), flags & 11, q.data(), kv.data(),
                      (flags & 4) ? km.data() : nullptr);
         hipEvent_t e0, e1;
         ACEMI_HIP(hipEventCreate(&e0));

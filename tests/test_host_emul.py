@@ -191,7 +191,7 @@ def test_generation_loop_ex_ode_sde_cover_and_cross_cache(host_lib, tiny_ckpt):
                 tn = np.float32(sched[i + 1])
                 xt = tn * noise[i] + (np.float32(1.0) - tn) * xc
             else:
-                xt = xt - v * np.float32(t - sched[i + 1])
+                xt = xt - v * (np.float32(t) - np.float32(sched[i + 1]))  # the library's f32 dt
         return xt
 
     for sde, cover, cache in ((False, None, True), (True, None, True), (False, 2, True), (True, 3, False)):

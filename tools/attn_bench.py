@@ -23,11 +23,14 @@ def main():
     for name, B, hq, hkv, nq, nk, win, masked in CASES:
         if only and name != only:
             continue
-        for split in ((True,) if only else (True, False)):
-            ms = capi.bench_attention(B, hq, hkv, nq, nk, win, split=split, masked=masked, iters=10)
+        modes = {"split": (True, False), "pvsplit": (True, True), "fast": (False, False)}
+        for mode, (split, pvs) in modes.items():
+            if only and mode != "split":
+                continue
+            ms = capi.bench_attention(B, hq, hkv, nq, nk, win, split=split, masked=masked, iters=10, pv_split=pvs)
             nk_eff = min(nk, 2 * win + 1) if win else nk
             flop = 4.0 * B * nq * nk_eff * 128 * hq
-            print(json.dumps({"case": name, "split": split, "ms": round(ms, 4),
+            print(json.dumps({"case": name, "mode": mode, "ms": round(ms, 4),
                               "tflops_alg": round(flop / (ms * 1e-3) / 1e12, 1)}), flush=True)
 
 
