@@ -885,6 +885,10 @@ void launch_gemm(const uint16_t* A, int lda, const WeightView& W, int M, int N, 
         ACEMI_CHECK(N == 128 * ((epi.prep.q_col >= 0 ? epi.prep.hq : 0) + (epi.prep.k_col >= 0 ? epi.prep.hkv : 0) +
                                 (epi.prep.v_col >= 0 ? epi.prep.hkv : 0)),
                     "gemm: fused attention prep column count");
+        const int nqc = epi.prep.q_col >= 0 ? epi.prep.hq : 0, nkc = epi.prep.k_col >= 0 ? epi.prep.hkv : 0;
+        ACEMI_CHECK(epi.prep.q_col <= 0 && (epi.prep.k_col < 0 || epi.prep.k_col == 128 * nqc) &&
+                        (epi.prep.v_col < 0 || epi.prep.v_col == 128 * (nqc + nkc)),
+                    "gemm: fused attention prep expects the [q | k | v] head order");
         v = v == 2 ? 3 : v == 5 ? 4 : v == 6 ? 1 : v == 9 ? 8 : v;
     }
     switch (W.fmt) {

@@ -15,6 +15,8 @@ DitEngine::DitEngine(int device) : device_(device) {
     const AttnPrecision prec = attn_precision_from_env(AttnPrecision::FP16);
     attn_split_ = prec != AttnPrecision::FP16;
     attn_pv_split_ = prec == AttnPrecision::F32;
+    const char* u = std::getenv("ACE_MI_UNFUSED_PREP");
+    fused_prep_ = !(u && u[0] && u[0] != '0');
 }
 
 DitEngine::~DitEngine() {
@@ -313,18 +315,9 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
         launch_rmsnorm_mod(at, x, (int)M, H, ly.self_norm, scale_msa, shift_msa, mstride, Np, c.eps, act, s);
         toc("rmsnorm_mod", s);
         {
-            GemmEpilogue e;
-            e.kind = EPI_STORE_F32;
-            e.c_f32 = qkv;
-            e.ldc = qd + 2 * kd;
-            tic(s);
-            launch_gemm(act, H, ly.w_qkv.view(), (int)M, qd + 2 * kd, H, e, s);
-            toc("gemm_qkv", s);
-        }
-        {
+            // QKV projection with QK-RMSNorm, RoPE and the attention re-layout fused into its epilogue
+            // (EPI_QKV_PREP; ACE_MI_UNFUSED_PREP=1 runs the f32 store + attn_prep pair instead)
             PrepArgs pa{};
-            pa.src = qkv;
-            pa.ld = qd + 2 * kd;
             pa.q_col = 0;
             pa.k_col = qd;
             pa.v_col = qd + kd;
@@ -344,9 +337,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
             pa.q_plane = split ? q_plane : 0;
             pa.k_plane = split ? k_plane : 0;
             pa.v_plane = attn_pv_split_ ? k_plane : 0;
-            tic(s);
-            launch_attn_prep(pa, s);
-            toc("attn_prep", s);
+            qkv_gemm(act, ly.w_qkv.view(), (int)M, qd + 2 * kd, pa, qkv, "gemm_qkv", s);
         }
         {
             AttnArgs aa{};
@@ -394,18 +385,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
             launch_rmsnorm_mod(at, x, (int)M, H, ly.cross_norm, nullptr, nullptr, 0, Np, c.eps, act, s);
             toc("rmsnorm_mod", s);
             {
-                GemmEpilogue e;
-                e.kind = EPI_STORE_F32;
-                e.c_f32 = qkv;
-                e.ldc = qd;
-                tic(s);
-                launch_gemm(act, H, ly.w_cq.view(), (int)M, qd, H, e, s);
-                toc("gemm_cross_q", s);
-            }
-            {
                 PrepArgs pa{};
-                pa.src = qkv;
-                pa.ld = qd;
                 pa.q_col = 0;
                 pa.k_col = -1;
                 pa.v_col = -1;
@@ -418,9 +398,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
                 pa.eps = c.eps;
                 pa.qh = get<uint16_t>(qh_);
                 pa.q_plane = split ? q_plane : 0;
-                tic(s);
-                launch_attn_prep(pa, s);
-                toc("attn_prep", s);
+                qkv_gemm(act, ly.w_cq.view(), (int)M, qd, pa, qkv, "gemm_cross_q", s);
             }
             {
                 AttnArgs aa{};
@@ -507,6 +485,34 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
         launch_gemm(head_in, kout * H, m.proj_out_w.view(), (int)M, P * c.audio_dim, kout * H, e, s);
         toc("gemm_proj_out", s);
     }
+}
+
+// A projection feeding attention: with EPI_QKV_PREP the GEMM epilogue writes the attention operands of
+// `pa` directly; the unfused path (ACE_MI_UNFUSED_PREP=1, A/B and debugging) stores f32 to `scratch`
+// and runs attn_prep over it.
+void DitEngine::qkv_gemm(const uint16_t* act, const WeightView& w, int M, int N, PrepArgs pa, float* scratch,
+                         const char* name, hipStream_t s) {
+    const int H = model_.cfg.hidden;
+    GemmEpilogue e;
+    if (fused_prep_) {
+        e.kind = EPI_QKV_PREP;
+        e.prep = pa;
+        tic(s);
+        launch_gemm(act, H, w, M, N, H, e, s);
+        toc(name, s);
+        return;
+    }
+    e.kind = EPI_STORE_F32;
+    e.c_f32 = scratch;
+    e.ldc = N;
+    tic(s);
+    launch_gemm(act, H, w, M, N, H, e, s);
+    toc(name, s);
+    pa.src = scratch;
+    pa.ld = N;
+    tic(s);
+    launch_attn_prep(pa, s);
+    toc("attn_prep", s);
 }
 
 void DitEngine::encode(const EncodeIO& io, hipStream_t s) {

@@ -104,6 +104,9 @@ class DitEngine {
     void rope_table(int n, Buf& cs, Buf& sn, hipStream_t s);
     bool attn_split_ = false;  // hi/lo fp16 Q.K operands (ACE_MI_ATTN_PRECISION)
     bool attn_pv_split_ = false;  // hi/lo fp16 P.V operands too
+    bool fused_prep_ = true;      // EPI_QKV_PREP (ACE_MI_UNFUSED_PREP=1: f32 store + attn_prep)
+    void qkv_gemm(const uint16_t* act, const WeightView& w, int M, int N, PrepArgs pa, float* scratch,
+                  const char* name, hipStream_t s);
     // profiling
     bool profiling_ = false;
     hipEvent_t ev0_ = nullptr, ev1_ = nullptr;

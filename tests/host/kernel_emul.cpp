@@ -149,6 +149,15 @@ void launch_gemm(const uint16_t* A, int lda, const WeightView& W, int M, int N, 
             acc[(size_t)m * N + n] = s;
         }
     }
+    if (e.kind == EPI_QKV_PREP) {  // the f32 result through the attn_prep contract
+        std::vector<float> tmp((size_t)M * N);
+        for (size_t i = 0; i < tmp.size(); ++i) tmp[i] = (float)acc[i];
+        PrepArgs pa = e.prep;
+        pa.src = tmp.data();
+        pa.ld = N;
+        launch_attn_prep(pa, nullptr);
+        return;
+    }
     for (int m = 0; m < M; ++m) {
         if (e.kind == EPI_SWIGLU) {
             for (int n = 0; n < N; n += 32)

@@ -268,3 +268,53 @@ def test_decoder_forward_hook_device_path(tiny_bridge):
         ref = tiny_bridge.dit_forward_tfirst(h[b], c[b], e[b], None, em[b].astype(np.int32), float(t[b]), float(t[b]))
         l2, _ = rel_errors(got[b], ref)
         assert l2 < 1e-6, (b, l2)
+
+
+def _batched(br, h, c, e, t):
+    import torch
+    dev = torch.device("cuda:0")
+    B, T = h.shape[:2]
+    L = e.shape[1]
+    th, tc, te = (torch.from_numpy(x).to(dev) for x in (h, c, e))
+    tt = torch.full((B,), t, dtype=torch.float32, device=dev)
+    out = torch.empty((B, T, 64), dtype=torch.float32, device=dev)
+    torch.cuda.synchronize()
+    br.dit_forward_batched_device(B, T, L, th.data_ptr(), tc.data_ptr(), te.data_ptr(), 0, 0, tt.data_ptr(),
+                                  tt.data_ptr(), out.data_ptr(), 0)
+    br.synchronize()
+    return out.cpu().numpy()
+
+
+@pytest.mark.parametrize("width", ["tiny", "full"])
+def test_fused_qkv_prep_is_bit_exact(tiny_ckpt, monkeypatch, width):
+    """The QKV / cross-q GEMMs with QK-norm, RoPE and the attention re-layout fused into their epilogue
+    (EPI_QKV_PREP) give the same bits as the f32 store + attn_prep pair (ACE_MI_UNFUSED_PREP=1): batched
+    items whose token counts are not multiples of 16 or of the GEMM's row tile, so V^T key groups are cut
+    by chunk and item edges."""
+    from acestep_mi355x.capi import GGMLCAPIBridge
+    if width == "tiny":
+        d, H, cases = tiny_ckpt, 256, [(1, 37, 5), (2, 301, 9), (3, 1001, 17)]
+    else:
+        from acestep_mi355x.synthetic import cached_checkpoint, make_config
+        d, H, cases = cached_checkpoint(make_config(num_hidden_layers=2), seed=0, backend="torch"), 2048, [(2, 601, 64)]
+        monkeypatch.setenv("ACE_GGML_DIT_MAX_LAYERS", "2")
+    rng = np.random.default_rng(8)
+    outs = {}
+    for fused in (True, False):
+        if fused:
+            monkeypatch.delenv("ACE_MI_UNFUSED_PREP", raising=False)
+        else:
+            monkeypatch.setenv("ACE_MI_UNFUSED_PREP", "1")
+        br = GGMLCAPIBridge()
+        br.load_dit(d)
+        for B, T, L in cases:
+            r = np.random.default_rng(B * 7 + T)
+            h = r.standard_normal((B, T, 64)).astype(np.float32)
+            c = r.standard_normal((B, T, 128)).astype(np.float32)
+            e = r.standard_normal((B, L, H)).astype(np.float32)
+            outs[(fused, B, T)] = _batched(br, h, c, e, 0.7)
+        br.close()
+    for B, T, L in cases:
+        a, b = outs[(True, B, T)], outs[(False, B, T)]
+        assert np.isfinite(a).all()
+        np.testing.assert_array_equal(a, b, err_msg=f"B={B} T={T}")
