@@ -17,8 +17,8 @@ once over RCCL before the timed region; no collective inside it.
 
 Prints ONE JSON line on rank 0 (driver contract), with `roofline` for the
 dominant kernel (the MLP gate|up GEMM, measured with HIP events on the launch
-stream) and `cpu_baseline` (the numpy oracle restatement of ggml's forward_dit on
-the host cores, one 240 s forward).
+stream) and `cpu_baseline` (oracle/cpu/dit_cpu.cpp, the C++/OpenMP restatement of ggml's CPU
+forward_dit, on the host cores: one 240 s forward plus the configs[0] 10 s F16 forward).
 """
 import argparse
 import json
@@ -193,7 +193,7 @@ def main():
                     "frac_of_bf16_peak": round(per_layer * info.num_layers / (lin_ms / 1000.0) / 1e12
                                                / BF16_PEAK_TFLOPS, 4)}
 
-    # ---- CPU baseline: the numpy oracle (restatement of ggml forward_dit) on the host cores
+    # ---- CPU baseline: the C++/OpenMP restatement of ggml's CPU forward_dit on the host cores
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and os.environ.get("ACE_MI_CPU_BASELINE", "1") != "0":
         try:
@@ -257,31 +257,51 @@ def pmc_traffic(T, L, b_loc, weights):
         return None
 
 
-def cpu_baseline(ckpt, T, L, qtype=None):
-    """Time one 240 s DiT forward of the numpy oracle (the checker restatement of ggml's CPU graph,
-    oracle/dit_oracle.py) on the host; steps/s = 1 / seconds."""
-    import numpy as np
+def _cpu_model():
     try:
-        from threadpoolctl import threadpool_info
-        cores = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
-    except Exception:  # noqa: BLE001
-        cores = os.cpu_count() or 1
-    from oracle.dit_oracle import DitWeights, forward_dit
-    if qtype not in (None, "q8_0"):
-        qtype = None  # the numpy K-quant encoder is too slow for 1.5 B weights; time the bf16 graph
-    W = DitWeights(ckpt, qtype=qtype)
-    rng = np.random.default_rng(1234)
-    h = rng.standard_normal((T, 64)).astype(np.float32)
-    c = np.concatenate([rng.standard_normal((T, 64)), np.ones((T, 64))], axis=1).astype(np.float32)
-    e = rng.standard_normal((L, W.cfg.hidden_size)).astype(np.float32)
-    t0 = time.perf_counter()
-    forward_dit(W, h, c, e, None, None, T, L, 0.9, 0.9)
-    sec = time.perf_counter() - t0
-    return {"value": round(1.0 / sec, 5), "unit": "steps/s", "cores": cores, "kind": "port",
-            "seconds_per_step": round(sec, 3),
-            "sample": f"1 full 24-layer DiT forward, T={T}, L={L}, bs=1 (numpy/OpenBLAS f32 restatement "
-                      f"of acestep_ggml forward_dit, {qtype or 'bf16'} weights, ggml's activation rounding for "
-                      "that weight type)"}
+        with open("/proc/cpuinfo", "r", encoding="utf-8") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(ckpt, T, L, qtype=None):
+    """The acestep_ggml CPU path, restated in C++/OpenMP (oracle/cpu/dit_cpu.cpp: ggml-cpu's precision
+    rules, vdpbf16ps / vcvtph2ps dot products, streamed f32 attention) because ggml itself cannot be built
+    (SURVEY §8c), timed on the host cores: one full 24-layer forward of the bench workload (steps/s =
+    1 / seconds) and BASELINE configs[0] (10 s, F16 weights, bs = 1).  Bench infrastructure only."""
+    from acestep_mi355x.synthetic import cached_checkpoint, make_config
+    from oracle import cpu_restatement as cr
+    from oracle.dit_oracle import DitWeights
+    import numpy as np
+    cr.build()
+    threads = int(os.environ.get("OMP_NUM_THREADS") or (os.cpu_count() or 1))
+
+    def one(ckpt_dir, T_, L_, seed):
+        cd = cr.CpuDit(DitWeights(ckpt_dir))
+        rng = np.random.default_rng(seed)
+        h = rng.standard_normal((T_, 64)).astype(np.float32)
+        c = np.concatenate([rng.standard_normal((T_, 64)), np.ones((T_, 64))], axis=1).astype(np.float32)
+        e = rng.standard_normal((L_, cd.cfg.hidden_size)).astype(np.float32)
+        t0 = time.perf_counter()
+        out = cd.forward(h, c, e, None, None, T_, L_, 0.9, 0.9)
+        sec = time.perf_counter() - t0
+        cd.close()
+        return sec, bool(np.isfinite(out).all())
+
+    sec, finite = one(ckpt, T, L, 1234)
+    c0 = cached_checkpoint(make_config(), seed=0, dtype="F16", backend="torch")
+    sec0, finite0 = one(c0, 250, 512, 1234)
+    return {"value": round(1.0 / sec, 5), "unit": "steps/s", "cores": threads, "kind": "port",
+            "impl": "restatement-cpp (oracle/cpu/dit_cpu.cpp, OpenMP, " + cr.isa_name() + ")",
+            "cpu": _cpu_model(), "seconds_per_step": round(sec, 3), "finite": finite and finite0,
+            "sample": f"1 full 24-layer DiT forward, T={T}, L={L}, bs=1, bf16 weights (ggml CPU precision rules; "
+                      f"GPU line: {qtype or 'bf16'}), attention streamed (a lower bound on ggml's materialised scores)",
+            "configs0": {"workload": "acestep_ggml CPU DiT single forward, 10 s (T=250), L=512, bs=1, F16 weights",
+                         "seconds_per_forward": round(sec0, 3), "steps_per_s": round(1.0 / sec0, 4)}}
 
 
 if __name__ == "__main__":

@@ -488,6 +488,24 @@ def forward_dit(W: DitWeights, hidden_states, context_latents, encoder_hidden_st
     return np.ascontiguousarray(y2[:seq_len].astype(np.float32))
 
 
+def forward_with_floor_stats(W: DitWeights, *args, perturb: float = 1e-7, **kw):
+    """(out, floor_l2, floor_max): forward_with_floor's output and floor, plus the floor of the
+    element-wise metric -- the max relative change over elements with |out| > 1e-2 rms(out) (SURVEY
+    §8(d)'s max-abs-rel) under the same perturbation."""
+    out = forward_dit(W, *args, **kw)
+    old = ggml_numerics.MULMAT_PERTURB
+    ggml_numerics.MULMAT_PERTURB = perturb
+    try:
+        pert = forward_dit(W, *args, **kw)
+    finally:
+        ggml_numerics.MULMAT_PERTURB = old
+    o64, p64 = out.astype(np.float64), pert.astype(np.float64)
+    floor = float(np.linalg.norm(p64 - o64) / np.linalg.norm(o64))
+    sel = np.abs(o64) > 1e-2 * np.sqrt(np.mean(o64 * o64))
+    fmax = float(np.max(np.abs(p64 - o64)[sel] / np.abs(o64[sel]))) if sel.any() else 0.0
+    return out, floor, fmax
+
+
 def forward_with_floor(W: DitWeights, *args, perturb: float = 1e-7, **kw):
     """(out, floor): the oracle output and its relative L2 change when every mul_mat result is
     perturbed by `perturb` (a stand-in for another f32 summation order).  bf16 activation

@@ -430,10 +430,21 @@ def mul_mat(w: GgmlWeight, x: np.ndarray) -> np.ndarray:
     return y
 
 
+# Optional block encoder (values [rows][K] f32, qtype) -> packed ggml blocks, used by make_weight instead of
+# the numpy encoders below.  The tests set it to the product library's C++ encoder (acestep_mi355x.capi.
+# quantize) for large K-quant checkpoints, where the numpy make_qkx2_quants search takes minutes: the two
+# encoders are byte-identical (tests/test_quant_cpu.py), and the dequantization stays this module's.
+QUANTIZER = None
+
+
 def make_weight(f32_values: np.ndarray, src_dtype: str, qtype: str | None) -> GgmlWeight:
     """`load_tensor_2d_transposed` + `try_quantize_matrix` (acestep_dit_model.cpp:156-192,228-277):
     quantize when a qtype is requested and in_dim % block == 0, else keep the file dtype."""
     v = np.asarray(f32_values, dtype=np.float32)
+    if QUANTIZER is not None and qtype in ("q4_k", "q6_k") and v.shape[1] % QK_K == 0:
+        raw = np.asarray(QUANTIZER(v, qtype), dtype=np.uint8)
+        deq = dequantize_q4_k(raw) if qtype == "q4_k" else dequantize_q6_k(raw)
+        return GgmlWeight(deq.reshape(v.shape), qtype, raw=raw)
     if qtype == "q8_0" and v.shape[1] % QK8_0 == 0:
         d, q = quantize_q8_0_weights(v)
         return GgmlWeight(dequantize_q8_0(d, q), "q8_0", raw=pack_q8_0(d, q))

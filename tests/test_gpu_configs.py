@@ -1,0 +1,164 @@
+"""GPU parity at the BASELINE.json workloads, each against the oracle (not only against the library's own
+serial path):
+
+  configs[0]  F16-safetensors weights, 10 s (T = 250, N = 125), L = 512, all 24 layers
+  configs[2]  Q8_0 weights, 240 s (T = 6000, N = 3000), L = 512, 2 layers: engine arithmetic and ggml's
+  configs[3]  bs = 8 at 240 s, 2 layers, every item of one batched call
+  configs[4]  Q4_K weights at 600 s (T = 15000, N = 7500), 2 layers; the full-width VAE decode over 192
+              latent frames through the windowed plan (128-frame windows, 32 frames of overlap)
+
+Every comparison asserts both SURVEY §8(d) metrics floor-relatively: rel-L2 <= max(1e-3, 1.5 x the
+oracle's own 1e-7-perturbation spread) and the max element-wise relative error over |ref| > 1e-2 rms(ref)
+<= max(1e-3, MAX_K x the same spread of that metric) (test_gpu_forward.check).  Layer counts are capped
+with ACE_GGML_DIT_MAX_LAYERS (acestep_dit_model.cpp:1457-1464) where the numpy oracle would otherwise
+take minutes; the sequence lengths, widths and weight formats are the configs' own.
+"""
+import numpy as np
+import pytest
+
+from test_gpu_forward import check
+from test_gpu_quant import QUANT_FLOOR_K, engine_view
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+
+
+def _inputs(T, L, seed, H=2048, B=None):
+    rng = np.random.default_rng(seed)
+    shp = (T,) if B is None else (B, T)
+    h = rng.standard_normal(shp + (64,)).astype(np.float32)
+    c = np.concatenate([rng.standard_normal(shp + (64,)), np.ones(shp + (64,))], axis=-1).astype(np.float32)
+    e = rng.standard_normal(((L,) if B is None else (B, L)) + (H,)).astype(np.float32)
+    return h, c, e
+
+
+def test_config0_f16_weights_10s_full_model():
+    """configs[0]: the reference's CPU plumbing case -- F16 weights, whose activations ggml rounds to fp16
+    (3 more mantissa bits than bf16, so the floor is ~3x lower than with bf16 weights)."""
+    from acestep_mi355x.capi import GGMLCAPIBridge
+    from acestep_mi355x.synthetic import cached_checkpoint, make_config
+    from oracle.dit_oracle import DitWeights, forward_with_floor_stats
+    d = cached_checkpoint(make_config(), seed=0, dtype="F16", backend="torch")
+    T, L = 250, 512
+    h, c, e = _inputs(T, L, 1234)
+    br = GGMLCAPIBridge()
+    br.load_dit(d)
+    got = br.dit_forward_tfirst(h, c, e, None, None, 0.6428571429, 0.6428571429)
+    br.close()
+    ref, floor, fmax = forward_with_floor_stats(DitWeights(d), h, c, e, None, None, T, L, 0.6428571429,
+                                                0.6428571429)
+    l2 = check(got, ref, floor, "configs[0] F16 10 s, 24 layers", fmax)
+    print(f"configs[0]: rel_l2 {'<=' if l2 <= 1e-3 else '>'} 1e-3 (north-star literal bound)")
+
+
+@pytest.mark.parametrize("qtype,T,seed", [("q8_0", 6000, 2), ("q4_k", 15000, 4)])
+def test_quantized_configs_full_width(monkeypatch, qtype, T, seed):
+    """configs[2] (Q8_0, 240 s) and configs[4] (Q4_K, 600 s) at full width: vs the oracle on the same
+    quantized bytes with the engine's arithmetic (bf16 activations x bf16(dequant W)), floor-relative,
+    and vs ggml's own Q8_0 / Q8_K activation quantization within QUANT_FLOOR_K x that path's floor."""
+    from acestep_mi355x import capi
+    from acestep_mi355x.capi import GGMLCAPIBridge
+    from acestep_mi355x.synthetic import cached_checkpoint, make_config
+    from oracle import ggml_numerics
+    from oracle.dit_oracle import DitWeights, forward_with_floor, forward_with_floor_stats
+    d = cached_checkpoint(make_config(num_hidden_layers=2), seed=0, backend="torch")
+    monkeypatch.setenv("ACE_GGML_DIT_MAX_LAYERS", "2")
+    monkeypatch.setenv("ACE_GGML_DIT_WEIGHT_QTYPE", qtype)
+    L = 512
+    h, c, e = _inputs(T, L, seed)
+    br = GGMLCAPIBridge()
+    br.load_dit(d)
+    got = br.dit_forward_tfirst(h, c, e, None, None, 0.75, 0.75)
+    br.close()
+    monkeypatch.setattr(ggml_numerics, "QUANTIZER", capi.quantize)  # byte-identical C++ encoder (K-quants)
+    W = DitWeights(d, qtype=qtype)
+    ref, floor, fmax = forward_with_floor_stats(engine_view(W), h, c, e, None, None, T, L, 0.75, 0.75, max_layers=2)
+    check(got, ref, floor, f"{qtype} T={T} (dequant semantics)", fmax)
+    gref, gfloor = forward_with_floor(W, h, c, e, None, None, T, L, 0.75, 0.75, max_layers=2)
+    l2 = float(np.linalg.norm(got.astype(np.float64) - gref) / np.linalg.norm(gref.astype(np.float64)))
+    print(f"{qtype} T={T} vs ggml Q8 activation semantics: rel_l2={l2:.3e} floor={gfloor:.3e} ratio={l2 / gfloor:.2f}")
+    assert l2 <= QUANT_FLOOR_K * gfloor, (l2, gfloor)
+
+
+def test_config3_batch8_240s_every_item():
+    """configs[3]'s per-GPU work at bs = 8: one batched call over 8 items of 240 s (M = 24000 rows: the
+    256x256 GEMM tiles and the bs-8 attention grid), every item vs the oracle with its own timestep."""
+    import torch
+    from acestep_mi355x.capi import GGMLCAPIBridge
+    from acestep_mi355x.synthetic import cached_checkpoint, make_config
+    from oracle.dit_oracle import DitWeights, forward_dit, forward_with_floor_stats
+    import os
+    d = cached_checkpoint(make_config(num_hidden_layers=2), seed=0, backend="torch")
+    os.environ["ACE_GGML_DIT_MAX_LAYERS"] = "2"
+    try:
+        B, T, L = 8, 6000, 512
+        h, c, e = _inputs(T, L, 88, B=B)
+        ts = np.linspace(1.0, 0.3, B).astype(np.float32)
+        dev = torch.device("cuda:0")
+        th, tc, te, tt = (torch.from_numpy(x).to(dev) for x in (h, c, e, ts))
+        out = torch.empty((B, T, 64), dtype=torch.float32, device=dev)
+        br = GGMLCAPIBridge()
+        br.load_dit(d)
+        torch.cuda.synchronize()
+        br.dit_forward_batched_device(B, T, L, th.data_ptr(), tc.data_ptr(), te.data_ptr(), 0, 0, tt.data_ptr(),
+                                      tt.data_ptr(), out.data_ptr(), 0)
+        br.synchronize()
+        got = out.cpu().numpy()
+        br.close()
+    finally:
+        os.environ.pop("ACE_GGML_DIT_MAX_LAYERS", None)
+    W = DitWeights(d)
+    _, floor, fmax = forward_with_floor_stats(W, h[0], c[0], e[0], None, None, T, L, float(ts[0]), float(ts[0]),
+                                              max_layers=2)
+    for b in range(B):
+        ref = forward_dit(W, h[b], c[b], e[b], None, None, T, L, float(ts[b]), float(ts[b]), max_layers=2)
+        check(got[b], ref, floor, f"configs[3] bs=8 item {b}", fmax)
+
+
+def _python_plan(T, chunk, overlap):
+    """The reference tiled-decode window plan (scripts/run_non_ggml_real_case.py:597-611), restated."""
+    overlap = min(overlap, max(0, chunk // 2 - 1))
+    stride = chunk - 2 * overlap
+    return [(cs, min(cs + stride, T), max(0, cs - overlap), min(T, cs + stride + overlap))
+            for cs in range(0, T, stride)]
+
+
+def test_config4_vae_decode_192_frames_windowed():
+    """The full-size decoder (128 x [1,2,4,8,16] channels, hop 1920) over 192 latent frames through the
+    decode hook with 128-frame windows and 32 frames of overlap (three windows of 96 / 128 / 96 frames,
+    368,640 samples), vs the oracle decoding the same windows and trimming them the same way."""
+    import torch
+    import types
+    from acestep_mi355x.capi import GGMLCAPIBridge
+    from acestep_mi355x.hook import install_vae_backend
+    from acestep_mi355x.synthetic import VAE_FULL_CONFIG
+    from oracle import vae_oracle as V
+    from test_gpu_vae import _ckpt
+    d = _ckpt(VAE_FULL_CONFIG)
+    br = GGMLCAPIBridge()
+    br.load_vae(d)
+    handler = types.SimpleNamespace()
+    install_vae_backend(handler, br, chunk_size_default=128, overlap_default=32)
+    T = 192
+    lat = np.random.default_rng(19).standard_normal((1, 64, T)).astype(np.float32)
+    got = handler.tiled_decode(torch.from_numpy(lat).cuda(), offload_wav_to_cpu=True).numpy()[0].T
+    br.close()
+    W = V.VaeWeights(d)
+
+    def windowed():
+        parts = []
+        for cs, ce, ws, we in _python_plan(T, 128, 32):
+            wav = V.decode(W, lat[0, :, ws:we].T)
+            up = wav.shape[0] / max(1, we - ws)
+            ts, te = int(round((cs - ws) * up)), int(round((we - ce) * up))
+            parts.append(wav[ts:wav.shape[0] - te if te > 0 else wav.shape[0]])
+        return np.concatenate(parts, axis=0)
+
+    ref = windowed()
+    V.CONV_PERTURB = 1e-6
+    try:
+        pert = windowed()
+    finally:
+        V.CONV_PERTURB = 0.0
+    floor = float(np.linalg.norm(pert.astype(np.float64) - ref) / np.linalg.norm(ref.astype(np.float64)))
+    assert got.shape == ref.shape, (got.shape, ref.shape)
+    check(got, ref, floor, "full VAE, 192 frames windowed")

@@ -30,7 +30,10 @@ def _causal_ref(q, kv, hq, hkv, kmask, scale):
 
 @pytest.mark.parametrize("B,hq,hkv,n,masked", [(1, 2, 1, 64, False), (2, 16, 8, 300, False), (1, 4, 2, 257, True),
                                               (1, 4, 1, 31, False)])
-def test_causal_attention_kernel(B, hq, hkv, n, masked):
+@pytest.mark.parametrize("mode", ["f32", "fp16"])
+def test_causal_attention_kernel(B, hq, hkv, n, masked, mode):
+    """Causal mode of the attention kernel: hi/lo Q.K and P.V (the text encoder's default precision) to
+    the bf16 rounding of the output, and single-fp16 operands within fp16 + bf16 rounding."""
     from acestep_mi355x import capi
     rng = np.random.default_rng(n + hq)
     q = rng.standard_normal((B, n, hq * 128)).astype(np.float32) * 2.0
@@ -40,10 +43,11 @@ def test_causal_attention_kernel(B, hq, hkv, n, masked):
         kmask = (rng.random((B, n)) > 0.3).astype(np.int32)
         kmask[:, 0] = 1
     scale = 1.0 / np.sqrt(128.0)
-    got = capi.kernel_attention(q, kv, hq, hkv, kmask=kmask, scale=scale, split=True, causal=True)
+    f32 = mode == "f32"
+    got = capi.kernel_attention(q, kv, hq, hkv, kmask=kmask, scale=scale, split=f32, pv_split=f32, causal=True)
     ref = _causal_ref(q, kv, hq, hkv, kmask, scale)
     err = np.abs(got - ref)
-    assert np.all(err <= 2.0 ** -8 * np.abs(ref) + 1e-5), float(err.max())
+    assert np.all(err <= 2.0 ** -8 * np.abs(ref) + (1e-5 if f32 else 2e-3)), float(err.max())
 
 
 @pytest.fixture(scope="module")
@@ -91,7 +95,9 @@ def test_text_encoder_prefix_causality(text_bridge):
 def test_generate_entries_end_to_end(text_ckpt):
     """ace_ggml_generate_audio_simple / _style_lyric_simple / _style_lyric_timbre_simple on the GPU vs
     oracle/pipeline_oracle.py (same x_T: the reference's std::mt19937 stream).  8 Euler steps through
-    bf16 DiT forwards and a VAE decode amplify the per-forward floor; the bound is 2e-2 rel. L2."""
+    bf16 DiT forwards and a VAE decode amplify the per-forward floor; the bound is 5e-3 rel. L2 (~3.5x
+    the 1.3-1.4e-3 measured on MI355X) and the sample count must match exactly (the decode plan's
+    window trimming, acestep_ggml.cpp:2114-2223)."""
     from acestep_mi355x.capi import GGMLCAPIBridge
     from acestep_mi355x.synthetic import TINY_COND_CONFIG, VAE_TINY_CONFIG, write_checkpoint, write_vae_checkpoint
     from oracle import pipeline_oracle as po
@@ -119,8 +125,9 @@ def test_generate_entries_end_to_end(text_ckpt):
         else:
             ref, _ = po.generate_style_lyric_timbre(DW, VW, TW, kw.get("style_ids"), kw.get("lyric_ids"),
                                                     kw.get("refer"), seq_len, 3.0, 11 + i, hop, 2)
-        n = min(len(ref), len(got))
-        l2 = float(np.linalg.norm(got[:n] - ref[:n]) / np.linalg.norm(ref[:n]))
-        print(f"generate case {i}: rel_l2={l2:.3e} samples got={len(got)} ref={len(ref)}")
-        assert abs(len(got) - len(ref)) <= hop and l2 < 2e-2, (i, l2)
+        print(f"generate case {i}: samples got={len(got)} ref={len(ref)}")
+        assert len(got) == len(ref), (i, len(got), len(ref))
+        l2 = float(np.linalg.norm(got - ref) / np.linalg.norm(ref))
+        print(f"generate case {i}: rel_l2={l2:.3e}")
+        assert l2 < 5e-3, (i, l2)
     br.close()
