@@ -221,7 +221,7 @@ def main():
             "config": {
                 "workload": f"DiT {args.sample_steps}-step sample, {args.seconds:g} s audio "
                             f"(T={T} latent frames @25 Hz, N={(T + 1) // 2} tokens), enc_len={L}, "
-                            f"bs={b_loc}/GPU, {wdesc} weights, f32-faithful fp16x3 attention",
+                            f"bs={b_loc}/GPU, {wdesc} weights, fp16-operand f32-accumulate attention",
                 "weights": args.qtype or "bf16",
                 "sampler": "ace_mi_dit_sample_ex (device loop: batched DiT forward + Euler kernel per step)",
                 "cross_attention_cache": bool(args.cross_cache),

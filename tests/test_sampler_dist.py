@@ -41,7 +41,8 @@ def _worker(rank, world, port, B, q):
         x_local = got.noise[items] + torch.tensor(items, dtype=torch.float32)[:, None, None]
         full = gather_latents(x_local, B)
         digest = (float(got.noise.sum()), float(got.enc.sum()), int(got.mask.sum()))
-        q.put((rank, digest, None if full is None else full.clone(), got.noise.clone()))
+        # numpy, not torch tensors: a torch tensor crosses the queue as a shared fd that dies with this process
+        q.put((rank, digest, None if full is None else full.numpy().copy(), got.noise.numpy().copy()))
     finally:
         dist.destroy_process_group()
 
@@ -57,7 +58,7 @@ def test_broadcast_and_gather_world2(B):
     res = {}
     for _ in range(2):
         r, digest, full, noise = q.get(timeout=120)
-        res[r] = (digest, full, noise)
+        res[r] = (digest, None if full is None else torch.from_numpy(full), torch.from_numpy(noise))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -105,7 +106,7 @@ def _gen_worker(rank, world, port, lib, ckpt, vae, B, method, cover, decode, q):
         x = _run_flow(br, got, B, shard_indices(B, world, rank), method, cover, decode, got_nc)
         full = gather_latents(x.contiguous(), B)
         br.close()
-        q.put((rank, None if full is None else full.clone()))
+        q.put((rank, None if full is None else full.numpy().copy()))
     finally:
         dist.destroy_process_group()
 
@@ -145,7 +146,7 @@ def test_sharded_flow_equals_single_process(tiny_ckpt, tiny_vae, world, B, metho
              for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=600) for _ in range(world))
+    res = {r: (None if a is None else torch.from_numpy(a)) for r, a in (q.get(timeout=600) for _ in range(world))}
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
