@@ -236,33 +236,25 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
 // written straight into the attention operand layouts with attn_prep's arithmetic (prep_math.h): 16
 // lanes per token for q / k (QK-RMSNorm, RoPE, fp16 hi/lo), one lane per (d, 16-key group) for V^T.
 // This removes the f32 [M][4096] round trip through HBM and the separate prep launch.
-template <int BM, int NW, int TM, int TN, int SMEM>
-__device__ __forceinline__ void qkv_prep_tile(const GemmParams& p, f32x4 (&acc)[TM][TN], int m0, int n0, int wm0,
-                                              int wn0, int tid, char* smem) {
-    constexpr int LD = 144;
+constexpr int PREP_LD = 144;  // LDS row stride (floats) of the accumulator tile in the fused prep
+
+// `fill(tile, c0, CH)` writes the block's accumulators of tile rows [c0, c0 + CH) of head `hd` (128 columns)
+// into the LDS tile (row stride PREP_LD)
+template <int BM, int NW, int SMEM, class Fill>
+__device__ __forceinline__ void qkv_prep_head(const GemmParams& p, int m0, int hd, int tid, char* smem, Fill fill) {
+    constexpr int LD = PREP_LD;
     constexpr int CH = (BM * LD * 4 <= SMEM) ? BM : ((BM / 2) * LD * 4 <= SMEM ? BM / 2 : BM / 4);
     static_assert(CH * LD * 4 <= SMEM && BM % CH == 0 && CH % 16 == 0, "qkv prep chunking");
     constexpr int NT = NW * 64;
     const PrepArgs& a = p.e.prep;
     float* tile = reinterpret_cast<float*>(smem);
-    const int lane = tid & 63;
-    const int ccol = lane & 15, crow = (lane >> 4) * 4;
     const int nq = a.q_col >= 0 ? a.hq : 0;
     const int nk = a.k_col >= 0 ? a.hkv : 0;
-    const int hd = n0 >> 7;
     for (int c0 = 0; c0 < BM; c0 += CH) {
         const int mc0 = m0 + c0;
         if (mc0 >= p.M) break;
         __syncthreads();  // the main loop's (or the previous chunk's) LDS readers are done
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-            const int rb = wm0 + i * 16 - c0;
-            if (rb < 0 || rb >= CH) continue;
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-#pragma unroll
-                for (int j = 0; j < TN; ++j) tile[(rb + crow + r) * LD + wn0 + j * 16 + ccol] = acc[i][j][r];
-        }
+        fill(tile, c0, CH);
         __syncthreads();
         const int rows = min(CH, p.M - mc0);
         if (hd < nq + nk) {
@@ -325,6 +317,25 @@ __device__ __forceinline__ void qkv_prep_tile(const GemmParams& p, f32x4 (&acc)[
             }
         }
     }
+}
+
+// the 4-wave kernels' fused prep: the block's BM x 128 tile is one head, wave tile TM x TN at (wm0, wn0)
+template <int BM, int NW, int TM, int TN, int SMEM>
+__device__ __forceinline__ void qkv_prep_tile(const GemmParams& p, f32x4 (&acc)[TM][TN], int m0, int n0, int wm0,
+                                              int wn0, int tid, char* smem) {
+    const int lane = tid & 63;
+    const int ccol = lane & 15, crow = (lane >> 4) * 4;
+    qkv_prep_head<BM, NW, SMEM>(p, m0, n0 >> 7, tid, smem, [&](float* tile, int c0, int CH) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int rb = wm0 + i * 16 - c0;
+            if (rb < 0 || rb >= CH) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) tile[(rb + crow + r) * PREP_LD + wn0 + j * 16 + ccol] = acc[i][j][r];
+        }
+    });
 }
 
 // PIPE 0: stage(t+1) ; compute(t) ; vmcnt(0) ; __syncthreads        (2 LDS buffers)
@@ -502,6 +513,200 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(GemmParams p) {
         gemm_epilogue<TM, TN, F16, EPI, NW>(p, acc, m0 + wm0, n0 + wn0, lane);
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// 8-wave ping-pong GEMM: BM x 256 tile, 512 threads as 2 (M) x 4 (N) waves, two wave groups
+// (wr = 0 / 1, one wave of each on every SIMD) offset by one barrier, so one group's MFMA segment
+// runs while the other group issues its LDS reads and LDS-DMA (CDNA guide §5, "256² 8-phase
+// template": 8 barrier-separated segments per K-tile pair, counted vmcnt, raw s_barrier, setprio).
+//
+// A K-tile (64 deep) lives in one of two LDS buffers as four half-tiles: A0 / A1 (rows [0, BM/2),
+// [BM/2, BM)) and B0 / B1 (columns [0, 128), [128, 256)).  A wave owns rows wr*QM*16.. of each A half
+// and columns wc*32.. of each B half, i.e. four QM x 2 quadrants of 16x16 accumulators, one per phase:
+//   ph1: read A0, B0 -> acc[0][0]   stage B1(t+1)
+//   ph2: read B1     -> acc[0][1]   stage A1(t+1)
+//   ph3: read A1     -> acc[1][1]   stage A0(t+2)
+//   ph4: (no reads)  -> acc[1][0]   stage B0(t+2)
+// Each phase: ds_reads, one half-tile of LDS-DMA, vmcnt(keep the 4 youngest half-tiles), barrier,
+// lgkmcnt(0), MFMAs, barrier.  A half-tile is re-staged >= 2 phases after its last read (WAR across
+// the staggered groups) and read >= 1 phase after the wait that retires it (RAW); stages past the
+// last K-tile go to a scratch LDS region so the per-phase vmcnt counts stay uniform.
+template <int BM, bool F16, int EPI>
+__global__ void __launch_bounds__(512) gemm8_kernel(GemmParams p) {
+    constexpr int BN = 256, BK = 64, ROWB = BK * 2;
+    constexpr int HA = BM / 2;         // rows per A half-tile
+    constexpr int QM = BM / 64;        // 16-row tiles per wave per A half
+    constexpr int QN = 2;              // 16-col tiles per wave per B half
+    constexpr int PA = HA / 8;         // 1 KiB LDS-DMA pieces per A half (B half: 16)
+    constexpr int STAGE = (BM + BN) * ROWB;
+    constexpr int SCRATCH = 2 * STAGE;
+    static_assert(BM == 256 || BM == 192, "gemm8 tile rows");
+    static_assert(EPI != EPI_SWIGLU || (QN % 2 == 0), "swiglu needs column pairs");
+
+    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 16 * 1024];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wid = tid >> 6;
+    const int wr = wid >> 2, wc = wid & 3;
+    int m0, n0;
+    block_tile<BM, BN>(p, m0, n0);
+    const int M = p.M;
+    const int nk = p.K / BK;
+
+    // LDS-DMA sources: this wave stages pieces wid and wid + 8 of every half-tile (A halves of BM = 192
+    // have 12 pieces: waves 4..7 stage one).  Piece rows are wid*8 + (lane >> 3) (+ 64, + half offset),
+    // all with the same chunk swizzle since the offsets are multiples of 16 rows.
+    constexpr bool A2 = PA == 16;
+    const bool a_second = A2 || wid + 8 < PA;
+    const int prow = wid * 8 + (lane >> 3);
+    const int pch = (lane & 7) ^ swz(prow);
+    const uint16_t* srcA[2][2];
+    const uint16_t* srcB[2][2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int ra = min(m0 + h * HA + j * 64 + prow, M - 1);
+            srcA[h][j] = p.A + (int64_t)ra * p.lda + pch * 8;
+            srcB[h][j] = p.W + (int64_t)(n0 + h * 128 + j * 64 + prow) * p.ldw + pch * 8;
+        }
+    auto stage_a = [&](int h, int t) {
+        char* dst = t < nk ? smem + (t & 1) * STAGE + h * HA * ROWB : smem + SCRATCH;
+        const int kt = min(t, nk - 1);
+        __builtin_amdgcn_global_load_lds((const void*)(srcA[h][0] + kt * BK), (lds_void*)(dst + wid * 1024), 16, 0, 0);
+        if (a_second)
+            __builtin_amdgcn_global_load_lds((const void*)(srcA[h][1] + kt * BK), (lds_void*)(dst + (wid + 8) * 1024),
+                                             16, 0, 0);
+    };
+    auto stage_b = [&](int h, int t) {
+        char* dst = t < nk ? smem + (t & 1) * STAGE + (BM + h * 128) * ROWB : smem + SCRATCH;
+        const int kt = min(t, nk - 1);
+        __builtin_amdgcn_global_load_lds((const void*)(srcB[h][0] + kt * BK), (lds_void*)(dst + wid * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)(srcB[h][1] + kt * BK), (lds_void*)(dst + (wid + 8) * 1024), 16,
+                                         0, 0);
+    };
+    // retire all but the 4 youngest half-tiles (2 A + 2 B in any 4 consecutive phases) of this wave
+    auto wait_stages = [&]() {
+        if (a_second)
+            wait_vmcnt<8>();
+        else
+            wait_vmcnt<6>();
+    };
+
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+    const int lrow = lane & 15, lchunk = lane >> 4;
+    const int rsw = (lrow >> 1) & 7;
+    auto read_a = [&](int buf, int h, uint4 (&a)[QM][2]) {
+        const uint32_t base = lds0 + buf * STAGE + (h * HA + wr * QM * 16 + lrow) * ROWB;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) ReadRows<0, QM, 16 * ROWB>::run(base + (((kk * 4 + lchunk) ^ rsw) * 16), a, kk);
+    };
+    auto read_b = [&](int buf, int h, uint4 (&b)[QN][2]) {
+        const uint32_t base = lds0 + buf * STAGE + (BM + h * 128 + wc * 32 + lrow) * ROWB;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) ReadRows<0, QN, 16 * ROWB>::run(base + (((kk * 4 + lchunk) ^ rsw) * 16), b, kk);
+    };
+
+    f32x4 acc[2][2][QM][QN];
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y)
+#pragma unroll
+            for (int i = 0; i < QM; ++i)
+#pragma unroll
+                for (int j = 0; j < QN; ++j) acc[x][y][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    auto mma = [&](const uint4 (&a)[QM][2], const uint4 (&b)[QN][2], f32x4 (&c)[QM][QN]) {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int i = 0; i < QM; ++i)
+#pragma unroll
+                for (int j = 0; j < QN; ++j) c[i][j] = mfma16<F16>(a[i][kk], b[j][kk], c[i][j]);
+        __builtin_amdgcn_s_setprio(0);
+    };
+    // segment boundary: the barrier that hands over to the other group
+    auto seg = [&]() { __builtin_amdgcn_s_barrier(); };
+
+    // prologue: A0 B0 B1 A1 of tile 0, A0 B0 of tile 1 (the steady-state stage order)
+    stage_a(0, 0);
+    stage_b(0, 0);
+    stage_b(1, 0);
+    stage_a(1, 0);
+    stage_a(0, 1);
+    stage_b(0, 1);
+    wait_stages();
+    __builtin_amdgcn_s_barrier();
+    if (wr == 1) __builtin_amdgcn_s_barrier();  // group 1 runs one segment behind group 0
+
+    uint4 a[QM][2], b0[QN][2], b1[QN][2];
+    for (int kt = 0; kt < nk; ++kt) {
+        const int buf = kt & 1;
+        // ph1
+        read_a(buf, 0, a);
+        read_b(buf, 0, b0);
+        stage_b(1, kt + 1);
+        wait_stages();
+        seg();
+        lds_wait_all();
+        mma(a, b0, acc[0][0]);
+        seg();
+        // ph2
+        read_b(buf, 1, b1);
+        stage_a(1, kt + 1);
+        wait_stages();
+        seg();
+        lds_wait_all();
+        mma(a, b1, acc[0][1]);
+        seg();
+        // ph3: ph4 reads nothing, so no stage has to retire here (a wait here measured neutral)
+        read_a(buf, 1, a);
+        stage_a(0, kt + 2);
+        seg();
+        lds_wait_all();
+        mma(a, b1, acc[1][1]);
+        seg();
+        // ph4
+        stage_b(0, kt + 2);
+        wait_stages();
+        seg();
+        __builtin_amdgcn_sched_barrier(0);
+        mma(a, b0, acc[1][0]);
+        seg();
+    }
+    if (wr == 0) __builtin_amdgcn_s_barrier();  // both groups now at the same barrier count
+    wait_vmcnt<0>();                            // the scratch-region stages of the last tiles
+
+    if constexpr (EPI == EPI_QKV_PREP) {
+        const int ccol = lane & 15, crow = (lane >> 4) * 4;
+#pragma unroll
+        for (int hb = 0; hb < 2; ++hb)
+            qkv_prep_head<BM, 8, 2 * STAGE>(p, m0, (n0 >> 7) + hb, tid, smem, [&](float* tile, int c0, int CH) {
+#pragma unroll
+                for (int ha = 0; ha < 2; ++ha)
+#pragma unroll
+                    for (int i = 0; i < QM; ++i) {
+                        const int rb = ha * HA + wr * QM * 16 + i * 16 - c0;
+                        if (rb < 0 || rb >= CH) continue;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+#pragma unroll
+                            for (int j = 0; j < QN; ++j)
+                                tile[(rb + crow + r) * PREP_LD + wc * 32 + j * 16 + ccol] = acc[ha][hb][i][j][r];
+                    }
+            });
+    } else {
+#pragma unroll
+        for (int ha = 0; ha < 2; ++ha)
+#pragma unroll
+            for (int hb = 0; hb < 2; ++hb)
+                gemm_epilogue<QM, QN, F16, EPI, 8>(p, acc[ha][hb], m0 + ha * HA + wr * QM * 16,
+                                                   n0 + hb * 128 + wc * 32, lane);
+    }
+}
 
 // ---------------------------------------------------------------------------------------------
 // Dequant-fused variant: W arrives as a ggml block format re-laid out at load (runtime/quant.h).
@@ -763,9 +968,17 @@ void launch_cfg(const GemmParams& p, hipStream_t s) {
         hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, F16, EPI, PIPE>), grid, block, 0, s, p);
 }
 
+template <int BM, bool F16, int EPI>
+void launch_cfg8(const GemmParams& p, hipStream_t s) {
+    if (p.N % 256 != 0) throw std::runtime_error("gemm: the 8-wave tiles need N % 256 == 0");
+    const int nbm = (p.M + BM - 1) / BM;
+    hipLaunchKernelGGL((gemm8_kernel<BM, F16, EPI>), dim3(nbm * (p.N / 256)), dim3(512), 0, s, p);
+}
+
 // variant: 0 = 128x128 PIPE0, 1 = 128x128 PIPE1, 2 = 256x256 PIPE1 (8 waves 2x4), 3 = 256x128 PIPE1,
 // 4 = 192x128 PIPE1, 5 = 192x256 PIPE1 (8 waves 2x4), 6 = 192x64 PIPE1 (dense only), 7 = 96x128 PIPE1,
-// 8 = 64x128 PIPE1, 9 = 64x64 PIPE1 (8, 9 dense only: short sequences)
+// 8 = 64x128 PIPE1, 9 = 64x64 PIPE1 (8, 9 dense only: short sequences), 10 = 256x256 / 11 = 192x256 8-wave
+// ping-pong (dense only, N % 256 == 0)
 template <bool F16, int EPI>
 void launch_variant(int variant, const GemmParams& p, hipStream_t s) {
     switch (variant) {
@@ -779,6 +992,8 @@ void launch_variant(int variant, const GemmParams& p, hipStream_t s) {
         case 7: launch_cfg<96, 128, 2, 2, F16, EPI, 1>(p, s); break;
         case 8: launch_cfg<64, 128, 2, 2, F16, EPI, 1>(p, s); break;
         case 9: launch_cfg<64, 64, 2, 2, F16, EPI, 1>(p, s); break;
+        case 10: launch_cfg8<256, F16, EPI>(p, s); break;
+        case 11: launch_cfg8<192, F16, EPI>(p, s); break;
         default: throw std::runtime_error("gemm: bad variant");
     }
 }
@@ -850,8 +1065,13 @@ int g_forced_variant = -1;
 // o / cross 662 vs 569).
 double m_edge(int M, int bm) { return (double)M / (double)(((M + bm - 1) / bm) * bm); }
 
-int pick_variant(int M, int N, bool quant) {
-    if (g_forced_variant >= 0) return g_forced_variant;
+int pick_variant(int M, int N, int K, bool quant) {
+    if (g_forced_variant >= 0) {  // forced (tests / micro-benchmarks), where that tile supports the shape
+        const int f = g_forced_variant;
+        const bool wide = f == 2 || f == 5 || f == 10 || f == 11;
+        const bool dense_only = f == 6 || f >= 8;
+        if (!(wide && N % 256 != 0) && !(quant && dense_only)) return f;
+    }
     const int64_t mb192 = (M + 191) / 192;
     const bool edge_ok = m_edge(M, 192) >= m_edge(M, 128) - 0.02;
     if (quant) {
@@ -859,7 +1079,16 @@ int pick_variant(int M, int N, bool quant) {
         if (m_edge(M, 96) >= m_edge(M, 128) - 0.02) return 7;  // down 590 vs 493, o / cross 474 vs 396
         return 1;
     }
-    if (N % 256 == 0 && M >= 8192) return 2;
+    // 8-wave ping-pong tiles for batched sequences (tools/gemm_msweep.py on MI355X, TFLOP/s): M = 12000 gate|up
+    // 1011 (256x256) vs 941 (v2), qkv 933 vs 902, down 922 (192x256) vs 818, o 814 vs 786; M = 24000 gate|up
+    // 1089 vs 1016, qkv 941 vs 897, down 955 vs 915, o 767 (v2) vs 724; M = 6000 down 921 (192x256) vs 853.
+    // At M = 3000 the 4-wave tiles stay ahead (their second block per CU hides prologue and epilogue).
+    if (N % 256 == 0 && M >= 8192) {
+        if (N >= 4096) return 10;
+        if (M >= 20000) return K >= 4096 ? 10 : 2;
+        return 11;
+    }
+    if (N % 256 == 0 && M >= 4500 && N <= 2048 && K >= 4096) return 11;
     if (edge_ok && mb192 * (N / 128) >= 384) return 4;
     // short sequences (60 s: M = 750): too few 96-row tiles to cover the CUs -> 64-row tiles, and
     // 64x64 when even those leave CUs idle (M = 750: N = 2048 projections 273-337 -> 364-453 TFLOP/s,
@@ -878,7 +1107,7 @@ void launch_gemm(const uint16_t* A, int lda, const WeightView& W, int M, int N, 
     ACEMI_CHECK(lda % 8 == 0, "gemm: leading dims must be multiples of 8");
     ACEMI_CHECK(W.q != nullptr, "gemm: null weight");
     GemmParams p{A, (const uint16_t*)W.q, W.q, W.s, lda, W.ld, M, N, K, epi};
-    int v = pick_variant(M, N, weight_quantized(W.fmt));
+    int v = pick_variant(M, N, K, weight_quantized(W.fmt));
     if (epi.kind == EPI_QKV_PREP) {  // 128-wide column tiles: one head per tile
         ACEMI_CHECK(epi.bias == nullptr && epi.prep.n_tok > 0 && M % epi.prep.n_tok == 0,
                     "gemm: fused attention prep needs no bias and whole items");

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Benchmark: ACE-Step 1.5 DiT denoising steps/s on MI355X (BASELINE.json metric).
 
-Workload (BASELINE.json configs[2] shape at bf16, see DESIGN.md "Measurement"):
+Workload (BASELINE.json configs[2]: Q8_0 weights by default, `--qtype bf16` for bf16; see DESIGN.md "Measurement"):
 240 s of audio = T = 6000 latent frames at 25 Hz (the DiT's frame rate; "5Hz" in
 BASELINE.json is the LM code rate) -> N = 3000 patch tokens, encoder
 length L = 512, full 24-layer DiT with synthetic bf16 weights of the real
@@ -48,8 +48,11 @@ def parse():
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--cross-cache", action="store_true",
                     help="reuse cross-attention K/V across steps (MLXCrossAttentionCache); off = ggml C sampler")
-    ap.add_argument("--qtype", default="", choices=["", "q8_0", "q4_k", "q6_k"],
-                    help="online weight quantization (ACE_GGML_DIT_WEIGHT_QTYPE): BASELINE configs[2] is q8_0")
+    ap.add_argument("--qtype", default="q8_0", choices=["bf16", "q8_0", "q4_k", "q6_k"],
+                    help="DiT weights: online quantization (ACE_GGML_DIT_WEIGHT_QTYPE) or bf16; the default is "
+                         "BASELINE configs[2] (240 s, bs=1, Q8_0 dequant-fused matmul)")
+    ap.add_argument("--no-bf16-line", action="store_true",
+                    help="skip the bf16-weight run that is reported beside a quantized line")
     return ap.parse_args()
 
 
@@ -83,11 +86,9 @@ def main():
     if rank != 0:
         ckpt = cached_checkpoint(cfg, seed=0, backend="torch")
 
-    if args.qtype:
-        os.environ["ACE_GGML_DIT_WEIGHT_QTYPE"] = args.qtype
-    else:
-        os.environ.pop("ACE_GGML_DIT_WEIGHT_QTYPE", None)
-        os.environ.pop("ACE_GGML_WEIGHT_QTYPE", None)
+    if args.qtype == "bf16":
+        args.qtype = ""
+    set_weights(args.qtype)
     br = GGMLCAPIBridge(device=local)
     br.load_dit(ckpt)
     wdesc = f"{args.qtype.upper()} dequant-fused (bf16 MFMA)" if args.qtype else "bf16"
@@ -178,20 +179,41 @@ def main():
             traffic = pmc_traffic(T, L, b_loc, args.qtype or "bf16")
             if traffic is not None:
                 roofline["traffic"] = traffic
-        lin = [p for p in prof if p[0].startswith("gemm_")]
-        if lin:
-            Np = (T + 1) // 2
-            M = b_loc * Np
-            H_, I_ = info.hidden_size, info.intermediate_size
-            qd, kd = info.num_heads * info.head_dim, info.num_kv_heads * info.head_dim
-            per_layer = 2.0 * M * H_ * ((qd + 2 * kd) + qd + qd + qd + 2 * I_) + 2.0 * M * I_ * H_
-            lin_ms = sum(p[1] for p in lin if p[0] in ("gemm_qkv", "gemm_o", "gemm_cross_q", "gemm_cross_o",
-                                                          "gemm_gate_up", "gemm_down")) / nprof
-            if lin_ms > 0:
-                breakdown["_dit_block_linears"] = {
-                    "tflops": round(per_layer * info.num_layers / (lin_ms / 1000.0) / 1e12, 1),
-                    "frac_of_bf16_peak": round(per_layer * info.num_layers / (lin_ms / 1000.0) / 1e12
-                                               / BF16_PEAK_TFLOPS, 4)}
+        frac = block_linear_frac(prof, nprof, T, b_loc, info)
+        if frac is not None:
+            breakdown["_dit_block_linears"] = {"tflops": round(frac * BF16_PEAK_TFLOPS, 1), "frac_of_bf16_peak": frac}
+
+    # ---- the same workload with bf16 weights, reported beside a quantized line (single GPU only)
+    bf16_line = None
+    if args.qtype and world == 1 and not args.no_bf16_line:
+        br.close()
+        set_weights("")
+        br = GGMLCAPIBridge(device=local)
+        br.load_dit(ckpt)
+        if args.warmup > 0:
+            run(0, args.warmup)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        run(args.warmup, args.steps)
+        torch.cuda.synchronize()
+        el_bf16 = time.perf_counter() - t1
+        bf16_line = {"value": round(B * args.steps / el_bf16, 3), "unit": "steps/s",
+                     "ms_per_step": round(1000.0 * el_bf16 / args.steps, 3),
+                     "workload": "the same 240 s bs=1 sampling loop with bf16 weights (no quantization)"}
+        if not args.no_profile:
+            br.profile_enable(True)
+            br.profile_reset()
+            for i in range(2):
+                step(i)
+            torch.cuda.synchronize()
+            prof_b = br.profile_get()
+            br.profile_enable(False)
+            frac = block_linear_frac(prof_b, 2, T, b_loc, info)
+            if frac is not None:
+                bf16_line["dit_block_linears_frac_of_bf16_peak"] = frac
+            gu = [p for p in prof_b if p[0] == "gemm_gate_up"]
+            if gu:
+                bf16_line["gate_up_avg_launch_us"] = round(1000.0 * gu[0][1] / gu[0][2], 2)
 
     # ---- CPU baseline: the C++/OpenMP restatement of ggml's CPU forward_dit on the host cores
     cpu = None
@@ -219,7 +241,8 @@ def main():
             "data": "synthetic: random N(0,0.02) bf16 weights with the real DiT tensor names/shapes; "
                     "N(0,1) latents/conditioning",
             "config": {
-                "workload": f"DiT {args.sample_steps}-step sample, {args.seconds:g} s audio "
+                "workload": ("BASELINE configs[2]: " if (args.qtype == "q8_0" and args.seconds == 240.0 and b_loc == 1)
+                             else "") + f"DiT {args.sample_steps}-step sample, {args.seconds:g} s audio "
                             f"(T={T} latent frames @25 Hz, N={(T + 1) // 2} tokens), enc_len={L}, "
                             f"bs={b_loc}/GPU, {wdesc} weights, fp16-operand f32-accumulate attention",
                 "weights": args.qtype or "bf16",
@@ -232,6 +255,7 @@ def main():
             },
             "finite": finite,
             "roofline": roofline,
+            "bf16_line": bf16_line,
             "cpu_baseline": cpu,
             "breakdown": breakdown,
         }
@@ -239,6 +263,29 @@ def main():
     br.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def set_weights(qtype):
+    """ACE_GGML_DIT_WEIGHT_QTYPE for the next load_dit: online quantization, or none (bf16 as stored)."""
+    if qtype:
+        os.environ["ACE_GGML_DIT_WEIGHT_QTYPE"] = qtype
+    else:
+        os.environ.pop("ACE_GGML_DIT_WEIGHT_QTYPE", None)
+        os.environ.pop("ACE_GGML_WEIGHT_QTYPE", None)
+
+
+def block_linear_frac(prof, nprof, T, b_loc, info):
+    """DiT block linears (qkv, o, cross q/o, gate|up, down: F_lin of SURVEY §8(d) without the cross K/V) per
+    step over their HIP-event time, as a fraction of the 2.5 PFLOP/s dense bf16 MFMA peak."""
+    M = b_loc * ((T + 1) // 2)
+    H_, I_ = info.hidden_size, info.intermediate_size
+    qd, kd = info.num_heads * info.head_dim, info.num_kv_heads * info.head_dim
+    per_layer = 2.0 * M * H_ * ((qd + 2 * kd) + qd + qd + qd + 2 * I_) + 2.0 * M * I_ * H_
+    lin_ms = sum(p[1] for p in prof if p[0] in ("gemm_qkv", "gemm_o", "gemm_cross_q", "gemm_cross_o",
+                                                  "gemm_gate_up", "gemm_down")) / nprof
+    if lin_ms <= 0:
+        return None
+    return round(per_layer * info.num_layers / (lin_ms / 1000.0) / 1e12 / BF16_PEAK_TFLOPS, 4)
 
 
 def pmc_traffic(T, L, b_loc, weights):

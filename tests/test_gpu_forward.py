@@ -298,12 +298,13 @@ def _batched(br, h, c, e, t):
     return out.cpu().numpy()
 
 
+@pytest.mark.parametrize("variant", [-1, 10, 11])
 @pytest.mark.parametrize("width", ["tiny", "full"])
-def test_fused_qkv_prep_is_bit_exact(tiny_ckpt, monkeypatch, width):
+def test_fused_qkv_prep_is_bit_exact(tiny_ckpt, monkeypatch, width, variant):
     """The QKV / cross-q GEMMs with QK-norm, RoPE and the attention re-layout fused into their epilogue
     (EPI_QKV_PREP) give the same bits as the f32 store + attn_prep pair (ACE_MI_UNFUSED_PREP=1): batched
     items whose token counts are not multiples of 16 or of the GEMM's row tile, so V^T key groups are cut
-    by chunk and item edges."""
+    by chunk and item edges; the automatic tile choice and the forced 8-wave 256-column tiles."""
     from acestep_mi355x.capi import GGMLCAPIBridge
     if width == "tiny":
         d, H, cases = tiny_ckpt, 256, [(1, 37, 5), (2, 301, 9), (3, 1001, 17)]
@@ -311,7 +312,7 @@ def test_fused_qkv_prep_is_bit_exact(tiny_ckpt, monkeypatch, width):
         from acestep_mi355x.synthetic import cached_checkpoint, make_config
         d, H, cases = cached_checkpoint(make_config(num_hidden_layers=2), seed=0, backend="torch"), 2048, [(2, 601, 64)]
         monkeypatch.setenv("ACE_GGML_DIT_MAX_LAYERS", "2")
-    rng = np.random.default_rng(8)
+    from acestep_mi355x import capi
     outs = {}
     for fused in (True, False):
         if fused:
@@ -325,7 +326,11 @@ def test_fused_qkv_prep_is_bit_exact(tiny_ckpt, monkeypatch, width):
             h = r.standard_normal((B, T, 64)).astype(np.float32)
             c = r.standard_normal((B, T, 128)).astype(np.float32)
             e = r.standard_normal((B, L, H)).astype(np.float32)
-            outs[(fused, B, T)] = _batched(br, h, c, e, 0.7)
+            capi.gemm_variant(variant if fused else -1)  # the 8-wave tiles' two-heads-per-tile prep (10, 11)
+            try:
+                outs[(fused, B, T)] = _batched(br, h, c, e, 0.7)
+            finally:
+                capi.gemm_variant(-1)
         br.close()
     for B, T, L in cases:
         a, b = outs[(True, B, T)], outs[(False, B, T)]

@@ -6,7 +6,7 @@
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
-ARGS="--steps 2 --warmup 1 --no-cpu-baseline --no-profile ${BENCH_ARGS}"
+ARGS="--steps 2 --warmup 1 --no-cpu-baseline --no-profile --no-bf16-line ${BENCH_ARGS}"
 for ctr in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 600 rocprofv3 --pmc $ctr -d "$GRAFT_REPO_ROOT/gpurun_out/pmc/$ctr" -o pmc --output-format csv \
         -- python bench.py $ARGS > "gpurun_out/pmc/$ctr.log" 2>&1
