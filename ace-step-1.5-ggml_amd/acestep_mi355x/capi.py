@@ -35,7 +35,7 @@ EXPORTED_SYMBOLS = (
     "ace_mi_synchronize", "ace_mi_kernel_gemm", "ace_mi_kernel_attention", "ace_mi_bench_attention", "ace_mi_bench_gemm",
     "ace_mi_gemm_variant", "ace_ggml_load_vae", "ace_ggml_vae_get_info", "ace_ggml_vae_decode",
     "ace_mi_vae_out_len", "ace_mi_vae_decode_device", "ace_ggml_vae_encode", "ace_mi_vae_enc_out_len",
-    "ace_mi_vae_encode_device", "ace_mi_quantize", "ace_mi_dequantize", "ace_mi_kernel_gemm_q", "ace_mi_bench_gemm_q",
+    "ace_mi_vae_encode_device", "ace_mi_quantize", "ace_mi_dequantize", "ace_mi_kernel_gemm_q", "ace_mi_kernel_dequant", "ace_mi_bench_gemm_q",
     "ace_mi_cond_get_info", "ace_mi_text_project", "ace_mi_lyric_encode", "ace_mi_timbre_encode",
     "ace_mi_build_condition", "ace_ggml_load_lm", "ace_ggml_load_text_encoder", "ace_ggml_text_encoder_forward",
     "ace_ggml_text_encoder_forward_masked", "ace_ggml_text_encoder_forward_embeddings",
@@ -155,6 +155,8 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.ace_mi_dequantize.restype = ctypes.c_int
     lib.ace_mi_kernel_gemm_q.argtypes = [i32, i32, i32, i32, i32, i32, u16p, u8p, fp, fp, u16p]
     lib.ace_mi_kernel_gemm_q.restype = ctypes.c_int
+    lib.ace_mi_kernel_dequant.argtypes = [i32, i32, i32, u8p, u16p]
+    lib.ace_mi_kernel_dequant.restype = ctypes.c_int
     lib.ace_mi_bench_gemm_q.argtypes = [i32, i32, i32, i32, i32, i32, i32, fp]
     lib.ace_mi_bench_gemm_q.restype = ctypes.c_int
     for name in ("ace_ggml_load_lm", "ace_ggml_load_text_encoder"):
@@ -612,6 +614,20 @@ def dequantize(raw: np.ndarray, qtype: str) -> np.ndarray:
                                _fptr(out))
     if st != ACE_GGML_OK:
         raise ValueError(f"ace_mi_dequantize failed (status={st})")
+    return out
+
+
+def kernel_dequant(w_blocks: np.ndarray, qtype: str) -> np.ndarray:
+    """Staged dequant kernel: ggml block bytes [N][nb][bb] -> bf16 words [N][K] of bf16(dequant(W))."""
+    lib = load_library()
+    w = np.ascontiguousarray(w_blocks, dtype=np.uint8)
+    N, nb = w.shape[0], w.shape[1]
+    K = nb * _BLOCK[qtype][0]
+    out = np.empty((N, K), dtype=np.uint16)
+    st = lib.ace_mi_kernel_dequant(QTYPES[qtype], N, K, w.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
+                                   out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16)))
+    if st != ACE_GGML_OK:
+        raise RuntimeError(f"ace_mi_kernel_dequant failed (status={st})")
     return out
 
 

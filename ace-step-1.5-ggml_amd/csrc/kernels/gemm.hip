@@ -784,10 +784,10 @@ __device__ __forceinline__ void deq_u4x4(uint32_t w, float d, float nm, uint32_t
     o1 = pk_bf16(f2, f3);
 }
 
-// dequantize one 32-value block and store it as 4 swizzled 16-byte chunks of an LDS row
+// dequantize one 32-value block to 16 packed bf16 pairs in k order (ggml's dequant arithmetic, one f32
+// rounding, then RNE to bf16)
 template <int WQ>
-__device__ __forceinline__ void dequant_store(const WRaw& r, uint32_t row_addr, int wh, int sw) {
-    uint32_t o[16];
+__device__ __forceinline__ void dequant_block(const WRaw& r, uint32_t (&o)[16]) {
     if constexpr (WQ == WF_Q4_K) {
         const float d = r.s0, nm = -r.s1;
         const uint32_t w[4] = {r.q0[0], r.q0[1], r.q0[2], r.q0[3]};
@@ -806,9 +806,42 @@ __device__ __forceinline__ void dequant_store(const WRaw& r, uint32_t row_addr, 
             deq_i8x4(w[i], s, c, o[2 * i], o[2 * i + 1]);
         }
     }
+}
+
+// dequantize one 32-value block and store it as 4 swizzled 16-byte chunks of an LDS row
+template <int WQ>
+__device__ __forceinline__ void dequant_store(const WRaw& r, uint32_t row_addr, int wh, int sw) {
+    uint32_t o[16];
+    dequant_block<WQ>(r, o);
 #pragma unroll
     for (int c = 0; c < 4; ++c)
         ds_write_b128_v(row_addr + (((wh * 4 + c) ^ sw) * 16), o[4 * c], o[4 * c + 1], o[4 * c + 2], o[4 * c + 3]);
+}
+
+// Staged dequant: the bf16 image of a quantized [N][K] weight (the exact values the dequant-fused GEMM
+// writes to LDS: the same deq_* arithmetic), one thread per 8 consecutive weights, so a wave reads 512
+// (Q8_0, Q6_K) or 256 (Q4_K) contiguous bytes and writes 1 KiB contiguous.  HBM-bound: 1.0625 (Q8_0),
+// 0.5625 (Q4_K), 1.125 (Q6_K) bytes read + 2 bytes written per weight.
+template <int WQ>
+__global__ void __launch_bounds__(256) dequant_bf16_kernel(const char* __restrict__ q, const float* __restrict__ sc,
+                                                          int64_t nchunks, uint16_t* __restrict__ out) {
+    const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;  // 8-weight chunk: block g = c / 4, part j = c % 4
+    if (c >= nchunks) return;
+    const int64_t g = c >> 2;
+    const int j = (int)(c & 3);
+    uint32_t o0, o1, o2, o3;
+    if constexpr (WQ == WF_Q4_K) {
+        const uint32_t w = *reinterpret_cast<const uint32_t*>(q + g * 16 + j * 4);  // k 8j..8j+3 low, +4..7 high
+        const float2 dm = *reinterpret_cast<const float2*>(sc + 2 * g);
+        deq_u4x4(w & 0x0f0f0f0fu, dm.x, -dm.y, o0, o1);
+        deq_u4x4((w >> 4) & 0x0f0f0f0fu, dm.x, -dm.y, o2, o3);
+    } else {
+        const uint2 w = *reinterpret_cast<const uint2*>(q + g * 32 + j * 8);
+        const float d = WQ == WF_Q8_0 ? sc[g] : sc[2 * g + (j >> 1)];  // Q6_K: one scale per 16 values
+        deq_i8x4(w.x, d, -128.0f * d, o0, o1);
+        deq_i8x4(w.y, d, -128.0f * d, o2, o3);
+    }
+    *reinterpret_cast<uint4*>(out + c * 8) = make_uint4(o0, o1, o2, o3);
 }
 
 template <int BM, int BN, int WM, int WN, int EPI, int WQ>
@@ -1156,5 +1189,24 @@ void launch_gemm(ActType t, const uint16_t* A, int lda, const uint16_t* W, int l
 }
 
 void gemm_force_variant(int v) { g_forced_variant = v; }
+
+void launch_dequant_bf16(const WeightView& W, int N, int K, uint16_t* out, hipStream_t s) {
+    ACEMI_CHECK(weight_quantized(W.fmt) && W.q && W.s && K % 32 == 0 && N > 0, "dequant: quantized [N][K] weight");
+    const int64_t nb = (int64_t)N * (K / 8);  // 8-weight chunks
+    const dim3 grid((unsigned)((nb + 255) / 256));
+    switch (W.fmt) {
+        case WF_Q8_0:
+            hipLaunchKernelGGL(dequant_bf16_kernel<WF_Q8_0>, grid, dim3(256), 0, s, (const char*)W.q, W.s, nb, out);
+            break;
+        case WF_Q4_K:
+            hipLaunchKernelGGL(dequant_bf16_kernel<WF_Q4_K>, grid, dim3(256), 0, s, (const char*)W.q, W.s, nb, out);
+            break;
+        case WF_Q6_K:
+            hipLaunchKernelGGL(dequant_bf16_kernel<WF_Q6_K>, grid, dim3(256), 0, s, (const char*)W.q, W.s, nb, out);
+            break;
+        default: throw std::runtime_error("dequant: bad weight format");
+    }
+    ACEMI_HIP(hipGetLastError());
+}
 
 }  // namespace acemi

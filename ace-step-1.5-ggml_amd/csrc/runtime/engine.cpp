@@ -17,6 +17,8 @@ DitEngine::DitEngine(int device) : device_(device) {
     attn_pv_split_ = prec == AttnPrecision::F32;
     const char* u = std::getenv("ACE_MI_UNFUSED_PREP");
     fused_prep_ = !(u && u[0] && u[0] != '0');
+    const char* q = std::getenv("ACE_MI_QUANT_STAGED");
+    staged_quant_ = !(q && q[0] == '0');
 }
 
 DitEngine::~DitEngine() {
@@ -27,6 +29,45 @@ DitEngine::~DitEngine() {
     }
     if (ev0_) (void)hipEventDestroy(ev0_);
     if (ev1_) (void)hipEventDestroy(ev1_);
+    if (wring_.p) (void)hipFree(wring_.p);
+}
+
+namespace {
+size_t wbytes(const DevWeight& w) { return (size_t)w.rows * w.cols * 2; }
+}  // namespace
+
+// The six block matrices of layer li: views of the bf16 staging slot (staged) or of the resident weights.
+DitEngine::LayerViews DitEngine::layer_views(int li, bool staged) {
+    const DevLayer& ly = model_.layers[li];
+    const DevWeight* ws[6] = {&ly.w_qkv, &ly.w_o, &ly.w_cq, &ly.w_co, &ly.w_gu, &ly.w_down};
+    WeightView v[6];
+    char* base = staged ? static_cast<char*>(wring_.p) : nullptr;
+    size_t off = 0;
+    for (int i = 0; i < 6; ++i) {
+        v[i] = ws[i]->view();
+        if (staged && weight_quantized(ws[i]->fmt)) {
+            v[i].fmt = WF_BF16;
+            v[i].q = base + off;
+            v[i].s = nullptr;
+            v[i].ld = ws[i]->cols;
+        }
+        off += wbytes(*ws[i]);
+    }
+    return LayerViews{v[0], v[1], v[2], v[3], v[4], v[5]};
+}
+
+void DitEngine::stage_layer(int li, hipStream_t st) {
+    const DevLayer& ly = model_.layers[li];
+    const DevWeight* ws[6] = {&ly.w_qkv, &ly.w_o, &ly.w_cq, &ly.w_co, &ly.w_gu, &ly.w_down};
+    char* base = static_cast<char*>(wring_.p);
+    size_t off = 0;
+    tic(st);
+    for (int i = 0; i < 6; ++i) {
+        if (weight_quantized(ws[i]->fmt) && ws[i]->q)
+            launch_dequant_bf16(ws[i]->view(), ws[i]->rows, ws[i]->cols, reinterpret_cast<uint16_t*>(base + off), st);
+        off += wbytes(*ws[i]);
+    }
+    toc("dequant_stage", st);
 }
 
 void DitEngine::ensure(Buf& b, size_t bytes) {
@@ -300,8 +341,19 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
     const int64_t mstride = 6LL * H;  // per item within a layer
     const float scale = 1.0f / std::sqrt((float)D);
 
+    // staged dequant: each layer's quantized block matrices are expanded to their bf16 image right before the
+    // layer, in stream order, into one workspace slot (see engine.h)
+    const bool staged = staged_quant_ && n_layers > 0 && weight_quantized(m.layers[0].w_gu.fmt);
+    if (staged) {
+        const DevLayer& l0 = m.layers[0];
+        ensure(wring_, wbytes(l0.w_qkv) + wbytes(l0.w_o) + wbytes(l0.w_cq) + wbytes(l0.w_co) + wbytes(l0.w_gu) +
+                           wbytes(l0.w_down));
+    }
+
     for (int li = 0; li < n_layers; ++li) {  // :1466-1535
         const DevLayer& ly = m.layers[li];
+        if (staged) stage_layer(li, s);
+        const LayerViews lw = layer_views(li, staged);
         const float* lm = mods + (size_t)li * B * 6 * H;
         const float* shift_msa = lm + 0 * H;
         const float* scale_msa = lm + 1 * H;
@@ -337,7 +389,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
             pa.q_plane = split ? q_plane : 0;
             pa.k_plane = split ? k_plane : 0;
             pa.v_plane = attn_pv_split_ ? k_plane : 0;
-            qkv_gemm(act, ly.w_qkv.view(), (int)M, qd + 2 * kd, pa, qkv, "gemm_qkv", s);
+            qkv_gemm(act, lw.qkv, (int)M, qd + 2 * kd, pa, qkv, "gemm_qkv", s);
         }
         {
             AttnArgs aa{};
@@ -375,7 +427,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
             e.gate_stride = mstride;
             e.rows_per_item = Np;
             tic(s);
-            launch_gemm(attn, qd, ly.w_o.view(), (int)M, H, qd, e, s);
+            launch_gemm(attn, qd, lw.o, (int)M, H, qd, e, s);
             toc("gemm_o", s);
         }
 
@@ -398,7 +450,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
                 pa.eps = c.eps;
                 pa.qh = get<uint16_t>(qh_);
                 pa.q_plane = split ? q_plane : 0;
-                qkv_gemm(act, ly.w_cq.view(), (int)M, qd, pa, qkv, "gemm_cross_q", s);
+                qkv_gemm(act, lw.cq, (int)M, qd, pa, qkv, "gemm_cross_q", s);
             }
             {
                 AttnArgs aa{};
@@ -432,7 +484,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
                 e.c_f32 = x;
                 e.ldc = H;
                 tic(s);
-                launch_gemm(attn, qd, ly.w_co.view(), (int)M, H, qd, e, s);
+                launch_gemm(attn, qd, lw.co, (int)M, H, qd, e, s);
                 toc("gemm_cross_o", s);
             }
         }
@@ -447,7 +499,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
             e.c_act = act2;
             e.ldc = I;
             tic(s);
-            launch_gemm(act, H, ly.w_gu.view(), (int)M, 2 * I, H, e, s);
+            launch_gemm(act, H, lw.gu, (int)M, 2 * I, H, e, s);
             toc("gemm_gate_up", s);
         }
         {
@@ -459,7 +511,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
             e.gate_stride = mstride;
             e.rows_per_item = Np;
             tic(s);
-            launch_gemm(act2, I, ly.w_down.view(), (int)M, H, I, e, s);
+            launch_gemm(act2, I, lw.down, (int)M, H, I, e, s);
             toc("gemm_down", s);
         }
     }

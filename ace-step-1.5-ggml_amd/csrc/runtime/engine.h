@@ -107,6 +107,20 @@ class DitEngine {
     bool fused_prep_ = true;      // EPI_QKV_PREP (ACE_MI_UNFUSED_PREP=1: f32 store + attn_prep)
     void qkv_gemm(const uint16_t* act, const WeightView& w, int M, int N, PrepArgs pa, float* scratch,
                   const char* name, hipStream_t s);
+    // Staged dequant of quantized block weights (ACE_MI_QUANT_STAGED, default on; 0 = the dequant-fused GEMMs):
+    // right before each layer its Q8_0 / Q4_K / Q6_K matrices are expanded to their bf16 image
+    // (launch_dequant_bf16, bit-identical to the dequant-fused GEMM's LDS tiles) in one workspace slot, and
+    // the block GEMMs run the dense bf16 kernels.  In stream order: a side-stream ring overlapped with the
+    // previous layer gained nothing measurable (the GEMMs leave no CU resources for it) and, for Q4_K only,
+    // changed the results of the concurrently running layer (tools/diag_staged.py) — not understood, so
+    // not used.
+    struct LayerViews {
+        WeightView qkv, o, cq, co, gu, down;
+    };
+    bool staged_quant_ = true;
+    Buf wring_;
+    LayerViews layer_views(int li, bool staged);
+    void stage_layer(int li, hipStream_t st);
     // profiling
     bool profiling_ = false;
     hipEvent_t ev0_ = nullptr, ev1_ = nullptr;

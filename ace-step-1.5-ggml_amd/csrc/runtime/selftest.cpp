@@ -322,6 +322,34 @@ ace_ggml_status ace_mi_dequantize(int32_t qtype, const uint8_t* src, int64_t row
     return ACE_GGML_OK;
 }
 
+// Staged dequant kernel on ggml block rows W [N][K]: out = bf16 bits of bf16(dequant(W)) [N][K].
+ace_ggml_status ace_mi_kernel_dequant(int32_t qtype, int32_t N, int32_t K, const uint8_t* W_blocks, uint16_t* out) {
+    using namespace acemi;
+    const auto t = static_cast<quant::QType>(qtype);
+    if (!W_blocks || !out || N <= 0 || K <= 0) return ACE_GGML_ERR_INVALID_ARG;
+    if (t != quant::Q8_0 && t != quant::Q4_K && t != quant::Q6_K) return ACE_GGML_ERR_INVALID_ARG;
+    if (!quant::applies(t, K)) return ACE_GGML_ERR_INVALID_ARG;
+    try {
+        std::vector<uint8_t> qp(quant::q_plane_bytes(t, N, K));
+        std::vector<float> sp(quant::s_plane_floats(t, N, K));
+        quant::to_planes(t, W_blocks, N, K, qp.data(), sp.data());
+        DevMem dq(qp.size()), ds(sp.size() * 4), dout((size_t)N * K * 2);
+        ACEMI_HIP(hipMemcpy(dq.p, qp.data(), qp.size(), hipMemcpyHostToDevice));
+        ACEMI_HIP(hipMemcpy(ds.p, sp.data(), sp.size() * 4, hipMemcpyHostToDevice));
+        WeightView w;
+        w.fmt = t == quant::Q8_0 ? WF_Q8_0 : t == quant::Q4_K ? WF_Q4_K : WF_Q6_K;
+        w.q = dq.p;
+        w.s = ds.as<float>();
+        launch_dequant_bf16(w, N, K, dout.as<uint16_t>(), nullptr);
+        ACEMI_HIP(hipDeviceSynchronize());
+        ACEMI_HIP(hipMemcpy(out, dout.p, (size_t)N * K * 2, hipMemcpyDeviceToHost));
+    } catch (const std::exception& ex) {
+        std::fprintf(stderr, "ace_mi_kernel_dequant: %s\n", ex.what());
+        return ACE_GGML_ERR;
+    }
+    return ACE_GGML_OK;
+}
+
 // Dequant-fused GEMM on ggml block rows W [N][K]: out = A(bf16) . bf16(dequant(W))^T (+ bias).
 ace_ggml_status ace_mi_kernel_gemm_q(int32_t qtype, int32_t epi, int32_t variant, int32_t M, int32_t N, int32_t K,
                                      const uint16_t* A, const uint8_t* W_blocks, const float* bias, float* out_f32,

@@ -143,10 +143,14 @@ ACE_GGML_API int64_t ace_mi_quantize(int32_t qtype, const float* src, int64_t ro
 ACE_GGML_API ace_ggml_status ace_mi_dequantize(int32_t qtype, const uint8_t* src, int64_t rows, int64_t cols,
                                                float* dst);
 /* Dequant-fused GEMM on ggml block rows W [N][K]: out = A . bf16(dequant(W))^T (+ bias), A bf16 [M][K];
- * epi 0 (f32 store) or 4 (SwiGLU, bf16 out [M][N/2]); variant -1 automatic, 0..7 forced (6 dense only; 8, 9 are dense-only tiles). */
+ * epi 0 (f32 store) or 4 (SwiGLU, bf16 out [M][N/2]); variant -1 automatic, 0..7 forced (6 dense only; 8..11 are dense-only tiles). */
 ACE_GGML_API ace_ggml_status ace_mi_kernel_gemm_q(int32_t qtype, int32_t epi, int32_t variant, int32_t M, int32_t N,
                                                   int32_t K, const uint16_t* A, const uint8_t* W_blocks,
                                                   const float* bias, float* out_f32, uint16_t* out_u16);
+/* Staged dequant kernel (the bf16 weight image the DiT's staged-dequant ring multiplies): out = bf16 bits of
+ * bf16(dequant(W)) [N][K] for ggml block rows W [N][K]. */
+ACE_GGML_API ace_ggml_status ace_mi_kernel_dequant(int32_t qtype, int32_t N, int32_t K, const uint8_t* W_blocks,
+                                                   uint16_t* out);
 /* Dequant-fused GEMM micro-benchmark: average ms per launch (HIP events). */
 ACE_GGML_API ace_ggml_status ace_mi_bench_gemm_q(int32_t qtype, int32_t epi, int32_t variant, int32_t M, int32_t N,
                                                  int32_t K, int32_t iters, float* avg_ms);

@@ -55,6 +55,11 @@ hipError_t hipEventCreate(hipEvent_t* e) {
     *e = reinterpret_cast<hipEvent_t>(0x1);
     return hipSuccess;
 }
+hipError_t hipEventCreateWithFlags(hipEvent_t* e, unsigned int) {
+    *e = reinterpret_cast<hipEvent_t>(0x1);
+    return hipSuccess;
+}
+hipError_t hipStreamWaitEvent(hipStream_t, hipEvent_t, unsigned int) { return hipSuccess; }
 hipError_t hipEventDestroy(hipEvent_t) { return hipSuccess; }
 hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipSuccess; }
 hipError_t hipEventSynchronize(hipEvent_t) { return hipSuccess; }
@@ -129,6 +134,12 @@ float weight_val(const WeightView& W, int K, int n, int k) {
 }  // namespace
 
 void gemm_force_variant(int) {}
+
+void launch_dequant_bf16(const WeightView& W, int N, int K, uint16_t* out, hipStream_t) {
+    ACEMI_CHECK(weight_quantized(W.fmt) && K % 32 == 0, "dequant: quantized [N][K] weight");
+    for (int n = 0; n < N; ++n)
+        for (int k = 0; k < K; ++k) out[(int64_t)n * K + k] = to_bf16(weight_val(W, K, n, k));
+}
 
 void launch_gemm(const uint16_t* A, int lda, const WeightView& W, int M, int N, int K, const GemmEpilogue& e,
                  hipStream_t) {

@@ -29,6 +29,24 @@ def _q_ref(a_bits, w_blocks, qtype):
 
 
 @pytest.mark.parametrize("qtype", ["q8_0", "q4_k", "q6_k"])
+@pytest.mark.parametrize("N,K", [(1, 256), (7, 512), (256, 2048), (96, 6144)])
+def test_staged_dequant_kernel_is_exact(qtype, N, K):
+    """launch_dequant_bf16 (the staged dequant's kernel) equals bf16(ggml dequant(W)), bit for bit except the
+    sign of zero: q = 0 with a negative Q6_K scale is -0 in ggml's d*sc*q and +0 in the kernel's
+    fma(q + 128, s, -128 s) (the dequant-fused GEMM computes the same +0; a product term of either sign is 0)."""
+    from oracle import ggml_numerics as g
+    rng = np.random.default_rng(N + K)
+    w = (rng.standard_normal((N, K)) * 0.02).astype(np.float32)
+    blocks = _capi().quantize(w, qtype)
+    deq = {"q8_0": lambda r: g.dequantize_q8_0(*g.unpack_q8_0(r)), "q4_k": g.dequantize_q4_k,
+           "q6_k": g.dequantize_q6_k}[qtype](blocks)
+    want = f32_to_bf16_bits(np.asarray(deq, dtype=np.float32).reshape(N, K))
+    got = _capi().kernel_dequant(blocks, qtype)
+    bad = np.argwhere((got != want) & ~(((got | want) & 0x7FFF) == 0))
+    assert len(bad) == 0, (len(bad), bad[:8].tolist())
+
+
+@pytest.mark.parametrize("qtype", ["q8_0", "q4_k", "q6_k"])
 @pytest.mark.parametrize("variant", [-1, 1, 2, 3, 4, 5, 7])
 @pytest.mark.parametrize("M,N,K", [(1, 256, 256), (300, 512, 512), (1000, 256, 2048), (129, 768, 6144)])
 def test_gemm_q_matches_dequantized_product(qtype, variant, M, N, K):
@@ -178,3 +196,34 @@ def test_gguf_tiny_matches_oracle(tiny_ckpt, monkeypatch, quant):
     check(got, ref, floor, f"tiny GGUF {quant}")
 
 
+
+
+@pytest.mark.parametrize("qtype", ["q8_0", "q4_k", "q6_k"])
+@pytest.mark.parametrize("width", ["tiny", "full"])
+def test_staged_dequant_equals_fused(tiny_ckpt, monkeypatch, qtype, width):
+    """The staged dequant (ACE_MI_QUANT_STAGED, default: each layer's bf16 weight image expanded right before the
+    layer, dense GEMMs) and the dequant-fused GEMMs (ACE_MI_QUANT_STAGED=0) give the same bits: both multiply
+    bf16 activations by bf16(dequant(W)) with the same per-element summation order."""
+    from acestep_mi355x.capi import GGMLCAPIBridge
+    if width == "tiny":
+        d, H, T, L = tiny_ckpt, 256, 301, 20
+    else:
+        from acestep_mi355x.synthetic import cached_checkpoint, make_config
+        d, H, T, L = cached_checkpoint(make_config(num_hidden_layers=3), seed=0, backend="torch"), 2048, 400, 64
+        monkeypatch.setenv("ACE_GGML_DIT_MAX_LAYERS", "3")
+    monkeypatch.setenv("ACE_GGML_DIT_WEIGHT_QTYPE", qtype)
+    rng = np.random.default_rng(5)
+    h = rng.standard_normal((T, 64)).astype(np.float32)
+    c = rng.standard_normal((T, 128)).astype(np.float32)
+    e = rng.standard_normal((L, H)).astype(np.float32)
+    outs = []
+    for staged in ("1", "0"):
+        monkeypatch.setenv("ACE_MI_QUANT_STAGED", staged)
+        br = GGMLCAPIBridge()
+        br.load_dit(d)
+        outs.append(br.dit_forward_tfirst(h, c, e, None, None, 0.6, 0.6))
+        outs.append(br.dit_forward_tfirst(h, c, e, None, None, 0.6, 0.6))  # slot reused by a second forward
+        br.close()
+    assert np.isfinite(outs[0]).all()
+    for o in outs[1:]:
+        np.testing.assert_array_equal(o, outs[0])
