@@ -84,6 +84,13 @@ void launch_gemm(ActType t, const uint16_t* A, int lda, const uint16_t* W, int l
 void gemm_force_variant(int v);
 // bf16 image [N][K] (ld K) of a quantized weight: bit-identical to what the dequant-fused GEMM feeds its MFMAs
 void launch_dequant_bf16(const WeightView& W, int N, int K, uint16_t* out, hipStream_t s);
+// the same for 1..8 matrices of one format in one launch
+struct DequantJob {
+    WeightView w;
+    int N = 0, K = 0;
+    uint16_t* out = nullptr;
+};
+void launch_dequant_bf16_batch(const DequantJob* jobs, int n, hipStream_t s);
 
 // ------------------------------------------------------------ attention
 // Flash-style fp16 attention, f32 softmax/accumulate.  D = 128.
@@ -194,6 +201,13 @@ struct ConvGemmArgs {
     // independent sequences in one launch (windows of the tiled decode): the M rows split into
     // `items` equal runs; S is [items][T_in][Cin], X / S_out are [items][T_out][Cout]
     int items = 1;
+    // Fused second conv of a residual unit (residual_forward, acestep_vae_model.cpp:724-733) when
+    // Cout = N = 128: the tile's conv output y = Snake2(acc + bias) goes through LDS as fp16 into
+    // z = y . W2^T + bias2 (the k1 conv), and the residual / store / S_out epilogue applies to z.
+    const uint16_t* W2 = nullptr;  // [Cout][Cout] fp16
+    const float* bias2 = nullptr;
+    const float* snake2_ea = nullptr;
+    const float* snake2_eb = nullptr;
 };
 void launch_conv_gemm(const ConvGemmArgs& a, hipStream_t s);
 void launch_to_f16(const float* x, int64_t n, uint16_t* y, hipStream_t s);

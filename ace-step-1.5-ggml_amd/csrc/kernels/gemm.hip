@@ -822,11 +822,24 @@ __device__ __forceinline__ void dequant_store(const WRaw& r, uint32_t row_addr, 
 // writes to LDS: the same deq_* arithmetic), one thread per 8 consecutive weights, so a wave reads 512
 // (Q8_0, Q6_K) or 256 (Q4_K) contiguous bytes and writes 1 KiB contiguous.  HBM-bound: 1.0625 (Q8_0),
 // 0.5625 (Q4_K), 1.125 (Q6_K) bytes read + 2 bytes written per weight.
+struct DequantBatch {  // up to 8 same-format matrices expanded by one launch
+    const char* q[8];
+    const float* s[8];
+    uint16_t* out[8];
+    int64_t end[8];  // exclusive prefix sums of the 8-weight chunk counts
+    int n;
+};
+
 template <int WQ>
-__global__ void __launch_bounds__(256) dequant_bf16_kernel(const char* __restrict__ q, const float* __restrict__ sc,
-                                                          int64_t nchunks, uint16_t* __restrict__ out) {
-    const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;  // 8-weight chunk: block g = c / 4, part j = c % 4
-    if (c >= nchunks) return;
+__global__ void __launch_bounds__(256) dequant_bf16_kernel(DequantBatch b) {
+    int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;  // 8-weight chunk: block g = c / 4, part j = c % 4
+    if (c >= b.end[b.n - 1]) return;
+    int mi = 0;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) mi += (i + 1 < b.n && c >= b.end[i]) ? 1 : 0;
+    if (mi > 0) c -= b.end[mi - 1];
+    const char* __restrict__ q = b.q[mi];
+    const float* __restrict__ sc = b.s[mi];
     const int64_t g = c >> 2;
     const int j = (int)(c & 3);
     uint32_t o0, o1, o2, o3;
@@ -841,7 +854,7 @@ __global__ void __launch_bounds__(256) dequant_bf16_kernel(const char* __restric
         deq_i8x4(w.x, d, -128.0f * d, o0, o1);
         deq_i8x4(w.y, d, -128.0f * d, o2, o3);
     }
-    *reinterpret_cast<uint4*>(out + c * 8) = make_uint4(o0, o1, o2, o3);
+    *reinterpret_cast<uint4*>(b.out[mi] + c * 8) = make_uint4(o0, o1, o2, o3);
 }
 
 template <int BM, int BN, int WM, int WN, int EPI, int WQ>
@@ -1190,23 +1203,35 @@ void launch_gemm(ActType t, const uint16_t* A, int lda, const uint16_t* W, int l
 
 void gemm_force_variant(int v) { g_forced_variant = v; }
 
-void launch_dequant_bf16(const WeightView& W, int N, int K, uint16_t* out, hipStream_t s) {
-    ACEMI_CHECK(weight_quantized(W.fmt) && W.q && W.s && K % 32 == 0 && N > 0, "dequant: quantized [N][K] weight");
-    const int64_t nb = (int64_t)N * (K / 8);  // 8-weight chunks
-    const dim3 grid((unsigned)((nb + 255) / 256));
-    switch (W.fmt) {
-        case WF_Q8_0:
-            hipLaunchKernelGGL(dequant_bf16_kernel<WF_Q8_0>, grid, dim3(256), 0, s, (const char*)W.q, W.s, nb, out);
-            break;
-        case WF_Q4_K:
-            hipLaunchKernelGGL(dequant_bf16_kernel<WF_Q4_K>, grid, dim3(256), 0, s, (const char*)W.q, W.s, nb, out);
-            break;
-        case WF_Q6_K:
-            hipLaunchKernelGGL(dequant_bf16_kernel<WF_Q6_K>, grid, dim3(256), 0, s, (const char*)W.q, W.s, nb, out);
-            break;
+void launch_dequant_bf16_batch(const DequantJob* jobs, int n, hipStream_t s) {
+    ACEMI_CHECK(n >= 1 && n <= 8, "dequant: 1..8 matrices per launch");
+    DequantBatch b{};
+    int64_t tot = 0;
+    for (int i = 0; i < n; ++i) {
+        const DequantJob& jb = jobs[i];
+        ACEMI_CHECK(weight_quantized(jb.w.fmt) && jb.w.fmt == jobs[0].w.fmt && jb.w.q && jb.w.s && jb.K % 32 == 0 &&
+                        jb.N > 0 && jb.out,
+                    "dequant: same-format quantized [N][K] weights");
+        b.q[i] = static_cast<const char*>(jb.w.q);
+        b.s[i] = jb.w.s;
+        b.out[i] = jb.out;
+        tot += (int64_t)jb.N * (jb.K / 8);  // 8-weight chunks
+        b.end[i] = tot;
+    }
+    b.n = n;
+    const dim3 grid((unsigned)((tot + 255) / 256));
+    switch (jobs[0].w.fmt) {
+        case WF_Q8_0: hipLaunchKernelGGL(dequant_bf16_kernel<WF_Q8_0>, grid, dim3(256), 0, s, b); break;
+        case WF_Q4_K: hipLaunchKernelGGL(dequant_bf16_kernel<WF_Q4_K>, grid, dim3(256), 0, s, b); break;
+        case WF_Q6_K: hipLaunchKernelGGL(dequant_bf16_kernel<WF_Q6_K>, grid, dim3(256), 0, s, b); break;
         default: throw std::runtime_error("dequant: bad weight format");
     }
     ACEMI_HIP(hipGetLastError());
+}
+
+void launch_dequant_bf16(const WeightView& W, int N, int K, uint16_t* out, hipStream_t s) {
+    const DequantJob j{W, N, K, out};
+    launch_dequant_bf16_batch(&j, 1, s);
 }
 
 }  // namespace acemi

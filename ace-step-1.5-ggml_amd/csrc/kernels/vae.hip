@@ -59,6 +59,7 @@ struct ReadRows<N, N, STRIDE> {
     __device__ __forceinline__ static void run(uint32_t, uint4 (&)[N][2], int) {}
 };
 
+template <bool FUSE2>
 __global__ void __launch_bounds__(256) conv_gemm_kernel(ConvGemmArgs p) {
     constexpr int BM = 128, BN = 128, WM = 2, WN = 2, NW = 4;
     constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
@@ -187,6 +188,63 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(ConvGemmArgs p) {
         }
     }
 
+    if constexpr (FUSE2) {
+        // k1 conv of the residual unit on this tile (N = Cout = 128: the tile holds every channel).
+        // W2 fragments straight from global memory (32 KB, L2-resident), issued before the LDS round trip.
+        const int lrow2 = lane & 15, lch2 = lane >> 4;
+        uint4 b2f[TN][4];
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks)
+                b2f[j][ks] = *reinterpret_cast<const uint4*>(p.W2 + (int64_t)(wn0 + j * 16 + lrow2) * 128 + ks * 32 +
+                                                            lch2 * 8);
+        // y = Snake2(acc + bias) as fp16 into a [128][128] LDS tile, 16-byte chunks XOR-swizzled by row
+        __builtin_amdgcn_s_barrier();  // every wave's last fragment reads of the main loop are done
+        const int ccol2 = lane & 15, crow2 = (lane >> 4) * 4;
+        char* ytile = smem;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int col = wn0 + j * 16 + ccol2;
+            const float b1 = p.bias ? p.bias[col] : 0.f;
+            const float ea = p.snake2_ea[col], reb = __builtin_amdgcn_rcpf(p.snake2_eb[col]);
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = wm0 + i * 16 + crow2 + r;
+                    const float v = __fadd_rn(acc[i][j][r], b1);
+                    *reinterpret_cast<uint16_t*>(ytile + row * 256 + (((col >> 3) ^ (row & 15)) << 4) + (col & 7) * 2) =
+                        f32_to_f16(snake_f(v, ea, reb));
+                }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __syncthreads();
+        const uint32_t y0 = lds_addr(ytile);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            uint4 a2[TM];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int row = wm0 + i * 16 + lrow2;
+                a2[i] = *reinterpret_cast<const uint4*>(ytile + row * 256 + (((ks * 4 + lch2) ^ (row & 15)) << 4));
+            }
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a2[i]),
+                                                                       __builtin_bit_cast(f16x8, b2f[j][ks]),
+                                                                       acc[i][j], 0, 0, 0);
+        }
+        (void)y0;
+    }
+    const float* bias_e = FUSE2 ? p.bias2 : p.bias;
+
     // epilogue: (m, n) -> output time u and channel co; bias, residual, store, next Snake
     // A thread's TN output columns are fixed, so their channel, transposed-conv phase, bias and Snake
     // parameters are loaded once (not per element); the sequence split is one division per row.
@@ -198,7 +256,7 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(ConvGemmArgs p) {
         const int n = n0 + wn0 + j * 16 + ccol;
         rr_j[j] = p.up > 1 ? n / p.Cout : 0;
         co_j[j] = n - rr_j[j] * p.Cout;
-        bias_j[j] = p.bias ? p.bias[co_j[j]] : 0.f;
+        bias_j[j] = bias_e ? bias_e[co_j[j]] : 0.f;
         ea_j[j] = p.snake_ea ? p.snake_ea[co_j[j]] : 0.f;
         reb_j[j] = p.snake_eb ? __builtin_amdgcn_rcpf(p.snake_eb[co_j[j]]) : 0.f;
     }
@@ -231,7 +289,7 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(ConvGemmArgs p) {
                 if (u < 0 || u >= p.T_out) continue;
                 const int64_t o = (obase + u) * p.Cout + co_j[j];
                 float v = acc[i][j][r];
-                if (p.bias) v = __fadd_rn(v, bias_j[j]);
+                if (bias_e) v = __fadd_rn(v, bias_j[j]);
                 if (p.resid) v = __fadd_rn(xo[r][j], v);
                 if (p.store_x) p.X[o] = v;
                 if (p.S_out) p.S_out[o] = f32_to_f16(p.snake_ea ? snake_f(v, ea_j[j], reb_j[j]) : v);
@@ -256,49 +314,83 @@ __global__ void pack_f16_kernel(const float* __restrict__ x, int64_t rows, int C
 }
 
 // decoder.conv2: C -> out_ch (2), kernel 7, pad 3, no bias, on the fp16 Snake output.  Too narrow
-// for MFMA tiles: one thread per output time, the 7 input rows read as 16-byte vectors (shared
-// through L1/L2 by neighbouring threads), weights staged in LDS; f32 accumulation of exact
-// fp16 products.
+// for MFMA tiles and HBM-bound (the C = 128-channel input is read once, OUT channels written).  A 16-lane
+// group owns a strip of R = 8 consecutive output times of one sequence: each lane holds 8 input channels
+// (16-byte loads, a group reads each 256-byte row once and keeps the R + 6 rows it needs in registers) and
+// its 7 x 8 x OUT weights as f32 in registers; the exact fp16 products are accumulated in f32 per lane and
+// combined over the 16 lanes by xor shuffles.
 template <int OUT>
-__global__ void __launch_bounds__(256) conv_out_kernel(const uint16_t* __restrict__ S, int T, int C,
+__global__ void __launch_bounds__(256) conv_out_kernel(const uint16_t* __restrict__ S, int T,
                                                        const uint16_t* __restrict__ W, float* __restrict__ out,
                                                        int items) {
-    extern __shared__ float wsh[];  // [7][C][OUT] as f32
-    for (int i = threadIdx.x; i < 7 * C * OUT; i += blockDim.x) {
-        const int o = i % OUT, c = (i / OUT) % C, k = i / (OUT * C);
-        wsh[i] = (float)__builtin_bit_cast(_Float16, W[((int64_t)o * 7 + k) * C + c]);
+    constexpr int C = 128, R = 8;
+    const int l16 = threadIdx.x & 15;
+    float wr[7][8][OUT];  // this lane's channels 8*l16 .. 8*l16+7
+#pragma unroll
+    for (int k = 0; k < 7; ++k)
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+#pragma unroll
+            for (int o = 0; o < OUT; ++o)
+                wr[k][c][o] = (float)__builtin_bit_cast(_Float16, W[((int64_t)o * 7 + k) * C + l16 * 8 + c]);
+    const int strips = (T + R - 1) / R;
+    const int64_t strip = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
+    if (strip >= (int64_t)strips * items) return;  // whole 16-lane groups leave together
+    const int item = (int)(strip / strips);
+    const int t0 = (int)(strip - (int64_t)item * strips) * R;
+    const uint16_t* Si = S + (int64_t)item * T * C + l16 * 8;
+    uint4 rows[R + 6];
+#pragma unroll
+    for (int i = 0; i < R + 6; ++i) {
+        const int ti = t0 - 3 + i;
+        rows[i] = (ti >= 0 && ti < T) ? *reinterpret_cast<const uint4*>(Si + (int64_t)ti * C) : make_uint4(0, 0, 0, 0);
     }
-    __syncthreads();
-    const int tg = blockIdx.x * blockDim.x + threadIdx.x;  // row over all sequences
-    if (tg >= T * items) return;
-    const int item = tg / T, t = tg - item * T;
-    S += (int64_t)item * T * C;
-    out += (int64_t)item * T * OUT;
-    float acc[OUT];
+    float acc[R][OUT];
 #pragma unroll
-    for (int o = 0; o < OUT; ++o) acc[o] = 0.f;
-    for (int k = 0; k < 7; ++k) {
-        const int ti = t + k - 3;
-        if (ti < 0 || ti >= T) continue;
-        const uint4* row = (const uint4*)(S + (int64_t)ti * C);
-        for (int c8 = 0; c8 < C / 8; ++c8) {
-            const uint4 v = row[c8];
-            const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+    for (int r = 0; r < R; ++r)
 #pragma unroll
-            for (int h = 0; h < 4; ++h) {
-                const float x0 = (float)__builtin_bit_cast(_Float16, (uint16_t)(w4[h] & 0xffffu));
-                const float x1 = (float)__builtin_bit_cast(_Float16, (uint16_t)(w4[h] >> 16));
-                const int c = c8 * 8 + 2 * h;
+        for (int o = 0; o < OUT; ++o) acc[r][o] = 0.f;
 #pragma unroll
-                for (int o = 0; o < OUT; ++o) {
-                    acc[o] = fmaf(x0, wsh[(k * C + c) * OUT + o], acc[o]);
-                    acc[o] = fmaf(x1, wsh[(k * C + c + 1) * OUT + o], acc[o]);
-                }
-            }
+    for (int i = 0; i < R + 6; ++i) {
+        const uint32_t w4[4] = {rows[i].x, rows[i].y, rows[i].z, rows[i].w};
+        float x[8];
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+            x[2 * h] = (float)__builtin_bit_cast(_Float16, (uint16_t)(w4[h] & 0xffffu));
+            x[2 * h + 1] = (float)__builtin_bit_cast(_Float16, (uint16_t)(w4[h] >> 16));
+        }
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {  // input row t0 - 3 + i feeds output r = i - k through tap k
+            const int r = i - k;
+            if (r < 0 || r >= R) continue;
+#pragma unroll
+            for (int c = 0; c < 8; ++c)
+#pragma unroll
+                for (int o = 0; o < OUT; ++o) acc[r][o] = fmaf(x[c], wr[k][c][o], acc[r][o]);
         }
     }
 #pragma unroll
-    for (int o = 0; o < OUT; ++o) out[(int64_t)t * OUT + o] = acc[o];
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int o = 0; o < OUT; ++o)
+#pragma unroll
+            for (int off = 8; off >= 1; off >>= 1) acc[r][o] += __shfl_xor(acc[r][o], off);
+    if (l16 < R) {  // lane r writes output row t0 + r
+        const int t = t0 + l16;
+        if (t < T) {
+            float v[OUT];
+#pragma unroll
+            for (int o = 0; o < OUT; ++o) {
+                float a = acc[0][o];
+#pragma unroll
+                for (int r = 1; r < R; ++r) a = l16 == r ? acc[r][o] : a;
+                v[o] = a;
+            }
+            float* dst = out + ((int64_t)item * T + t) * OUT;
+#pragma unroll
+            for (int o = 0; o < OUT; ++o) dst[o] = v[o];
+        }
+    }
 }
 
 }  // namespace
@@ -311,7 +403,13 @@ void launch_conv_gemm(const ConvGemmArgs& a, hipStream_t s) {
     ACEMI_CHECK(!(a.resid || a.store_x) || a.X, "conv_gemm: null X");
     ACEMI_CHECK(a.items >= 1 && a.M % a.items == 0, "conv_gemm: rows must split evenly into the sequences");
     const int nbm = (a.M + 127) / 128, nbn = a.N / 128;
-    hipLaunchKernelGGL(conv_gemm_kernel, dim3(nbm * nbn), dim3(256), 0, s, a);
+    if (a.W2) {
+        ACEMI_CHECK(a.N == 128 && a.Cout == 128 && a.up <= 1 && a.snake2_ea && a.snake2_eb,
+                    "conv_gemm: the fused k1 conv needs Cout = N = 128 and a Snake between the convs");
+        hipLaunchKernelGGL(conv_gemm_kernel<true>, dim3(nbm * nbn), dim3(256), 0, s, a);
+    } else {
+        hipLaunchKernelGGL(conv_gemm_kernel<false>, dim3(nbm * nbn), dim3(256), 0, s, a);
+    }
     ACEMI_HIP(hipGetLastError());
 }
 
@@ -330,15 +428,14 @@ void launch_pack_f16(const float* x, int64_t rows, int C, int Cpad, uint16_t* y,
 
 void launch_conv_out(const uint16_t* S, int T, int C, const uint16_t* W, int out_ch, float* out, hipStream_t s,
                      int items) {
-    ACEMI_CHECK(C % 8 == 0, "conv_out: channels must be a multiple of 8");
+    ACEMI_CHECK(C == 128, "conv_out: decoder.conv2 input channels must be 128");
     ACEMI_CHECK(items >= 1 && (int64_t)T * items < (1LL << 31), "conv_out: bad sequence count");
-    const size_t shm = (size_t)7 * C * out_ch * 4;
-    ACEMI_CHECK(shm <= 64 * 1024, "conv_out: weights do not fit LDS");
-    const dim3 grid((unsigned)(((int64_t)T * items + 255) / 256));
+    const int64_t strips = (int64_t)((T + 7) / 8) * items;  // 8 output times per 16-lane group
+    const dim3 grid((unsigned)((strips + 15) / 16));
     if (out_ch == 1)
-        hipLaunchKernelGGL(conv_out_kernel<1>, grid, dim3(256), shm, s, S, T, C, W, out, items);
+        hipLaunchKernelGGL(conv_out_kernel<1>, grid, dim3(256), 0, s, S, T, W, out, items);
     else if (out_ch == 2)
-        hipLaunchKernelGGL(conv_out_kernel<2>, grid, dim3(256), shm, s, S, T, C, W, out, items);
+        hipLaunchKernelGGL(conv_out_kernel<2>, grid, dim3(256), 0, s, S, T, W, out, items);
     else
         throw std::runtime_error("conv_out: audio_channels must be 1 or 2");
     ACEMI_HIP(hipGetLastError());

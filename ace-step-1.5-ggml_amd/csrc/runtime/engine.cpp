@@ -61,12 +61,20 @@ void DitEngine::stage_layer(int li, hipStream_t st) {
     const DevWeight* ws[6] = {&ly.w_qkv, &ly.w_o, &ly.w_cq, &ly.w_co, &ly.w_gu, &ly.w_down};
     char* base = static_cast<char*>(wring_.p);
     size_t off = 0;
-    tic(st);
+    DequantJob jobs[6];
+    int n = 0;
     for (int i = 0; i < 6; ++i) {
-        if (weight_quantized(ws[i]->fmt) && ws[i]->q)
-            launch_dequant_bf16(ws[i]->view(), ws[i]->rows, ws[i]->cols, reinterpret_cast<uint16_t*>(base + off), st);
+        if (weight_quantized(ws[i]->fmt) && ws[i]->q) {
+            if (n > 0 && ws[i]->fmt != jobs[0].w.fmt) {  // one launch per weight format
+                launch_dequant_bf16_batch(jobs, n, st);
+                n = 0;
+            }
+            jobs[n++] = DequantJob{ws[i]->view(), ws[i]->rows, ws[i]->cols, reinterpret_cast<uint16_t*>(base + off)};
+        }
         off += wbytes(*ws[i]);
     }
+    tic(st);
+    if (n > 0) launch_dequant_bf16_batch(jobs, n, st);
     toc("dequant_stage", st);
 }
 

@@ -349,15 +349,34 @@ void VaeEngine::run_conv(const VaeConv& c, const uint16_t* S, int T_in, int T_ou
         a.snake_ea = next->ea;
         a.snake_eb = next->eb;
     }
+    if (fused2_) {
+        a.W2 = fused2_->c2.w;
+        a.bias2 = fused2_->c2.b;
+        a.snake2_ea = fused2_->s2.ea;
+        a.snake2_eb = fused2_->s2.eb;
+    }
     launch_conv_gemm(a, s);
 }
 
 // residual_forward (:724-733): x += conv2(snake2(conv1(snake1(x)))); Sin holds snake1(x); the new x's
 // Snake for the next consumer goes to Snext_out
-void VaeEngine::run_res(const VaeRes& r, int L, float* X, uint16_t* Sin, uint16_t* Stmp, uint16_t* Snext_out,
-                        const VaeSnake* next, hipStream_t s) {
-    run_conv(r.c1, Sin, L, L, nullptr, false, false, Stmp, &r.s2, s);
-    run_conv(r.c2, Stmp, L, L, X, true, true, Snext_out, next, s);
+// residual_forward (:724-733): x += conv2(snake2(conv1(snake1(x)))); Sin holds snake1(x).  The new x's Snake
+// for the next consumer goes to Sout, or (Sout null) to any free buffer of {Sin, Sspare}; returns that buffer.
+uint16_t* VaeEngine::run_res(const VaeRes& r, int L, float* X, uint16_t* Sin, uint16_t* Sspare, uint16_t* Sout,
+                             const VaeSnake* next, hipStream_t s) {
+    if (fuse_res_ && r.c1.cout == 128 && r.c2.cin == 128 && r.c2.cout == 128 && r.c2.taps == 1 && !r.c1.transposed) {
+        // one launch: the k1 conv runs on the k7 conv's output tile (ConvGemmArgs::W2), no Stmp round trip;
+        // its output cannot overwrite Sin, which other tiles still read (dilated taps)
+        uint16_t* out = Sout ? Sout : Sspare;
+        fused2_ = &r;
+        run_conv(r.c1, Sin, L, L, X, true, true, out, next, s);
+        fused2_ = nullptr;
+        return out;
+    }
+    uint16_t* out = Sout ? Sout : Sin;
+    run_conv(r.c1, Sin, L, L, nullptr, false, false, Sspare, &r.s2, s);
+    run_conv(r.c2, Sspare, L, L, X, true, true, out, next, s);
+    return out;
 }
 
 namespace {
@@ -407,9 +426,10 @@ void VaeEngine::decode(const float* d_latents, int n_frames, float* d_out, hipSt
         // snake1 was applied by the producer of Sa; conv_t1 -> X, Sb = res1.snake1(X)
         run_conv(b.ct, Sa, (int)L, (int)Lo, X, false, true, Sb, &b.res[0].s1, s);
         L = Lo;
+        uint16_t* cur = Sb;
         for (int j = 0; j < 3; ++j) {
             const VaeSnake* next = j < 2 ? &b.res[j + 1].s1 : (i + 1 < m.blocks.size() ? &m.blocks[i + 1].s1 : &m.snake1);
-            run_res(b.res[j], (int)L, X, Sb, Sc, j < 2 ? Sb : Sa, next, s);
+            cur = run_res(b.res[j], (int)L, X, cur, cur == Sb ? Sc : Sb, j < 2 ? nullptr : Sa, next, s);
         }
     }
     // decoder.snake1 (applied into Sa) -> decoder.conv2
@@ -459,9 +479,10 @@ void VaeEngine::encode(const float* d_audio, int n_samples, float* d_out, hipStr
     run_conv(m.enc_conv1, Sa, n_samples, (int)L, X, false, true, Sb, first, s);
     for (size_t i = 0; i < m.enc_blocks.size(); ++i) {
         const VaeEncBlock& b = m.enc_blocks[i];
+        uint16_t* cur = Sb;
         for (int j = 0; j < 3; ++j) {
             const VaeSnake* next = j < 2 ? &b.res[j + 1].s1 : &b.s1;
-            run_res(b.res[j], (int)L, X, Sb, Sc, j < 2 ? Sb : Sa, next, s);
+            cur = run_res(b.res[j], (int)L, X, cur, cur == Sb ? Sc : Sb, j < 2 ? nullptr : Sa, next, s);
         }
         // block snake1 (in Sa) -> strided conv -> X, Sb = snake(next)(X)
         const int64_t Lo = conv_len(L, b.conv);

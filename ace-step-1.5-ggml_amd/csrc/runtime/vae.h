@@ -8,6 +8,8 @@
 // Snake parameters as exp(alpha), exp(beta) (expf on the host, as ggml_exp does on the CPU).
 #pragma once
 
+#include <cstdlib>
+
 #include <string>
 #include <vector>
 
@@ -76,7 +78,10 @@ void load_vae_model(const std::string& dir, VaeModel& m, int& status_hint);
 
 class VaeEngine {
 public:
-    explicit VaeEngine(int device) : device_(device) {}
+    explicit VaeEngine(int device) : device_(device) {
+        const char* e = std::getenv("ACE_MI_VAE_FUSE_RES");
+        fuse_res_ = !(e && e[0] == '0');
+    }
     ~VaeEngine();
     VaeModel& model() { return model_; }
     int device() const { return device_; }
@@ -102,10 +107,13 @@ private:
     VaeModel model_;
     Buf x_, sa_, sb_, sc_, lat_, zero_;
     int items_ = 1;  // sequences per conv launch during decode (ConvGemmArgs::items)
+    // 128-channel residual units as one launch (ConvGemmArgs::W2); ACE_MI_VAE_FUSE_RES=0: two launches
+    bool fuse_res_ = true;
+    const VaeRes* fused2_ = nullptr;  // set while run_conv launches the fused k7 + k1 of this unit
     void run_conv(const VaeConv& c, const uint16_t* S, int T_in, int T_out, float* X, bool resid, bool store,
                   uint16_t* S_out, const VaeSnake* next, hipStream_t s);
-    void run_res(const VaeRes& r, int L, float* X, uint16_t* Sin, uint16_t* Stmp, uint16_t* Snext_out,
-                 const VaeSnake* next, hipStream_t s);
+    uint16_t* run_res(const VaeRes& r, int L, float* X, uint16_t* Sin, uint16_t* Sspare, uint16_t* Sout,
+                      const VaeSnake* next, hipStream_t s);
 };
 
 }  // namespace acemi

@@ -140,6 +140,9 @@ void launch_dequant_bf16(const WeightView& W, int N, int K, uint16_t* out, hipSt
     for (int n = 0; n < N; ++n)
         for (int k = 0; k < K; ++k) out[(int64_t)n * K + k] = to_bf16(weight_val(W, K, n, k));
 }
+void launch_dequant_bf16_batch(const DequantJob* jobs, int n, hipStream_t s) {
+    for (int i = 0; i < n; ++i) launch_dequant_bf16(jobs[i].w, jobs[i].N, jobs[i].K, jobs[i].out, s);
+}
 
 void launch_gemm(const uint16_t* A, int lda, const WeightView& W, int M, int N, int K, const GemmEpilogue& e,
                  hipStream_t) {
@@ -502,10 +505,32 @@ void launch_conv_gemm(const ConvGemmArgs& a, hipStream_t) {
             for (int c = 0; c < a.Cin; ++c)
                 row[(size_t)tap * a.Cin + c] = (t >= 0 && t < a.T_in) ? f16f(S[(int64_t)t * a.Cin + c]) : 0.f;
         }
+        std::vector<float> z;  // fused k1 conv: z = W2 . fp16(Snake2(acc + bias)) (ConvGemmArgs::W2)
+        if (a.W2) {
+            std::vector<float> y((size_t)a.N);
+            for (int n = 0; n < a.N; ++n) {
+                double s = 0;
+                const uint16_t* w = a.W + (int64_t)n * K;
+                for (int k = 0; k < K; ++k) s += (double)row[k] * f16f(w[k]);
+                const float v = (float)s + (a.bias ? a.bias[n] : 0.f);
+                const float sv = sinf(a.snake2_ea[n] * v);
+                y[n] = f16f(to_f16(v + (sv * sv) / a.snake2_eb[n]));
+            }
+            z.resize((size_t)a.N);
+            for (int n = 0; n < a.N; ++n) {
+                double s = 0;
+                for (int k = 0; k < a.N; ++k) s += (double)y[k] * f16f(a.W2[(int64_t)n * a.N + k]);
+                z[n] = (float)s;
+            }
+        }
         for (int n = 0; n < a.N; ++n) {
             double s = 0;
-            const uint16_t* w = a.W + (int64_t)n * K;
-            for (int k = 0; k < K; ++k) s += (double)row[k] * f16f(w[k]);
+            if (a.W2) {
+                s = z[n];
+            } else {
+                const uint16_t* w = a.W + (int64_t)n * K;
+                for (int k = 0; k < K; ++k) s += (double)row[k] * f16f(w[k]);
+            }
             int u, co;
             if (a.up > 1) {
                 const int rr = n / a.Cout;
@@ -517,7 +542,8 @@ void launch_conv_gemm(const ConvGemmArgs& a, hipStream_t) {
             }
             if (u < 0 || u >= a.T_out) continue;
             float v = (float)s;
-            if (a.bias) v += a.bias[co];
+            const float* bias = a.W2 ? a.bias2 : a.bias;
+            if (bias) v += bias[co];
             const int64_t o = (obase + u) * a.Cout + co;
             if (a.resid) v = a.X[o] + v;
             if (a.store_x) a.X[o] = v;

@@ -6,8 +6,8 @@ long latent sequence on one MI355X, per conv stage.
                                                                  -> per-stage TFLOP/s from a rocprofv3 trace
 
 The launch plan below restates VaeEngine::decode's order (runtime/vae.cpp): conv1, then per decoder block the
-ConvTranspose1d and three residual units (k7 dilated conv, k1 conv), all as conv_gemm_kernel launches, then
-the VALU conv_out.  Algorithmic FLOPs per launch = 2 * (output rows) * Cout * taps * Cin (the transposed conv:
+ConvTranspose1d and three residual units (k7 dilated conv, k1 conv; one fused launch at 128 channels), all as
+conv_gemm_kernel launches, then the VALU conv_out.  Algorithmic FLOPs per launch = 2 * (output rows) * Cout * taps * Cin (the transposed conv:
 two taps per output sample).  Under rocprofv3 --kernel-trace the tool decodes once (warm) then `--runs` more
 times; the summary takes the last run's conv_gemm_kernel dispatches in order and joins them with the plan.
 """
@@ -42,6 +42,9 @@ def plan(cfg, frames):
         out.append((f"block{i} convT x{s} {cin}->{cout}", L + 1, s * cout, 2 * cin, 2.0 * Lo * cout * 2 * cin))
         L = Lo
         for j in range(3):
+            if cout == 128:  # one launch: k1 fused into the k7 conv's tile (ConvGemmArgs::W2)
+                out.append((f"block{i} res{j} k7+k1 {cout} (fused)", L, cout, 8 * cout, 2.0 * L * cout * 8 * cout))
+                continue
             out.append((f"block{i} res{j} k7 {cout}", L, cout, 7 * cout, 2.0 * L * cout * 7 * cout))
             out.append((f"block{i} res{j} k1 {cout}", L, cout, cout, 2.0 * L * cout * cout))
     out.append((f"conv_out k7 {ch}->{cfg['audio_channels']} (VALU)", L, cfg["audio_channels"], 7 * ch,
