@@ -53,6 +53,9 @@ def parse():
                          "BASELINE configs[2] (240 s, bs=1, Q8_0 dequant-fused matmul)")
     ap.add_argument("--no-bf16-line", action="store_true",
                     help="skip the bf16-weight run that is reported beside a quantized line")
+    ap.add_argument("--emulate", action="store_true",
+                    help="TEST MODE: the multi-rank code path on CPU (gloo, the host-emulated library of tests/, "
+                         "tiny config); its numbers are not a measurement")
     return ap.parse_args()
 
 
@@ -64,10 +67,19 @@ def main():
     import torch
     import torch.distributed as dist
 
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    if args.emulate:
+        dev = torch.device("cpu")
+        if world > 1:
+            dist.init_process_group("gloo")
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        if world > 1:
+            dist.init_process_group("nccl", device_id=dev)
+
+    def sync():
+        if not args.emulate:
+            torch.cuda.synchronize()
 
     def barrier():
         if world > 1:
@@ -78,7 +90,17 @@ def main():
     from acestep_mi355x.schedule import shifted_linear_schedule
     from acestep_mi355x.synthetic import cached_checkpoint, make_config
 
-    cfg = make_config()
+    if args.emulate:
+        from acestep_mi355x.synthetic import TINY_CONFIG
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from hostlib import build_host_lib  # test infrastructure: the CPU restatement of every launch_*
+        cfg = TINY_CONFIG
+        lib_path = build_host_lib() if rank == 0 else None
+        barrier()
+        lib_path = lib_path or build_host_lib()
+    else:
+        cfg = make_config()
+        lib_path = None
     # rank 0 writes the synthetic checkpoint, the others wait for it
     if rank == 0:
         ckpt = cached_checkpoint(cfg, seed=0, backend="torch")
@@ -89,7 +111,7 @@ def main():
     if args.qtype == "bf16":
         args.qtype = ""
     set_weights(args.qtype)
-    br = GGMLCAPIBridge(device=local)
+    br = GGMLCAPIBridge(device=local, lib_path=lib_path) if lib_path else GGMLCAPIBridge(device=local)
     br.load_dit(ckpt)
     wdesc = f"{args.qtype.upper()} dequant-fused (bf16 MFMA)" if args.qtype else "bf16"
     info = br.info
@@ -108,16 +130,16 @@ def main():
         context = torch.cat([src, torch.ones((B, T, ctxd - audio))], dim=-1)  # silence latent | chunk mask
         enc = torch.randn((B, L, H), generator=g)
         cond = Conditioning(noise=noise, context=context, enc=enc)
-    torch.cuda.synchronize()
+    sync()
     cond = broadcast_conditioning(cond, shapes, dev)
     items = shard_indices(B, world, rank)
     idx = torch.tensor(items, device=dev)
     xt = cond.noise.index_select(0, idx).contiguous()
     ctx = cond.context.index_select(0, idx).contiguous()
     enc = cond.enc.index_select(0, idx).contiguous()
-    torch.cuda.synchronize()  # the library runs on its own stream: inputs complete before the warmup reads them
+    sync()  # the library runs on its own stream: inputs complete before the warmup reads them
     sched = shifted_linear_schedule(args.sample_steps, 3.0)
-    stream = torch.cuda.current_stream().cuda_stream
+    stream = 0 if args.emulate else torch.cuda.current_stream().cuda_stream
 
     def run(first, k):
         """k denoising steps of the schedule (cyclic) in ONE device-side generation-loop call
@@ -133,14 +155,14 @@ def main():
 
     if args.warmup > 0:
         run(0, args.warmup)
-    torch.cuda.synchronize()
+    sync()
     barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     run(args.warmup, args.steps)
-    torch.cuda.synchronize()
+    sync()
     barrier()
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t0
     if world > 1:
         el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -157,7 +179,7 @@ def main():
         nprof = 2
         for i in range(nprof):
             step(i)
-        torch.cuda.synchronize()
+        sync()
         prof = br.profile_get()
         br.profile_enable(False)
         for name, ms, cnt in prof:
@@ -192,10 +214,10 @@ def main():
         br.load_dit(ckpt)
         if args.warmup > 0:
             run(0, args.warmup)
-        torch.cuda.synchronize()
+        sync()
         t1 = time.perf_counter()
         run(args.warmup, args.steps)
-        torch.cuda.synchronize()
+        sync()
         el_bf16 = time.perf_counter() - t1
         bf16_line = {"value": round(B * args.steps / el_bf16, 3), "unit": "steps/s",
                      "ms_per_step": round(1000.0 * el_bf16 / args.steps, 3),
@@ -205,7 +227,7 @@ def main():
             br.profile_reset()
             for i in range(2):
                 step(i)
-            torch.cuda.synchronize()
+            sync()
             prof_b = br.profile_get()
             br.profile_enable(False)
             frac = block_linear_frac(prof_b, 2, T, b_loc, info)
@@ -227,7 +249,7 @@ def main():
         ms_per_step = 1000.0 * elapsed / args.steps
         value = B * args.steps / elapsed
         line = {
-            "metric": METRIC,
+            "metric": METRIC if not args.emulate else "EMULATED (host CPU restatement, tiny config): not a measurement",
             "value": round(value, 3),
             "unit": "steps/s",
             "n_gpus": world,
