@@ -80,7 +80,8 @@ void launch_gemm(const uint16_t* A, int lda, const WeightView& W, int M, int N, 
 // dense shorthand: W 16-bit of type t
 void launch_gemm(ActType t, const uint16_t* A, int lda, const uint16_t* W, int ldw, int M, int N, int K,
                  const GemmEpilogue& epi, hipStream_t s);
-// -1 = automatic tile choice; 0..11 force a kernel variant (micro-benchmarks / tests)
+// -1 = automatic tile choice; 0..11 force a kernel variant, + 100 * S (S = 2..4) split-K over S blocks per
+// tile for the 4-wave tiles (micro-benchmarks / tests)
 void gemm_force_variant(int v);
 // bf16 image [N][K] (ld K) of a quantized weight: bit-identical to what the dequant-fused GEMM feeds its MFMAs
 void launch_dequant_bf16(const WeightView& W, int N, int K, uint16_t* out, hipStream_t s);

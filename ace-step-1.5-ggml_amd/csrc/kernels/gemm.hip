@@ -16,7 +16,11 @@
 // ds_read, which makes every ds_read_b128 lane group conflict-free.
 // Blocks are remapped XCD-aware (blocks b, b+8 share an XCD) and grouped
 // along M so co-resident tiles share weight panels in L2.
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
+#include <mutex>
+#include <unordered_map>
 
 #include "../kernels.h"
 #include "prep_math.h"
@@ -37,6 +41,13 @@ struct GemmParams {
     const float* Ws;
     int lda, ldw, M, N, K;
     GemmEpilogue e;
+    // split-K (gemm_kernel only): ksplit blocks per output tile, each over a contiguous 1/ksplit of the
+    // K-tiles; the last adds the others' partial tiles (sk_ws, slot = K part) in K order and runs the
+    // epilogue.  sk_cnt / sk_ready: per-tile ticket / ready counters, zero between launches (splitk_join).
+    int ksplit;
+    f32x4* sk_ws;
+    unsigned* sk_cnt;
+    unsigned* sk_ready;
 };
 
 __device__ __forceinline__ uint16_t f32_to_bf16_rne(float f) {
@@ -112,11 +123,13 @@ __device__ __forceinline__ void wait_vmcnt() {
 
 // block -> tile: XCD-aware bijective remap (blocks b, b+8 share an XCD), then M-grouped order
 template <int BM, int BN>
-__device__ __forceinline__ void block_tile(const GemmParams& p, int& m0, int& n0) {
+__device__ __forceinline__ void block_tile(const GemmParams& p, int& m0, int& n0, int bid = -1, int nwg = 0) {
     const int nbm = (p.M + BM - 1) / BM;
     const int nbn = p.N / BN;
-    const int nwg = gridDim.x;
-    int bid = blockIdx.x;
+    if (bid < 0) {
+        bid = blockIdx.x;
+        nwg = gridDim.x;
+    }
     {
         const int xcd = bid & 7;
         const int q = nwg >> 3, r = nwg & 7;
@@ -134,7 +147,7 @@ __device__ __forceinline__ void block_tile(const GemmParams& p, int& m0, int& n0
 
 // Fused epilogue of one wave's TM x TN grid of 16x16 accumulators at (mw, nw).
 // C/D map of 16x16x32: col = lane & 15, row = (lane >> 4) * 4 + r.
-template <int TM, int TN, bool F16, int EPI, int NW>
+template <int TM, int TN, bool F16, int EPI, int PRE>
 __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[TM][TN], int mw, int nw, int lane) {
     const GemmEpilogue& e = p.e;
     const int M = p.M;
@@ -144,10 +157,11 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
         // Residual read-modify-write: the old x (and gate) values of a chunk of GI 16-row groups are all
         // loaded before the chunk's first store.  Interleaved, the compiler cannot move a load of x above
         // an earlier store to x (same pointer), so each element paid a full memory round trip in
-        // sequence.  A whole-tile preload fits the 512-register budget of the 4-wave tiles; the 8-wave
-        // tiles (256 registers, accumulators included) preload 64 values per chunk instead of spilling.
+        // sequence.  A whole-tile preload (PRE = 1024 values) fits the 512-register budget of the 4-wave
+        // tiles; the 8-wave tiles (256 registers, accumulators included) preload 64 values per chunk
+        // instead of spilling, the 256-register split-K instances 32.
         constexpr int PER_I = 4 * TN * (EPI == EPI_RESID_GATED ? 2 : 1);
-        constexpr int GI0 = (NW >= 8 ? 64 : 1024) / PER_I;
+        constexpr int GI0 = PRE / PER_I;
         constexpr int GI = GI0 < 1 ? 1 : (GI0 > TM ? TM : GI0);
 #pragma unroll
         for (int i0 = 0; i0 < TM; i0 += GI) {
@@ -338,12 +352,140 @@ __device__ __forceinline__ void qkv_prep_tile(const GemmParams& p, f32x4 (&acc)[
     });
 }
 
+constexpr int CPOL_SC1 = 16;  // cache-policy bit of buffer / global ops: device-scope coherent (gfx94x/gfx950)
+
+// largest split-K factor of a tile: the last block gathers the other parts through its LDS share
+template <int BM, int BN>
+struct SplitKMax {
+    static constexpr int value = BM * BN >= 128 * 128 ? 2 : 4;
+};
+
+// Split-K: block -> (tile, K part).  When the tile count is a multiple of 8 the S parts of a tile are
+// blocks 8 apart (same XCD: the partial tiles stay in that XCD's L2); otherwise adjacent blocks.
+__device__ __forceinline__ void splitk_block(int S, int& tile, int& part, int& ntiles) {
+    const int b = blockIdx.x;
+    ntiles = gridDim.x / S;
+    if ((ntiles & 7) == 0) {
+        part = (b >> 3) % S;
+        tile = (b / (8 * S)) * 8 + (b & 7);
+    } else {
+        part = b % S;
+        tile = b / S;
+    }
+}
+
+// The last block of a split-K tile adds the other parts' partial tiles: each wave brings its own fragments
+// of the S-1 other slots into its share of the (now free) LDS by LDS-DMA (no VGPRs held by loads in flight),
+// CH fragments at a time, then acc = ((part_0 + part_1) + ...) in K order, its own sum at index `part`.
+template <int TM, int TN, int NW, int SS, int SMEM>
+__device__ __forceinline__ void splitk_gather(f32x4 (&acc)[TM][TN], const f32x4* slot0, int64_t slot_stride,
+                                              int part, char* smem, int wid, int lane) {
+    constexpr int F = TM * TN;
+    constexpr int LDSW = SMEM / NW;  // bytes of LDS per wave
+    constexpr int CH0 = LDSW / ((SS - 1) * 1024);
+    constexpr int CH = CH0 < F ? CH0 : F;
+    static_assert(CH >= 1, "split-K gather: LDS share too small");
+    char* wl = smem + wid * LDSW;
+#pragma unroll
+    for (int f0 = 0; f0 < F; f0 += CH) {
+        if (f0 > 0) lds_wait_all();  // the previous chunk's LDS reads are done before it is overwritten
+#pragma unroll
+        for (int f = f0; f < f0 + CH && f < F; ++f)
+#pragma unroll
+            for (int qi = 0; qi < SS - 1; ++qi) {
+                const int q = qi < part ? qi : qi + 1;
+                __builtin_amdgcn_global_load_lds((const void*)(slot0 + q * slot_stride + f * 64),
+                                                 (lds_void*)(wl + ((f - f0) * (SS - 1) + qi) * 1024), 16, 0,
+                                                 CPOL_SC1);  // device-coherent load
+            }
+        wait_vmcnt<0>();
+#pragma unroll
+        for (int f = f0; f < f0 + CH && f < F; ++f) {
+            if ((f - f0) % 4 == 0) __builtin_amdgcn_sched_barrier(0);  // LDS reads in groups of 4 fragments
+            const f32x4* l = reinterpret_cast<const f32x4*>(wl + (f - f0) * (SS - 1) * 1024) + lane;
+            const int i = f / TN, j = f % TN;
+            if constexpr (SS == 2) {
+                acc[i][j] += l[0];  // two parts: a + b == b + a, whichever is this block's
+            } else {
+                f32x4 t = part == 0 ? acc[i][j] : l[0];
+#pragma unroll
+                for (int q = 1; q < SS; ++q) t += q == part ? acc[i][j] : l[(q < part ? q : q - 1) * 64];
+                acc[i][j] = t;
+            }
+        }
+    }
+}
+
+// Join of the S blocks of one tile after their main loops.  Each block takes a ticket (atomic add on
+// sk_cnt[tile]) when it starts (taken after the main loop, the returned value live across the loop made
+// hipcc rotate the accumulators through AGPRs, > 256 VGPRs); the S-1 first write their accumulators to slot `part` of the tile's workspace (in the
+// MFMA register layout: coalesced, device-coherent 16-byte stores), wait for their completion, and bump
+// sk_ready[tile], then exit.  The last
+// waits until the S-1 writes are visible and adds the slots into its accumulators in K order
+// (deterministic: the same sum whichever block arrives last), then runs the epilogue.  Deadlock-free for
+// any residency: a waiting block only waits for blocks that already took their ticket, i.e. are resident
+// and finish without waiting on anything.  The last block resets the tile's two counters once the others
+// are in, so every launch starts from zero whatever the split factor of the previous one.  Returns false
+// for the blocks that exit.
+template <int TM, int TN, int NW, int SKMAX, int SMEM>
+__device__ __forceinline__ bool splitk_join(const GemmParams& p, f32x4 (&acc)[TM][TN], int S, int tile, int part,
+                                           int tid, char* smem, unsigned ticket0) {
+    __syncthreads();  // every wave is past its main loop's LDS reads: LDS is free
+    if (tid == 0) *reinterpret_cast<unsigned*>(smem) = ticket0;  // (a separate __shared__ word would cost
+    __syncthreads();                                               //  the 192x128 tile its second block per CU)
+    const unsigned ticket = *reinterpret_cast<const unsigned*>(smem);
+    __syncthreads();
+    const bool last = ticket == (unsigned)(S - 1);
+    const int wid = tid >> 6, lane = tid & 63;
+    constexpr int PER_TILE = NW * TM * TN * 64;  // f32x4 per (tile, part) slot
+    f32x4* slot0 = p.sk_ws + (int64_t)tile * S * PER_TILE + (wid * TM * TN) * 64 + lane;
+    if (!last) {
+        // device-coherent (sc1) stores of the partial tile, completed (vmcnt 0) before the ready count: no
+        // device-scope fence, whose L2 write-back / invalidate (per block, or per spin) cost ~4x the GEMM
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc((void*)(slot0 - lane + (int64_t)part * PER_TILE), 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs,
+                                                       ((i * TN + j) * 64 + lane) * 16, 0, CPOL_SC1);
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+        if (tid == 0) __hip_atomic_fetch_add(p.sk_ready + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return false;
+    }
+    if (tid == 0) {
+        // bounded (~0.2 s; a real wait is a few microseconds): a protocol bug gives wrong tiles, never a hung GPU
+        for (int it = 0; it < (1 << 22); ++it) {
+            if (__hip_atomic_load(p.sk_ready + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(S - 1))
+                break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+        // every ticket of this tile is taken and every ready count is in: reset both for the next launch
+        // on this stream (ordered after this kernel)
+        __hip_atomic_store(p.sk_cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(p.sk_ready + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (S == 2 || SKMAX == 2) {
+        splitk_gather<TM, TN, NW, 2, SMEM>(acc, slot0, PER_TILE, part, smem, wid, lane);
+    } else if constexpr (SKMAX >= 4) {
+        if (S == 3)
+            splitk_gather<TM, TN, NW, 3, SMEM>(acc, slot0, PER_TILE, part, smem, wid, lane);
+        else
+            splitk_gather<TM, TN, NW, 4, SMEM>(acc, slot0, PER_TILE, part, smem, wid, lane);
+    }
+    return true;
+}
+
 // PIPE 0: stage(t+1) ; compute(t) ; vmcnt(0) ; __syncthreads        (2 LDS buffers)
 // PIPE 1: compute first half of tile t from registers read up front, release the LDS buffer with
 //         a raw s_barrier, stage tile t+2 into it, compute the second half, then a COUNTED
 //         vmcnt(G) retires tile t+1 while t+2 stays in flight across the next barrier.
-template <int BM, int BN, int WM, int WN, bool F16, int EPI, int PIPE>
-__global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(GemmParams p) {
+// SK: split-K instance, held to 256 VGPRs (two blocks per CU where their LDS fits) with a chunked residual preload
+template <int BM, int BN, int WM, int WN, bool F16, int EPI, int PIPE, bool SK = false>
+__global__ void __launch_bounds__(WM * WN * 64, SK && (BM + BN) * 512 <= 160 * 1024 ? 2 : 1) gemm_kernel(GemmParams p) {
     constexpr int NW = WM * WN;
     constexpr int WTM = BM / WM;
     constexpr int WTN = BN / WN;
@@ -362,16 +504,28 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(GemmParams p) {
     const int lane = tid & 63;
     const int wid = tid >> 6;
 
-    int m0, n0;
-    block_tile<BM, BN>(p, m0, n0);
+    const int S = SK ? p.ksplit : 1;
+    int m0, n0, sk_tile = 0, sk_part = 0;
+    unsigned ticket0 = 0;  // thread 0's split-K ticket
+    if constexpr (SK) {
+        int ntiles;
+        splitk_block(S, sk_tile, sk_part, ntiles);
+        block_tile<BM, BN>(p, m0, n0, sk_tile, ntiles);
+        if (tid == 0) ticket0 = __hip_atomic_fetch_add(p.sk_cnt + sk_tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        block_tile<BM, BN>(p, m0, n0);
+    }
 
     const int wm = wid / WN;
     const int wn = wid % WN;
     const int wm0 = wm * WTM;
     const int wn0 = wn * WTN;
 
-    const uint16_t* __restrict__ A = p.A;
-    const uint16_t* __restrict__ W = p.W;
+    const int nk_all = p.K / BK;
+    const int kt_begin = sk_part * nk_all / S;  // this block's K-tiles [kt_begin, kt_end)
+    const int kt_end = (sk_part + 1) * nk_all / S;
+    const uint16_t* __restrict__ A = p.A + kt_begin * BK;
+    const uint16_t* __restrict__ W = p.W + kt_begin * BK;
     const int M = p.M;
     const int lda = p.lda, ldw = p.ldw;
 
@@ -407,7 +561,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(GemmParams p) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    const int nk = p.K / BK;
+    const int nk = kt_end - kt_begin;
     const int lrow = lane & 15;
     const int lchunk = lane >> 4;
 
@@ -477,7 +631,9 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(GemmParams p) {
         // For the plain-store epilogues the register allocator then rotates that half's accumulators
         // through VGPRs every iteration (48 v_accvgpr copies per 32 MFMAs in the 128x128 ISA, 96 per 64
         // in 256x128; none for the other epilogues), so those instances issue every MFMA after it.
-        constexpr int I_EARLY = (EPI == EPI_STORE_F32 || EPI == EPI_STORE_ACT) ? 0 : TM / 2;
+        // The split-K instances (held to 256 VGPRs) issue all of them before the barrier: with the half
+        // split, hipcc rotated that half through AGPRs there too.
+        constexpr int I_EARLY = SK ? TM : (EPI == EPI_STORE_F32 || EPI == EPI_STORE_ACT) ? 0 : TM / 2;
         for (int kt = 0; kt < nk; ++kt) {
             const int cur = kt & 1;
             uint4 a[TM][2], b[TN][2];
@@ -507,10 +663,14 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(GemmParams p) {
         }
     }
 
+    if constexpr (SK)
+        if (!splitk_join<TM, TN, NW, SplitKMax<BM, BN>::value, 2 * STAGE>(p, acc, S, sk_tile, sk_part, tid, smem,
+                                                                                ticket0))
+            return;
     if constexpr (EPI == EPI_QKV_PREP)
         qkv_prep_tile<BM, NW, TM, TN, 2 * STAGE>(p, acc, m0, n0, wm0, wn0, tid, smem);
     else
-        gemm_epilogue<TM, TN, F16, EPI, NW>(p, acc, m0 + wm0, n0 + wn0, lane);
+        gemm_epilogue<TM, TN, F16, EPI, SK ? 32 : 1024>(p, acc, m0 + wm0, n0 + wn0, lane);
 }
 
 
@@ -703,7 +863,7 @@ __global__ void __launch_bounds__(512) gemm8_kernel(GemmParams p) {
         for (int ha = 0; ha < 2; ++ha)
 #pragma unroll
             for (int hb = 0; hb < 2; ++hb)
-                gemm_epilogue<QM, QN, F16, EPI, 8>(p, acc[ha][hb], m0 + ha * HA + wr * QM * 16,
+                gemm_epilogue<QM, QN, F16, EPI, 64>(p, acc[ha][hb], m0 + ha * HA + wr * QM * 16,
                                                    n0 + hb * 128 + wc * 32, lane);
     }
 }
@@ -831,30 +991,44 @@ struct DequantBatch {  // up to 8 same-format matrices expanded by one launch
 };
 
 template <int WQ>
-__global__ void __launch_bounds__(256) dequant_bf16_kernel(DequantBatch b) {
-    int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;  // 8-weight chunk: block g = c / 4, part j = c % 4
-    if (c >= b.end[b.n - 1]) return;
+__device__ __forceinline__ void dequant_chunk(const DequantBatch& b, int64_t c, uint4& o, uint16_t*& dst) {
     int mi = 0;
 #pragma unroll
     for (int i = 0; i < 7; ++i) mi += (i + 1 < b.n && c >= b.end[i]) ? 1 : 0;
     if (mi > 0) c -= b.end[mi - 1];
     const char* __restrict__ q = b.q[mi];
     const float* __restrict__ sc = b.s[mi];
-    const int64_t g = c >> 2;
+    const int64_t g = c >> 2;  // 8-weight chunk c: block g = c / 4, part j = c % 4
     const int j = (int)(c & 3);
-    uint32_t o0, o1, o2, o3;
     if constexpr (WQ == WF_Q4_K) {
         const uint32_t w = *reinterpret_cast<const uint32_t*>(q + g * 16 + j * 4);  // k 8j..8j+3 low, +4..7 high
         const float2 dm = *reinterpret_cast<const float2*>(sc + 2 * g);
-        deq_u4x4(w & 0x0f0f0f0fu, dm.x, -dm.y, o0, o1);
-        deq_u4x4((w >> 4) & 0x0f0f0f0fu, dm.x, -dm.y, o2, o3);
+        deq_u4x4(w & 0x0f0f0f0fu, dm.x, -dm.y, o.x, o.y);
+        deq_u4x4((w >> 4) & 0x0f0f0f0fu, dm.x, -dm.y, o.z, o.w);
     } else {
         const uint2 w = *reinterpret_cast<const uint2*>(q + g * 32 + j * 8);
         const float d = WQ == WF_Q8_0 ? sc[g] : sc[2 * g + (j >> 1)];  // Q6_K: one scale per 16 values
-        deq_i8x4(w.x, d, -128.0f * d, o0, o1);
-        deq_i8x4(w.y, d, -128.0f * d, o2, o3);
+        deq_i8x4(w.x, d, -128.0f * d, o.x, o.y);
+        deq_i8x4(w.y, d, -128.0f * d, o.z, o.w);
     }
-    *reinterpret_cast<uint4*>(b.out[mi] + c * 8) = make_uint4(o0, o1, o2, o3);
+    dst = b.out[mi] + c * 8;
+}
+
+// CPT chunks per thread, strided by the grid so each wave instruction stays coalesced; all loads of a
+// thread are issued before its first store
+template <int WQ, int CPT>
+__global__ void __launch_bounds__(256) dequant_bf16_kernel(DequantBatch b) {
+    const int64_t tot = b.end[b.n - 1];
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    const int64_t c0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    uint4 o[CPT];
+    uint16_t* dst[CPT];
+#pragma unroll
+    for (int k = 0; k < CPT; ++k)
+        if (c0 + k * stride < tot) dequant_chunk<WQ>(b, c0 + k * stride, o[k], dst[k]);
+#pragma unroll
+    for (int k = 0; k < CPT; ++k)
+        if (c0 + k * stride < tot) *reinterpret_cast<uint4*>(dst[k]) = o[k];
 }
 
 template <int BM, int BN, int WM, int WN, int EPI, int WQ>
@@ -999,19 +1173,70 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_q_kernel(GemmParams p) {
     if constexpr (EPI == EPI_QKV_PREP)
         qkv_prep_tile<BM, NW, TM, TN, 2 * STAGE>(p, acc, m0, n0, wm0, wn0, tid, smem);
     else
-        gemm_epilogue<TM, TN, false, EPI, NW>(p, acc, m0 + wm0, n0 + wn0, lane);
+        gemm_epilogue<TM, TN, false, EPI, NW >= 8 ? 64 : 1024>(p, acc, m0 + wm0, n0 + wn0, lane);
+}
+
+// split-K workspace of one stream: partial tiles + per-tile ticket / ready counters (zeroed once; each
+// launch leaves them zero, see splitk_join).  Launches on one stream are ordered, so one set per
+// stream suffices; it only grows (a grow waits for the stream before freeing the old buffers).
+struct SplitKWs {
+    void* ws = nullptr;
+    size_t ws_bytes = 0;
+    unsigned* cnt = nullptr;  // [2][tiles]: tickets, ready counts
+    size_t tiles = 0;
+};
+std::mutex g_sk_mu;
+std::unordered_map<hipStream_t, SplitKWs> g_sk;
+
+void splitk_setup(GemmParams& p, int ntiles, int S, size_t tile_bytes, hipStream_t s) {
+    std::lock_guard<std::mutex> lk(g_sk_mu);
+    SplitKWs& w = g_sk[s];
+    const size_t need = (size_t)ntiles * S * tile_bytes;
+    if (w.ws_bytes < need || w.tiles < (size_t)ntiles) ACEMI_HIP(hipStreamSynchronize(s));
+    if (w.ws_bytes < need) {
+        if (w.ws) ACEMI_HIP(hipFree(w.ws));
+        w.ws = nullptr;
+        w.ws_bytes = 0;
+        ACEMI_HIP(hipMalloc(&w.ws, need));
+        w.ws_bytes = need;
+    }
+    if (w.tiles < (size_t)ntiles) {
+        if (w.cnt) ACEMI_HIP(hipFree(w.cnt));
+        w.cnt = nullptr;
+        w.tiles = 0;
+        const size_t t = std::max<size_t>((size_t)ntiles, 4096);
+        ACEMI_HIP(hipMalloc(&w.cnt, 2 * t * sizeof(unsigned)));
+        ACEMI_HIP(hipMemsetAsync(w.cnt, 0, 2 * t * sizeof(unsigned), s));
+        w.tiles = t;
+    }
+    p.ksplit = S;
+    p.sk_ws = static_cast<f32x4*>(w.ws);
+    p.sk_cnt = w.cnt;
+    p.sk_ready = w.cnt + w.tiles;
 }
 
 template <int BM, int BN, int WM, int WN, bool F16, int EPI, int PIPE>
-void launch_cfg(const GemmParams& p, hipStream_t s) {
+void launch_cfg(GemmParams p, int S, hipStream_t s) {
     const int nbm = (p.M + BM - 1) / BM;
     const int nbn = p.N / BN;
-    const dim3 grid(nbm * nbn);
+    if (S > 1) {
+        if (p.K / 64 < 2 * S) throw std::runtime_error("gemm: split-K needs at least two K-tiles per part");
+        if (S > SplitKMax<BM, BN>::value) throw std::runtime_error("gemm: split-K factor too large for this tile");
+        splitk_setup(p, nbm * nbn, S, (size_t)BM * BN * 4, s);
+    }
+    const dim3 grid(nbm * nbn * (S > 1 ? S : 1));
     const dim3 block(WM * WN * 64);
-    if constexpr (EPI == EPI_QKV_PREP && BN != 128)
+    if constexpr (EPI == EPI_QKV_PREP && BN != 128) {
         throw std::runtime_error("gemm: the fused attention prep needs 128-wide column tiles");
-    else
+    } else if constexpr (WM * WN == 4 && PIPE == 1) {  // split-K instances: the 4-wave pipelined tiles
+        if (S > 1)
+            hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, F16, EPI, PIPE, true>), grid, block, 0, s, p);
+        else
+            hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, F16, EPI, PIPE>), grid, block, 0, s, p);
+    } else {
+        if (S > 1) throw std::runtime_error("gemm: split-K is for the 4-wave pipelined tiles");
         hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, F16, EPI, PIPE>), grid, block, 0, s, p);
+    }
 }
 
 template <int BM, bool F16, int EPI>
@@ -1025,19 +1250,22 @@ void launch_cfg8(const GemmParams& p, hipStream_t s) {
 // 4 = 192x128 PIPE1, 5 = 192x256 PIPE1 (8 waves 2x4), 6 = 192x64 PIPE1 (dense only), 7 = 96x128 PIPE1,
 // 8 = 64x128 PIPE1, 9 = 64x64 PIPE1 (8, 9 dense only: short sequences), 10 = 256x256 / 11 = 192x256 8-wave
 // ping-pong (dense only, N % 256 == 0)
+// variant + 100 * S (S = 2..4): the 4-wave tiles with split-K over S blocks per tile (splitk_join)
 template <bool F16, int EPI>
 void launch_variant(int variant, const GemmParams& p, hipStream_t s) {
-    switch (variant) {
-        case 0: launch_cfg<128, 128, 2, 2, F16, EPI, 0>(p, s); break;
-        case 1: launch_cfg<128, 128, 2, 2, F16, EPI, 1>(p, s); break;
-        case 2: launch_cfg<256, 256, 2, 4, F16, EPI, 1>(p, s); break;
-        case 3: launch_cfg<256, 128, 2, 2, F16, EPI, 1>(p, s); break;
-        case 4: launch_cfg<192, 128, 2, 2, F16, EPI, 1>(p, s); break;
-        case 5: launch_cfg<192, 256, 2, 4, F16, EPI, 1>(p, s); break;
-        case 6: launch_cfg<192, 64, 2, 2, F16, EPI, 1>(p, s); break;
-        case 7: launch_cfg<96, 128, 2, 2, F16, EPI, 1>(p, s); break;
-        case 8: launch_cfg<64, 128, 2, 2, F16, EPI, 1>(p, s); break;
-        case 9: launch_cfg<64, 64, 2, 2, F16, EPI, 1>(p, s); break;
+    const int S = variant / 100;
+    if (S > 1 && variant % 100 >= 10) throw std::runtime_error("gemm: split-K is for the 4-wave tiles");
+    switch (variant % 100) {
+        case 0: launch_cfg<128, 128, 2, 2, F16, EPI, 0>(p, S, s); break;
+        case 1: launch_cfg<128, 128, 2, 2, F16, EPI, 1>(p, S, s); break;
+        case 2: launch_cfg<256, 256, 2, 4, F16, EPI, 1>(p, S, s); break;
+        case 3: launch_cfg<256, 128, 2, 2, F16, EPI, 1>(p, S, s); break;
+        case 4: launch_cfg<192, 128, 2, 2, F16, EPI, 1>(p, S, s); break;
+        case 5: launch_cfg<192, 256, 2, 4, F16, EPI, 1>(p, S, s); break;
+        case 6: launch_cfg<192, 64, 2, 2, F16, EPI, 1>(p, S, s); break;
+        case 7: launch_cfg<96, 128, 2, 2, F16, EPI, 1>(p, S, s); break;
+        case 8: launch_cfg<64, 128, 2, 2, F16, EPI, 1>(p, S, s); break;
+        case 9: launch_cfg<64, 64, 2, 2, F16, EPI, 1>(p, S, s); break;
         case 10: launch_cfg8<256, F16, EPI>(p, s); break;
         case 11: launch_cfg8<192, F16, EPI>(p, s); break;
         default: throw std::runtime_error("gemm: bad variant");
@@ -1113,10 +1341,12 @@ double m_edge(int M, int bm) { return (double)M / (double)(((M + bm - 1) / bm) *
 
 int pick_variant(int M, int N, int K, bool quant) {
     if (g_forced_variant >= 0) {  // forced (tests / micro-benchmarks), where that tile supports the shape
-        const int f = g_forced_variant;
+        const int f = g_forced_variant % 100, S = g_forced_variant / 100;
         const bool wide = f == 2 || f == 5 || f == 10 || f == 11;
-        const bool dense_only = f == 6 || f >= 8;
-        if (!(wide && N % 256 != 0) && !(quant && dense_only)) return f;
+        const bool dense_only = f == 6 || f >= 8 || S > 1;
+        const bool sk_ok = S <= 1 || ((f == 1 || f == 3 || f == 4 ? S <= 2 : (f >= 6 && f <= 9 && S <= 4)) &&
+                                      K / 64 >= 2 * S);
+        if (!(wide && N % 256 != 0) && !(quant && dense_only) && sk_ok) return g_forced_variant;
     }
     const int64_t mb192 = (M + 191) / 192;
     const bool edge_ok = m_edge(M, 192) >= m_edge(M, 128) - 0.02;
@@ -1139,6 +1369,10 @@ int pick_variant(int M, int N, int K, bool quant) {
     // short sequences (60 s: M = 750): too few 96-row tiles to cover the CUs -> 64-row tiles, and
     // 64x64 when even those leave CUs idle (M = 750: N = 2048 projections 273-337 -> 364-453 TFLOP/s,
     // qkv 519 -> 567, tools/gemm_small_m.py)
+    // split-K (tools/gemm_msweep.py, MI355X): only the K = 6144 down projection between the short and the
+    // full-length tiles gains (M = 1500: 96x128 over 2 parts 722 vs 637 TFLOP/s for 64x128); elsewhere the
+    // join's device-coherent partial round trip (~3-4 us after the main loop) costs more than the fuller grid
+    if (N <= 2048 && K >= 4096 && M >= 1000 && M < 2000) return 207;
     const int64_t mb96 = (M + 95) / 96, mb64 = (M + 63) / 64;
     if (mb96 * (N / 128) <= 256) return mb64 * (N / 128) >= 256 ? 8 : 9;
     if (m_edge(M, 96) >= m_edge(M, 128) - 0.02) return 7;  // N = 2048: 512 tiles, two per CU
@@ -1219,13 +1453,26 @@ void launch_dequant_bf16_batch(const DequantJob* jobs, int n, hipStream_t s) {
         b.end[i] = tot;
     }
     b.n = n;
-    const dim3 grid((unsigned)((tot + 255) / 256));
+    static const int cpt = [] {  // chunks per thread (A/B knob; 2 by default: 46 vs 47.5 / 49 us for 1 / 4)
+        const char* e = std::getenv("ACE_MI_DEQ_CPT");
+        const int v = e ? std::atoi(e) : 2;
+        return v == 1 || v == 4 || v == 8 ? v : 2;
+    }();
+    const dim3 grid((unsigned)((tot + 256 * cpt - 1) / (256 * cpt)));
+#define ACEMI_DEQ(WQ)                                                                         \
+    switch (cpt) {                                                                            \
+        case 1: hipLaunchKernelGGL((dequant_bf16_kernel<WQ, 1>), grid, dim3(256), 0, s, b); break; \
+        case 4: hipLaunchKernelGGL((dequant_bf16_kernel<WQ, 4>), grid, dim3(256), 0, s, b); break; \
+        case 8: hipLaunchKernelGGL((dequant_bf16_kernel<WQ, 8>), grid, dim3(256), 0, s, b); break; \
+        default: hipLaunchKernelGGL((dequant_bf16_kernel<WQ, 2>), grid, dim3(256), 0, s, b); break; \
+    }
     switch (jobs[0].w.fmt) {
-        case WF_Q8_0: hipLaunchKernelGGL(dequant_bf16_kernel<WF_Q8_0>, grid, dim3(256), 0, s, b); break;
-        case WF_Q4_K: hipLaunchKernelGGL(dequant_bf16_kernel<WF_Q4_K>, grid, dim3(256), 0, s, b); break;
-        case WF_Q6_K: hipLaunchKernelGGL(dequant_bf16_kernel<WF_Q6_K>, grid, dim3(256), 0, s, b); break;
+        case WF_Q8_0: ACEMI_DEQ(WF_Q8_0); break;
+        case WF_Q4_K: ACEMI_DEQ(WF_Q4_K); break;
+        case WF_Q6_K: ACEMI_DEQ(WF_Q6_K); break;
         default: throw std::runtime_error("dequant: bad weight format");
     }
+#undef ACEMI_DEQ
     ACEMI_HIP(hipGetLastError());
 }
 

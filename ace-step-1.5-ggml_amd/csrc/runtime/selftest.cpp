@@ -287,7 +287,7 @@ ace_ggml_status ace_mi_bench_gemm(int32_t act_type, int32_t epi, int32_t variant
 
 // Force a GEMM kernel variant for subsequent launches (-1 = automatic).
 ace_ggml_status ace_mi_gemm_variant(int32_t variant) {
-    if (variant < -1 || variant > 11) return ACE_GGML_ERR_INVALID_ARG;
+    if (variant < -1 || variant % 100 > 11 || variant > 411) return ACE_GGML_ERR_INVALID_ARG;
     acemi::gemm_force_variant(variant);
     return ACE_GGML_OK;
 }

@@ -190,11 +190,12 @@ def test_attention_running_max_moves_mid_sequence(nk, mode):
     _check_attn(got, q, kv, hq, hkv, 0, None, scale, mode)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 204, 207, 208, 307, 409])
 @pytest.mark.parametrize("M,N,K", [(1, 256, 64), (300, 512, 128), (1000, 768, 2048), (513, 256, 6144)])
 def test_gemm_all_variants(variant, M, N, K):
-    """Every GEMM kernel variant (128x128 / 256x256 / 256x128 / 192x128 / 192x256, both pipelines),
-    incl. M edges and K = 1, 2 and many tiles (pipeline prologue/epilogue paths)."""
+    """Every GEMM kernel variant (128x128 / 256x256 / 256x128 / 192x128 / 192x256, both pipelines, and
+    split-K over 2..4 blocks per tile: variant + 100 * S), incl. M edges and K = 1, 2 and many tiles
+    (pipeline prologue/epilogue paths; split-K falls back to the automatic tile below 2 K-tiles per part)."""
     capi = _capi()
     if N % 256 and variant in (2, 5, 10, 11):
         pytest.skip("256-wide tiles need N % 256 == 0")
@@ -219,7 +220,7 @@ def test_gemm_all_variants(variant, M, N, K):
     np.testing.assert_allclose(_vals(got_sw, 0), sw, rtol=2.0 ** -8, atol=1e-4)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 204, 207, 408])
 @pytest.mark.parametrize("epi", [2, 3])
 @pytest.mark.parametrize("M,N,K", [(300, 512, 128), (1000, 768, 2048), (9001, 512, 256)])
 def test_gemm_residual_epilogues(variant, epi, M, N, K):
@@ -258,3 +259,28 @@ def test_attention_key_split_with_one_part_fully_masked():
     for mode in ("split", "pvsplit"):
         got = _capi().kernel_attention(q, kv, hq, hkv, window=0, kmask=kmask, scale=scale, **MODES[mode])
         _check_attn(got, q, kv, hq, hkv, 0, kmask, scale, mode)
+
+
+@pytest.mark.parametrize("variant", [204, 207, 307, 408])
+def test_gemm_splitk_deterministic(variant):
+    """Split-K: the last block of a tile adds the parts in K order, so repeated launches (with the per-tile
+    ticket counters carried over between launches of different tile counts) give identical bits, equal to
+    the fp32 sum of the S partial products in K order to within the MFMA accumulation rounding."""
+    capi = _capi()
+    rng = np.random.default_rng(variant)
+    outs = []
+    for M, N, K in [(3000, 2048, 2048), (700, 512, 1024), (3000, 2048, 2048)]:
+        a = _bits(rng.standard_normal((M, K)).astype(np.float32), 0) if not outs or M != 3000 else a0
+        w = _bits((rng.standard_normal((N, K)) * 0.05).astype(np.float32), 0) if not outs or M != 3000 else w0
+        if not outs:
+            a0, w0 = a, w
+        capi.gemm_variant(variant)
+        try:
+            outs.append(capi.kernel_gemm(a, w, act_type=0, epi=0))
+            outs.append(capi.kernel_gemm(a, w, act_type=0, epi=0))
+        finally:
+            capi.gemm_variant(-1)
+        np.testing.assert_array_equal(outs[-1], outs[-2])
+        av, wv = _vals(a, 0).astype(np.float64), _vals(w, 0).astype(np.float64)
+        assert np.all(np.abs(outs[-1] - av @ wv.T) <= 2e-6 * (np.abs(av) @ np.abs(wv).T) + 1e-6)
+    np.testing.assert_array_equal(outs[0], outs[4])
