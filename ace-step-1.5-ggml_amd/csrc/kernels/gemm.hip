@@ -627,13 +627,14 @@ __global__ void __launch_bounds__(WM * WN * 64, SK && (BM + BN) * 512 <= 160 * 1
             wait_vmcnt<0>();
         }
         __builtin_amdgcn_s_barrier();
-        // The first half of the tile's MFMAs normally issues before the barrier (overlapping the wait).
-        // For the plain-store epilogues the register allocator then rotates that half's accumulators
-        // through VGPRs every iteration (48 v_accvgpr copies per 32 MFMAs in the 128x128 ISA, 96 per 64
-        // in 256x128; none for the other epilogues), so those instances issue every MFMA after it.
-        // The split-K instances (held to 256 VGPRs) issue all of them before the barrier: with the half
-        // split, hipcc rotated that half through AGPRs there too.
-        constexpr int I_EARLY = SK ? TM : (EPI == EPI_STORE_F32 || EPI == EPI_STORE_ACT) ? 0 : TM / 2;
+        // MFMAs issued before the buffer-release barrier: the first half of the tile for the SwiGLU
+        // (gate|up) instances, none elsewhere (240 s step, tools/ab_multi.sh: qkv with the fused prep 66.5
+        // -> 61.6 us, the N = 2048 projections ~1 % faster; gate|up 1 % slower with none).  For the plain
+        // stores the half split also made the register allocator rotate that half's accumulators through
+        // VGPRs every iteration (48 v_accvgpr copies per 32 MFMAs in the 128x128 ISA).  The split-K
+        // instances (held to 256 VGPRs) issue all of them before it: with the half split, hipcc rotated
+        // that half through AGPRs there.
+        constexpr int I_EARLY = SK ? TM : EPI == EPI_SWIGLU ? TM / 2 : 0;
         for (int kt = 0; kt < nk; ++kt) {
             const int cur = kt & 1;
             uint4 a[TM][2], b[TN][2];

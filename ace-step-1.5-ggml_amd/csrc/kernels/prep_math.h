@@ -32,13 +32,13 @@ __device__ __forceinline__ int vperm(int k) {
 }
 
 // One token's head row, 16 lanes per token (lane & 15 = d / 4): y[0..3] = dims d..d+3, y[4..7] = dims
-// 64+d..64+d+3 (the NEOX rotation pairs d with d+64 inside the lane).  w: norm weights or null (plain
-// copy); cs / sn: the position's RoPE row (+ d) or null.  Writes fp16 hi into dst[0..127] and, when
-// plane > 0, lo into dst[plane..].
-__device__ __forceinline__ void head_row(float (&y)[8], const float* w, int d, float eps, const float* cs,
-                                         const float* sn, uint16_t* dst, int64_t plane) {
-    if (w) {
-        const float4 w0 = *(const float4*)(w + d), w1 = *(const float4*)(w + 64 + d);
+// 64+d..64+d+3 (the NEOX rotation pairs d with d+64 inside the lane).  has_w: RMSNorm with weights w0 / w1
+// (dims d.. / 64+d..); has_rope: rotate by the position's c4 / s4 (dims d..d+3 of its RoPE row).  Writes fp16
+// hi into dst[0..127] and, when plane > 0, lo into dst[plane..].
+__device__ __forceinline__ void head_row_v(float (&y)[8], bool has_w, const float4& w0, const float4& w1, int d,
+                                           float eps, bool has_rope, const float4& c4, const float4& s4,
+                                           uint16_t* dst, int64_t plane) {
+    if (has_w) {
         float ss = 0.f;
 #pragma unroll
         for (int j = 0; j < 8; ++j) ss += y[j] * y[j];
@@ -50,8 +50,7 @@ __device__ __forceinline__ void head_row(float (&y)[8], const float* w, int d, f
         for (int j = 0; j < 8; ++j) y[j] = __fmul_rn(__fmul_rn(y[j], sc), wv[j]);
     }
     float r[8];
-    if (cs) {
-        const float4 c4 = *(const float4*)cs, s4 = *(const float4*)sn;
+    if (has_rope) {
         const float c[4] = {c4.x, c4.y, c4.z, c4.w}, s[4] = {s4.x, s4.y, s4.z, s4.w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -68,6 +67,15 @@ __device__ __forceinline__ void head_row(float (&y)[8], const float* w, int d, f
         *(uint2*)(dst + plane + d) = pk4(f16_lo(r[0]), f16_lo(r[1]), f16_lo(r[2]), f16_lo(r[3]));
         *(uint2*)(dst + plane + 64 + d) = pk4(f16_lo(r[4]), f16_lo(r[5]), f16_lo(r[6]), f16_lo(r[7]));
     }
+}
+
+// head_row_v with the weights and RoPE row read here: w = norm weights or null (plain copy), cs / sn = the
+// position's RoPE row (+ d) or null
+__device__ __forceinline__ void head_row(float (&y)[8], const float* w, int d, float eps, const float* cs,
+                                         const float* sn, uint16_t* dst, int64_t plane) {
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    head_row_v(y, w != nullptr, w ? *(const float4*)(w + d) : z, w ? *(const float4*)(w + 64 + d) : z, d, eps,
+               cs != nullptr, cs ? *(const float4*)cs : z, cs ? *(const float4*)sn : z, dst, plane);
 }
 
 // 16 values of one V^T row segment (keys g0 + vperm(k), k = 0..15) as fp16 hi / lo words.
