@@ -144,6 +144,67 @@ __global__ void __launch_bounds__(256) rmsnorm_mod_kernel(const float* __restric
     }
 }
 
+// Same operator, one 64-lane wave per row (4 rows per workgroup): H = 512 * NC, each lane holds NC runs of 8
+// consecutive values (two 16-B loads, one 16-B store per run), the row sum is a wave reduction (no LDS, no
+// barrier), and the w / scale / shift loads are issued before it so their latency hides under the shuffles.
+template <bool F16, int NC>
+__global__ void __launch_bounds__(256) rmsnorm_mod_rows_kernel(const float* __restrict__ x, int M, int H,
+                                                               const float* __restrict__ w,
+                                                               const float* __restrict__ scale,
+                                                               const float* __restrict__ shift, int64_t mod_stride,
+                                                               int rows_per_item, float eps,
+                                                               uint16_t* __restrict__ out) {
+    const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (m >= M) return;
+    const int lane = threadIdx.x & 63;
+    const float* xr = x + (int64_t)m * H;
+    float4 v[2 * NC], wv[2 * NC];
+    float ss = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const int i = c * 512 + lane * 8;
+        v[2 * c] = *(const float4*)(xr + i);
+        v[2 * c + 1] = *(const float4*)(xr + i + 4);
+        wv[2 * c] = *(const float4*)(w + i);
+        wv[2 * c + 1] = *(const float4*)(w + i + 4);
+    }
+#pragma unroll
+    for (int k = 0; k < 2 * NC; ++k) ss += v[k].x * v[k].x + v[k].y * v[k].y + v[k].z * v[k].z + v[k].w * v[k].w;
+    const int item = m / rows_per_item;
+    const float* scp = scale ? scale + (int64_t)item * mod_stride : nullptr;
+    const float* shp = shift ? shift + (int64_t)item * mod_stride : nullptr;
+    ss = wave_sum(ss);
+    const float sc = 1.0f / sqrtf(ss / (float)H + eps);
+    uint16_t* orow = out + (int64_t)m * H;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const int i = c * 512 + lane * 8;
+        float y[8] = {v[2 * c].x, v[2 * c].y, v[2 * c].z, v[2 * c].w,
+                      v[2 * c + 1].x, v[2 * c + 1].y, v[2 * c + 1].z, v[2 * c + 1].w};
+        const float ww[8] = {wv[2 * c].x, wv[2 * c].y, wv[2 * c].z, wv[2 * c].w,
+                             wv[2 * c + 1].x, wv[2 * c + 1].y, wv[2 * c + 1].z, wv[2 * c + 1].w};
+        float s8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, h8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (scp) {
+            const float4 a0 = *(const float4*)(scp + i), a1 = *(const float4*)(scp + i + 4);
+            const float4 b0 = *(const float4*)(shp + i), b1 = *(const float4*)(shp + i + 4);
+            s8[0] = a0.x; s8[1] = a0.y; s8[2] = a0.z; s8[3] = a0.w; s8[4] = a1.x; s8[5] = a1.y; s8[6] = a1.z; s8[7] = a1.w;
+            h8[0] = b0.x; h8[1] = b0.y; h8[2] = b0.z; h8[3] = b0.w; h8[4] = b1.x; h8[5] = b1.y; h8[6] = b1.z; h8[7] = b1.w;
+        }
+        uint32_t pk[4];
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) {
+            float t0 = __fmul_rn(__fmul_rn(y[j], sc), ww[j]);
+            float t1 = __fmul_rn(__fmul_rn(y[j + 1], sc), ww[j + 1]);
+            if (scp) {
+                t0 = __fadd_rn(__fmul_rn(t0, __fadd_rn(s8[j], 1.0f)), h8[j]);
+                t1 = __fadd_rn(__fmul_rn(t1, __fadd_rn(s8[j + 1], 1.0f)), h8[j + 1]);
+            }
+            pk[j / 2] = (uint32_t)to_act(F16, t0) | ((uint32_t)to_act(F16, t1) << 16);
+        }
+        *(uint4*)(orow + i) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+    }
+}
+
 // f32 output variant for the condition encoders' final norm: ggml_rms_norm + ggml_mul by w
 template <int VPT>
 __global__ void __launch_bounds__(256) rmsnorm_f32_kernel(const float* __restrict__ x, int64_t row_step, int H,
@@ -449,6 +510,30 @@ void launch_rmsnorm_mod(ActType t, const float* x, int M, int H, const float* w,
 #define ACEMI_RMS(F, V, X)                                                                                   \
     hipLaunchKernelGGL((rmsnorm_mod_kernel<F, V, X>), dim3(M), dim3(256), 0, s, x, H, w, scale, shift, mod_stride, \
                        rows_per_item, eps, out)
+    // the DiT widths (H = 512 * NC): wave-per-row kernel (ACE_MI_RMSNORM_ROWS=0 keeps the workgroup-per-row one)
+    static const bool rows = [] {
+        const char* e = std::getenv("ACE_MI_RMSNORM_ROWS");
+        return !(e && e[0] == '0');
+    }();
+    if (!x3 && rows && H % 512 == 0 && H <= 4096) {
+        const dim3 g((M + 3) / 4);
+#define ACEMI_RMSR(F, NC) \
+    hipLaunchKernelGGL((rmsnorm_mod_rows_kernel<F, NC>), g, dim3(256), 0, s, x, M, H, w, scale, shift, mod_stride, \
+                       rows_per_item, eps, out)
+        switch (H / 512) {
+            case 1: if (f16) ACEMI_RMSR(true, 1); else ACEMI_RMSR(false, 1); break;
+            case 2: if (f16) ACEMI_RMSR(true, 2); else ACEMI_RMSR(false, 2); break;
+            case 3: if (f16) ACEMI_RMSR(true, 3); else ACEMI_RMSR(false, 3); break;
+            case 4: if (f16) ACEMI_RMSR(true, 4); else ACEMI_RMSR(false, 4); break;
+            case 5: if (f16) ACEMI_RMSR(true, 5); else ACEMI_RMSR(false, 5); break;
+            case 6: if (f16) ACEMI_RMSR(true, 6); else ACEMI_RMSR(false, 6); break;
+            case 7: if (f16) ACEMI_RMSR(true, 7); else ACEMI_RMSR(false, 7); break;
+            default: if (f16) ACEMI_RMSR(true, 8); else ACEMI_RMSR(false, 8); break;
+        }
+#undef ACEMI_RMSR
+        ACEMI_HIP(hipGetLastError());
+        return;
+    }
     if (x3) {
         if (vpt == 1) ACEMI_RMS(true, 1, true);
         else if (vpt == 2) ACEMI_RMS(true, 2, true);

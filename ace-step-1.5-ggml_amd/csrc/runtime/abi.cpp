@@ -269,6 +269,7 @@ ace_ggml_status run_sampler(ace_ggml_context* ctx, int32_t batch, float* d_xt, c
                 fresh = true;
             }
             io.reuse_cross = cache_cross && !fresh;
+            io.reuse_stage = i > 0;  // quantized weights: dequantized once per call (engine.h)
             io.t = ctx->d_sched + (size_t)i * batch;
             io.r = io.t;
             ctx->dit->forward(io, s);

@@ -19,6 +19,8 @@ DitEngine::DitEngine(int device) : device_(device) {
     fused_prep_ = !(u && u[0] && u[0] != '0');
     const char* q = std::getenv("ACE_MI_QUANT_STAGED");
     staged_quant_ = !(q && q[0] == '0');
+    const char* h = std::getenv("ACE_MI_QUANT_STAGE_SCOPE");
+    stage_per_call_ = !(h && std::strcmp(h, "layer") == 0);
 }
 
 DitEngine::~DitEngine() {
@@ -41,7 +43,7 @@ DitEngine::LayerViews DitEngine::layer_views(int li, bool staged) {
     const DevLayer& ly = model_.layers[li];
     const DevWeight* ws[6] = {&ly.w_qkv, &ly.w_o, &ly.w_cq, &ly.w_co, &ly.w_gu, &ly.w_down};
     WeightView v[6];
-    char* base = staged ? static_cast<char*>(wring_.p) : nullptr;
+    char* base = staged ? stage_slot(li) : nullptr;
     size_t off = 0;
     for (int i = 0; i < 6; ++i) {
         v[i] = ws[i]->view();
@@ -59,7 +61,7 @@ DitEngine::LayerViews DitEngine::layer_views(int li, bool staged) {
 void DitEngine::stage_layer(int li, hipStream_t st) {
     const DevLayer& ly = model_.layers[li];
     const DevWeight* ws[6] = {&ly.w_qkv, &ly.w_o, &ly.w_cq, &ly.w_co, &ly.w_gu, &ly.w_down};
-    char* base = static_cast<char*>(wring_.p);
+    char* base = stage_slot(li);
     size_t off = 0;
     DequantJob jobs[6];
     int n = 0;
@@ -76,6 +78,12 @@ void DitEngine::stage_layer(int li, hipStream_t st) {
     tic(st);
     if (n > 0) launch_dequant_bf16_batch(jobs, n, st);
     toc("dequant_stage", st);
+}
+
+// Layer li's bf16 image: its own slot when the images of the whole model are kept for the sampling call,
+// else the single slot every layer shares.
+char* DitEngine::stage_slot(int li) {
+    return static_cast<char*>(wring_.p) + (stage_per_call_ ? (size_t)li * stage_slot_bytes_ : 0);
 }
 
 void DitEngine::ensure(Buf& b, size_t bytes) {
@@ -352,15 +360,21 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
     // staged dequant: each layer's quantized block matrices are expanded to their bf16 image right before the
     // layer, in stream order, into one workspace slot (see engine.h)
     const bool staged = staged_quant_ && n_layers > 0 && weight_quantized(m.layers[0].w_gu.fmt);
+    bool restage = true;
     if (staged) {
         const DevLayer& l0 = m.layers[0];
-        ensure(wring_, wbytes(l0.w_qkv) + wbytes(l0.w_o) + wbytes(l0.w_cq) + wbytes(l0.w_co) + wbytes(l0.w_gu) +
-                           wbytes(l0.w_down));
+        stage_slot_bytes_ = wbytes(l0.w_qkv) + wbytes(l0.w_o) + wbytes(l0.w_cq) + wbytes(l0.w_co) +
+                            wbytes(l0.w_gu) + wbytes(l0.w_down);
+        ensure(wring_, stage_slot_bytes_ * (stage_per_call_ ? n_layers : 1));
+        // per-call scope: the images written by the first forward of a sampling call serve its later steps
+        // (the weights are loop-invariant); any other forward expands them again
+        restage = !(stage_per_call_ && io.reuse_stage && stage_layers_ >= n_layers);
+        stage_layers_ = stage_per_call_ ? n_layers : 0;
     }
 
     for (int li = 0; li < n_layers; ++li) {  // :1466-1535
         const DevLayer& ly = m.layers[li];
-        if (staged) stage_layer(li, s);
+        if (staged && restage) stage_layer(li, s);
         const LayerViews lw = layer_views(li, staged);
         const float* lm = mods + (size_t)li * B * 6 * H;
         const float* shift_msa = lm + 0 * H;

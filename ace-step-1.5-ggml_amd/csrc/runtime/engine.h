@@ -33,6 +33,9 @@ struct ForwardIO {
     // valid when enc / enc_mask / B / L / layer count are those of that forward; the sampler entry
     // guarantees it.
     bool reuse_cross = false;
+    // Reuse the bf16 images of the quantized block weights written by the previous forward of this engine
+    // (staged dequant at sampling-call scope): set by the sampler entry for steps 1.. of one call.
+    bool reuse_stage = false;
 };
 
 // One condition-encoder pass for B items of n tokens each (forward_lyric_encoder /
@@ -117,8 +120,16 @@ class DitEngine {
     struct LayerViews {
         WeightView qkv, o, cq, co, gu, down;
     };
+    // Scope of the staged images (ACE_MI_QUANT_STAGE_SCOPE): "call" (default) keeps one slot per layer, so
+    // the dequant runs once per sampling call (step 0) instead of once per step, at the cost of a bf16
+    // image of the block weights as workspace (2.8 GB for the 24-layer DiT: 1 % of HBM); "layer" = the
+    // single shared slot, expanded before every layer of every forward.
     bool staged_quant_ = true;
+    bool stage_per_call_ = true;
+    size_t stage_slot_bytes_ = 0;
+    int stage_layers_ = 0;  // layers whose images wring_ holds (per-call scope)
     Buf wring_;
+    char* stage_slot(int li);
     LayerViews layer_views(int li, bool staged);
     void stage_layer(int li, hipStream_t st);
     // profiling

@@ -227,3 +227,43 @@ def test_staged_dequant_equals_fused(tiny_ckpt, monkeypatch, qtype, width):
     assert np.isfinite(outs[0]).all()
     for o in outs[1:]:
         np.testing.assert_array_equal(o, outs[0])
+
+
+@pytest.mark.parametrize("qtype", ["q8_0", "q4_k"])
+def test_sampling_call_scope_staging_equals_per_layer(tiny_ckpt, monkeypatch, qtype):
+    """ace_mi_dit_sample_ex with quantized weights: the bf16 images expanded once per sampling call
+    (ACE_MI_QUANT_STAGE_SCOPE=call, default; steps 1.. reuse them) give the same bits as expanding them
+    before every layer of every step (=layer) and as the dequant-fused GEMMs (ACE_MI_QUANT_STAGED=0).
+    A first call on fewer layers (ACE_GGML_DIT_MAX_LAYERS) must not leave images a later call reuses."""
+    import torch
+    from acestep_mi355x.capi import GGMLCAPIBridge
+    monkeypatch.setenv("ACE_GGML_DIT_WEIGHT_QTYPE", qtype)
+    rng = np.random.default_rng(9)
+    B, T, L = 2, 301, 20
+    x0 = rng.standard_normal((B, T, 64)).astype(np.float32)
+    c = rng.standard_normal((B, T, 128)).astype(np.float32)
+    e = rng.standard_normal((B, L, 256)).astype(np.float32)
+    sched = [1.0, 0.75, 0.5, 0.25]
+    dc, de = (torch.from_numpy(a).cuda() for a in (c, e))
+    outs = []
+    for scope, staged in (("call", "1"), ("layer", "1"), ("call", "0")):
+        monkeypatch.setenv("ACE_MI_QUANT_STAGE_SCOPE", scope)
+        monkeypatch.setenv("ACE_MI_QUANT_STAGED", staged)
+        br = GGMLCAPIBridge()
+        br.load_dit(tiny_ckpt)
+        monkeypatch.setenv("ACE_GGML_DIT_MAX_LAYERS", "1")
+        xt = torch.from_numpy(x0).cuda()
+        torch.cuda.synchronize()
+        br.dit_sample_ex_device(B, T, L, xt.data_ptr(), dc.data_ptr(), de.data_ptr(), 0, 0, sched)
+        br.synchronize()
+        monkeypatch.delenv("ACE_GGML_DIT_MAX_LAYERS")
+        for _ in range(2):  # the second call expands the images again and must give the same bits
+            xt = torch.from_numpy(x0).cuda()
+            torch.cuda.synchronize()
+            br.dit_sample_ex_device(B, T, L, xt.data_ptr(), dc.data_ptr(), de.data_ptr(), 0, 0, sched)
+            br.synchronize()
+            outs.append(xt.cpu().numpy())
+        br.close()
+    assert np.isfinite(outs[0]).all()
+    for o in outs[1:]:
+        np.testing.assert_array_equal(o, outs[0])
