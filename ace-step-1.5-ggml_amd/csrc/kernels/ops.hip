@@ -510,10 +510,12 @@ void launch_rmsnorm_mod(ActType t, const float* x, int M, int H, const float* w,
 #define ACEMI_RMS(F, V, X)                                                                                   \
     hipLaunchKernelGGL((rmsnorm_mod_kernel<F, V, X>), dim3(M), dim3(256), 0, s, x, H, w, scale, shift, mod_stride, \
                        rows_per_item, eps, out)
-    // the DiT widths (H = 512 * NC): wave-per-row kernel (ACE_MI_RMSNORM_ROWS=0 keeps the workgroup-per-row one)
+    // ACE_MI_RMSNORM_ROWS=1: wave-per-row kernel for H = 512 * NC.  Measured equal to the workgroup-per-row
+    // kernel at 240 s (rocprof 9.4 vs 9.2 us per launch, 3.9 TB/s: the ~37 MB launch is ramp/tail bound), so
+    // not the default.
     static const bool rows = [] {
         const char* e = std::getenv("ACE_MI_RMSNORM_ROWS");
-        return !(e && e[0] == '0');
+        return e && e[0] == '1';
     }();
     if (!x3 && rows && H % 512 == 0 && H <= 4096) {
         const dim3 g((M + 3) / 4);

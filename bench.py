@@ -150,9 +150,6 @@ def main():
         br.dit_sample_ex_device(b_loc, T, L, xt.data_ptr(), ctx.data_ptr(), enc.data_ptr(), 0, 0, sch,
                                 cache_cross=args.cross_cache, stream=stream)
 
-    def step(i):  # single step (profiling pass)
-        run(i, 1)
-
     if args.warmup > 0:
         run(0, args.warmup)
     sync()
@@ -176,14 +173,15 @@ def main():
     if not args.no_profile:
         br.profile_enable(True)
         br.profile_reset()
-        nprof = 2
-        for i in range(nprof):
-            step(i)
+        # one generation-loop call of the timed region's length (per-call work such as the staged dequant of
+        # quantized weights is then spread over its steps exactly as in the timed run)
+        nprof = args.steps
+        run(0, nprof)
         sync()
         prof = br.profile_get()
         br.profile_enable(False)
         for name, ms, cnt in prof:
-            breakdown[name] = {"ms_per_step": round(ms / nprof, 4), "launches_per_step": cnt // nprof,
+            breakdown[name] = {"ms_per_step": round(ms / nprof, 4), "launches_per_step": round(cnt / nprof, 3),
                                "avg_us": round(1000.0 * ms / max(cnt, 1), 2)}
         gu = [p for p in prof if p[0] == "gemm_gate_up"]
         if gu:
@@ -225,12 +223,11 @@ def main():
         if not args.no_profile:
             br.profile_enable(True)
             br.profile_reset()
-            for i in range(2):
-                step(i)
+            run(0, args.steps)
             sync()
             prof_b = br.profile_get()
             br.profile_enable(False)
-            frac = block_linear_frac(prof_b, 2, T, b_loc, info)
+            frac = block_linear_frac(prof_b, args.steps, T, b_loc, info)
             if frac is not None:
                 bf16_line["dit_block_linears_frac_of_bf16_peak"] = frac
             gu = [p for p in prof_b if p[0] == "gemm_gate_up"]
