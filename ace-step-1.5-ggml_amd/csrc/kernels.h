@@ -26,6 +26,11 @@ struct PrepArgs {
     uint16_t* kh;
     uint16_t* vt;
     int64_t q_plane = 0, k_plane = 0, v_plane = 0;  // >0: also write lo = f16(x - f16(x)) planes
+    // > 1 (k / v sections only): one launch for `layers` consecutive layers, layer l reading src + l*src_layer,
+    // writing kh + l*kh_layer / vt + l*vt_layer, normalising by k_norm_layers[l] (a device table)
+    int layers = 1;
+    int64_t src_layer = 0, kh_layer = 0, vt_layer = 0;
+    const float* const* k_norm_layers = nullptr;
 };
 
 // ---------------------------------------------------------------- GEMM

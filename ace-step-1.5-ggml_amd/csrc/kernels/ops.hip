@@ -277,7 +277,14 @@ __global__ void __launch_bounds__(256) embed_rows_kernel(const void* __restrict_
 // grid: (n_pad/64 token tiles, nq + nk + nv head slots, B).  Slot < nq: one q head; < nq+nk: one k
 // head; else the V^T transpose of one kv head.  One workgroup = 64 tokens of one head.
 __global__ void __launch_bounds__(256) attn_prep_kernel(PrepArgs a) {
-    const int b = blockIdx.z;
+    const int layer = blockIdx.z / a.B;
+    const int b = blockIdx.z - layer * a.B;
+    if (a.layers > 1) {  // PrepArgs::layers: this block's layer
+        a.src += layer * a.src_layer;
+        a.kh += layer * a.kh_layer;
+        a.vt += layer * a.vt_layer;
+        a.k_norm = a.k_norm_layers[layer];
+    }
     const int n0 = blockIdx.x * 64;
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
@@ -585,7 +592,9 @@ void launch_attn_prep(const PrepArgs& a, hipStream_t s) {
     ACEMI_CHECK(a.n_pad % 64 == 0, "attn_prep: n_pad % 64");
     const int slots = (a.q_col >= 0 ? a.hq : 0) + (a.k_col >= 0 ? a.hkv : 0) + (a.v_col >= 0 ? a.hkv : 0);
     ACEMI_CHECK(a.ld % 4 == 0 && (a.v_col < 0 || a.v_col % 4 == 0), "attn_prep: alignment");
-    hipLaunchKernelGGL(attn_prep_kernel, dim3(a.n_pad / 64, slots, a.B), dim3(256), 0, s, a);
+    ACEMI_CHECK(a.layers >= 1 && (a.layers == 1 || (a.q_col < 0 && a.k_norm_layers && a.src_layer % 4 == 0)),
+                "attn_prep: multi-layer launches are for k / v sections with a k-norm table");
+    hipLaunchKernelGGL(attn_prep_kernel, dim3(a.n_pad / 64, slots, a.B * a.layers), dim3(256), 0, s, a);
     ACEMI_HIP(hipGetLastError());
 }
 

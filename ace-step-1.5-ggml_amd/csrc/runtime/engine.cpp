@@ -26,7 +26,7 @@ DitEngine::DitEngine(int device) : device_(device) {
 DitEngine::~DitEngine() {
     for (Buf* b : {&a0_, &x_, &act_, &attn_, &act2_, &qkv_, &qh_, &kh_, &vt_, &kbias_, &enc_act_, &encp_, &ckv_, &kc_,
                    &vc_, &kbias_c_, &attn_part_, &freq_, &freq_act_, &th_, &th_act_, &temb_t_, &temb_r_, &temb_act_, &proj_,
-                   &mods_, &outmod_, &cos_, &sin_, &ein_}) {
+                   &mods_, &outmod_, &cos_, &sin_, &ein_, &knorm_tab_}) {
         if (b->p) (void)hipFree(b->p);
     }
     if (ev0_) (void)hipEventDestroy(ev0_);
@@ -84,6 +84,19 @@ void DitEngine::stage_layer(int li, hipStream_t st) {
 // else the single slot every layer shares.
 char* DitEngine::stage_slot(int li) {
     return static_cast<char*>(wring_.p) + (stage_per_call_ ? (size_t)li * stage_slot_bytes_ : 0);
+}
+
+// Device table of every layer's cross-attention k-norm weights (PrepArgs::k_norm_layers), built once.
+const float* const* DitEngine::cross_norm_table() {
+    const size_t n = model_.layers.size();
+    if (!knorm_tab_.p || knorm_tab_n_ != n) {
+        std::vector<const float*> h(n);
+        for (size_t i = 0; i < n; ++i) h[i] = model_.layers[i].ck_norm;
+        ensure(knorm_tab_, n * sizeof(const float*));
+        ACEMI_HIP(hipMemcpy(knorm_tab_.p, h.data(), n * sizeof(const float*), hipMemcpyHostToDevice));
+        knorm_tab_n_ = n;
+    }
+    return static_cast<const float* const*>(knorm_tab_.p);
 }
 
 void DitEngine::ensure(Buf& b, size_t bytes) {
@@ -347,9 +360,17 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
             pa.vt = get<uint16_t>(vc_) + (size_t)li * B * c.hkv * D * Lpad;
             pa.k_plane = split ? kc_plane : 0;
             pa.v_plane = attn_pv_split_ ? kc_plane : 0;
+            if (fused) {  // every layer's cross K/V re-layout in one launch (PrepArgs::layers)
+                pa.layers = n_layers;
+                pa.src_layer = 2 * kd;
+                pa.kh_layer = (int64_t)B * c.hkv * Lpad * D;
+                pa.vt_layer = (int64_t)B * c.hkv * D * Lpad;
+                pa.k_norm_layers = cross_norm_table();
+            }
             tic(s);
             launch_attn_prep(pa, s);
             toc("attn_prep", s);
+            if (fused) break;
         }
     }
 

@@ -102,6 +102,9 @@ class DitEngine {
     } cross_key_;
     Buf freq_, freq_act_, th_, th_act_, temb_t_, temb_r_, temb_act_, proj_, mods_, outmod_, cos_, sin_;
     int rope_np_ = -1;
+    Buf knorm_tab_;  // [layers] device pointers to the cross k-norm weights
+    size_t knorm_tab_n_ = 0;
+    const float* const* cross_norm_table();
     Buf ein_;             // condition-encoder input activations
     BlockRunner cond_;    // condition-encoder blocks (own workspace: the DiT buffers stay untouched)
     void rope_table(int n, Buf& cs, Buf& sn, hipStream_t s);

@@ -367,6 +367,18 @@ void launch_embed_rows(const void* table, int fmt, const int32_t* ids, int n, in
 }
 
 void launch_attn_prep(const PrepArgs& a, hipStream_t) {
+    if (a.layers > 1) {  // PrepArgs::layers: the layers one after another
+        for (int l = 0; l < a.layers; ++l) {
+            PrepArgs p = a;
+            p.layers = 1;
+            p.src += l * a.src_layer;
+            p.kh += l * a.kh_layer;
+            p.vt += l * a.vt_layer;
+            p.k_norm = a.k_norm_layers[l];
+            launch_attn_prep(p, nullptr);
+        }
+        return;
+    }
     auto head = [&](bool isq, int b, int h) {
         const float* w = isq ? a.q_norm : a.k_norm;
         const int col = (isq ? a.q_col : a.k_col) + h * 128;

@@ -36,7 +36,7 @@ def main(root, bench_json=None):
         wb = 1024.0 * sum(w) / len(w) if w else None
         out["kernels"][k] = {"fetch_bytes": fb, "write_bytes": wb, "launches": max(len(f), len(w)),
                              "hbm_bytes": (fb or 0.0) + (wb or 0.0)}
-    pat = re.compile(r"gemm_kernel<\d+, \d+, \d+, \d+, (?:true|false), 4, \d+>|gemm_q_kernel<\d+, \d+, \d+, \d+, 4, \d+>")
+    pat = re.compile(r"gemm_kernel<\d+, \d+, \d+, \d+, (?:true|false), 4, \d+[,>]|gemm_q_kernel<\d+, \d+, \d+, \d+, 4, \d+[,>]")
     gu = [k for k in out["kernels"] if pat.search(k)]
     if gu:
         out["gate_up"] = {"kernel": gu[0], **out["kernels"][gu[0]]}
