@@ -173,6 +173,10 @@ void launch_timestep_freq(const float* t, const float* r, int B, int dim, float 
 // y[m][n] = accumulate ? y[m][n] + v : v.  M <= 8, K % 512 == 0.
 void launch_gemv(ActType t, const uint16_t* x_act, int M, const uint16_t* W, int N, int K, const float* bias,
                  bool silu_out, bool accumulate, float* y, hipStream_t s);
+// Same with f32 x rounded to the act type in the kernel (after silu when silu_in): launch_to_act + launch_gemv
+// in one launch, same bits.
+void launch_gemv_f32(ActType t, const float* x, bool silu_in, int M, const uint16_t* W, int N, int K,
+                     const float* bias, bool silu_out, bool accumulate, float* y, hipStream_t s);
 // mod[l][b][j][c] = table[l][j][c] + proj[b][j*H + c]  (j < 6)
 void launch_layer_mods(const float* tables, const float* proj, int n_layers, int B, int H, float* mod,
                        hipStream_t s);

@@ -634,7 +634,11 @@ __global__ void __launch_bounds__(WM * WN * 64, SK && (BM + BN) * 512 <= 160 * 1
         // VGPRs every iteration (48 v_accvgpr copies per 32 MFMAs in the 128x128 ISA).  The split-K
         // instances (held to 256 VGPRs) issue all of them before it: with the half split, hipcc rotated
         // that half through AGPRs there.
-        constexpr int I_EARLY = SK ? TM : EPI == EPI_SWIGLU ? TM / 2 : 0;
+        // The 2x4-wave tiles (256x256, 192x256: batched sequences only) keep the round-1 rule (half before
+        // the barrier for every non-store epilogue), the state they were measured in.
+        constexpr int I_EARLY = SK ? TM
+                                   : (EPI == EPI_SWIGLU ||
+                                      (WN == 4 && EPI != EPI_STORE_F32 && EPI != EPI_STORE_ACT)) ? TM / 2 : 0;
         for (int kt = 0; kt < nk; ++kt) {
             const int cur = kt & 1;
             uint4 a[TM][2], b[TN][2];
@@ -671,7 +675,9 @@ __global__ void __launch_bounds__(WM * WN * 64, SK && (BM + BN) * 512 <= 160 * 1
     if constexpr (EPI == EPI_QKV_PREP)
         qkv_prep_tile<BM, NW, TM, TN, 2 * STAGE>(p, acc, m0, n0, wm0, wn0, tid, smem);
     else
-        gemm_epilogue<TM, TN, F16, EPI, SK ? 32 : 1024>(p, acc, m0 + wm0, n0 + wn0, lane);
+        // residual preload chunk: whole tile for the 4-wave tiles; the 8-wave (2x4) tiles keep the round-1
+        // one-row-group chunks (a whole-tile preload spilled 796 B per lane in the 256x256 gated residual)
+        gemm_epilogue<TM, TN, F16, EPI, (SK ? 32 : (NW > 4 ? NW : 1024))>(p, acc, m0 + wm0, n0 + wn0, lane);
 }
 
 

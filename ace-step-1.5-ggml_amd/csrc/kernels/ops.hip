@@ -389,10 +389,14 @@ __global__ void timestep_freq_kernel(const float* __restrict__ t, const float* _
 }
 
 // small-M GEMV: one wave computes 4 output columns for all M rows.
-template <bool F16>
-__global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ x, int M, const uint16_t* __restrict__ W,
+// XF32: x arrives as f32 and is rounded to the act type in the kernel, after silu when silu_in — the values
+// to_act_kernel would have written, so the pair (to_act, gemv) is one launch with the same bits.
+template <bool F16, bool XF32 = false>
+__global__ void __launch_bounds__(256) gemv_kernel(const void* __restrict__ xv_, int M, const uint16_t* __restrict__ W,
                                                    int N, int K, const float* __restrict__ bias, bool silu_out,
-                                                   bool accumulate, float* __restrict__ y) {
+                                                   bool accumulate, float* __restrict__ y, bool silu_in = false) {
+    const uint16_t* x = static_cast<const uint16_t*>(xv_);
+    const float* xf32 = static_cast<const float*>(xv_);
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     const int n0 = (blockIdx.x * 4 + wid) * 4;
@@ -414,8 +418,19 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
 #pragma unroll
         for (int m = 0; m < 8; ++m) {
             if (m < M) {
-                const uint4 xv = *(const uint4*)(x + (int64_t)m * K + k);
-                const uint16_t* xs = (const uint16_t*)&xv;
+                uint16_t xs[8];
+                if constexpr (XF32) {
+                    const float4 a0 = *(const float4*)(xf32 + (int64_t)m * K + k);
+                    const float4 a1 = *(const float4*)(xf32 + (int64_t)m * K + k + 4);
+                    const float xr[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) xs[j] = to_act(F16, silu_in ? silu_f(xr[j]) : xr[j]);
+                } else {
+                    const uint4 xv = *(const uint4*)(x + (int64_t)m * K + k);
+                    const uint16_t* xp = (const uint16_t*)&xv;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) xs[j] = xp[j];
+                }
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const float xf = act_to_f32(F16, xs[j]);
@@ -608,6 +623,20 @@ void launch_key_bias(const int32_t* mask, int B, int frames, int patch, int nk, 
 void launch_timestep_freq(const float* t, const float* r, int B, int dim, float scale, float log_max, float* f,
                           hipStream_t s) {
     hipLaunchKernelGGL(timestep_freq_kernel, dim3(B), dim3(128), 0, s, t, r, B, dim, scale, log_max, f);
+    ACEMI_HIP(hipGetLastError());
+}
+
+void launch_gemv_f32(ActType t, const float* x, bool silu_in, int M, const uint16_t* W, int N, int K,
+                     const float* bias, bool silu_out, bool accumulate, float* y, hipStream_t s) {
+    ACEMI_CHECK(M >= 1 && M <= 8, "gemv: M must be 1..8");
+    ACEMI_CHECK(N % 16 == 0 && K % 8 == 0, "gemv: N % 16, K % 8");
+    const dim3 grid(N / 16);
+    if (t == ActType::F16)
+        hipLaunchKernelGGL((gemv_kernel<true, true>), grid, dim3(256), 0, s, x, M, W, N, K, bias, silu_out, accumulate,
+                           y, silu_in);
+    else
+        hipLaunchKernelGGL((gemv_kernel<false, true>), grid, dim3(256), 0, s, x, M, W, N, K, bias, silu_out,
+                           accumulate, y, silu_in);
     ACEMI_HIP(hipGetLastError());
 }
 

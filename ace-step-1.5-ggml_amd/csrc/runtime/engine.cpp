@@ -275,22 +275,17 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
     {
         const float log_max = std::log(10000.0f);
         float* freq = get<float>(freq_);
-        uint16_t* freq_act = get<uint16_t>(freq_act_);
         float* th = get<float>(th_);
-        uint16_t* th_act = get<uint16_t>(th_act_);
-        uint16_t* temb_act = get<uint16_t>(temb_act_);
         float* proj = get<float>(proj_);
         tic(s);
         for (int e = 0; e < 2; ++e) {
             float* temb = get<float>(e == 0 ? temb_t_ : temb_r_);
             launch_timestep_freq(io.t, e == 0 ? nullptr : io.r, B, 256, 1000.0f, log_max, freq, s);
             const ActType ta = m.te[e].act;
-            launch_to_act(ta, freq, (int64_t)B * 256, false, freq_act, s);
-            launch_gemv(ta, freq_act, B, m.te[e].w1, H, 256, m.te[e].b1, true, false, th, s);
-            launch_to_act(ta, th, (int64_t)B * H, false, th_act, s);
-            launch_gemv(ta, th_act, B, m.te[e].w2, H, H, m.te[e].b2, false, false, temb, s);
-            launch_to_act(ta, temb, (int64_t)B * H, true, temb_act, s);
-            launch_gemv(ta, temb_act, B, m.te[e].wp, 6 * H, H, m.te[e].bp, false, e == 1, proj, s);
+            // each linear rounds its f32 input to the weight type itself (launch_gemv_f32 = to_act + gemv)
+            launch_gemv_f32(ta, freq, false, B, m.te[e].w1, H, 256, m.te[e].b1, true, false, th, s);
+            launch_gemv_f32(ta, th, false, B, m.te[e].w2, H, H, m.te[e].b2, false, false, temb, s);
+            launch_gemv_f32(ta, temb, true, B, m.te[e].wp, 6 * H, H, m.te[e].bp, false, e == 1, proj, s);
         }
         launch_layer_mods(m.tables, proj, n_layers, B, H, get<float>(mods_), s);
         launch_out_mods(m.out_table, get<float>(temb_t_), get<float>(temb_r_), B, H, get<float>(outmod_), s);

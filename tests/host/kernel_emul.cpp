@@ -474,6 +474,13 @@ void launch_gemv(ActType t, const uint16_t* x, int M, const uint16_t* W, int N, 
         }
 }
 
+void launch_gemv_f32(ActType t, const float* x, bool silu_in, int M, const uint16_t* W, int N, int K, const float* bias,
+                     bool sl, bool accumulate, float* y, hipStream_t) {
+    std::vector<uint16_t> xa((size_t)M * K);
+    launch_to_act(t, x, (int64_t)M * K, silu_in, xa.data(), nullptr);
+    launch_gemv(t, xa.data(), M, W, N, K, bias, sl, accumulate, y, nullptr);
+}
+
 void launch_layer_mods(const float* tables, const float* proj, int L, int B, int H, float* mod, hipStream_t) {
     for (int l = 0; l < L; ++l)
         for (int b = 0; b < B; ++b)
