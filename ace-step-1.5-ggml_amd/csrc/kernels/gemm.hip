@@ -135,7 +135,10 @@ __device__ __forceinline__ void block_tile(const GemmParams& p, int& m0, int& n0
         const int q = nwg >> 3, r = nwg & 7;
         bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
     }
-    constexpr int GM = 8;
+#ifndef ACEMI_GEMM_GM
+#define ACEMI_GEMM_GM 8
+#endif
+    constexpr int GM = ACEMI_GEMM_GM;  // M blocks per group of the tile order
     const int group = bid / (GM * nbn);
     const int first_m = group * GM;
     const int gm = min(nbm - first_m, GM);
