@@ -31,7 +31,7 @@ EXPORTED_SYMBOLS = (
     "ace_ggml_create", "ace_ggml_destroy", "ace_ggml_last_error", "ace_ggml_load_dit", "ace_ggml_dit_forward",
     "ace_mi_create_on_device", "ace_mi_dit_get_info", "ace_mi_dit_forward_batched", "ace_mi_dit_sample",
     "ace_mi_dit_sample_ex",
-    "ace_mi_profile_enable", "ace_mi_profile_reset", "ace_mi_profile_get", "ace_mi_probe_gemm",
+    "ace_mi_profile_enable", "ace_mi_dit_set_attn_precision", "ace_mi_profile_reset", "ace_mi_profile_get", "ace_mi_probe_gemm",
     "ace_mi_synchronize", "ace_mi_kernel_gemm", "ace_mi_kernel_attention", "ace_mi_bench_attention", "ace_mi_bench_gemm",
     "ace_mi_gemm_variant", "ace_ggml_load_vae", "ace_ggml_vae_get_info", "ace_ggml_vae_decode",
     "ace_mi_vae_out_len", "ace_mi_vae_decode_device", "ace_ggml_vae_encode", "ace_mi_vae_enc_out_len",
@@ -112,6 +112,8 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.ace_mi_dit_sample_ex.argtypes = [vp, i32, vp, vp, vp, vp, vp, i32, i32, fp, i32, i32, vp, i32, vp, vp, i32, vp]
     lib.ace_mi_dit_sample_ex.restype = ctypes.c_int
     lib.ace_mi_profile_enable.argtypes = [vp, i32]
+    lib.ace_mi_dit_set_attn_precision.argtypes = [vp, i32]
+    lib.ace_mi_dit_set_attn_precision.restype = ctypes.c_int
     lib.ace_mi_profile_enable.restype = ctypes.c_int
     lib.ace_mi_profile_reset.argtypes = [vp]
     lib.ace_mi_profile_reset.restype = ctypes.c_int
@@ -492,6 +494,11 @@ class GGMLCAPIBridge:
 
     def synchronize(self) -> None:
         self._ensure_ok(self.lib.ace_mi_synchronize(self.ctx), "ace_mi_synchronize")
+
+    def set_attn_precision(self, mode: str) -> None:
+        """DiT attention operand precision for subsequent forwards: "fp16", "split" or "f32"."""
+        code = {"fp16": 0, "split": 1, "f32": 2}[mode]
+        self._ensure_ok(self.lib.ace_mi_dit_set_attn_precision(self.ctx, code), "ace_mi_dit_set_attn_precision")
 
     def profile_enable(self, on: bool) -> None:
         self._ensure_ok(self.lib.ace_mi_profile_enable(self.ctx, 1 if on else 0), "ace_mi_profile_enable")

@@ -134,28 +134,26 @@ def _tile_plan(T: int, chunk_size: int, overlap: int):
     return plan
 
 
+HIP_STREAM_LEGACY = 1  # hipStreamLegacy: the legacy default stream, which torch's default stream is
+
+
 class _OrderedCall:
-    """Order one library call on device tensors against torch's current stream.  A non-default torch
-    stream is handed to the library, so both sides run in stream order.  torch's legacy default stream
-    has handle 0, which the C-ABI reads as "the context's own stream" (a non-blocking stream,
-    include/acestep_mi355x.h): then torch's pending work is drained before the call and the library's
-    stream after it, so neither side reads a buffer the other is still writing."""
+    """Order one library call on device tensors against torch's current stream: the library runs on that
+    stream, so both sides are in stream order with no host synchronisation.  torch's default stream has
+    handle 0, which the C-ABI reads as "the context's own stream" (include/acestep_mi355x.h), so it is handed
+    over as hipStreamLegacy, the same legacy default stream under its explicit handle."""
 
     def __init__(self, bridge, dev):
         import torch
         self.bridge = bridge
         # host tensors (the host-emulated library of the CPU tests) are ordered by program order
-        self.torch_stream = torch.cuda.current_stream(dev) if torch.device(dev).type == "cuda" else None
-        self.stream = self.torch_stream.cuda_stream if self.torch_stream is not None else 0
+        ts = torch.cuda.current_stream(dev) if torch.device(dev).type == "cuda" else None
+        self.stream = (ts.cuda_stream or HIP_STREAM_LEGACY) if ts is not None else 0
 
     def __enter__(self):
-        if self.torch_stream is not None and self.stream == 0:
-            self.torch_stream.synchronize()
         return self.stream
 
     def __exit__(self, *exc):
-        if self.torch_stream is not None and self.stream == 0:
-            self.bridge.synchronize()
         return False
 
 

@@ -163,11 +163,16 @@ def text_tensor_specs(cfg: dict) -> Iterator[Tuple[str, Tuple[int, ...], str]]:
 
 
 def write_checkpoint(out_dir: str, cfg: dict, seed: int = 0, dtype: str = "BF16", std: float = 0.02,
-                     backend: str = "numpy", specs=None) -> str:
+                     backend: str = "numpy", specs=None, qk_norm_scale: float = 1.0,
+                     qk_norm_tags=("self_attn", "cross_attn")) -> str:
     """Write config.json + model.safetensors into out_dir; returns out_dir.
     backend "numpy" (default, used by the golden fixtures) or "torch" (multi-threaded, ~10x
     faster for the 1.5 B-parameter benchmark checkpoint; different random values).
-    specs: tensor list (default: the DiT's, tensor_specs(cfg); text_tensor_specs for Qwen3)."""
+    specs: tensor list (default: the DiT's, tensor_specs(cfg); text_tensor_specs for Qwen3).
+    qk_norm_scale: multiplies the DiT's q_norm / k_norm weights (self and cross attention), so the
+    post-norm logits q.k/sqrt(D) have a standard deviation of ~scale^2 instead of ~1: the peaked-softmax
+    regime of trained checkpoints (|logit| of tens) for the attention-precision tests; qk_norm_tags picks the
+    attention blocks it applies to."""
     os.makedirs(out_dir, exist_ok=True)
     with open(os.path.join(out_dir, "config.json"), "w", encoding="utf-8") as f:
         json.dump(cfg, f, indent=1)
@@ -196,28 +201,41 @@ def write_checkpoint(out_dir: str, cfg: dict, seed: int = 0, dtype: str = "BF16"
                 t = torch.randn(shape, generator=gen, dtype=torch.float32) * std
                 if kind == "norm":
                     t = t + 1.0
+                    if _is_qk_norm(name, qk_norm_tags):
+                        t = t * qk_norm_scale
                 tt = {"BF16": torch.bfloat16, "F16": torch.float16, "F32": torch.float32}[dtype]
                 f.write(t.to(tt).view(torch.int16 if dtype != "F32" else torch.int32).numpy().tobytes())
                 continue
             v = rng.standard_normal(size=shape, dtype=np.float32) * np.float32(std)
             if kind == "norm":
                 v = v + np.float32(1.0)
+                if _is_qk_norm(name, qk_norm_tags):
+                    v = v * np.float32(qk_norm_scale)
             f.write(_encode(v, dtype))
     os.replace(tmp, os.path.join(out_dir, "model.safetensors"))
     return out_dir
 
 
+def _is_qk_norm(name: str, tags=("self_attn", "cross_attn")) -> bool:
+    return (name.startswith("decoder.layers.") and name.endswith(("q_norm.weight", "k_norm.weight")) and
+            any(f".{t}." in name for t in tags))
+
+
 def cached_checkpoint(cfg: dict, seed: int = 0, dtype: str = "BF16", root: str | None = None,
-                      backend: str = "numpy", kind: str = "dit") -> str:
-    """Write the checkpoint once per (cfg, seed, dtype, backend, kind) under a cache dir and reuse it.
-    kind "dit" (tensor_specs) or "text" (the Qwen3 text encoder, text_tensor_specs)."""
-    key_parts = [cfg, seed, dtype, backend] + ([kind] if kind != "dit" else [])
+                      backend: str = "numpy", kind: str = "dit", qk_norm_scale: float = 1.0,
+                      qk_norm_tags=("self_attn", "cross_attn")) -> str:
+    """Write the checkpoint once per (cfg, seed, dtype, backend, kind, qk_norm_scale) under a cache dir and
+    reuse it.  kind "dit" (tensor_specs) or "text" (the Qwen3 text encoder, text_tensor_specs)."""
+    key_parts = [cfg, seed, dtype, backend] + ([kind] if kind != "dit" else []) + \
+        ([float(qk_norm_scale)] if qk_norm_scale != 1.0 else []) + \
+        ([list(qk_norm_tags)] if tuple(qk_norm_tags) != ("self_attn", "cross_attn") else [])
     key = hashlib.sha1(json.dumps(key_parts, sort_keys=True).encode()).hexdigest()[:16]
     root = root or os.environ.get("ACE_MI_SYNTH_DIR") or os.path.join(tempfile.gettempdir(), "acestep_mi355x_synth")
     d = os.path.join(root, key)
     if not os.path.exists(os.path.join(d, "model.safetensors")):
         specs = text_tensor_specs(cfg) if kind == "text" else None
-        write_checkpoint(d, cfg, seed=seed, dtype=dtype, backend=backend, specs=specs)
+        write_checkpoint(d, cfg, seed=seed, dtype=dtype, backend=backend, specs=specs, qk_norm_scale=qk_norm_scale,
+                         qk_norm_tags=qk_norm_tags)
     return d
 
 

@@ -88,6 +88,9 @@ void launch_gemm(ActType t, const uint16_t* A, int lda, const uint16_t* W, int l
 // -1 = automatic tile choice; 0..11 force a kernel variant, + 100 * S (S = 2..4) split-K over S blocks per
 // tile for the 4-wave tiles (micro-benchmarks / tests)
 void gemm_force_variant(int v);
+// Throws if any split-K GEMM join on the current device timed out since the workspace was created (synchronizes
+// the streams that ran split-K GEMMs; called at the library's synchronisation points).
+void gemm_splitk_check();
 // bf16 image [N][K] (ld K) of a quantized weight: bit-identical to what the dequant-fused GEMM feeds its MFMAs
 void launch_dequant_bf16(const WeightView& W, int N, int K, uint16_t* out, hipStream_t s);
 // the same for 1..8 matrices of one format in one launch
@@ -183,6 +186,9 @@ void launch_layer_mods(const float* tables, const float* proj, int n_layers, int
 // outmod[b][j][c] = out_table[j][c] + (temb_t[b][c] + temb_r[b][c]) (j < 2)
 void launch_out_mods(const float* out_table, const float* temb_t, const float* temb_r, int B, int H,
                      float* outmod, hipStream_t s);
+// TEST ONLY (fault injection for the parity negative control): x[r][c] += amp for r in [row0, row0 + 16),
+// c in [col0, col0 + 128)
+void launch_fault_tile(float* x, int ld, int rows, int row0, int col0, float amp, hipStream_t s);
 // xt -= v * dt
 void launch_euler(float* xt, const float* v, int64_t n, float dt, hipStream_t s);
 // SDE re-noise step: xt = t_next * noise + (1 - t_next) * (xt - v * t)

@@ -16,471 +16,14 @@
 // ds_read, which makes every ds_read_b128 lane group conflict-free.
 // Blocks are remapped XCD-aware (blocks b, b+8 share an XCD) and grouped
 // along M so co-resident tiles share weight panels in L2.
-#include <algorithm>
-#include <cmath>
-#include <cstdlib>
 #include <mutex>
-#include <unordered_map>
+#include <map>
+#include <utility>
 
-#include "../kernels.h"
-#include "prep_math.h"
+#include "gemm_common.h"
 
 namespace acemi {
-namespace {
-
-typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
-typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
-typedef __attribute__((ext_vector_type(4))) float f32x4;
-
-typedef __attribute__((address_space(3))) void lds_void;
-
-struct GemmParams {
-    const uint16_t* A;
-    const uint16_t* W;   // dense weight
-    const void* Wq;      // quantized weight planes (runtime/quant.h)
-    const float* Ws;
-    int lda, ldw, M, N, K;
-    GemmEpilogue e;
-    // split-K (gemm_kernel only): ksplit blocks per output tile, each over a contiguous 1/ksplit of the
-    // K-tiles; the last adds the others' partial tiles (sk_ws, slot = K part) in K order and runs the
-    // epilogue.  sk_cnt / sk_ready: per-tile ticket / ready counters, zero between launches (splitk_join).
-    int ksplit;
-    f32x4* sk_ws;
-    unsigned* sk_cnt;
-    unsigned* sk_ready;
-};
-
-__device__ __forceinline__ uint16_t f32_to_bf16_rne(float f) {
-    uint32_t u = __float_as_uint(f);
-    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 64u);
-    u += 0x7fffu + ((u >> 16) & 1u);
-    return (uint16_t)(u >> 16);
-}
-
-template <bool F16>
-__device__ __forceinline__ uint16_t to_act(float f) {
-    if constexpr (F16) {
-        _Float16 h = (_Float16)f;
-        return __builtin_bit_cast(uint16_t, h);
-    } else {
-        return f32_to_bf16_rne(f);
-    }
-}
-
-__device__ __forceinline__ float silu_f(float x) { return x / (1.0f + expf(-x)); }
-
-template <bool F16>
-__device__ __forceinline__ f32x4 mfma16(const uint4& a, const uint4& b, f32x4 c) {
-    if constexpr (F16) {
-        return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c,
-                                                      0, 0, 0);
-    } else {
-        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
-                                                       __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
-    }
-}
-
-// chunk swizzle of a 128-byte LDS row
-__device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
-
-typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
-
-// ds_read_b128 hidden from the compiler's waitcnt pass (it would otherwise drain every in-flight
-// LDS-DMA with vmcnt(0) before the read, serialising the prefetch).  The caller waits with
-// lds_wait_all() + sched_barrier before consuming the registers (guide §5.7 item 1, rule 18).
-template <int OFF>
-__device__ __forceinline__ uint4 ds_read_b128_off(uint32_t addr) {
-    u32x4 v;
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
-    return make_uint4(v[0], v[1], v[2], v[3]);
-}
-__device__ __forceinline__ void lds_wait_all() {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-}
-
-template <int I, int N, int STRIDE>
-struct ReadRows {  // dst[i] = 16 bytes at base + i*STRIDE, i = I..N-1 (compile-time offsets)
-    __device__ __forceinline__ static void run(uint32_t base, uint4 (&dst)[N][2], int kk) {
-        if (kk == 0)
-            dst[I][0] = ds_read_b128_off<I * STRIDE>(base);
-        else
-            dst[I][1] = ds_read_b128_off<I * STRIDE>(base);
-        ReadRows<I + 1, N, STRIDE>::run(base, dst, kk);
-    }
-};
-template <int N, int STRIDE>
-struct ReadRows<N, N, STRIDE> {
-    __device__ __forceinline__ static void run(uint32_t, uint4 (&)[N][2], int) {}
-};
-
-// s_waitcnt vmcnt(N) with N a compile-time constant (lgkmcnt/expcnt untouched)
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-    static_assert(N >= 0 && N < 64, "vmcnt range");
-    __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
-}
-
-// block -> tile: XCD-aware bijective remap (blocks b, b+8 share an XCD), then M-grouped order
-template <int BM, int BN>
-__device__ __forceinline__ void block_tile(const GemmParams& p, int& m0, int& n0, int bid = -1, int nwg = 0) {
-    const int nbm = (p.M + BM - 1) / BM;
-    const int nbn = p.N / BN;
-    if (bid < 0) {
-        bid = blockIdx.x;
-        nwg = gridDim.x;
-    }
-    {
-        const int xcd = bid & 7;
-        const int q = nwg >> 3, r = nwg & 7;
-        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-    }
-#ifndef ACEMI_GEMM_GM
-#define ACEMI_GEMM_GM 8
-#endif
-    constexpr int GM = ACEMI_GEMM_GM;  // M blocks per group of the tile order
-    const int group = bid / (GM * nbn);
-    const int first_m = group * GM;
-    const int gm = min(nbm - first_m, GM);
-    const int bm = first_m + (bid % (GM * nbn)) % gm;
-    const int bn = (bid % (GM * nbn)) / gm;
-    m0 = bm * BM;
-    n0 = bn * BN;
-}
-
-// Fused epilogue of one wave's TM x TN grid of 16x16 accumulators at (mw, nw).
-// C/D map of 16x16x32: col = lane & 15, row = (lane >> 4) * 4 + r.
-template <int TM, int TN, bool F16, int EPI, int PRE>
-__device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[TM][TN], int mw, int nw, int lane) {
-    const GemmEpilogue& e = p.e;
-    const int M = p.M;
-    const int ccol = lane & 15;
-    const int crow = (lane >> 4) * 4;
-    if constexpr (EPI == EPI_RESID_GATED || EPI == EPI_RESID) {
-        // Residual read-modify-write: the old x (and gate) values of a chunk of GI 16-row groups are all
-        // loaded before the chunk's first store.  Interleaved, the compiler cannot move a load of x above
-        // an earlier store to x (same pointer), so each element paid a full memory round trip in
-        // sequence.  A whole-tile preload (PRE = 1024 values) fits the 512-register budget of the 4-wave
-        // tiles; the 8-wave tiles (256 registers, accumulators included) preload 64 values per chunk
-        // instead of spilling, the 256-register split-K instances 32.
-        constexpr int PER_I = 4 * TN * (EPI == EPI_RESID_GATED ? 2 : 1);
-        constexpr int GI0 = PRE / PER_I;
-        constexpr int GI = GI0 < 1 ? 1 : (GI0 > TM ? TM : GI0);
-#pragma unroll
-        for (int i0 = 0; i0 < TM; i0 += GI) {
-            float xo[GI][4][TN], gt[GI][4][TN];
-#pragma unroll
-            for (int ii = 0; ii < GI; ++ii)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int m = mw + (i0 + ii) * 16 + crow + r;
-                    const bool ok = i0 + ii < TM && m < M;
-                    const int item = EPI == EPI_RESID_GATED ? m / e.rows_per_item : 0;
-#pragma unroll
-                    for (int j = 0; j < TN; ++j) {
-                        const int n = nw + j * 16 + ccol;
-                        xo[ii][r][j] = ok ? e.c_f32[(int64_t)m * e.ldc + n] : 0.f;
-                        if constexpr (EPI == EPI_RESID_GATED)
-                            gt[ii][r][j] = ok ? e.gate[(int64_t)item * e.gate_stride + n] : 0.f;
-                    }
-                }
-#pragma unroll
-            for (int ii = 0; ii < GI; ++ii) {
-                if (i0 + ii >= TM) break;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int m = mw + (i0 + ii) * 16 + crow + r;
-                    if (m >= M) continue;
-#pragma unroll
-                    for (int j = 0; j < TN; ++j) {
-                        const int n = nw + j * 16 + ccol;
-                        float v = acc[i0 + ii][j][r];
-                        if constexpr (EPI == EPI_RESID_GATED) v = __fmul_rn(v, gt[ii][r][j]);
-                        e.c_f32[(int64_t)m * e.ldc + n] = __fadd_rn(xo[ii][r][j], v);
-                    }
-                }
-            }
-        }
-        return;
-    }
-    float bias_j[TN];  // a thread's columns are fixed: their bias is loaded once, before any store
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-        bias_j[j] = ((EPI == EPI_STORE_F32 || EPI == EPI_STORE_ACT) && e.bias) ? e.bias[nw + j * 16 + ccol] : 0.f;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int m = mw + i * 16 + crow + r;
-            if (m >= M) continue;
-            if constexpr (EPI == EPI_SWIGLU) {
-#pragma unroll
-                for (int j = 0; j < TN; j += 2) {
-                    const int n = nw + j * 16;  // multiple of 32
-                    const float g = acc[i][j][r];
-                    const float u = acc[i][j + 1][r];
-                    e.c_act[(int64_t)m * e.ldc + (n >> 1) + ccol] = to_act<F16>(silu_f(g) * u);
-                }
-            } else {
-#pragma unroll
-                for (int j = 0; j < TN; ++j) {
-                    const int n = nw + j * 16 + ccol;
-                    float v = acc[i][j][r];
-                    if constexpr (EPI == EPI_STORE_F32) {
-                        if (e.bias) v = v + bias_j[j];
-                        e.c_f32[(int64_t)m * e.ldc + n] = v;
-                    } else if constexpr (EPI == EPI_STORE_ACT) {
-                        if (e.bias) v = v + bias_j[j];
-                        e.c_act[(int64_t)m * e.ldc + n] = to_act<F16>(v);
-                    } else if constexpr (EPI == EPI_PROJ_OUT) {
-                        const int item = m / e.rows_per_item;
-                        const int pp = m - item * e.rows_per_item;
-                        const int kpos = n / e.out_ch;
-                        const int c = n - kpos * e.out_ch;
-                        const int t = pp * e.patch + kpos;
-                        if (t < e.out_T) {
-                            e.c_f32[((int64_t)item * e.out_T + t) * e.out_ch + c] = __fadd_rn(v, e.bias[c]);
-                        }
-                    }
-                }
-            }
-        }
-    }
-}
-
-// EPI_QKV_PREP: the block's BM x 128 f32 accumulator tile (one head of the [q | k | v] projection) goes
-// through LDS in row chunks (rows 144 floats apart: the 16x4 accumulator writes are conflict-free) and is
-// written straight into the attention operand layouts with attn_prep's arithmetic (prep_math.h): 16
-// lanes per token for q / k (QK-RMSNorm, RoPE, fp16 hi/lo), one lane per (d, 16-key group) for V^T.
-// This removes the f32 [M][4096] round trip through HBM and the separate prep launch.
-constexpr int PREP_LD = 144;  // LDS row stride (floats) of the accumulator tile in the fused prep
-
-// `fill(tile, c0, CH)` writes the block's accumulators of tile rows [c0, c0 + CH) of head `hd` (128 columns)
-// into the LDS tile (row stride PREP_LD)
-template <int BM, int NW, int SMEM, class Fill>
-__device__ __forceinline__ void qkv_prep_head(const GemmParams& p, int m0, int hd, int tid, char* smem, Fill fill) {
-    constexpr int LD = PREP_LD;
-    constexpr int CH = (BM * LD * 4 <= SMEM) ? BM : ((BM / 2) * LD * 4 <= SMEM ? BM / 2 : BM / 4);
-    static_assert(CH * LD * 4 <= SMEM && BM % CH == 0 && CH % 16 == 0, "qkv prep chunking");
-    constexpr int NT = NW * 64;
-    const PrepArgs& a = p.e.prep;
-    float* tile = reinterpret_cast<float*>(smem);
-    const int nq = a.q_col >= 0 ? a.hq : 0;
-    const int nk = a.k_col >= 0 ? a.hkv : 0;
-    for (int c0 = 0; c0 < BM; c0 += CH) {
-        const int mc0 = m0 + c0;
-        if (mc0 >= p.M) break;
-        __syncthreads();  // the main loop's (or the previous chunk's) LDS readers are done
-        fill(tile, c0, CH);
-        __syncthreads();
-        const int rows = min(CH, p.M - mc0);
-        if (hd < nq + nk) {
-            const bool isq = hd < nq;
-            const int head = isq ? hd : hd - nq;
-            const float* w = isq ? a.q_norm : a.k_norm;
-            uint16_t* base = isq ? a.qh + (int64_t)head * a.n_pad * 128 : a.kh + (int64_t)head * a.n_pad * 128;
-            const int64_t bstride = (int64_t)(isq ? a.hq : a.hkv) * a.n_pad * 128;
-            const int64_t plane = isq ? a.q_plane : a.k_plane;
-            const int d = (tid & 15) * 4;
-            for (int t = tid >> 4; t < rows; t += NT / 16) {
-                const int m = mc0 + t;
-                const int b = m / a.n_tok, n = m - b * a.n_tok;
-                const float4 x0 = *(const float4*)(tile + t * LD + d), x1 = *(const float4*)(tile + t * LD + 64 + d);
-                float y[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-                prep::head_row(y, w, d, a.eps, a.rope_cos ? a.rope_cos + (int64_t)n * 64 + d : nullptr,
-                               a.rope_cos ? a.rope_sin + (int64_t)n * 64 + d : nullptr,
-                               base + b * bstride + (int64_t)n * 128, plane);
-            }
-        } else {
-            // V^T: groups of 16 keys of one item; a group cut by the chunk edge is written key by key
-            // (its other keys belong to the neighbouring chunk or tile), padding keys as zeros, and the
-            // tile holding an item's last token also zero-fills the item's groups up to n_pad
-            const int hk = hd - nq - nk;
-            const int d = tid & 127;
-            const int b_lo = mc0 / a.n_tok, b_hi = (mc0 + rows - 1) / a.n_tok;
-            for (int b = b_lo; b <= b_hi; ++b) {
-                const int n_lo = max(0, mc0 - b * a.n_tok), n_hi = min(a.n_tok, mc0 + rows - b * a.n_tok);
-                uint16_t* vdst = a.vt + (((int64_t)b * a.hkv + hk) * 128 + d) * a.n_pad;
-                const int g_end = n_hi == a.n_tok ? a.n_pad / 16 : ((n_hi - 1) >> 4) + 1;
-                for (int g = (n_lo >> 4) + (tid >> 7); g < g_end; g += NT / 128) {
-                    const int g0 = g * 16;
-                    float v[16];
-                    uint32_t have = 0;
-#pragma unroll
-                    for (int k = 0; k < 16; ++k) {
-                        const int n = g0 + prep::vperm(k);
-                        const bool mine = n >= n_lo && n < n_hi;
-                        v[k] = mine ? tile[(b * a.n_tok + n - mc0) * LD + d] : 0.f;
-                        have |= (mine || n >= a.n_tok) ? (1u << k) : 0u;
-                    }
-                    uint32_t wv[8], wl[8];
-                    prep::v_words(v, wv, wl);
-                    if (have == 0xffffu) {
-                        *(uint4*)(vdst + g0) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
-                        *(uint4*)(vdst + g0 + 8) = make_uint4(wv[4], wv[5], wv[6], wv[7]);
-                        if (a.v_plane > 0) {
-                            *(uint4*)(vdst + a.v_plane + g0) = make_uint4(wl[0], wl[1], wl[2], wl[3]);
-                            *(uint4*)(vdst + a.v_plane + g0 + 8) = make_uint4(wl[4], wl[5], wl[6], wl[7]);
-                        }
-                    } else {
-#pragma unroll
-                        for (int k = 0; k < 16; ++k) {
-                            if (!((have >> k) & 1u)) continue;
-                            vdst[g0 + k] = (uint16_t)(wv[k >> 1] >> (16 * (k & 1)));
-                            if (a.v_plane > 0) vdst[a.v_plane + g0 + k] = (uint16_t)(wl[k >> 1] >> (16 * (k & 1)));
-                        }
-                    }
-                }
-            }
-        }
-    }
-}
-
-// the 4-wave kernels' fused prep: the block's BM x 128 tile is one head, wave tile TM x TN at (wm0, wn0)
-template <int BM, int NW, int TM, int TN, int SMEM>
-__device__ __forceinline__ void qkv_prep_tile(const GemmParams& p, f32x4 (&acc)[TM][TN], int m0, int n0, int wm0,
-                                              int wn0, int tid, char* smem) {
-    const int lane = tid & 63;
-    const int ccol = lane & 15, crow = (lane >> 4) * 4;
-    qkv_prep_head<BM, NW, SMEM>(p, m0, n0 >> 7, tid, smem, [&](float* tile, int c0, int CH) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-            const int rb = wm0 + i * 16 - c0;
-            if (rb < 0 || rb >= CH) continue;
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-#pragma unroll
-                for (int j = 0; j < TN; ++j) tile[(rb + crow + r) * PREP_LD + wn0 + j * 16 + ccol] = acc[i][j][r];
-        }
-    });
-}
-
-constexpr int CPOL_SC1 = 16;  // cache-policy bit of buffer / global ops: device-scope coherent (gfx94x/gfx950)
-
-// largest split-K factor of a tile: the last block gathers the other parts through its LDS share
-template <int BM, int BN>
-struct SplitKMax {
-    static constexpr int value = BM * BN >= 128 * 128 ? 2 : 4;
-};
-
-// Split-K: block -> (tile, K part).  When the tile count is a multiple of 8 the S parts of a tile are
-// blocks 8 apart (same XCD: the partial tiles stay in that XCD's L2); otherwise adjacent blocks.
-__device__ __forceinline__ void splitk_block(int S, int& tile, int& part, int& ntiles) {
-    const int b = blockIdx.x;
-    ntiles = gridDim.x / S;
-    if ((ntiles & 7) == 0) {
-        part = (b >> 3) % S;
-        tile = (b / (8 * S)) * 8 + (b & 7);
-    } else {
-        part = b % S;
-        tile = b / S;
-    }
-}
-
-// The last block of a split-K tile adds the other parts' partial tiles: each wave brings its own fragments
-// of the S-1 other slots into its share of the (now free) LDS by LDS-DMA (no VGPRs held by loads in flight),
-// CH fragments at a time, then acc = ((part_0 + part_1) + ...) in K order, its own sum at index `part`.
-template <int TM, int TN, int NW, int SS, int SMEM>
-__device__ __forceinline__ void splitk_gather(f32x4 (&acc)[TM][TN], const f32x4* slot0, int64_t slot_stride,
-                                              int part, char* smem, int wid, int lane) {
-    constexpr int F = TM * TN;
-    constexpr int LDSW = SMEM / NW;  // bytes of LDS per wave
-    constexpr int CH0 = LDSW / ((SS - 1) * 1024);
-    constexpr int CH = CH0 < F ? CH0 : F;
-    static_assert(CH >= 1, "split-K gather: LDS share too small");
-    char* wl = smem + wid * LDSW;
-#pragma unroll
-    for (int f0 = 0; f0 < F; f0 += CH) {
-        if (f0 > 0) lds_wait_all();  // the previous chunk's LDS reads are done before it is overwritten
-#pragma unroll
-        for (int f = f0; f < f0 + CH && f < F; ++f)
-#pragma unroll
-            for (int qi = 0; qi < SS - 1; ++qi) {
-                const int q = qi < part ? qi : qi + 1;
-                __builtin_amdgcn_global_load_lds((const void*)(slot0 + q * slot_stride + f * 64),
-                                                 (lds_void*)(wl + ((f - f0) * (SS - 1) + qi) * 1024), 16, 0,
-                                                 CPOL_SC1);  // device-coherent load
-            }
-        wait_vmcnt<0>();
-#pragma unroll
-        for (int f = f0; f < f0 + CH && f < F; ++f) {
-            if ((f - f0) % 4 == 0) __builtin_amdgcn_sched_barrier(0);  // LDS reads in groups of 4 fragments
-            const f32x4* l = reinterpret_cast<const f32x4*>(wl + (f - f0) * (SS - 1) * 1024) + lane;
-            const int i = f / TN, j = f % TN;
-            if constexpr (SS == 2) {
-                acc[i][j] += l[0];  // two parts: a + b == b + a, whichever is this block's
-            } else {
-                f32x4 t = part == 0 ? acc[i][j] : l[0];
-#pragma unroll
-                for (int q = 1; q < SS; ++q) t += q == part ? acc[i][j] : l[(q < part ? q : q - 1) * 64];
-                acc[i][j] = t;
-            }
-        }
-    }
-}
-
-// Join of the S blocks of one tile after their main loops.  Each block takes a ticket (atomic add on
-// sk_cnt[tile]) when it starts (taken after the main loop, the returned value live across the loop made
-// hipcc rotate the accumulators through AGPRs, > 256 VGPRs); the S-1 first write their accumulators to slot `part` of the tile's workspace (in the
-// MFMA register layout: coalesced, device-coherent 16-byte stores), wait for their completion, and bump
-// sk_ready[tile], then exit.  The last
-// waits until the S-1 writes are visible and adds the slots into its accumulators in K order
-// (deterministic: the same sum whichever block arrives last), then runs the epilogue.  Deadlock-free for
-// any residency: a waiting block only waits for blocks that already took their ticket, i.e. are resident
-// and finish without waiting on anything.  The last block resets the tile's two counters once the others
-// are in, so every launch starts from zero whatever the split factor of the previous one.  Returns false
-// for the blocks that exit.
-template <int TM, int TN, int NW, int SKMAX, int SMEM>
-__device__ __forceinline__ bool splitk_join(const GemmParams& p, f32x4 (&acc)[TM][TN], int S, int tile, int part,
-                                           int tid, char* smem, unsigned ticket0) {
-    __syncthreads();  // every wave is past its main loop's LDS reads: LDS is free
-    if (tid == 0) *reinterpret_cast<unsigned*>(smem) = ticket0;  // (a separate __shared__ word would cost
-    __syncthreads();                                               //  the 192x128 tile its second block per CU)
-    const unsigned ticket = *reinterpret_cast<const unsigned*>(smem);
-    __syncthreads();
-    const bool last = ticket == (unsigned)(S - 1);
-    const int wid = tid >> 6, lane = tid & 63;
-    constexpr int PER_TILE = NW * TM * TN * 64;  // f32x4 per (tile, part) slot
-    f32x4* slot0 = p.sk_ws + (int64_t)tile * S * PER_TILE + (wid * TM * TN) * 64 + lane;
-    if (!last) {
-        // device-coherent (sc1) stores of the partial tile, completed (vmcnt 0) before the ready count: no
-        // device-scope fence, whose L2 write-back / invalidate (per block, or per spin) cost ~4x the GEMM
-        const __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc((void*)(slot0 - lane + (int64_t)part * PER_TILE), 0, 0x7fffffff, 0x00020000);
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs,
-                                                       ((i * TN + j) * 64 + lane) * 16, 0, CPOL_SC1);
-        __builtin_amdgcn_s_waitcnt(0);
-        __syncthreads();
-        if (tid == 0) __hip_atomic_fetch_add(p.sk_ready + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return false;
-    }
-    if (tid == 0) {
-        // bounded (~0.2 s; a real wait is a few microseconds): a protocol bug gives wrong tiles, never a hung GPU
-        for (int it = 0; it < (1 << 22); ++it) {
-            if (__hip_atomic_load(p.sk_ready + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(S - 1))
-                break;
-            __builtin_amdgcn_s_sleep(2);
-        }
-        // every ticket of this tile is taken and every ready count is in: reset both for the next launch
-        // on this stream (ordered after this kernel)
-        __hip_atomic_store(p.sk_cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(p.sk_ready + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    if (S == 2 || SKMAX == 2) {
-        splitk_gather<TM, TN, NW, 2, SMEM>(acc, slot0, PER_TILE, part, smem, wid, lane);
-    } else if constexpr (SKMAX >= 4) {
-        if (S == 3)
-            splitk_gather<TM, TN, NW, 3, SMEM>(acc, slot0, PER_TILE, part, smem, wid, lane);
-        else
-            splitk_gather<TM, TN, NW, 4, SMEM>(acc, slot0, PER_TILE, part, smem, wid, lane);
-    }
-    return true;
-}
+namespace gemm_detail {
 
 // PIPE 0: stage(t+1) ; compute(t) ; vmcnt(0) ; __syncthreads        (2 LDS buffers)
 // PIPE 1: compute first half of tile t from registers read up front, release the LDS buffer with
@@ -878,329 +421,24 @@ __global__ void __launch_bounds__(512) gemm8_kernel(GemmParams p) {
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Dequant-fused variant: W arrives as a ggml block format re-laid out at load (runtime/quant.h).
-// Each thread owns one 32-value block of the BN x 64 weight tile (BN*2 == threads): it loads the
-// block's bytes + scale(s) into registers one k-tile ahead, turns them into bf16 with the exact
-// ggml dequant arithmetic (q*d, d*sc*q - dmin*m, (d*sc)*q; one f32 rounding, then RNE bf16) and
-// writes the bf16 image into the same swizzled LDS layout the dense kernel reads.  A (bf16
-// activations) is still staged by LDS-DMA.  Pipeline (PIPE 1 shape): fragments of tile t are read
-// up front, a raw barrier frees the buffer, A(t+2) is DMA'd and W(t+2) dequantized into it while
-// the second half of tile t's MFMAs runs, and W(t+3)'s bytes are requested.
-struct WRaw {
-    u32x4 q0, q1;
-    float s0, s1;
-};
-
-__device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) {
-    typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
-    bf16x2_t v;
-    v[0] = (__bf16)lo;
-    v[1] = (__bf16)hi;
-    return __builtin_bit_cast(uint32_t, v);
-}
-
-// A compiler-visible LDS store, not inline asm: the hazard recognizer does not cover an asm
-// ds_write_b128's data VGPRs, and on gfx950 the VALU overwrote them before the DS unit had read the
-// last lanes (lanes 48-63 of the dequantized W rows came out wrong on the GPU).
-__device__ __forceinline__ void ds_write_b128_v(uint32_t addr, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-    typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
-    *(lds_u32x4*)(uintptr_t)addr = u32x4{a, b, c, d};
-}
-
-// Weight bytes are plain (compiler-tracked) loads issued one k-tile ahead; the loop consumes them
-// BEFORE it issues the next A DMA, so the vmcnt the compiler places at that use only drains what
-// must have landed by the end of the iteration anyway (tile kt+1's A, issued earlier).
-template <int WQ>
-__device__ __forceinline__ WRaw load_wq(const char* qbase, const float* sbase, int kt) {
-    WRaw r;
-    if constexpr (WQ == WF_Q4_K) {
-        r.q0 = *(const u32x4*)(qbase + kt * 32);
-        const float2 sm = *(const float2*)(sbase + kt * 4);
-        r.s0 = sm.x;
-        r.s1 = sm.y;
-    } else {
-        r.q0 = *(const u32x4*)(qbase + kt * 64);
-        r.q1 = *(const u32x4*)(qbase + kt * 64 + 16);
-        if constexpr (WQ == WF_Q8_0) {
-            r.s0 = sbase[kt * 2];
-            r.s1 = r.s0;
-        } else {
-            const float2 sc = *(const float2*)(sbase + kt * 4);
-            r.s0 = sc.x;
-            r.s1 = sc.y;
-        }
-    }
-    return r;
-}
-
-// signed bytes of w (k order b0..b3) * s, via the unsigned-byte converts: (u - 128) * s = fma(u, s, -128 s)
-__device__ __forceinline__ void deq_i8x4(uint32_t w, float s, float c, uint32_t& o0, uint32_t& o1) {
-    const uint32_t u = w ^ 0x80808080u;
-    const float f0 = fmaf((float)(u & 0xffu), s, c);
-    const float f1 = fmaf((float)((u >> 8) & 0xffu), s, c);
-    const float f2 = fmaf((float)((u >> 16) & 0xffu), s, c);
-    const float f3 = fmaf((float)(u >> 24), s, c);
-    o0 = pk_bf16(f0, f1);
-    o1 = pk_bf16(f2, f3);
-}
-// unsigned nibble bytes (0..15) of w * d - m
-__device__ __forceinline__ void deq_u4x4(uint32_t w, float d, float nm, uint32_t& o0, uint32_t& o1) {
-    const float f0 = fmaf((float)(w & 0xffu), d, nm);
-    const float f1 = fmaf((float)((w >> 8) & 0xffu), d, nm);
-    const float f2 = fmaf((float)((w >> 16) & 0xffu), d, nm);
-    const float f3 = fmaf((float)(w >> 24), d, nm);
-    o0 = pk_bf16(f0, f1);
-    o1 = pk_bf16(f2, f3);
-}
-
-// dequantize one 32-value block to 16 packed bf16 pairs in k order (ggml's dequant arithmetic, one f32
-// rounding, then RNE to bf16)
-template <int WQ>
-__device__ __forceinline__ void dequant_block(const WRaw& r, uint32_t (&o)[16]) {
-    if constexpr (WQ == WF_Q4_K) {
-        const float d = r.s0, nm = -r.s1;
-        const uint32_t w[4] = {r.q0[0], r.q0[1], r.q0[2], r.q0[3]};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {  // dword i: k = 8i..8i+3 in low nibbles, 8i+4..8i+7 in high nibbles
-            deq_u4x4(w[i] & 0x0f0f0f0fu, d, nm, o[4 * i + 0], o[4 * i + 1]);
-            deq_u4x4((w[i] >> 4) & 0x0f0f0f0fu, d, nm, o[4 * i + 2], o[4 * i + 3]);
-        }
-    } else {
-        const uint32_t w[8] = {r.q0[0], r.q0[1], r.q0[2], r.q0[3], r.q1[0], r.q1[1], r.q1[2], r.q1[3]};
-        const float c0 = -128.0f * r.s0, c1 = -128.0f * r.s1;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const float s = i < 4 ? r.s0 : r.s1;
-            const float c = i < 4 ? c0 : c1;
-            deq_i8x4(w[i], s, c, o[2 * i], o[2 * i + 1]);
-        }
-    }
-}
-
-// dequantize one 32-value block and store it as 4 swizzled 16-byte chunks of an LDS row
-template <int WQ>
-__device__ __forceinline__ void dequant_store(const WRaw& r, uint32_t row_addr, int wh, int sw) {
-    uint32_t o[16];
-    dequant_block<WQ>(r, o);
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-        ds_write_b128_v(row_addr + (((wh * 4 + c) ^ sw) * 16), o[4 * c], o[4 * c + 1], o[4 * c + 2], o[4 * c + 3]);
-}
-
-// Staged dequant: the bf16 image of a quantized [N][K] weight (the exact values the dequant-fused GEMM
-// writes to LDS: the same deq_* arithmetic), one thread per 8 consecutive weights, so a wave reads 512
-// (Q8_0, Q6_K) or 256 (Q4_K) contiguous bytes and writes 1 KiB contiguous.  HBM-bound: 1.0625 (Q8_0),
-// 0.5625 (Q4_K), 1.125 (Q6_K) bytes read + 2 bytes written per weight.
-struct DequantBatch {  // up to 8 same-format matrices expanded by one launch
-    const char* q[8];
-    const float* s[8];
-    uint16_t* out[8];
-    int64_t end[8];  // exclusive prefix sums of the 8-weight chunk counts
-    int n;
-};
-
-template <int WQ>
-__device__ __forceinline__ void dequant_chunk(const DequantBatch& b, int64_t c, uint4& o, uint16_t*& dst) {
-    int mi = 0;
-#pragma unroll
-    for (int i = 0; i < 7; ++i) mi += (i + 1 < b.n && c >= b.end[i]) ? 1 : 0;
-    if (mi > 0) c -= b.end[mi - 1];
-    const char* __restrict__ q = b.q[mi];
-    const float* __restrict__ sc = b.s[mi];
-    const int64_t g = c >> 2;  // 8-weight chunk c: block g = c / 4, part j = c % 4
-    const int j = (int)(c & 3);
-    if constexpr (WQ == WF_Q4_K) {
-        const uint32_t w = *reinterpret_cast<const uint32_t*>(q + g * 16 + j * 4);  // k 8j..8j+3 low, +4..7 high
-        const float2 dm = *reinterpret_cast<const float2*>(sc + 2 * g);
-        deq_u4x4(w & 0x0f0f0f0fu, dm.x, -dm.y, o.x, o.y);
-        deq_u4x4((w >> 4) & 0x0f0f0f0fu, dm.x, -dm.y, o.z, o.w);
-    } else {
-        const uint2 w = *reinterpret_cast<const uint2*>(q + g * 32 + j * 8);
-        const float d = WQ == WF_Q8_0 ? sc[g] : sc[2 * g + (j >> 1)];  // Q6_K: one scale per 16 values
-        deq_i8x4(w.x, d, -128.0f * d, o.x, o.y);
-        deq_i8x4(w.y, d, -128.0f * d, o.z, o.w);
-    }
-    dst = b.out[mi] + c * 8;
-}
-
-// CPT chunks per thread, strided by the grid so each wave instruction stays coalesced; all loads of a
-// thread are issued before its first store
-template <int WQ, int CPT>
-__global__ void __launch_bounds__(256) dequant_bf16_kernel(DequantBatch b) {
-    const int64_t tot = b.end[b.n - 1];
-    const int64_t stride = (int64_t)gridDim.x * 256;
-    const int64_t c0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    uint4 o[CPT];
-    uint16_t* dst[CPT];
-#pragma unroll
-    for (int k = 0; k < CPT; ++k)
-        if (c0 + k * stride < tot) dequant_chunk<WQ>(b, c0 + k * stride, o[k], dst[k]);
-#pragma unroll
-    for (int k = 0; k < CPT; ++k)
-        if (c0 + k * stride < tot) *reinterpret_cast<uint4*>(dst[k]) = o[k];
-}
-
-template <int BM, int BN, int WM, int WN, int EPI, int WQ>
-__global__ void __launch_bounds__(WM * WN * 64) gemm_q_kernel(GemmParams p) {
-    constexpr int NW = WM * WN;
-    constexpr int WTM = BM / WM;
-    constexpr int WTN = BN / WN;
-    constexpr int TM = WTM / 16;
-    constexpr int TN = WTN / 16;
-    constexpr int BK = 64;
-    constexpr int ROWB = BK * 2;
-    constexpr int STAGE = (BM + BN) * ROWB;
-    constexpr int G_A = BM / 8 / NW;
-    static_assert(BM % (8 * NW) == 0, "A staging split");
-    static_assert(BN * 2 == NW * 64, "one 32-value weight block per thread");
-    static_assert(EPI != EPI_SWIGLU || (TN % 2 == 0), "swiglu needs column pairs");
-
-    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wid = tid >> 6;
-    int m0, n0;
-    block_tile<BM, BN>(p, m0, n0);
-    const int wm0 = (wid / WN) * WTM;
-    const int wn0 = (wid % WN) * WTN;
-    const int M = p.M, K = p.K;
-
-    // A staging sources (LDS-DMA, swizzled source chunk)
-    const uint16_t* src[G_A];
-#pragma unroll
-    for (int j = 0; j < G_A; ++j) {
-        const int row = (wid + NW * j) * 8 + (lane >> 3);
-        const int c = (lane & 7) ^ swz(row);
-        src[j] = p.A + (int64_t)min(m0 + row, M - 1) * p.lda + c * 8;
-    }
-    const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
-    auto stage_a = [&](int buf, int kt) {
-        char* base = smem + buf * STAGE;
-#pragma unroll
-        for (int j = 0; j < G_A; ++j)
-            __builtin_amdgcn_global_load_lds((const void*)(src[j] + kt * BK), (lds_void*)(base + (wid + NW * j) * 1024),
-                                             16, 0, 0);
-    };
-
-    // W block owned by this thread: row wr of the tile, K half wh of each 64-wide k-tile
-    const int wr = tid >> 1, wh = tid & 1;
-    const int64_t grow = n0 + wr;
-    const char* qbase;
-    const float* sbase;
-    if constexpr (WQ == WF_Q4_K) {
-        qbase = (const char*)p.Wq + grow * (K / 2) + wh * 16;
-        sbase = p.Ws + (grow * (K / 32) + wh) * 2;
-    } else if constexpr (WQ == WF_Q8_0) {
-        qbase = (const char*)p.Wq + grow * K + wh * 32;
-        sbase = p.Ws + grow * (K / 32) + wh;
-    } else {
-        qbase = (const char*)p.Wq + grow * K + wh * 32;
-        sbase = p.Ws + grow * (K / 16) + wh * 2;
-    }
-    const int wsw = swz(wr);
-    const uint32_t wrow_off = BM * ROWB + wr * ROWB;
-
-    f32x4 acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    const int nk = K / BK;
-    const int lrow = lane & 15;
-    const int lchunk = lane >> 4;
-    auto read_frags_asm = [&](int buf, uint4 (&a)[TM][2], uint4 (&b)[TN][2]) {
-        const uint32_t sb = lds0 + buf * STAGE;
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-            const int ch = (kk * 4 + lchunk) ^ ((lrow >> 1) & 7);
-            const uint32_t bb = sb + BM * ROWB + (wn0 + lrow) * ROWB + ch * 16;
-            const uint32_t ab = sb + (wm0 + lrow) * ROWB + ch * 16;
-            ReadRows<0, TN, 16 * ROWB>::run(bb, b, kk);
-            ReadRows<0, TM, 16 * ROWB>::run(ab, a, kk);
-        }
-        lds_wait_all();
-    };
-
-    // prologue: tiles 0 and 1 complete in LDS, W(min(2, nk-1)) requested
-    WRaw wnext = load_wq<WQ>(qbase, sbase, 0);
-    stage_a(0, 0);
-    dequant_store<WQ>(wnext, lds0 + wrow_off, wh, wsw);
-    if (nk > 1) {
-        wnext = load_wq<WQ>(qbase, sbase, 1);
-        stage_a(1, 1);
-        dequant_store<WQ>(wnext, lds0 + STAGE + wrow_off, wh, wsw);
-    }
-    wnext = load_wq<WQ>(qbase, sbase, min(2, nk - 1));
-    wait_vmcnt<0>();
-    lds_wait_all();
-    __builtin_amdgcn_s_barrier();
-
-    auto mfma_all = [&](const uint4 (&a)[TM][2], const uint4 (&b)[TN][2]) {
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<false>(a[i][kk], b[j][kk], acc[i][j]);
-    };
-
-    // One branch-free body for every tile: past the end, the tile indices clamp to nk-1, so the last
-    // two iterations re-stage the final tile into a buffer nobody reads again (harmless, and it keeps
-    // the accumulators in one loop so they stay put in AGPRs).
-    for (int kt = 0; kt < nk; ++kt) {
-        const int cur = kt & 1;
-        uint4 a[TM][2], b[TN][2];
-        read_frags_asm(cur, a, b);
-        // Every MFMA of the tile issues after this barrier (the dequant VALU work interleaves with them).
-        __builtin_amdgcn_s_barrier();  // every wave holds its fragments of tile kt: buffer `cur` is free
-        asm volatile("" ::: "memory");  // the LDS stores below stay after the barrier
-        // W(kt+2): waiting for its bytes also retires the older A(kt+1) DMA
-        dequant_store<WQ>(wnext, lds0 + cur * STAGE + wrow_off, wh, wsw);
-        // Every wave's ds_writes retire before any wave issues its LDS-DMA: measured on gfx950, an LDS
-        // DMA issued while ds_write_b128s of the workgroup are still in flight corrupts lanes 48-63 of
-        // those writes (random W elements of rows 24-31 of every 32, on some launches).  A per-wave
-        // lgkmcnt(0) cleared the 4-wave tiles but not the 8-wave 256x256 one; lgkmcnt(0) + barrier
-        // cleared all (tools/diag_gemm_q.py stress: 0 bad launches of 20 per variant and format).
-        lds_wait_all();
-        __builtin_amdgcn_s_barrier();
-        stage_a(cur, min(kt + 2, nk - 1));
-        // keep the W(kt+3) loads behind the A(kt+2) DMA in issue order: the vmcnt the compiler
-        // places before the next iteration's dequant (waiting for those bytes) then also retires
-        // A(kt+2) before the barrier that ends that iteration publishes buffer `cur` again
-        asm volatile("" ::: "memory");
-        wnext = load_wq<WQ>(qbase, sbase, min(kt + 3, nk - 1));
-        mfma_all(a, b);
-        // retire this wave's LDS traffic before the barrier that hands buffer `cur` to the other waves
-        // (gfx950 does not wait at s_barrier)
-        lds_wait_all();
-        __builtin_amdgcn_s_barrier();
-    }
-    wait_vmcnt<0>();
-
-    if constexpr (EPI == EPI_QKV_PREP)
-        qkv_prep_tile<BM, NW, TM, TN, 2 * STAGE>(p, acc, m0, n0, wm0, wn0, tid, smem);
-    else
-        gemm_epilogue<TM, TN, false, EPI, NW >= 8 ? 64 : 1024>(p, acc, m0 + wm0, n0 + wn0, lane);
-}
-
-// split-K workspace of one stream: partial tiles + per-tile ticket / ready counters (zeroed once; each
-// launch leaves them zero, see splitk_join).  Launches on one stream are ordered, so one set per
-// stream suffices; it only grows (a grow waits for the stream before freeing the old buffers).
+// split-K workspace of one (device, stream): partial tiles + per-tile ticket / ready counters (zeroed once;
+// each launch leaves them zero, see splitk_join) + an error word.  Launches on one stream are ordered, so one
+// set per stream suffices; keyed by the device too, since the null stream has the same handle on every
+// device.  It only grows (a grow waits for the stream before freeing the old buffers).
 struct SplitKWs {
     void* ws = nullptr;
     size_t ws_bytes = 0;
-    unsigned* cnt = nullptr;  // [2][tiles]: tickets, ready counts
+    unsigned* cnt = nullptr;  // [2][tiles] tickets, ready counts; then the error word
     size_t tiles = 0;
 };
 std::mutex g_sk_mu;
-std::unordered_map<hipStream_t, SplitKWs> g_sk;
+std::map<std::pair<int, hipStream_t>, SplitKWs> g_sk;
 
 void splitk_setup(GemmParams& p, int ntiles, int S, size_t tile_bytes, hipStream_t s) {
+    int dev = 0;
+    ACEMI_HIP(hipGetDevice(&dev));
     std::lock_guard<std::mutex> lk(g_sk_mu);
-    SplitKWs& w = g_sk[s];
+    SplitKWs& w = g_sk[std::make_pair(dev, s)];
     const size_t need = (size_t)ntiles * S * tile_bytes;
     if (w.ws_bytes < need || w.tiles < (size_t)ntiles) ACEMI_HIP(hipStreamSynchronize(s));
     if (w.ws_bytes < need) {
@@ -1215,14 +453,15 @@ void splitk_setup(GemmParams& p, int ntiles, int S, size_t tile_bytes, hipStream
         w.cnt = nullptr;
         w.tiles = 0;
         const size_t t = std::max<size_t>((size_t)ntiles, 4096);
-        ACEMI_HIP(hipMalloc(&w.cnt, 2 * t * sizeof(unsigned)));
-        ACEMI_HIP(hipMemsetAsync(w.cnt, 0, 2 * t * sizeof(unsigned), s));
+        ACEMI_HIP(hipMalloc(&w.cnt, (2 * t + 1) * sizeof(unsigned)));
+        ACEMI_HIP(hipMemsetAsync(w.cnt, 0, (2 * t + 1) * sizeof(unsigned), s));
         w.tiles = t;
     }
     p.ksplit = S;
     p.sk_ws = static_cast<f32x4*>(w.ws);
     p.sk_cnt = w.cnt;
     p.sk_ready = w.cnt + w.tiles;
+    p.sk_err = w.cnt + 2 * w.tiles;
 }
 
 template <int BM, int BN, int WM, int WN, bool F16, int EPI, int PIPE>
@@ -1296,43 +535,11 @@ void dispatch_epi(int variant, const GemmParams& p, hipStream_t s) {
     }
 }
 
-template <int BM, int BN, int WM, int WN, int EPI, int WQ>
-void launch_q_cfg(const GemmParams& p, hipStream_t s) {
-    const int nbm = (p.M + BM - 1) / BM;
-    const int nbn = p.N / BN;
-    if constexpr (EPI == EPI_QKV_PREP && BN != 128)
-        throw std::runtime_error("gemm: the fused attention prep needs 128-wide column tiles");
-    else
-        hipLaunchKernelGGL((gemm_q_kernel<BM, BN, WM, WN, EPI, WQ>), dim3(nbm * nbn), dim3(WM * WN * 64), 0, s, p);
-}
 
-template <int EPI, int WQ>
-void launch_q_variant(int variant, const GemmParams& p, hipStream_t s) {
-    switch (variant) {
-        case 0:
-        case 1: launch_q_cfg<128, 128, 2, 2, EPI, WQ>(p, s); break;
-        case 2: launch_q_cfg<256, 256, 2, 4, EPI, WQ>(p, s); break;
-        case 3: launch_q_cfg<256, 128, 2, 2, EPI, WQ>(p, s); break;
-        case 4: launch_q_cfg<192, 128, 2, 2, EPI, WQ>(p, s); break;
-        case 5: launch_q_cfg<192, 256, 2, 4, EPI, WQ>(p, s); break;
-        case 7: launch_q_cfg<96, 128, 2, 2, EPI, WQ>(p, s); break;
-        default: throw std::runtime_error("gemm: bad variant");
-    }
-}
+}  // namespace gemm_detail
 
-template <int WQ>
-void dispatch_q_epi(int variant, const GemmParams& p, hipStream_t s) {
-    switch (p.e.kind) {
-        case EPI_STORE_F32: launch_q_variant<EPI_STORE_F32, WQ>(variant, p, s); break;
-        case EPI_STORE_ACT: launch_q_variant<EPI_STORE_ACT, WQ>(variant, p, s); break;
-        case EPI_RESID_GATED: launch_q_variant<EPI_RESID_GATED, WQ>(variant, p, s); break;
-        case EPI_RESID: launch_q_variant<EPI_RESID, WQ>(variant, p, s); break;
-        case EPI_SWIGLU: launch_q_variant<EPI_SWIGLU, WQ>(variant, p, s); break;
-        case EPI_PROJ_OUT: launch_q_variant<EPI_PROJ_OUT, WQ>(variant, p, s); break;
-        case EPI_QKV_PREP: launch_q_variant<EPI_QKV_PREP, WQ>(variant, p, s); break;
-        default: throw std::runtime_error("gemm: bad epilogue kind");
-    }
-}
+namespace {
+using namespace gemm_detail;
 
 int g_forced_variant = -1;
 
@@ -1349,22 +556,38 @@ int g_forced_variant = -1;
 // o / cross 662 vs 569).
 double m_edge(int M, int bm) { return (double)M / (double)(((M + bm - 1) / bm) * bm); }
 
+// Quantized weights: the register-dequant kernel (gemm_qr_kernel, variants 20-24 [+ 100 S]); the round-1
+// LDS-dequant kernel (gemm_q_kernel, 0-7) only when forced.  Long sequences: 192-row tiles (8 waves where
+// N % 256 == 0 leaves a full round of 256-column tiles); short ones: 128 / 64-row tiles, split over K until
+// the grid covers the 256 CUs.
+int pick_variant_q(int M, int N, int K) {
+    const int64_t mb192 = (M + 191) / 192;
+    if (M > 1024) {
+        if (N % 256 == 0 && mb192 * (N / 256) >= 256) return 21;
+        return 20;
+    }
+    const int bm = M > 256 ? 128 : 64;
+    const int v = bm == 128 ? 22 : 23;
+    const int64_t tiles = (int64_t)((M + bm - 1) / bm) * (N / 128);
+    int S = 1;
+    while (S < 4 && tiles * S * 2 <= 512 && K / 64 >= 4 * S) S *= 2;
+    return S > 1 ? v + 100 * S : v;
+}
+
 int pick_variant(int M, int N, int K, bool quant) {
     if (g_forced_variant >= 0) {  // forced (tests / micro-benchmarks), where that tile supports the shape
         const int f = g_forced_variant % 100, S = g_forced_variant / 100;
-        const bool wide = f == 2 || f == 5 || f == 10 || f == 11;
-        const bool dense_only = f == 6 || f >= 8 || S > 1;
-        const bool sk_ok = S <= 1 || ((f == 1 || f == 3 || f == 4 ? S <= 2 : (f >= 6 && f <= 9 && S <= 4)) &&
-                                      K / 64 >= 2 * S);
-        if (!(wide && N % 256 != 0) && !(quant && dense_only) && sk_ok) return g_forced_variant;
+        const bool wide = f == 2 || f == 5 || f == 10 || f == 11 || f == 21;
+        const bool qr = f >= 20 && f <= 24;
+        const bool dense_only = (f == 6 || (f >= 8 && f < 20) || S > 1) && !qr;
+        const bool sk_ok = S <= 1 || (qr ? (f == 22 || f == 23) && S <= 4 && K / 64 >= 2 * S
+                                         : ((f == 1 || f == 3 || f == 4 ? S <= 2 : (f >= 6 && f <= 9 && S <= 4)) &&
+                                            K / 64 >= 2 * S));
+        if (!(wide && N % 256 != 0) && !(quant && dense_only) && !(!quant && qr) && sk_ok) return g_forced_variant;
     }
     const int64_t mb192 = (M + 191) / 192;
     const bool edge_ok = m_edge(M, 192) >= m_edge(M, 128) - 0.02;
-    if (quant) {
-        if (N % 256 == 0 && edge_ok && mb192 * (N / 256) >= 256) return 5;
-        if (m_edge(M, 96) >= m_edge(M, 128) - 0.02) return 7;  // down 590 vs 493, o / cross 474 vs 396
-        return 1;
-    }
+    if (quant) return pick_variant_q(M, N, K);
     // 8-wave ping-pong tiles for batched sequences (tools/gemm_msweep.py on MI355X, TFLOP/s): M = 12000 gate|up
     // 1011 (256x256) vs 941 (v2), qkv 933 vs 902, down 922 (192x256) vs 818, o 814 vs 786; M = 24000 gate|up
     // 1089 vs 1016, qkv 941 vs 897, down 955 vs 915, o 767 (v2) vs 724; M = 6000 down 921 (192x256) vs 853.
@@ -1408,7 +631,7 @@ void launch_gemm(const uint16_t* A, int lda, const WeightView& W, int M, int N, 
         ACEMI_CHECK(epi.prep.q_col <= 0 && (epi.prep.k_col < 0 || epi.prep.k_col == 128 * nqc) &&
                         (epi.prep.v_col < 0 || epi.prep.v_col == 128 * (nqc + nkc)),
                     "gemm: fused attention prep expects the [q | k | v] head order");
-        v = v == 2 ? 3 : v == 5 ? 4 : v == 6 ? 1 : v == 9 ? 8 : v;
+        v = v == 2 ? 3 : v == 5 ? 4 : v == 6 ? 1 : v == 9 ? 8 : v % 100 == 21 ? v - 1 : v;
     }
     switch (W.fmt) {
         case WF_BF16:
@@ -1421,15 +644,15 @@ void launch_gemm(const uint16_t* A, int lda, const WeightView& W, int M, int N, 
             break;
         case WF_Q8_0:
             ACEMI_CHECK(W.s != nullptr, "gemm: null scales");
-            dispatch_q_epi<WF_Q8_0>(v, p, s);
+            dispatch_quant(WF_Q8_0, v, p, s);
             break;
         case WF_Q4_K:
             ACEMI_CHECK(W.s != nullptr, "gemm: null scales");
-            dispatch_q_epi<WF_Q4_K>(v, p, s);
+            dispatch_quant(WF_Q4_K, v, p, s);
             break;
         case WF_Q6_K:
             ACEMI_CHECK(W.s != nullptr, "gemm: null scales");
-            dispatch_q_epi<WF_Q6_K>(v, p, s);
+            dispatch_quant(WF_Q6_K, v, p, s);
             break;
         default: throw std::runtime_error("gemm: bad weight format");
     }
@@ -1447,48 +670,18 @@ void launch_gemm(ActType t, const uint16_t* A, int lda, const uint16_t* W, int l
 
 void gemm_force_variant(int v) { g_forced_variant = v; }
 
-void launch_dequant_bf16_batch(const DequantJob* jobs, int n, hipStream_t s) {
-    ACEMI_CHECK(n >= 1 && n <= 8, "dequant: 1..8 matrices per launch");
-    DequantBatch b{};
-    int64_t tot = 0;
-    for (int i = 0; i < n; ++i) {
-        const DequantJob& jb = jobs[i];
-        ACEMI_CHECK(weight_quantized(jb.w.fmt) && jb.w.fmt == jobs[0].w.fmt && jb.w.q && jb.w.s && jb.K % 32 == 0 &&
-                        jb.N > 0 && jb.out,
-                    "dequant: same-format quantized [N][K] weights");
-        b.q[i] = static_cast<const char*>(jb.w.q);
-        b.s[i] = jb.w.s;
-        b.out[i] = jb.out;
-        tot += (int64_t)jb.N * (jb.K / 8);  // 8-weight chunks
-        b.end[i] = tot;
+void gemm_splitk_check() {
+    std::lock_guard<std::mutex> lk(g_sk_mu);
+    int cur = 0;
+    ACEMI_HIP(hipGetDevice(&cur));
+    for (auto& kv : g_sk) {
+        if (kv.first.first != cur || !kv.second.cnt) continue;
+        unsigned err = 0;
+        ACEMI_HIP(hipStreamSynchronize(kv.first.second));
+        ACEMI_HIP(hipMemcpy(&err, kv.second.cnt + 2 * kv.second.tiles, sizeof(unsigned), hipMemcpyDeviceToHost));
+        if (err) throw std::runtime_error("gemm: a split-K join timed out waiting for its partial tiles (results invalid)");
     }
-    b.n = n;
-    static const int cpt = [] {  // chunks per thread (A/B knob; 2 by default: 46 vs 47.5 / 49 us for 1 / 4)
-        const char* e = std::getenv("ACE_MI_DEQ_CPT");
-        const int v = e ? std::atoi(e) : 2;
-        return v == 1 || v == 4 || v == 8 ? v : 2;
-    }();
-    const dim3 grid((unsigned)((tot + 256 * cpt - 1) / (256 * cpt)));
-#define ACEMI_DEQ(WQ)                                                                         \
-    switch (cpt) {                                                                            \
-        case 1: hipLaunchKernelGGL((dequant_bf16_kernel<WQ, 1>), grid, dim3(256), 0, s, b); break; \
-        case 4: hipLaunchKernelGGL((dequant_bf16_kernel<WQ, 4>), grid, dim3(256), 0, s, b); break; \
-        case 8: hipLaunchKernelGGL((dequant_bf16_kernel<WQ, 8>), grid, dim3(256), 0, s, b); break; \
-        default: hipLaunchKernelGGL((dequant_bf16_kernel<WQ, 2>), grid, dim3(256), 0, s, b); break; \
-    }
-    switch (jobs[0].w.fmt) {
-        case WF_Q8_0: ACEMI_DEQ(WF_Q8_0); break;
-        case WF_Q4_K: ACEMI_DEQ(WF_Q4_K); break;
-        case WF_Q6_K: ACEMI_DEQ(WF_Q6_K); break;
-        default: throw std::runtime_error("dequant: bad weight format");
-    }
-#undef ACEMI_DEQ
-    ACEMI_HIP(hipGetLastError());
 }
 
-void launch_dequant_bf16(const WeightView& W, int N, int K, uint16_t* out, hipStream_t s) {
-    const DequantJob j{W, N, K, out};
-    launch_dequant_bf16_batch(&j, 1, s);
-}
 
 }  // namespace acemi

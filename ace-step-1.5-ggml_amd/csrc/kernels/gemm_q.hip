@@ -1,0 +1,639 @@
+// Quantized-weight GEMMs for the DiT block linears (gfx950): the register-dequant kernel (the default for
+// Q8_0 / Q4_K / Q6_K weights), round 1's LDS-dequant kernel (forced variants only) and the staged dequant
+// (the bf16 image of a quantized matrix, ACE_MI_QUANT_STAGED=1).  Weight planes: runtime/quant.h; the
+// dequant arithmetic is ggml's (dequantize_row_q8_0 / _q4_K / _q6_K: one f32 product, RNE to bf16).
+#include "gemm_common.h"
+
+namespace acemi {
+namespace gemm_detail {
+
+// ---------------------------------------------------------------------------------------------
+// Dequant-fused variant: W arrives as a ggml block format re-laid out at load (runtime/quant.h).
+// Each thread owns one 32-value block of the BN x 64 weight tile (BN*2 == threads): it loads the
+// block's bytes + scale(s) into registers one k-tile ahead, turns them into bf16 with the exact
+// ggml dequant arithmetic (q*d, d*sc*q - dmin*m, (d*sc)*q; one f32 rounding, then RNE bf16) and
+// writes the bf16 image into the same swizzled LDS layout the dense kernel reads.  A (bf16
+// activations) is still staged by LDS-DMA.  Pipeline (PIPE 1 shape): fragments of tile t are read
+// up front, a raw barrier frees the buffer, A(t+2) is DMA'd and W(t+2) dequantized into it while
+// the second half of tile t's MFMAs runs, and W(t+3)'s bytes are requested.
+struct WRaw {
+    u32x4 q0, q1;
+    float s0, s1;
+};
+
+__device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) {
+    typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+    bf16x2_t v;
+    v[0] = (__bf16)lo;
+    v[1] = (__bf16)hi;
+    return __builtin_bit_cast(uint32_t, v);
+}
+
+// A compiler-visible LDS store, not inline asm: the hazard recognizer does not cover an asm
+// ds_write_b128's data VGPRs, and on gfx950 the VALU overwrote them before the DS unit had read the
+// last lanes (lanes 48-63 of the dequantized W rows came out wrong on the GPU).
+__device__ __forceinline__ void ds_write_b128_v(uint32_t addr, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+    *(lds_u32x4*)(uintptr_t)addr = u32x4{a, b, c, d};
+}
+
+// Weight bytes are plain (compiler-tracked) loads issued one k-tile ahead; the loop consumes them
+// BEFORE it issues the next A DMA, so the vmcnt the compiler places at that use only drains what
+// must have landed by the end of the iteration anyway (tile kt+1's A, issued earlier).
+template <int WQ>
+__device__ __forceinline__ WRaw load_wq(const char* qbase, const float* sbase, int kt) {
+    WRaw r;
+    if constexpr (WQ == WF_Q4_K) {
+        r.q0 = *(const u32x4*)(qbase + kt * 32);
+        const float2 sm = *(const float2*)(sbase + kt * 4);
+        r.s0 = sm.x;
+        r.s1 = sm.y;
+    } else {
+        r.q0 = *(const u32x4*)(qbase + kt * 64);
+        r.q1 = *(const u32x4*)(qbase + kt * 64 + 16);
+        if constexpr (WQ == WF_Q8_0) {
+            r.s0 = sbase[kt * 2];
+            r.s1 = r.s0;
+        } else {
+            const float2 sc = *(const float2*)(sbase + kt * 4);
+            r.s0 = sc.x;
+            r.s1 = sc.y;
+        }
+    }
+    return r;
+}
+
+// signed bytes of w (k order b0..b3) * s, via the unsigned-byte converts: (u - 128) * s = fma(u, s, -128 s)
+__device__ __forceinline__ void deq_i8x4(uint32_t w, float s, float c, uint32_t& o0, uint32_t& o1) {
+    const uint32_t u = w ^ 0x80808080u;
+    const float f0 = fmaf((float)(u & 0xffu), s, c);
+    const float f1 = fmaf((float)((u >> 8) & 0xffu), s, c);
+    const float f2 = fmaf((float)((u >> 16) & 0xffu), s, c);
+    const float f3 = fmaf((float)(u >> 24), s, c);
+    o0 = pk_bf16(f0, f1);
+    o1 = pk_bf16(f2, f3);
+}
+// unsigned nibble bytes (0..15) of w * d - m
+__device__ __forceinline__ void deq_u4x4(uint32_t w, float d, float nm, uint32_t& o0, uint32_t& o1) {
+    const float f0 = fmaf((float)(w & 0xffu), d, nm);
+    const float f1 = fmaf((float)((w >> 8) & 0xffu), d, nm);
+    const float f2 = fmaf((float)((w >> 16) & 0xffu), d, nm);
+    const float f3 = fmaf((float)(w >> 24), d, nm);
+    o0 = pk_bf16(f0, f1);
+    o1 = pk_bf16(f2, f3);
+}
+
+// dequantize one 32-value block to 16 packed bf16 pairs in k order (ggml's dequant arithmetic, one f32
+// rounding, then RNE to bf16)
+template <int WQ>
+__device__ __forceinline__ void dequant_block(const WRaw& r, uint32_t (&o)[16]) {
+    if constexpr (WQ == WF_Q4_K) {
+        const float d = r.s0, nm = -r.s1;
+        const uint32_t w[4] = {r.q0[0], r.q0[1], r.q0[2], r.q0[3]};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {  // dword i: k = 8i..8i+3 in low nibbles, 8i+4..8i+7 in high nibbles
+            deq_u4x4(w[i] & 0x0f0f0f0fu, d, nm, o[4 * i + 0], o[4 * i + 1]);
+            deq_u4x4((w[i] >> 4) & 0x0f0f0f0fu, d, nm, o[4 * i + 2], o[4 * i + 3]);
+        }
+    } else {
+        const uint32_t w[8] = {r.q0[0], r.q0[1], r.q0[2], r.q0[3], r.q1[0], r.q1[1], r.q1[2], r.q1[3]};
+        const float c0 = -128.0f * r.s0, c1 = -128.0f * r.s1;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const float s = i < 4 ? r.s0 : r.s1;
+            const float c = i < 4 ? c0 : c1;
+            deq_i8x4(w[i], s, c, o[2 * i], o[2 * i + 1]);
+        }
+    }
+}
+
+// dequantize one 32-value block and store it as 4 swizzled 16-byte chunks of an LDS row
+template <int WQ>
+__device__ __forceinline__ void dequant_store(const WRaw& r, uint32_t row_addr, int wh, int sw) {
+    uint32_t o[16];
+    dequant_block<WQ>(r, o);
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+        ds_write_b128_v(row_addr + (((wh * 4 + c) ^ sw) * 16), o[4 * c], o[4 * c + 1], o[4 * c + 2], o[4 * c + 3]);
+}
+
+// Staged dequant: the bf16 image of a quantized [N][K] weight (the exact values the dequant-fused GEMM
+// writes to LDS: the same deq_* arithmetic), one thread per 8 consecutive weights, so a wave reads 512
+// (Q8_0, Q6_K) or 256 (Q4_K) contiguous bytes and writes 1 KiB contiguous.  HBM-bound: 1.0625 (Q8_0),
+// 0.5625 (Q4_K), 1.125 (Q6_K) bytes read + 2 bytes written per weight.
+struct DequantBatch {  // up to 8 same-format matrices expanded by one launch
+    const char* q[8];
+    const float* s[8];
+    uint16_t* out[8];
+    int64_t end[8];  // exclusive prefix sums of the 8-weight chunk counts
+    int n;
+};
+
+template <int WQ>
+__device__ __forceinline__ void dequant_chunk(const DequantBatch& b, int64_t c, uint4& o, uint16_t*& dst) {
+    int mi = 0;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) mi += (i + 1 < b.n && c >= b.end[i]) ? 1 : 0;
+    if (mi > 0) c -= b.end[mi - 1];
+    const char* __restrict__ q = b.q[mi];
+    const float* __restrict__ sc = b.s[mi];
+    const int64_t g = c >> 2;  // 8-weight chunk c: block g = c / 4, part j = c % 4
+    const int j = (int)(c & 3);
+    if constexpr (WQ == WF_Q4_K) {
+        const uint32_t w = *reinterpret_cast<const uint32_t*>(q + g * 16 + j * 4);  // k 8j..8j+3 low, +4..7 high
+        const float2 dm = *reinterpret_cast<const float2*>(sc + 2 * g);
+        deq_u4x4(w & 0x0f0f0f0fu, dm.x, -dm.y, o.x, o.y);
+        deq_u4x4((w >> 4) & 0x0f0f0f0fu, dm.x, -dm.y, o.z, o.w);
+    } else {
+        const uint2 w = *reinterpret_cast<const uint2*>(q + g * 32 + j * 8);
+        const float d = WQ == WF_Q8_0 ? sc[g] : sc[2 * g + (j >> 1)];  // Q6_K: one scale per 16 values
+        deq_i8x4(w.x, d, -128.0f * d, o.x, o.y);
+        deq_i8x4(w.y, d, -128.0f * d, o.z, o.w);
+    }
+    dst = b.out[mi] + c * 8;
+}
+
+// CPT chunks per thread, strided by the grid so each wave instruction stays coalesced; all loads of a
+// thread are issued before its first store
+template <int WQ, int CPT>
+__global__ void __launch_bounds__(256) dequant_bf16_kernel(DequantBatch b) {
+    const int64_t tot = b.end[b.n - 1];
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    const int64_t c0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    uint4 o[CPT];
+    uint16_t* dst[CPT];
+#pragma unroll
+    for (int k = 0; k < CPT; ++k)
+        if (c0 + k * stride < tot) dequant_chunk<WQ>(b, c0 + k * stride, o[k], dst[k]);
+#pragma unroll
+    for (int k = 0; k < CPT; ++k)
+        if (c0 + k * stride < tot) *reinterpret_cast<uint4*>(dst[k]) = o[k];
+}
+
+template <int BM, int BN, int WM, int WN, int EPI, int WQ>
+__global__ void __launch_bounds__(WM * WN * 64) gemm_q_kernel(GemmParams p) {
+    constexpr int NW = WM * WN;
+    constexpr int WTM = BM / WM;
+    constexpr int WTN = BN / WN;
+    constexpr int TM = WTM / 16;
+    constexpr int TN = WTN / 16;
+    constexpr int BK = 64;
+    constexpr int ROWB = BK * 2;
+    constexpr int STAGE = (BM + BN) * ROWB;
+    constexpr int G_A = BM / 8 / NW;
+    static_assert(BM % (8 * NW) == 0, "A staging split");
+    static_assert(BN * 2 == NW * 64, "one 32-value weight block per thread");
+    static_assert(EPI != EPI_SWIGLU || (TN % 2 == 0), "swiglu needs column pairs");
+
+    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wid = tid >> 6;
+    int m0, n0;
+    block_tile<BM, BN>(p, m0, n0);
+    const int wm0 = (wid / WN) * WTM;
+    const int wn0 = (wid % WN) * WTN;
+    const int M = p.M, K = p.K;
+
+    // A staging sources (LDS-DMA, swizzled source chunk)
+    const uint16_t* src[G_A];
+#pragma unroll
+    for (int j = 0; j < G_A; ++j) {
+        const int row = (wid + NW * j) * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ swz(row);
+        src[j] = p.A + (int64_t)min(m0 + row, M - 1) * p.lda + c * 8;
+    }
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+    auto stage_a = [&](int buf, int kt) {
+        char* base = smem + buf * STAGE;
+#pragma unroll
+        for (int j = 0; j < G_A; ++j)
+            __builtin_amdgcn_global_load_lds((const void*)(src[j] + kt * BK), (lds_void*)(base + (wid + NW * j) * 1024),
+                                             16, 0, 0);
+    };
+
+    // W block owned by this thread: row wr of the tile, K half wh of each 64-wide k-tile
+    const int wr = tid >> 1, wh = tid & 1;
+    const int64_t grow = n0 + wr;
+    const char* qbase;
+    const float* sbase;
+    if constexpr (WQ == WF_Q4_K) {
+        qbase = (const char*)p.Wq + grow * (K / 2) + wh * 16;
+        sbase = p.Ws + (grow * (K / 32) + wh) * 2;
+    } else if constexpr (WQ == WF_Q8_0) {
+        qbase = (const char*)p.Wq + grow * K + wh * 32;
+        sbase = p.Ws + grow * (K / 32) + wh;
+    } else {
+        qbase = (const char*)p.Wq + grow * K + wh * 32;
+        sbase = p.Ws + grow * (K / 16) + wh * 2;
+    }
+    const int wsw = swz(wr);
+    const uint32_t wrow_off = BM * ROWB + wr * ROWB;
+
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int nk = K / BK;
+    const int lrow = lane & 15;
+    const int lchunk = lane >> 4;
+    auto read_frags_asm = [&](int buf, uint4 (&a)[TM][2], uint4 (&b)[TN][2]) {
+        const uint32_t sb = lds0 + buf * STAGE;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int ch = (kk * 4 + lchunk) ^ ((lrow >> 1) & 7);
+            const uint32_t bb = sb + BM * ROWB + (wn0 + lrow) * ROWB + ch * 16;
+            const uint32_t ab = sb + (wm0 + lrow) * ROWB + ch * 16;
+            ReadRows<0, TN, 16 * ROWB>::run(bb, b, kk);
+            ReadRows<0, TM, 16 * ROWB>::run(ab, a, kk);
+        }
+        lds_wait_all();
+    };
+
+    // prologue: tiles 0 and 1 complete in LDS, W(min(2, nk-1)) requested
+    WRaw wnext = load_wq<WQ>(qbase, sbase, 0);
+    stage_a(0, 0);
+    dequant_store<WQ>(wnext, lds0 + wrow_off, wh, wsw);
+    if (nk > 1) {
+        wnext = load_wq<WQ>(qbase, sbase, 1);
+        stage_a(1, 1);
+        dequant_store<WQ>(wnext, lds0 + STAGE + wrow_off, wh, wsw);
+    }
+    wnext = load_wq<WQ>(qbase, sbase, min(2, nk - 1));
+    wait_vmcnt<0>();
+    lds_wait_all();
+    __builtin_amdgcn_s_barrier();
+
+    auto mfma_all = [&](const uint4 (&a)[TM][2], const uint4 (&b)[TN][2]) {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<false>(a[i][kk], b[j][kk], acc[i][j]);
+    };
+
+    // One branch-free body for every tile: past the end, the tile indices clamp to nk-1, so the last
+    // two iterations re-stage the final tile into a buffer nobody reads again (harmless, and it keeps
+    // the accumulators in one loop so they stay put in AGPRs).
+    for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        uint4 a[TM][2], b[TN][2];
+        read_frags_asm(cur, a, b);
+        // Every MFMA of the tile issues after this barrier (the dequant VALU work interleaves with them).
+        __builtin_amdgcn_s_barrier();  // every wave holds its fragments of tile kt: buffer `cur` is free
+        asm volatile("" ::: "memory");  // the LDS stores below stay after the barrier
+        // W(kt+2): waiting for its bytes also retires the older A(kt+1) DMA
+        dequant_store<WQ>(wnext, lds0 + cur * STAGE + wrow_off, wh, wsw);
+        // Every wave's ds_writes retire before any wave issues its LDS-DMA: measured on gfx950, an LDS
+        // DMA issued while ds_write_b128s of the workgroup are still in flight corrupts lanes 48-63 of
+        // those writes (random W elements of rows 24-31 of every 32, on some launches).  A per-wave
+        // lgkmcnt(0) cleared the 4-wave tiles but not the 8-wave 256x256 one; lgkmcnt(0) + barrier
+        // cleared all (tools/diag_gemm_q.py stress: 0 bad launches of 20 per variant and format).
+        lds_wait_all();
+        __builtin_amdgcn_s_barrier();
+        stage_a(cur, min(kt + 2, nk - 1));
+        // keep the W(kt+3) loads behind the A(kt+2) DMA in issue order: the vmcnt the compiler
+        // places before the next iteration's dequant (waiting for those bytes) then also retires
+        // A(kt+2) before the barrier that ends that iteration publishes buffer `cur` again
+        asm volatile("" ::: "memory");
+        wnext = load_wq<WQ>(qbase, sbase, min(kt + 3, nk - 1));
+        mfma_all(a, b);
+        // retire this wave's LDS traffic before the barrier that hands buffer `cur` to the other waves
+        // (gfx950 does not wait at s_barrier)
+        lds_wait_all();
+        __builtin_amdgcn_s_barrier();
+    }
+    wait_vmcnt<0>();
+
+    if constexpr (EPI == EPI_QKV_PREP)
+        qkv_prep_tile<BM, NW, TM, TN, 2 * STAGE>(p, acc, m0, n0, wm0, wn0, tid, smem);
+    else
+        gemm_epilogue<TM, TN, false, EPI, NW >= 8 ? 64 : 1024>(p, acc, m0 + wm0, n0 + wn0, lane);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Register-dequant fused GEMM (the quantized default): NW waves side by side along N, each owning 32 columns
+// (two 16-wide MFMA column tiles) and ALL BM rows of a BM x (32 NW) output tile.  A [BM][64] k-tiles are
+// staged by LDS-DMA into a 3-slot ring of swizzled images shared by the NW waves (the dense kernel's A path);
+// W never touches LDS: each lane (column n = lane & 15, k group g = lane >> 4 of the 16x16x32 B operand) loads
+// its fragments' quantized bytes + scales straight from the resident planes two k-tiles ahead into registers
+// and forms the bf16 B fragments there with the staged dequant's arithmetic (deq_i8x4 / deq_u4x4: the same
+// f32 products, RNE to bf16).  The MFMA operands and the per-element k order therefore equal the staged
+// dequant + dense GEMM bit for bit, while the weights cross HBM / L2 at 1.0625 (Q8_0), 0.5625 (Q4_K) or
+// 1.125 (Q6_K) bytes each and no bf16 image exists.  One dequant per weight per block (the waves own
+// disjoint columns), reused by TM = BM / 16 MFMAs: ~20 VALU per 8-weight fragment against TM x 8 free issue
+// cycles per MFMA gap.  No ds_write anywhere (the LDS-DMA / ds_write hazard of DESIGN.md §10 cannot arise).
+// Pipeline per k-tile t: wait A(t) [vmcnt keeps A(t+1) and W(t+1) in flight], barrier, stage A(t+2) into the
+// slot last read at t-1, dequant W(t) -> B fragments, request W(t+2), then per kk: A fragments from LDS,
+// TM x 2 MFMAs.
+struct WFrag {  // one lane's quantized bytes of one k-tile: TN = 2 column tiles x 2 k halves
+    uint32_t q[2][2][2];  // [j][kk] 8 bytes (Q8_0 / Q6_K) or 4 bytes in q[..][0] (Q4_K)
+    float s[2][2][2];     // [j][kk] scale (Q8_0 / Q6_K: s[..][0]; Q4_K: d*sc, dmin*m)
+};
+
+template <int WQ>
+__device__ __forceinline__ void qr_load(WFrag& f, const char* __restrict__ qrow0, const char* __restrict__ qrow1,
+                                        const float* __restrict__ srow0, const float* __restrict__ srow1, int kt,
+                                        int g) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const char* q = j ? qrow1 : qrow0;
+        const float* sr = j ? srow1 : srow0;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int blk = kt * 2 + kk;  // 32-value block index along the row
+            if constexpr (WQ == WF_Q4_K) {
+                f.q[j][kk][0] = *reinterpret_cast<const uint32_t*>(q + blk * 16 + g * 4);
+                const float2 dm = *reinterpret_cast<const float2*>(sr + 2 * blk);
+                f.s[j][kk][0] = dm.x;
+                f.s[j][kk][1] = dm.y;
+            } else {
+                const uint2 w = *reinterpret_cast<const uint2*>(q + blk * 32 + g * 8);
+                f.q[j][kk][0] = w.x;
+                f.q[j][kk][1] = w.y;
+                f.s[j][kk][0] = WQ == WF_Q8_0 ? sr[blk] : sr[2 * blk + (g >> 1)];  // Q6_K: one scale per 16
+            }
+        }
+    }
+}
+
+template <int WQ>
+__device__ __forceinline__ void qr_dequant(const WFrag& f, uint4 (&b)[2][2]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            uint32_t o[4];
+            if constexpr (WQ == WF_Q4_K) {
+                const uint32_t w = f.q[j][kk][0];
+                const float d = f.s[j][kk][0], nm = -f.s[j][kk][1];
+                deq_u4x4(w & 0x0f0f0f0fu, d, nm, o[0], o[1]);
+                deq_u4x4((w >> 4) & 0x0f0f0f0fu, d, nm, o[2], o[3]);
+            } else {
+                const float d = f.s[j][kk][0];
+                deq_i8x4(f.q[j][kk][0], d, -128.0f * d, o[0], o[1]);
+                deq_i8x4(f.q[j][kk][1], d, -128.0f * d, o[2], o[3]);
+            }
+            b[j][kk] = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+}
+
+// two waves per SIMD (two 4-wave blocks or one 8-wave block per CU) where the LDS ring allows it
+template <int BM, int NW, int EPI, int WQ, bool SK = false>
+__global__ void __launch_bounds__(NW * 64, (NW == 8 || 2 * 3 * BM * 128 <= 160 * 1024) ? 2 : 1)
+    gemm_qr_kernel(GemmParams p) {
+    constexpr int BN = 32 * NW;
+    constexpr int TM = BM / 16;
+    constexpr int TN = 2;
+    constexpr int BK = 64;
+    constexpr int ROWB = BK * 2;
+    constexpr int SLOT = BM * ROWB;  // one A k-tile image
+    constexpr int G_A = BM / 8 / NW;  // 1 KiB LDS-DMA pieces per wave per k-tile
+    static_assert(BM % (8 * NW) == 0 && BM % 16 == 0, "A staging split");
+    static_assert(EPI != EPI_SWIGLU || (TN % 2 == 0), "swiglu needs column pairs");
+
+    __shared__ __attribute__((aligned(16))) char smem[3 * SLOT];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wid = tid >> 6;
+
+    const int S = SK ? p.ksplit : 1;
+    int m0, n0, sk_tile = 0, sk_part = 0;
+    unsigned ticket0 = 0;
+    if constexpr (SK) {
+        int ntiles;
+        splitk_block(S, sk_tile, sk_part, ntiles);
+        block_tile<BM, BN>(p, m0, n0, sk_tile, ntiles);
+        if (tid == 0) ticket0 = __hip_atomic_fetch_add(p.sk_cnt + sk_tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        block_tile<BM, BN>(p, m0, n0);
+    }
+    const int wn0 = wid * 32;
+    const int M = p.M, K = p.K;
+    const int nk_all = K / BK;
+    const int kt_begin = sk_part * nk_all / S;
+    const int nk = (sk_part + 1) * nk_all / S - kt_begin;
+
+    // A staging sources (swizzled source chunk, as the dense kernel)
+    const uint16_t* src[G_A];
+#pragma unroll
+    for (int j = 0; j < G_A; ++j) {
+        const int row = (wid + NW * j) * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ swz(row);
+        src[j] = p.A + (int64_t)min(m0 + row, M - 1) * p.lda + (int64_t)kt_begin * BK + c * 8;
+    }
+    auto stage = [&](int kt) {  // k-tile kt (relative) into slot kt % 3
+        char* base = smem + (kt % 3) * SLOT;
+#pragma unroll
+        for (int j = 0; j < G_A; ++j)
+            __builtin_amdgcn_global_load_lds((const void*)(src[j] + kt * BK), (lds_void*)(base + (wid + NW * j) * 1024),
+                                             16, 0, 0);
+    };
+
+    // this lane's two weight rows (column tiles j = 0, 1) and k group
+    const int g = lane >> 4;
+    const int64_t r0 = n0 + wn0 + (lane & 15), r1 = r0 + 16;
+    const int qrow_bytes = WQ == WF_Q4_K ? K / 2 : K;
+    const int srow = WQ == WF_Q8_0 ? K / 32 : (WQ == WF_Q4_K ? K / 16 : K / 16);
+    const char* qb = static_cast<const char*>(p.Wq) + (int64_t)kt_begin * (WQ == WF_Q4_K ? 32 : 64);
+    const float* sb = p.Ws + (int64_t)kt_begin * (WQ == WF_Q8_0 ? 2 : 4);
+    const char* qrow0 = qb + r0 * qrow_bytes;
+    const char* qrow1 = qb + r1 * qrow_bytes;
+    const float* srow0 = sb + r0 * srow;
+    const float* srow1 = sb + r1 * srow;
+
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+    const int lrow = lane & 15, lchunk = lane >> 4;
+    const int rsw = (lrow >> 1) & 7;
+
+    // prologue: A(0), W(0), A(1), W(1) in flight.  The two W register sets alternate by k-tile parity (a loop
+    // body per parity), so no copy of a register set with loads in flight forces an early vmcnt.
+    WFrag w0, w1;
+    stage(0);
+    qr_load<WQ>(w0, qrow0, qrow1, srow0, srow1, 0, g);
+    if (nk > 1) {
+        stage(1);
+        qr_load<WQ>(w1, qrow0, qrow1, srow0, srow1, 1, g);
+    }
+    // VMEM instructions younger than A(kt)'s pieces that may stay in flight at the top of k-tile kt: W(kt) and
+    // A(kt+1) (W(kt+1) too, so this is conservative): >= 4 W loads per k-tile whatever the compiler merges
+    constexpr int KEEP = G_A + 4;
+    auto step = [&](int kt, WFrag& w) {
+        if (kt + 1 < nk)
+            wait_vmcnt<KEEP>();
+        else
+            wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();  // every wave's pieces of A(kt) landed; slot (kt+2)%3 = (kt-1)%3 is free
+        if (kt + 2 < nk) stage(kt + 2);
+        uint4 b[TN][2];
+        qr_dequant<WQ>(w, b);
+        if (kt + 2 < nk) qr_load<WQ>(w, qrow0, qrow1, srow0, srow1, kt + 2, g);
+        const uint32_t sbase = lds0 + (kt % 3) * SLOT + lrow * ROWB;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            uint4 a[TM][2];
+            ReadRows<0, TM, 16 * ROWB>::run(sbase + (((kk * 4 + lchunk) ^ rsw) * 16), a, kk);
+            lds_wait_all();
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<false>(a[i][kk], b[j][kk], acc[i][j]);
+        }
+    };
+    for (int kt = 0; kt < nk; kt += 2) {
+        step(kt, w0);
+        if (kt + 1 < nk) step(kt + 1, w1);
+    }
+    __syncthreads();  // LDS reads done before the epilogue reuses the ring
+
+    if constexpr (SK)
+        if (!splitk_join<TM, TN, NW, 4, 3 * SLOT>(p, acc, S, sk_tile, sk_part, tid, smem, ticket0)) return;
+    if constexpr (EPI == EPI_QKV_PREP)
+        qkv_prep_tile<BM, NW, TM, TN, 3 * SLOT>(p, acc, m0, n0, 0, wn0, tid, smem);
+    else
+        gemm_epilogue<TM, TN, false, EPI, (SK ? 32 : 64)>(p, acc, m0, n0 + wn0, lane);
+}
+
+template <int BM, int BN, int WM, int WN, int EPI, int WQ>
+void launch_q_cfg(const GemmParams& p, hipStream_t s) {
+    const int nbm = (p.M + BM - 1) / BM;
+    const int nbn = p.N / BN;
+    if constexpr (EPI == EPI_QKV_PREP && BN != 128)
+        throw std::runtime_error("gemm: the fused attention prep needs 128-wide column tiles");
+    else
+        hipLaunchKernelGGL((gemm_q_kernel<BM, BN, WM, WN, EPI, WQ>), dim3(nbm * nbn), dim3(WM * WN * 64), 0, s, p);
+}
+
+// register-dequant kernel (gemm_qr_kernel): BM x (32 NW) tiles, split-K over S blocks per tile for the short ones
+template <int BM, int NW, int EPI, int WQ>
+void launch_qr_cfg(GemmParams p, int S, hipStream_t s) {
+    constexpr int BN = 32 * NW;
+    if (p.N % BN != 0) throw std::runtime_error("gemm: register-dequant tile needs N % (32 * waves) == 0");
+    const int nbm = (p.M + BM - 1) / BM;
+    const int nbn = p.N / BN;
+    if constexpr (EPI == EPI_QKV_PREP && NW != 4) {
+        throw std::runtime_error("gemm: the fused attention prep needs 128-wide column tiles");
+    } else {
+        if (S > 1) {
+            if constexpr (BM <= 128 && NW == 4) {
+                if (p.K / 64 < 2 * S || S > 4) throw std::runtime_error("gemm: bad split-K factor");
+                splitk_setup(p, nbm * nbn, S, (size_t)BM * BN * 4, s);
+                hipLaunchKernelGGL((gemm_qr_kernel<BM, NW, EPI, WQ, true>), dim3(nbm * nbn * S), dim3(NW * 64), 0, s,
+                                   p);
+            } else {
+                throw std::runtime_error("gemm: split-K is for the 64 / 128-row register-dequant tiles");
+            }
+        } else {
+            hipLaunchKernelGGL((gemm_qr_kernel<BM, NW, EPI, WQ>), dim3(nbm * nbn), dim3(NW * 64), 0, s, p);
+        }
+    }
+}
+
+template <int EPI, int WQ>
+void launch_q_variant(int variant, const GemmParams& p, hipStream_t s) {
+    const int S = variant / 100;
+    switch (variant % 100) {
+        case 20: launch_qr_cfg<192, 4, EPI, WQ>(p, S, s); return;
+        case 21: launch_qr_cfg<192, 8, EPI, WQ>(p, S, s); return;
+        case 22: launch_qr_cfg<128, 4, EPI, WQ>(p, S, s); return;
+        case 23: launch_qr_cfg<64, 4, EPI, WQ>(p, S, s); return;
+        case 24: launch_qr_cfg<256, 4, EPI, WQ>(p, S, s); return;
+        default: break;
+    }
+    if (S > 1) throw std::runtime_error("gemm: split-K is for the register-dequant tiles");
+    switch (variant) {
+        case 0:
+        case 1: launch_q_cfg<128, 128, 2, 2, EPI, WQ>(p, s); break;
+        case 2: launch_q_cfg<256, 256, 2, 4, EPI, WQ>(p, s); break;
+        case 3: launch_q_cfg<256, 128, 2, 2, EPI, WQ>(p, s); break;
+        case 4: launch_q_cfg<192, 128, 2, 2, EPI, WQ>(p, s); break;
+        case 5: launch_q_cfg<192, 256, 2, 4, EPI, WQ>(p, s); break;
+        case 7: launch_q_cfg<96, 128, 2, 2, EPI, WQ>(p, s); break;
+        default: throw std::runtime_error("gemm: bad variant");
+    }
+}
+
+template <int WQ>
+void dispatch_q_epi(int variant, const GemmParams& p, hipStream_t s) {
+    switch (p.e.kind) {
+        case EPI_STORE_F32: launch_q_variant<EPI_STORE_F32, WQ>(variant, p, s); break;
+        case EPI_STORE_ACT: launch_q_variant<EPI_STORE_ACT, WQ>(variant, p, s); break;
+        case EPI_RESID_GATED: launch_q_variant<EPI_RESID_GATED, WQ>(variant, p, s); break;
+        case EPI_RESID: launch_q_variant<EPI_RESID, WQ>(variant, p, s); break;
+        case EPI_SWIGLU: launch_q_variant<EPI_SWIGLU, WQ>(variant, p, s); break;
+        case EPI_PROJ_OUT: launch_q_variant<EPI_PROJ_OUT, WQ>(variant, p, s); break;
+        case EPI_QKV_PREP: launch_q_variant<EPI_QKV_PREP, WQ>(variant, p, s); break;
+        default: throw std::runtime_error("gemm: bad epilogue kind");
+    }
+}
+
+
+void dispatch_quant(int fmt, int variant, const GemmParams& p, hipStream_t s) {
+    switch (fmt) {
+        case WF_Q8_0: dispatch_q_epi<WF_Q8_0>(variant, p, s); break;
+        case WF_Q4_K: dispatch_q_epi<WF_Q4_K>(variant, p, s); break;
+        case WF_Q6_K: dispatch_q_epi<WF_Q6_K>(variant, p, s); break;
+        default: throw std::runtime_error("gemm: bad quantized weight format");
+    }
+}
+
+}  // namespace gemm_detail
+
+using namespace gemm_detail;
+
+void launch_dequant_bf16_batch(const DequantJob* jobs, int n, hipStream_t s) {
+    ACEMI_CHECK(n >= 1 && n <= 8, "dequant: 1..8 matrices per launch");
+    DequantBatch b{};
+    int64_t tot = 0;
+    for (int i = 0; i < n; ++i) {
+        const DequantJob& jb = jobs[i];
+        ACEMI_CHECK(weight_quantized(jb.w.fmt) && jb.w.fmt == jobs[0].w.fmt && jb.w.q && jb.w.s && jb.K % 32 == 0 &&
+                        jb.N > 0 && jb.out,
+                    "dequant: same-format quantized [N][K] weights");
+        b.q[i] = static_cast<const char*>(jb.w.q);
+        b.s[i] = jb.w.s;
+        b.out[i] = jb.out;
+        tot += (int64_t)jb.N * (jb.K / 8);  // 8-weight chunks
+        b.end[i] = tot;
+    }
+    b.n = n;
+    static const int cpt = [] {  // chunks per thread (A/B knob; 2 by default: 46 vs 47.5 / 49 us for 1 / 4)
+        const char* e = std::getenv("ACE_MI_DEQ_CPT");
+        const int v = e ? std::atoi(e) : 2;
+        return v == 1 || v == 4 || v == 8 ? v : 2;
+    }();
+    const dim3 grid((unsigned)((tot + 256 * cpt - 1) / (256 * cpt)));
+#define ACEMI_DEQ(WQ)                                                                         \
+    switch (cpt) {                                                                            \
+        case 1: hipLaunchKernelGGL((dequant_bf16_kernel<WQ, 1>), grid, dim3(256), 0, s, b); break; \
+        case 4: hipLaunchKernelGGL((dequant_bf16_kernel<WQ, 4>), grid, dim3(256), 0, s, b); break; \
+        case 8: hipLaunchKernelGGL((dequant_bf16_kernel<WQ, 8>), grid, dim3(256), 0, s, b); break; \
+        default: hipLaunchKernelGGL((dequant_bf16_kernel<WQ, 2>), grid, dim3(256), 0, s, b); break; \
+    }
+    switch (jobs[0].w.fmt) {
+        case WF_Q8_0: ACEMI_DEQ(WF_Q8_0); break;
+        case WF_Q4_K: ACEMI_DEQ(WF_Q4_K); break;
+        case WF_Q6_K: ACEMI_DEQ(WF_Q6_K); break;
+        default: throw std::runtime_error("dequant: bad weight format");
+    }
+#undef ACEMI_DEQ
+    ACEMI_HIP(hipGetLastError());
+}
+
+void launch_dequant_bf16(const WeightView& W, int N, int K, uint16_t* out, hipStream_t s) {
+    const DequantJob j{W, N, K, out};
+    launch_dequant_bf16_batch(&j, 1, s);
+}
+
+}  // namespace acemi

@@ -378,12 +378,16 @@ __global__ void timestep_freq_kernel(const float* __restrict__ t, const float* _
     float tv = t[b];
     if (r) tv = __fsub_rn(tv, r[b]);
     const float ts = __fmul_rn(tv, scale);
+    // exp / cos / sin evaluated in double and rounded once: the correctly rounded f32 results, i.e. the values
+    // any accurate f32 libm gives.  The sinusoid is the most ill-conditioned spot of the graph: arg reaches
+    // ~1000, so one ulp of fr moves arg by ~6e-5 and the feature by as much; a 1-2 ulp device expf / cosf
+    // put the timestep features ~1e-4 away from an accurate evaluation.
     for (int i = threadIdx.x; i < half; i += blockDim.x) {
         const float expo = __fdiv_rn(__fmul_rn(-log_max, (float)i), (float)half);
-        const float fr = expf(expo);
+        const float fr = (float)exp((double)expo);
         const float arg = __fmul_rn(ts, fr);
-        f[(int64_t)b * dim + i] = cosf(arg);
-        f[(int64_t)b * dim + i + half] = sinf(arg);
+        f[(int64_t)b * dim + i] = (float)cos((double)arg);
+        f[(int64_t)b * dim + i + half] = (float)sin((double)arg);
     }
     if ((dim & 1) && threadIdx.x == 0) f[(int64_t)b * dim + dim - 1] = 0.f;
 }
@@ -499,6 +503,14 @@ __global__ void sde_kernel(float* __restrict__ xt, const float* __restrict__ v, 
         const float x0 = __fsub_rn(xt[i], __fmul_rn(v[i], t));
         xt[i] = __fadd_rn(__fmul_rn(t_next, noise[i]), __fmul_rn(keep, x0));
     }
+}
+
+// Test-only fault injection (ACE_MI_TEST_FAULT, DitEngine): x[r][c] += amp over one 16-row x 128-column
+// tile, i.e. one row group of one GEMM output tile.  Exists to show that the parity checks fail on a
+// localised error (tests/test_gpu_parity_strict.py); never launched unless that variable is set.
+__global__ void fault_tile_kernel(float* __restrict__ x, int ld, int rows, int row0, int col0, float amp) {
+    const int r = row0 + (int)(blockIdx.x * 8 + (threadIdx.x >> 7)), c = col0 + (int)(threadIdx.x & 127);
+    if (r < rows) x[(int64_t)r * ld + c] = __fadd_rn(x[(int64_t)r * ld + c], amp);
 }
 
 inline dim3 grid_for(int64_t n, int block = 256) {
@@ -665,6 +677,12 @@ void launch_out_mods(const float* out_table, const float* temb_t, const float* t
                      float* outmod, hipStream_t s) {
     const int64_t n = (int64_t)B * 2 * H;
     hipLaunchKernelGGL(out_mods_kernel, grid_for(n), dim3(256), 0, s, out_table, temb_t, temb_r, B, H, outmod);
+    ACEMI_HIP(hipGetLastError());
+}
+
+void launch_fault_tile(float* x, int ld, int rows, int row0, int col0, float amp, hipStream_t s) {
+    ACEMI_CHECK(row0 >= 0 && col0 >= 0 && col0 + 128 <= ld, "fault_tile: tile outside the matrix");
+    hipLaunchKernelGGL(fault_tile_kernel, dim3(2), dim3(8 * 128), 0, s, x, ld, rows, row0, col0, amp);
     ACEMI_HIP(hipGetLastError());
 }
 

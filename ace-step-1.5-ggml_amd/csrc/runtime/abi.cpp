@@ -145,6 +145,7 @@ ace_ggml_status ace_ggml_dit_forward(ace_ggml_context* ctx, const float* hidden_
         const auto t1 = std::chrono::steady_clock::now();
         ctx->dit->forward(io, s);
         ACEMI_HIP(hipStreamSynchronize(s));
+        acemi::gemm_splitk_check();
         const auto t2 = std::chrono::steady_clock::now();
         ACEMI_HIP(hipMemcpyAsync(out, io.out, needed, hipMemcpyDeviceToHost, s));
         ACEMI_HIP(hipStreamSynchronize(s));
@@ -305,6 +306,14 @@ ace_ggml_status ace_mi_dit_sample_ex(ace_ggml_context* ctx, int32_t batch, float
                        sde != 0, d_noise, cover_steps, d_context_nc, d_enc_nc, cache_cross != 0, stream);
 }
 
+ace_ggml_status ace_mi_dit_set_attn_precision(ace_ggml_context* ctx, int32_t mode) {
+    if (!ctx || mode < 0 || mode > 2) return ACE_GGML_ERR_INVALID_ARG;
+    if (!ctx->dit) return set_error(ctx, ACE_GGML_ERR, "dit not loaded");
+    ctx->dit->set_attn_precision(mode == 0 ? acemi::AttnPrecision::FP16
+                                           : (mode == 1 ? acemi::AttnPrecision::SPLIT : acemi::AttnPrecision::F32));
+    return ACE_GGML_OK;
+}
+
 ace_ggml_status ace_mi_profile_enable(ace_ggml_context* ctx, int32_t on) {
     if (!ctx) return ACE_GGML_ERR_INVALID_ARG;
     if (!ctx->dit) return set_error(ctx, ACE_GGML_ERR, "dit not loaded");
@@ -363,6 +372,7 @@ ace_ggml_status ace_mi_synchronize(ace_ggml_context* ctx) {
         if (ctx->stream) {
             ACEMI_HIP(hipSetDevice(ctx->device));
             ACEMI_HIP(hipStreamSynchronize(ctx->stream));
+            acemi::gemm_splitk_check();
         }
     } catch (const std::exception& e) {
         return set_error(ctx, ACE_GGML_ERR, e.what());

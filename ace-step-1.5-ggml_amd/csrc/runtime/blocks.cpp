@@ -68,8 +68,8 @@ void BlockRunner::run(const BlockShape& sh, const std::vector<DevLayer>& layers,
         for (int p = 0; p < n; ++p) {
             float theta = (float)p;
             for (int i = 0; i < half; ++i) {
-                cs[(size_t)p * half + i] = cosf(theta);
-                sn[(size_t)p * half + i] = sinf(theta);
+                cs[(size_t)p * half + i] = (float)std::cos((double)theta);  // correctly rounded cosf / sinf
+                sn[(size_t)p * half + i] = (float)std::sin((double)theta);
                 theta *= theta_scale;
             }
         }

@@ -4,6 +4,7 @@
 
 #include <cmath>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <map>
 
@@ -21,6 +22,12 @@ DitEngine::DitEngine(int device) : device_(device) {
     staged_quant_ = !(q && q[0] == '0');
     const char* h = std::getenv("ACE_MI_QUANT_STAGE_SCOPE");
     stage_per_call_ = !(h && std::strcmp(h, "layer") == 0);
+    // TEST ONLY: ACE_MI_TEST_FAULT="layer,row,col,amp" adds amp to one 16 x 128 tile of the residual right after
+    // that layer's o-projection GEMM (the parity negative control of tests/test_gpu_parity_strict.py)
+    if (const char* f = std::getenv("ACE_MI_TEST_FAULT")) {
+        if (f[0] && std::sscanf(f, "%d,%d,%d,%f", &fault_.layer, &fault_.row, &fault_.col, &fault_.amp) != 4)
+            throw std::runtime_error("ACE_MI_TEST_FAULT must be layer,row,col,amp");
+    }
 }
 
 DitEngine::~DitEngine() {
@@ -203,8 +210,8 @@ void DitEngine::rope_table(int n, Buf& cb, Buf& sb, hipStream_t s) {
     for (int p = 0; p < n; ++p) {
         float theta = (float)p;
         for (int i = 0; i < half; ++i) {
-            cs[(size_t)p * half + i] = cosf(theta);
-            sn[(size_t)p * half + i] = sinf(theta);
+            cs[(size_t)p * half + i] = (float)std::cos((double)theta);  // correctly rounded cosf / sinf
+            sn[(size_t)p * half + i] = (float)std::sin((double)theta);
             theta *= theta_scale;
         }
     }
@@ -467,6 +474,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
             tic(s);
             launch_gemm(attn, qd, lw.o, (int)M, H, qd, e, s);
             toc("gemm_o", s);
+            if (li == fault_.layer) launch_fault_tile(x, H, (int)M, fault_.row, fault_.col, fault_.amp, s);
         }
 
         // cross-attention block (:1502-1520): no AdaLN, no gate, no RoPE

@@ -68,6 +68,11 @@ class DitEngine {
     int device() const { return device_; }
     void forward(const ForwardIO& io, hipStream_t s);
     void encode(const EncodeIO& io, hipStream_t s);
+    // attention operand precision of subsequent forwards (DiT blocks; the encoders keep their own)
+    void set_attn_precision(AttnPrecision p) {
+        attn_split_ = p != AttnPrecision::FP16;
+        attn_pv_split_ = p == AttnPrecision::F32;
+    }
     // enable per-kernel-class event timing for subsequent forwards
     void set_profiling(bool on);
     const KernelTimes& times() const { return times_; }
@@ -135,6 +140,10 @@ class DitEngine {
     char* stage_slot(int li);
     LayerViews layer_views(int li, bool staged);
     void stage_layer(int li, hipStream_t st);
+    struct Fault {  // ACE_MI_TEST_FAULT (test-only fault injection); layer -1 = off
+        int layer = -1, row = 0, col = 0;
+        float amp = 0.f;
+    } fault_;
     // profiling
     bool profiling_ = false;
     hipEvent_t ev0_ = nullptr, ev1_ = nullptr;

@@ -287,7 +287,7 @@ ace_ggml_status ace_mi_bench_gemm(int32_t act_type, int32_t epi, int32_t variant
 
 // Force a GEMM kernel variant for subsequent launches (-1 = automatic).
 ace_ggml_status ace_mi_gemm_variant(int32_t variant) {
-    if (variant < -1 || variant % 100 > 11 || variant > 411) return ACE_GGML_ERR_INVALID_ARG;
+    if (variant < -1 || variant % 100 > 24 || variant > 424) return ACE_GGML_ERR_INVALID_ARG;
     acemi::gemm_force_variant(variant);
     return ACE_GGML_OK;
 }
@@ -361,7 +361,7 @@ ace_ggml_status ace_mi_kernel_gemm_q(int32_t qtype, int32_t epi, int32_t variant
     if (!quant::applies(t, K)) return ACE_GGML_ERR_INVALID_ARG;
     if (epi != EPI_STORE_F32 && epi != EPI_SWIGLU) return ACE_GGML_ERR_UNSUPPORTED;
     if ((epi == EPI_STORE_F32 && !out_f32) || (epi == EPI_SWIGLU && !out_u16)) return ACE_GGML_ERR_INVALID_ARG;
-    if (variant < -1 || variant > 11) return ACE_GGML_ERR_INVALID_ARG;
+    if (variant < -1 || variant % 100 > 24 || variant > 424) return ACE_GGML_ERR_INVALID_ARG;
     try {
         std::vector<uint8_t> qp(quant::q_plane_bytes(t, N, K));
         std::vector<float> sp(quant::s_plane_floats(t, N, K));

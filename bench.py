@@ -19,6 +19,15 @@ Prints ONE JSON line on rank 0 (driver contract), with `roofline` for the
 dominant kernel (the MLP gate|up GEMM, measured with HIP events on the launch
 stream) and `cpu_baseline` (oracle/cpu/dit_cpu.cpp, the C++/OpenMP restatement of ggml's CPU
 forward_dit, on the host cores: one 240 s forward plus the configs[0] 10 s F16 forward).
+
+Extra lines beside the headline (one GPU only; each the same 27-step schedule, timed the same way):
+  hook_line        the reference pipeline's drop-in path: a Python Euler loop over torch ROCm tensors calling
+                   the installed `decoder.forward` (acestep_mi355x.hook, scripts/run_non_ggml_real_case.py:
+                   460-533) once per step, as model.generate_audio does
+  attn_split_line  the headline loop with f32-faithful `split` attention (hi/lo fp16 Q.K operands)
+  bf16_line        the same workload with bf16 weights (+ its own hook_line)
+  line_60s         BASELINE configs[1]: 60 s (T = 1500), bs = 1, bf16 weights
+  line_10s         10 s (T = 250, configs[0]'s shape) forward rate with the headline weights and with bf16
 """
 import argparse
 import json
@@ -53,6 +62,8 @@ def parse():
                          "BASELINE configs[2] (240 s, bs=1, Q8_0 dequant-fused matmul)")
     ap.add_argument("--no-bf16-line", action="store_true",
                     help="skip the bf16-weight run that is reported beside a quantized line")
+    ap.add_argument("--no-extra-lines", action="store_true",
+                    help="skip hook_line / attn_split_line / line_10s / line_60s")
     ap.add_argument("--emulate", action="store_true",
                     help="TEST MODE: the multi-rank code path on CPU (gloo, the host-emulated library of tests/, "
                          "tiny config); its numbers are not a measurement")
@@ -141,14 +152,61 @@ def main():
     sched = shifted_linear_schedule(args.sample_steps, 3.0)
     stream = 0 if args.emulate else torch.cuda.current_stream().cuda_stream
 
-    def run(first, k):
+    def run(first, k, inp=None, bridge=None):
         """k denoising steps of the schedule (cyclic) in ONE device-side generation-loop call
         (ace_mi_dit_sample_ex): per step one batched DiT forward + the Euler update, both HIP kernels.
         Cross-attention K/V are recomputed every step (as the ggml C sampler does) unless
         --cross-cache asks for the reference Python/MLX sampler's cache."""
+        x_, c_, e_, T_ = inp if inp is not None else (xt, ctx, enc, T)
         sch = [sched[(first + i) % len(sched)] for i in range(k)]
-        br.dit_sample_ex_device(b_loc, T, L, xt.data_ptr(), ctx.data_ptr(), enc.data_ptr(), 0, 0, sch,
-                                cache_cross=args.cross_cache, stream=stream)
+        (bridge or br).dit_sample_ex_device(x_.shape[0], T_, L, x_.data_ptr(), c_.data_ptr(), e_.data_ptr(), 0, 0, sch,
+                                            cache_cross=args.cross_cache, stream=stream)
+
+    def timed(fn, k=args.steps, w=args.warmup):
+        """seconds for k steps of fn(first, k) after w warmup steps (single GPU: synchronised around)"""
+        if w > 0:
+            fn(0, w)
+        sync()
+        t_0 = time.perf_counter()
+        fn(w, k)
+        sync()
+        return time.perf_counter() - t_0
+
+    def line(units, seconds, what):
+        return {"value": round(units / seconds, 3), "unit": "steps/s", "ms_per_step": round(1000.0 * seconds /
+                                                                                            args.steps, 3),
+                "workload": what}
+
+    def small_inputs(T_):
+        g_ = torch.Generator(device=dev).manual_seed(T_)
+        x_ = torch.randn((1, T_, audio), generator=g_, device=dev)
+        c_ = torch.cat([torch.randn((1, T_, audio), generator=g_, device=dev),
+                        torch.ones((1, T_, ctxd - audio), device=dev)], dim=-1).contiguous()
+        e_ = torch.randn((1, L, H), generator=g_, device=dev)
+        sync()
+        return x_, c_, e_, T_
+
+    def hook_runner(bridge, x_, c_, e_, T_):
+        """model.generate_audio's loop (acestep/handler.py:2827 via the ggml decoder hook): per step the installed
+        decoder.forward on torch tensors, then x <- x - v * dt as torch ops on the current stream"""
+        import types
+        from acestep_mi355x.hook import install_dit_backend
+        handler = types.SimpleNamespace(model=types.SimpleNamespace(decoder=types.SimpleNamespace(forward=None)))
+        install_dit_backend(handler, bridge)
+        dec = handler.model.decoder
+        state = {"x": x_.clone()}
+
+        def fn(first, k):
+            x = state["x"]
+            for i in range(k):
+                j = (first + i) % len(sched)
+                t_ = torch.full((x.shape[0],), float(sched[j]), dtype=torch.float32, device=dev)
+                v_, _ = dec.forward(hidden_states=x, timestep=t_, timestep_r=t_, attention_mask=None,
+                                    encoder_hidden_states=e_, encoder_attention_mask=None, context_latents=c_)
+                dt = sched[j] if j + 1 == len(sched) else sched[j] - sched[j + 1]
+                x = x - v_ * float(dt)
+            state["x"] = x
+        return fn
 
     if args.warmup > 0:
         run(0, args.warmup)
@@ -161,10 +219,16 @@ def main():
     barrier()
     sync()
     elapsed = time.perf_counter() - t0
+    rank_elapsed = [elapsed]
     if world > 1:
         el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        gathered = [torch.zeros_like(el) for _ in range(world)]
+        dist.all_gather(gathered, el)
+        rank_elapsed = [float(g.item()) for g in gathered]
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         elapsed = float(el.item())
+    # conditioning broadcast to every rank before the timed region (f32 noise, context, encoder states)
+    bcast_bytes = 4 * B * (T * audio + T * ctxd + L * H)
     finite = bool(torch.isfinite(xt).all().item())
 
     # ---- per-kernel timing (HIP events on the launch stream, one event pair per launch)
@@ -203,23 +267,33 @@ def main():
         if frac is not None:
             breakdown["_dit_block_linears"] = {"tflops": round(frac * BF16_PEAK_TFLOPS, 1), "frac_of_bf16_peak": frac}
 
+    extras = {}
+    single = world == 1 and not args.emulate
+    if single and not args.no_extra_lines:
+        # ---- the reference pipeline's drop-in path with the headline weights
+        extras["hook_line"] = line(B * args.steps, timed(hook_runner(br, xt, ctx, enc, T)),
+                                   "the headline workload through the installed decoder.forward hook: a Python "
+                                   "Euler loop on torch tensors, one hook call per step (model.generate_audio)")
+        # ---- f32-faithful attention operands
+        br.set_attn_precision("split")
+        extras["attn_split_line"] = line(B * args.steps, timed(run),
+                                         "the headline loop with split (hi/lo fp16 Q.K) attention operands")
+        br.set_attn_precision("fp16")
+        # ---- 10 s forward rate (configs[0]'s shape) with the headline weights
+        in10 = small_inputs(250)
+        extras["line_10s"] = {"weights": args.qtype or "bf16", **line(args.steps, timed(lambda f, k: run(f, k, in10)),
+                                                                       "10 s (T = 250, N = 125 tokens, L = 512), bs = 1:"
+                                                                       " DiT forwards + Euler per s")}
+
     # ---- the same workload with bf16 weights, reported beside a quantized line (single GPU only)
     bf16_line = None
-    if args.qtype and world == 1 and not args.no_bf16_line:
+    if args.qtype and single and not args.no_bf16_line:
         br.close()
         set_weights("")
-        br = GGMLCAPIBridge(device=local)
+        br = GGMLCAPIBridge(device=local, lib_path=lib_path) if lib_path else GGMLCAPIBridge(device=local)
         br.load_dit(ckpt)
-        if args.warmup > 0:
-            run(0, args.warmup)
-        sync()
-        t1 = time.perf_counter()
-        run(args.warmup, args.steps)
-        sync()
-        el_bf16 = time.perf_counter() - t1
-        bf16_line = {"value": round(B * args.steps / el_bf16, 3), "unit": "steps/s",
-                     "ms_per_step": round(1000.0 * el_bf16 / args.steps, 3),
-                     "workload": "the same 240 s bs=1 sampling loop with bf16 weights (no quantization)"}
+        el_bf16 = timed(run)
+        bf16_line = line(B * args.steps, el_bf16, "the same 240 s bs=1 sampling loop with bf16 weights (no quantization)")
         if not args.no_profile:
             br.profile_enable(True)
             br.profile_reset()
@@ -233,6 +307,19 @@ def main():
             gu = [p for p in prof_b if p[0] == "gemm_gate_up"]
             if gu:
                 bf16_line["gate_up_avg_launch_us"] = round(1000.0 * gu[0][1] / gu[0][2], 2)
+        if not args.no_extra_lines:
+            bf16_line["hook_line"] = line(B * args.steps, timed(hook_runner(br, xt, ctx, enc, T)),
+                                          "bf16 weights through the decoder.forward hook")
+            in10 = small_inputs(250)
+            extras["line_10s"]["bf16"] = line(args.steps, timed(lambda f, k: run(f, k, in10)),
+                                              "10 s forward rate with bf16 weights")
+            q = extras["line_10s"]["value"] / max(extras["line_10s"]["bf16"]["value"], 1e-9)
+            extras["line_10s"]["ratio_vs_bf16"] = round(q, 3)
+    if single and not args.no_extra_lines and (not args.qtype or bf16_line is not None):
+        # ---- BASELINE configs[1]: 60 s, bs = 1, bf16 weights (the bridge holds bf16 weights here)
+        in60 = small_inputs(1500)
+        extras["line_60s"] = line(args.steps, timed(lambda f, k: run(f, k, in60)),
+                                  "BASELINE configs[1]: DiT 27-step sample, 60 s (T = 1500, N = 750), bs = 1, bf16")
 
     # ---- CPU baseline: the C++/OpenMP restatement of ggml's CPU forward_dit on the host cores
     cpu = None
@@ -273,8 +360,11 @@ def main():
                 "parallelism": f"dp{world} (batch-sharded, RCCL broadcast of conditioning)",
             },
             "finite": finite,
+            "ranks": {"elapsed_s": [round(v, 5) for v in rank_elapsed], "broadcast_bytes_per_rank": bcast_bytes,
+                      "items_per_rank": [len(shard_indices(B, world, r)) for r in range(world)]},
             "roofline": roofline,
             "bf16_line": bf16_line,
+            **extras,
             "cpu_baseline": cpu,
             "breakdown": breakdown,
         }

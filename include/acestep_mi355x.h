@@ -77,6 +77,11 @@ ACE_GGML_API ace_ggml_status ace_mi_dit_sample_ex(ace_ggml_context* ctx, int32_t
                                                   const float* d_context_nc, const float* d_enc_nc,
                                                   int32_t cache_cross, void* stream);
 
+/* Operand precision of the DiT's attention MFMAs for subsequent forwards (the ACE_MI_ATTN_PRECISION
+ * default is read when the DiT is loaded): 0 = fp16 operands, 1 = `split` (hi/lo fp16 Q.K, fp16 P.V),
+ * 2 = `f32` (hi/lo fp16 for both products).  All accumulate in f32. */
+ACE_GGML_API ace_ggml_status ace_mi_dit_set_attn_precision(ace_ggml_context* ctx, int32_t mode);
+
 /* Per-kernel-class timing with hipEvents on the launch stream (adds a sync per kernel).
  * ace_mi_profile_get copies up to `cap` entries: names (NUL-separated into `names`, `names_cap`
  * bytes), total milliseconds and launch counts.  Returns the number of classes in *n_out. */

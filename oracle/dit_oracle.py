@@ -320,17 +320,21 @@ def silu(x):
 
 
 def timestep_freq(t: float, dim: int = 256, scale: float = 1000.0) -> np.ndarray:
-    """build_timestep_freq (:1261-1284), f32 arithmetic."""
+    """build_timestep_freq (:1261-1284), f32 arithmetic with correctly rounded exp / cos / sin (evaluated in
+    float64, rounded once: what an accurate libm returns; ggml-cpu's vectorised expf is within an ulp or two of
+    it).  The sinusoid is ill-conditioned -- arg reaches ~1000, so one ulp of the frequency moves the feature
+    by ~6e-5 -- so under the floor knob (ggml_numerics.MULMAT_PERTURB) the frequencies get the same relative
+    noise as the products: the spread of legitimate f32 evaluations of this node belongs in the floor."""
     half = dim // 2
     t_scaled = np.float32(t) * np.float32(scale)
     i = np.arange(half, dtype=np.float32)
     log_max = np.float32(math.log(10000.0))
     exponent = ((-log_max) * i / np.float32(half)).astype(np.float32)
-    f = np.exp(exponent).astype(np.float32)
+    f = ggml_numerics.perturb(np.exp(exponent.astype(np.float64)).astype(np.float32))
     arg = (t_scaled * f).astype(np.float32)
     out = np.zeros((1, dim), dtype=np.float32)
-    out[0, :half] = np.cos(arg)
-    out[0, half:2 * half] = np.sin(arg)
+    out[0, :half] = np.cos(arg.astype(np.float64)).astype(np.float32)
+    out[0, half:2 * half] = np.sin(arg.astype(np.float64)).astype(np.float32)
     return out
 
 
@@ -353,7 +357,8 @@ def rope_tables(n: int, head_dim: int, theta_base: float):
     for i in range(half):
         theta[:, i] = cur
         cur = (cur * theta_scale).astype(np.float32)
-    return np.cos(theta).astype(np.float32), np.sin(theta).astype(np.float32)
+    # correctly rounded cos / sin of the f32 angles (ggml_rope_cache_init calls libm cosf / sinf)
+    return np.cos(theta.astype(np.float64)).astype(np.float32), np.sin(theta.astype(np.float64)).astype(np.float32)
 
 
 def apply_rope_neox(x: np.ndarray, cos: np.ndarray, sin: np.ndarray) -> np.ndarray:
@@ -405,15 +410,20 @@ def attention(cfg: DitConfig, w: dict, xq, xkv, key_mask, sliding, window, rope,
         for h in range(nh):
             kh = k[:, h // rep, :]
             vh = v[:, h // rep, :]
-            s = (q[:, h, :] @ kh.T).astype(np.float32) * scale
+            s = ggml_numerics.perturb((q[:, h, :] @ kh.T).astype(np.float32)) * scale
             if bias is not None:
                 s = s + bias
             m = np.max(s, axis=1, keepdims=True)
             p = np.exp(s - m).astype(np.float32)
             ssum = np.sum(p.astype(np.float64), axis=1, keepdims=True)
             p = (p * (1.0 / ssum)).astype(np.float32)
-            out[:, h, :] = p @ vh
+            out[:, h, :] = ggml_numerics.perturb((p @ vh).astype(np.float32))
     return mul_mat(w["o"], out.reshape(q_len, nh * D))
+
+
+# (layer, row, col, amp): add amp to x[row:row+16, col:col+128] after that layer's self-attention residual --
+# the restatement of the engine's test-only ACE_MI_TEST_FAULT hook (negative-control tests); None = off
+FAULT = None
 
 
 def forward_dit(W: DitWeights, hidden_states, context_latents, encoder_hidden_states,
@@ -467,6 +477,9 @@ def forward_dit(W: DitWeights, hidden_states, context_latents, encoder_hidden_st
         a = attention(c, L["self_attn"], norm_msa, norm_msa, patch_mask, L["sliding"], c.sliding_window,
                       rope)
         x = (x + a * gate_msa).astype(np.float32)
+        if FAULT is not None and FAULT[0] == i:  # the engine's ACE_MI_TEST_FAULT hook, restated
+            _, r0, c0, amp = FAULT
+            x[r0:r0 + 16, c0:c0 + 128] = (x[r0:r0 + 16, c0:c0 + 128] + np.float32(amp)).astype(np.float32)
         if L["cross"] and enc is not None:
             cn = rms_norm(x, L["cross_attn_norm"], c.rms_norm_eps)
             co = attention(c, L["cross_attn"], cn, enc, encoder_attention_mask, False, 0, None)
@@ -488,22 +501,27 @@ def forward_dit(W: DitWeights, hidden_states, context_latents, encoder_hidden_st
     return np.ascontiguousarray(y2[:seq_len].astype(np.float32))
 
 
+def maxabs_rms(a, ref) -> float:
+    """max|a - ref| / rms(ref): the element-wise parity statistic (a localised error of a few rows shows up
+    here at full size, where the relative L2 over the whole output dilutes it)."""
+    a64, r64 = np.asarray(a, np.float64), np.asarray(ref, np.float64)
+    return float(np.max(np.abs(a64 - r64)) / np.sqrt(np.mean(r64 * r64)))
+
+
 def forward_with_floor_stats(W: DitWeights, *args, perturb: float = 1e-7, **kw):
-    """(out, floor_l2, floor_max): forward_with_floor's output and floor, plus the floor of the
-    element-wise metric -- the max relative change over elements with |out| > 1e-2 rms(out) (SURVEY
-    §8(d)'s max-abs-rel) under the same perturbation."""
+    """(out, floor_l2, floor_maxabs): forward_with_floor's output and floor, plus the floor of the
+    element-wise statistic max|pert - out| / rms(out) under the same perturbation (maxabs_rms)."""
     out = forward_dit(W, *args, **kw)
     old = ggml_numerics.MULMAT_PERTURB
     ggml_numerics.MULMAT_PERTURB = perturb
+    ggml_numerics.PERTURB_RNG = np.random.default_rng(12345)
     try:
         pert = forward_dit(W, *args, **kw)
     finally:
         ggml_numerics.MULMAT_PERTURB = old
     o64, p64 = out.astype(np.float64), pert.astype(np.float64)
     floor = float(np.linalg.norm(p64 - o64) / np.linalg.norm(o64))
-    sel = np.abs(o64) > 1e-2 * np.sqrt(np.mean(o64 * o64))
-    fmax = float(np.max(np.abs(p64 - o64)[sel] / np.abs(o64[sel]))) if sel.any() else 0.0
-    return out, floor, fmax
+    return out, floor, maxabs_rms(p64, o64)
 
 
 def forward_with_floor(W: DitWeights, *args, perturb: float = 1e-7, **kw):
@@ -514,6 +532,7 @@ def forward_with_floor(W: DitWeights, *args, perturb: float = 1e-7, **kw):
     out = forward_dit(W, *args, **kw)
     old = ggml_numerics.MULMAT_PERTURB
     ggml_numerics.MULMAT_PERTURB = perturb
+    ggml_numerics.PERTURB_RNG = np.random.default_rng(12345)
     try:
         pert = forward_dit(W, *args, **kw)
     finally:

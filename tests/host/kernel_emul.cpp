@@ -451,9 +451,9 @@ void launch_timestep_freq(const float* t, const float* r, int B, int dim, float 
         if (r) tv = tv - r[b];
         const float ts = tv * scale;
         for (int i = 0; i < half; ++i) {
-            const float arg = ts * expf((-log_max * (float)i) / (float)half);
-            f[(int64_t)b * dim + i] = cosf(arg);
-            f[(int64_t)b * dim + i + half] = sinf(arg);
+            const float arg = ts * (float)std::exp((double)((-log_max * (float)i) / (float)half));
+            f[(int64_t)b * dim + i] = (float)std::cos((double)arg);
+            f[(int64_t)b * dim + i + half] = (float)std::sin((double)arg);
         }
         if (dim & 1) f[(int64_t)b * dim + dim - 1] = 0.f;
     }
@@ -494,6 +494,13 @@ void launch_out_mods(const float* table, const float* tt, const float* tr, int B
         for (int j = 0; j < 2; ++j)
             for (int c = 0; c < H; ++c)
                 om[((int64_t)b * 2 + j) * H + c] = table[(int64_t)j * H + c] + (tt[(int64_t)b * H + c] + tr[(int64_t)b * H + c]);
+}
+
+void gemm_splitk_check() {}
+
+void launch_fault_tile(float* x, int ld, int rows, int row0, int col0, float amp, hipStream_t) {
+    for (int r = row0; r < row0 + 16 && r < rows; ++r)
+        for (int c = col0; c < col0 + 128; ++c) x[(int64_t)r * ld + c] += amp;
 }
 
 void launch_euler(float* xt, const float* v, int64_t n, float dt, hipStream_t) {

@@ -18,7 +18,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world,bpg", [(2, 1), (4, 2)])
+@pytest.mark.parametrize("world,bpg", [(2, 1), (4, 2), (8, 1)])
 def test_bench_multi_rank_path_emulated(world, bpg):
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from hostlib import CLANG
@@ -39,3 +39,8 @@ def test_bench_multi_rank_path_emulated(world, bpg):
     assert d["n_gpus"] == world and d["config"]["global_batch"] == world * bpg
     assert d["config"]["batch_per_gpu"] == bpg and d["finite"] is True
     assert d["value"] > 0 and d["steps"] == 2
+    # per-rank elapsed (max-over-ranks timing) and the conditioning broadcast of the multi-GPU path
+    assert len(d["ranks"]["elapsed_s"]) == world and max(d["ranks"]["elapsed_s"]) * d["value"] > 0
+    assert d["ranks"]["items_per_rank"] == [bpg] * world
+    T = int(round(2 * 25))
+    assert d["ranks"]["broadcast_bytes_per_rank"] == 4 * world * bpg * (T * 64 + T * 128 + 16 * 256)

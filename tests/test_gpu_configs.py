@@ -2,7 +2,9 @@
 serial path):
 
   configs[0]  F16-safetensors weights, 10 s (T = 250, N = 125), L = 512, all 24 layers
-  configs[2]  Q8_0 weights, 240 s (T = 6000, N = 3000), L = 512, 2 layers: engine arithmetic and ggml's
+  configs[1]  bf16 weights, 60 s (T = 1500, N = 750), L = 512, 2 layers (the short-sequence GEMM tiles)
+  configs[2]  Q8_0 weights, 240 s (T = 6000, N = 3000), L = 512, 2 layers: engine arithmetic and ggml's;
+              and the bench's exact path, 3 steps of the device sampling loop (ace_mi_dit_sample_ex)
   configs[3]  bs = 8 at 240 s, 2 layers, every item of one batched call
   configs[4]  Q4_K weights at 600 s (T = 15000, N = 7500), 2 layers; the full-width VAE decode over 192
               latent frames through the windowed plan (128-frame windows, 32 frames of overlap)
@@ -48,6 +50,75 @@ def test_config0_f16_weights_10s_full_model():
                                                 0.6428571429)
     l2 = check(got, ref, floor, "configs[0] F16 10 s, 24 layers", fmax)
     print(f"configs[0]: rel_l2 {'<=' if l2 <= 1e-3 else '>'} 1e-3 (north-star literal bound)")
+
+
+def test_config1_bf16_60s_two_layers(monkeypatch):
+    """configs[1]'s shape: bf16 weights, 60 s (T = 1500 frames, N = 750 tokens), L = 512, first 2 layers
+    (one sliding, one full): the M = 750 tile choice of the GEMMs and the 60 s attention grid vs the oracle."""
+    from acestep_mi355x.capi import GGMLCAPIBridge
+    from acestep_mi355x.synthetic import cached_checkpoint, make_config
+    from oracle.dit_oracle import DitWeights, forward_with_floor_stats
+    d = cached_checkpoint(make_config(num_hidden_layers=2), seed=0, backend="torch")
+    monkeypatch.setenv("ACE_GGML_DIT_MAX_LAYERS", "2")
+    T, L = 1500, 512
+    h, c, e = _inputs(T, L, 60)
+    br = GGMLCAPIBridge()
+    br.load_dit(d)
+    got = br.dit_forward_tfirst(h, c, e, None, None, 0.85, 0.85)
+    br.close()
+    ref, floor, fmax = forward_with_floor_stats(DitWeights(d), h, c, e, None, None, T, L, 0.85, 0.85, max_layers=2)
+    check(got, ref, floor, "configs[1] bf16 60 s, 2 layers", fmax)
+
+
+def test_config2_q8_0_sampling_loop_240s(monkeypatch):
+    """configs[2] through the bench's exact path: 3 steps of ace_mi_dit_sample_ex with Q8_0 weights at 240 s
+    (full width, 2 layers, cross K/V recomputed every step as in the bench) equal, bit for bit, 3 per-step
+    batched forwards (ace_mi_dit_forward_batched) with the same Euler updates; the first step's velocity is
+    checked against the oracle on the same quantized bytes (engine arithmetic)."""
+    import torch
+    from acestep_mi355x import capi
+    from acestep_mi355x.capi import GGMLCAPIBridge
+    from acestep_mi355x.synthetic import cached_checkpoint, make_config
+    from oracle import ggml_numerics
+    from oracle.dit_oracle import DitWeights, forward_with_floor_stats
+    d = cached_checkpoint(make_config(num_hidden_layers=2), seed=0, backend="torch")
+    monkeypatch.setenv("ACE_GGML_DIT_MAX_LAYERS", "2")
+    monkeypatch.setenv("ACE_GGML_DIT_WEIGHT_QTYPE", "q8_0")
+    T, L = 6000, 512
+    h, c, e = _inputs(T, L, 27)
+    sched = np.array([1.0, 0.9, 0.75], np.float32)
+    dev = torch.device("cuda:0")
+    x0, dc, de = (torch.from_numpy(a[None]).to(dev) for a in (h, c, e))
+    br = GGMLCAPIBridge()
+    br.load_dit(d)
+    xt = x0.clone()
+    torch.cuda.synchronize()
+    br.dit_sample_ex_device(1, T, L, xt.data_ptr(), dc.data_ptr(), de.data_ptr(), 0, 0, list(sched),
+                            cache_cross=False)
+    br.synchronize()
+    loop = xt.cpu().numpy()[0]
+    # per-step forwards + the same f32 Euler arithmetic (x -= v * dt; the last step x0 = x - v * t)
+    x = x0.clone()
+    v = torch.empty_like(x)
+    v0 = None
+    for i, t in enumerate(sched):
+        tt = torch.full((1,), float(t), dtype=torch.float32, device=dev)
+        torch.cuda.synchronize()
+        br.dit_forward_batched_device(1, T, L, x.data_ptr(), dc.data_ptr(), de.data_ptr(), 0, 0, tt.data_ptr(),
+                                      tt.data_ptr(), v.data_ptr(), 0)
+        br.synchronize()
+        if v0 is None:
+            v0 = v.cpu().numpy()[0]
+        dt = np.float32(t) if i + 1 == len(sched) else np.float32(np.float32(t) - np.float32(sched[i + 1]))
+        x = x - v * float(dt)
+    torch.cuda.synchronize()
+    br.close()
+    np.testing.assert_array_equal(loop, x.cpu().numpy()[0])
+    monkeypatch.setattr(ggml_numerics, "QUANTIZER", capi.quantize)
+    W = DitWeights(d, qtype="q8_0")
+    ref, floor, fmax = forward_with_floor_stats(engine_view(W), h, c, e, None, None, T, L, float(sched[0]),
+                                                float(sched[0]), max_layers=2)
+    check(v0, ref, floor, "configs[2] Q8_0 sampling loop, step 0 velocity", fmax)
 
 
 @pytest.mark.parametrize("qtype,T,seed", [("q8_0", 6000, 2), ("q4_k", 15000, 4)])

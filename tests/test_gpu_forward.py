@@ -8,10 +8,11 @@ where `floor` is the oracle's own rel_l2 change when every mul_mat result is per
 relative difference e into ~sqrt(e * 2^-8), so two correct implementations that differ
 only in f32 summation order agree to this floor and no better: measured 1.3e-3 after 2
 full-width layers and 3.4e-3 after 24 layers ("Parity").  Where the floor is
-below 1e-3 (tiny configs, shallow depth) the plain 1e-3 bound applies.  The max
-element-wise relative error (over |ref| > 1e-2 rms(ref)) is asserted the same way
-against the oracle's spread of that metric wherever the test computes it (the full-width cases here
-and tests/test_gpu_configs.py).
+below 1e-3 (tiny configs, shallow depth) the plain 1e-3 bound applies.  The
+element-wise statistic max|gpu - ref| / rms(ref) is asserted against 2.5x the oracle's own spread of
+that statistic wherever the test computes it (the full-width cases here, tests/test_gpu_configs.py and
+tests/test_gpu_parity_strict.py, whose fault-injection negative control shows that it catches one wrong
+16 x 128 tile that the L2 bound lets through).
 """
 import os
 
@@ -24,28 +25,37 @@ pytestmark = pytest.mark.gpu
 
 REL_L2 = 1e-3
 FLOOR_K = 1.5
-MAX_K = 2.0
+MAXABS_K = 2.5
 COS_MIN = 0.99999
 
 
 def check(got, ref, floor, tag, floor_max=None):
-    """rel-L2 floor-relative (module docstring); with `floor_max` (the oracle's own perturbation spread of
-    the element-wise metric, dit_oracle.forward_with_floor_stats) the SURVEY §8(d) max relative error over
-    |ref| > 1e-2 rms(ref) is asserted the same way: <= max(1e-3, MAX_K x floor_max).  Returns rel-L2."""
+    """rel-L2 floor-relative (module docstring).  With `floor_max` (the oracle's own perturbation spread of
+    the element-wise statistic max|d| / rms(ref), dit_oracle.forward_with_floor_stats) the element-wise
+    error is asserted against it with no absolute slack: max|got - ref| / rms(ref) <= MAXABS_K x floor_max,
+    so a wrong tile on a few rows fails even when the L2 over the whole output absorbs it
+    (test_gpu_parity_strict.py, fault-injection negative control).  SURVEY §8(d)'s max relative error over
+    |ref| > 1e-2 rms(ref) is printed for reference.  Returns rel-L2."""
     l2, mx = rel_errors(got, ref)
+    ma = maxabs_rms(got, ref)
     cos = float(np.dot(got.ravel().astype(np.float64), ref.ravel()) /
                 (np.linalg.norm(got.astype(np.float64)) * np.linalg.norm(ref.astype(np.float64))))
     bound = max(REL_L2, FLOOR_K * floor)
     extra = ""
     if floor_max is not None:
-        mbound = max(REL_L2, MAX_K * floor_max)
-        extra = f" floor_max={floor_max:.3e} max_ratio={mx / max(floor_max, 1e-12):.2f} max_bound={mbound:.3e}"
+        extra = (f" maxabs/rms={ma:.3e} floor_maxabs={floor_max:.3e} maxabs_ratio={ma / max(floor_max, 1e-12):.2f}"
+                 f" maxabs_bound={MAXABS_K * floor_max:.3e}")
     print(f"{tag}: rel_l2={l2:.3e} floor={floor:.3e} ratio={l2 / max(floor, 1e-12):.2f} cos={cos:.7f} "
           f"rel_max={mx:.3e} bound={bound:.3e}{extra}")
     assert np.isfinite(l2) and l2 <= bound and cos >= COS_MIN, (tag, l2, floor, cos)
     if floor_max is not None:
-        assert mx <= mbound, (tag, mx, floor_max)
+        assert ma <= MAXABS_K * floor_max, (tag, ma, floor_max)
     return l2
+
+
+def maxabs_rms(got, ref):
+    from oracle.dit_oracle import maxabs_rms as f
+    return f(got, ref)
 
 
 def rel_errors(got, ref):

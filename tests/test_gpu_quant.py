@@ -47,12 +47,16 @@ def test_staged_dequant_kernel_is_exact(qtype, N, K):
 
 
 @pytest.mark.parametrize("qtype", ["q8_0", "q4_k", "q6_k"])
-@pytest.mark.parametrize("variant", [-1, 1, 2, 3, 4, 5, 7])
+@pytest.mark.parametrize("variant", [-1, 1, 2, 3, 4, 5, 7, 20, 21, 22, 23, 24, 222, 223, 423])
 @pytest.mark.parametrize("M,N,K", [(1, 256, 256), (300, 512, 512), (1000, 256, 2048), (129, 768, 6144)])
 def test_gemm_q_matches_dequantized_product(qtype, variant, M, N, K):
+    """Both dequant-fused kernels (round 1's LDS-dequant tiles 1-7; the register-dequant tiles 20-24, + 100 S for
+    split-K over S blocks) against an fp64 product of the same bf16 operands."""
     capi = _capi()
-    if variant in (2, 5) and N % 256:
+    if variant in (2, 5, 21) and N % 256:
         pytest.skip("256-wide tiles need N % 256 == 0")
+    if variant >= 100 and K // 64 < 2 * (variant // 100):
+        pytest.skip("split-K needs two k-tiles per part")
     rng = np.random.default_rng(M + K + variant)
     a = f32_to_bf16_bits(rng.standard_normal((M, K)).astype(np.float32))
     w = (rng.standard_normal((N, K)) * 0.02).astype(np.float32)
