@@ -32,16 +32,21 @@ EXPORTED_SYMBOLS = (
     "ace_mi_create_on_device", "ace_mi_dit_get_info", "ace_mi_dit_forward_batched", "ace_mi_dit_sample",
     "ace_mi_dit_sample_ex",
     "ace_mi_profile_enable", "ace_mi_dit_set_attn_precision", "ace_mi_profile_reset", "ace_mi_profile_get", "ace_mi_probe_gemm",
-    "ace_mi_synchronize", "ace_mi_kernel_gemm", "ace_mi_kernel_attention", "ace_mi_bench_attention", "ace_mi_bench_gemm",
+    "ace_mi_synchronize",
     "ace_mi_gemm_variant", "ace_ggml_load_vae", "ace_ggml_vae_get_info", "ace_ggml_vae_decode",
     "ace_mi_vae_out_len", "ace_mi_vae_decode_device", "ace_ggml_vae_encode", "ace_mi_vae_enc_out_len",
-    "ace_mi_vae_encode_device", "ace_mi_quantize", "ace_mi_dequantize", "ace_mi_kernel_gemm_q", "ace_mi_kernel_dequant", "ace_mi_bench_gemm_q",
+    "ace_mi_vae_encode_device", "ace_mi_quantize", "ace_mi_dequantize",
     "ace_mi_cond_get_info", "ace_mi_text_project", "ace_mi_lyric_encode", "ace_mi_timbre_encode",
     "ace_mi_build_condition", "ace_ggml_load_lm", "ace_ggml_load_text_encoder", "ace_ggml_text_encoder_forward",
     "ace_ggml_text_encoder_forward_masked", "ace_ggml_text_encoder_forward_embeddings",
     "ace_ggml_text_encoder_forward_layers", "ace_ggml_generate_audio_simple", "ace_ggml_generate_audio_style_lyric_simple",
     "ace_ggml_generate_audio_style_lyric_timbre_simple", "ace_mi_reference_noise",
 )
+
+# Every symbol declared in include/acestep_mi355x_selftest.h: the TEST library (libacestep_mi355x_selftest.so = the
+# product objects + the kernel self-test / micro-benchmark entries); the product library does not export them.
+SELFTEST_SYMBOLS = ("ace_mi_kernel_gemm", "ace_mi_kernel_attention", "ace_mi_bench_attention", "ace_mi_bench_gemm",
+                    "ace_mi_kernel_gemm_q", "ace_mi_kernel_dequant", "ace_mi_bench_gemm_q")
 
 # qtype codes of ace_mi_quantize & co. (names as parse_quant_type, acestep_dit_model.cpp:27-37)
 QTYPES = {"q8_0": 1, "q4_k": 2, "q6_k": 3}
@@ -123,15 +128,6 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.ace_mi_probe_gemm.restype = ctypes.c_int
     lib.ace_mi_synchronize.argtypes = [vp]
     lib.ace_mi_synchronize.restype = ctypes.c_int
-    u16p = ctypes.POINTER(ctypes.c_uint16)
-    lib.ace_mi_kernel_gemm.argtypes = [i32, i32, i32, i32, i32, u16p, u16p, fp, fp, u16p]
-    lib.ace_mi_kernel_gemm.restype = ctypes.c_int
-    lib.ace_mi_kernel_attention.argtypes = [i32, i32, i32, i32, i32, i32, f32, i32, fp, fp, ip, fp]
-    lib.ace_mi_kernel_attention.restype = ctypes.c_int
-    lib.ace_mi_bench_gemm.argtypes = [i32, i32, i32, i32, i32, i32, i32, fp]
-    lib.ace_mi_bench_attention.argtypes = [i32, i32, i32, i32, i32, i32, i32, i32, fp]
-    lib.ace_mi_bench_attention.restype = ctypes.c_int
-    lib.ace_mi_bench_gemm.restype = ctypes.c_int
     lib.ace_mi_gemm_variant.argtypes = [i32]
     lib.ace_mi_gemm_variant.restype = ctypes.c_int
     i64, u8p = ctypes.c_int64, ctypes.POINTER(ctypes.c_uint8)
@@ -155,12 +151,6 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.ace_mi_quantize.restype = ctypes.c_int64
     lib.ace_mi_dequantize.argtypes = [i32, u8p, i64, i64, fp]
     lib.ace_mi_dequantize.restype = ctypes.c_int
-    lib.ace_mi_kernel_gemm_q.argtypes = [i32, i32, i32, i32, i32, i32, u16p, u8p, fp, fp, u16p]
-    lib.ace_mi_kernel_gemm_q.restype = ctypes.c_int
-    lib.ace_mi_kernel_dequant.argtypes = [i32, i32, i32, u8p, u16p]
-    lib.ace_mi_kernel_dequant.restype = ctypes.c_int
-    lib.ace_mi_bench_gemm_q.argtypes = [i32, i32, i32, i32, i32, i32, i32, fp]
-    lib.ace_mi_bench_gemm_q.restype = ctypes.c_int
     for name in ("ace_ggml_load_lm", "ace_ggml_load_text_encoder"):
         getattr(lib, name).argtypes = [vp, ctypes.c_char_p]
         getattr(lib, name).restype = ctypes.c_int
@@ -193,6 +183,43 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.ace_mi_build_condition.restype = ctypes.c_int
     if path is None:
         _LIB = lib
+    return lib
+
+
+_SELFTEST = None
+
+
+def load_selftest_library() -> ctypes.CDLL:
+    """The TEST library (kernel self-tests / micro-benchmarks, include/acestep_mi355x_selftest.h), built beside the
+    product library by the same make; the product library is loaded first (one HIP runtime per process)."""
+    global _SELFTEST
+    if _SELFTEST is not None:
+        return _SELFTEST
+    load_library()
+    p = os.environ.get("ACE_MI_SELFTEST_LIB") or os.path.join(os.path.dirname(LIB_PATH), "libacestep_mi355x_selftest.so")
+    if not os.path.exists(p):
+        raise RuntimeError(f"libacestep_mi355x_selftest.so not found at {p}: make -C ace-step-1.5-ggml_amd/csrc")
+    lib = ctypes.CDLL(p)
+    vp, i32, f32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_float
+    fp = ctypes.POINTER(ctypes.c_float)
+    ip = ctypes.POINTER(ctypes.c_int32)
+    u16p, u8p = ctypes.POINTER(ctypes.c_uint16), ctypes.POINTER(ctypes.c_uint8)
+    u16p = ctypes.POINTER(ctypes.c_uint16)
+    lib.ace_mi_kernel_gemm.argtypes = [i32, i32, i32, i32, i32, u16p, u16p, fp, fp, u16p]
+    lib.ace_mi_kernel_gemm.restype = ctypes.c_int
+    lib.ace_mi_kernel_attention.argtypes = [i32, i32, i32, i32, i32, i32, f32, i32, fp, fp, ip, fp]
+    lib.ace_mi_kernel_attention.restype = ctypes.c_int
+    lib.ace_mi_bench_gemm.argtypes = [i32, i32, i32, i32, i32, i32, i32, fp]
+    lib.ace_mi_bench_attention.argtypes = [i32, i32, i32, i32, i32, i32, i32, i32, fp]
+    lib.ace_mi_bench_attention.restype = ctypes.c_int
+    lib.ace_mi_bench_gemm.restype = ctypes.c_int
+    lib.ace_mi_kernel_gemm_q.argtypes = [i32, i32, i32, i32, i32, i32, u16p, u8p, fp, fp, u16p]
+    lib.ace_mi_kernel_gemm_q.restype = ctypes.c_int
+    lib.ace_mi_kernel_dequant.argtypes = [i32, i32, i32, u8p, u16p]
+    lib.ace_mi_kernel_dequant.restype = ctypes.c_int
+    lib.ace_mi_bench_gemm_q.argtypes = [i32, i32, i32, i32, i32, i32, i32, fp]
+    lib.ace_mi_bench_gemm_q.restype = ctypes.c_int
+    _SELFTEST = lib
     return lib
 
 
@@ -527,7 +554,7 @@ def kernel_gemm(a_bits: np.ndarray, w_bits: np.ndarray, act_type: int = 0, epi: 
                 bias: Optional[np.ndarray] = None, x: Optional[np.ndarray] = None) -> np.ndarray:
     """a_bits [M][K], w_bits [N][K] uint16 words; epi 0 -> f32 [M][N], epi 4 -> uint16 [M][N/2];
     epi 3 / 2 -> f32 x + C (* gate) with x [M][N] f32 and, for epi 2, the gate [N] passed as `bias`."""
-    lib = load_library()
+    lib = load_selftest_library()
     a = np.ascontiguousarray(a_bits, dtype=np.uint16)
     w = np.ascontiguousarray(w_bits, dtype=np.uint16)
     M, K = a.shape
@@ -556,7 +583,7 @@ def kernel_attention(q: np.ndarray, kv: np.ndarray, hq: int, hkv: int, window: i
                      split: bool = True, causal: bool = False, pv_split: bool = False) -> np.ndarray:
     """q [B][nq][hq*128] f32, kv [B][nk][2*hkv*128] f32 -> out [B][nq][hq*128] f32 (bf16-rounded).
     split: hi/lo fp16 Q.K; pv_split: hi/lo fp16 P.V too (both = the fully f32-faithful mode)."""
-    lib = load_library()
+    lib = load_selftest_library()
     q = np.ascontiguousarray(q, dtype=np.float32)
     kv = np.ascontiguousarray(kv, dtype=np.float32)
     B, nq, _ = q.shape
@@ -575,7 +602,7 @@ def kernel_attention(q: np.ndarray, kv: np.ndarray, hq: int, hkv: int, window: i
 def bench_attention(B: int, hq: int, hkv: int, nq: int, nk: int, window: int = 0, split: bool = True,
                     causal: bool = False, masked: bool = False, iters: int = 20, pv_split: bool = False) -> float:
     """Average ms per launch of the engine's attention kernel on pseudo-random operands (GPU)."""
-    lib = load_library()
+    lib = load_selftest_library()
     ms = ctypes.c_float(0.0)
     flags = (1 if split else 0) | (2 if causal else 0) | (4 if masked else 0) | (8 if pv_split else 0)
     st = lib.ace_mi_bench_attention(B, hq, hkv, nq, nk, int(window), flags, iters, ctypes.byref(ms))
@@ -586,7 +613,7 @@ def bench_attention(B: int, hq: int, hkv: int, nq: int, nk: int, window: int = 0
 
 def bench_gemm(M: int, N: int, K: int, variant: int = -1, epi: int = 0, act_type: int = 0, iters: int = 20) -> float:
     """Average ms per launch of the engine GEMM on random operands (GPU)."""
-    lib = load_library()
+    lib = load_selftest_library()
     ms = ctypes.c_float(0.0)
     st = lib.ace_mi_bench_gemm(act_type, epi, variant, M, N, K, iters, ctypes.byref(ms))
     if st != ACE_GGML_OK:
@@ -626,7 +653,7 @@ def dequantize(raw: np.ndarray, qtype: str) -> np.ndarray:
 
 def kernel_dequant(w_blocks: np.ndarray, qtype: str) -> np.ndarray:
     """Staged dequant kernel: ggml block bytes [N][nb][bb] -> bf16 words [N][K] of bf16(dequant(W))."""
-    lib = load_library()
+    lib = load_selftest_library()
     w = np.ascontiguousarray(w_blocks, dtype=np.uint8)
     N, nb = w.shape[0], w.shape[1]
     K = nb * _BLOCK[qtype][0]
@@ -641,7 +668,7 @@ def kernel_dequant(w_blocks: np.ndarray, qtype: str) -> np.ndarray:
 def kernel_gemm_q(a_bits: np.ndarray, w_blocks: np.ndarray, qtype: str, epi: int = 0, variant: int = -1,
                   bias: Optional[np.ndarray] = None) -> np.ndarray:
     """Dequant-fused GEMM: a_bits bf16 words [M][K], w_blocks ggml block bytes [N][nb][bb]."""
-    lib = load_library()
+    lib = load_selftest_library()
     a = np.ascontiguousarray(a_bits, dtype=np.uint16)
     w = np.ascontiguousarray(w_blocks, dtype=np.uint8)
     M, K = a.shape
@@ -663,7 +690,7 @@ def kernel_gemm_q(a_bits: np.ndarray, w_blocks: np.ndarray, qtype: str, epi: int
 
 
 def bench_gemm_q(M: int, N: int, K: int, qtype: str, variant: int = -1, epi: int = 0, iters: int = 20) -> float:
-    lib = load_library()
+    lib = load_selftest_library()
     ms = ctypes.c_float(0.0)
     st = lib.ace_mi_bench_gemm_q(QTYPES[qtype], epi, variant, M, N, K, iters, ctypes.byref(ms))
     if st != ACE_GGML_OK:

@@ -117,18 +117,22 @@ def euler_sample_local(bridge, cond: Conditioning, items: Sequence[int], schedul
     return xt
 
 
-def sde_noise(n_draws: int, global_batch: int, T: int, C: int, seed: Optional[int], device) -> torch.Tensor:
-    """SDE re-noise draws [n_draws][B_global][T][C] for the WHOLE batch from one generator, so every item
-    gets its own independent stream (as generate.py:187 draws one (bsz, T, C) normal per step) and a
-    rank selects its items' slices: the result does not depend on the world size.  Drawn on the CPU
-    (the same stream on every rank and backend) and moved to `device`.  seed None -> a fresh
-    nondeterministic seed (every rank must then be given an explicit seed to agree)."""
-    g = torch.Generator()
-    if seed is None:
-        g.seed()
-    else:
-        g.manual_seed(int(seed))
-    return torch.randn((n_draws, global_batch, T, C), generator=g, dtype=torch.float32).to(device)
+def sde_noise(n_draws: int, items: Sequence[int], T: int, C: int, seed: Optional[int], device) -> torch.Tensor:
+    """SDE re-noise draws [n_draws][len(items)][T][C] for this rank's `items` only: item b draws from its own
+    generator seeded from (seed, b), so every item gets an independent stream (as generate.py:187 draws one
+    (bsz, T, C) normal per step) that does not depend on the world size or on which rank owns it, and a rank
+    draws and moves nothing but its own slice.  Drawn on the CPU (the same stream on every backend) and moved
+    to `device`.  seed None -> fresh nondeterministic seeds (every rank must then be given an explicit seed to
+    agree)."""
+    out = torch.empty((n_draws, len(items), T, C), dtype=torch.float32)
+    for k, b in enumerate(items):
+        g = torch.Generator()
+        if seed is None:
+            g.seed()
+        else:
+            g.manual_seed((int(seed) * 1000003 + int(b)) % (1 << 63))
+        out[:, k] = torch.randn((n_draws, T, C), generator=g, dtype=torch.float32)
+    return out.to(device)
 
 
 def generate_local(bridge, cond: Conditioning, items: Sequence[int], schedule: Sequence[float],
@@ -152,7 +156,7 @@ def generate_local(bridge, cond: Conditioning, items: Sequence[int], schedule: S
     L = enc.shape[1]
     noise = None
     if infer_method == "sde" and len(schedule) > 1:
-        noise = sde_noise(len(schedule) - 1, cond.noise.shape[0], T, C, seed, dev).index_select(1, idx).contiguous()
+        noise = sde_noise(len(schedule) - 1, list(items), T, C, seed, dev).contiguous()
     elif infer_method not in ("ode", "sde"):
         raise ValueError(infer_method)
     _sync(xt)

@@ -10,16 +10,14 @@
 // only the key tiles inside the window, causal blocks stop at their last query.
 //
 // Numerics: the reference runs attention in F32.  The DiT runs SPLIT=false (single fp16 operands,
-// f32 accumulation, two workgroups per CU): at full width its parity equals the f32-faithful modes
-// because the bf16 activation rounding of every mul_mat dominates.  SPLIT=true (the
-// condition / text encoders' default, ACE_MI_ATTN_PRECISION=split for the DiT) keeps
-// Q and K as fp16 pairs x = hi + lo (hi = fp16(x), lo = fp16(x - hi)) and forms
+// f32 accumulation, two workgroups per CU): at full width its parity equals the f32-faithful modes,
+// also with peaked softmax rows (logits of tens), because the bf16 activation rounding of every mul_mat
+// dominates (tests/test_gpu_parity_strict.py).  SPLIT=true (ACE_MI_ATTN_PRECISION=split or
+// f32 for the DiT) keeps Q and K as fp16 pairs x = hi + lo (hi = fp16(x), lo = fp16(x - hi)) and forms
 // each score as hi*hi + hi*lo + lo*hi with three v_mfma_f32_32x32x16_f16 (f32
-// accumulate) -> ~22-bit operands: a score error moves exp() and is not
-// averaged out.  P.V runs on single fp16 operands (P rounded to nearest, V hi)
-// unless PVS (AttnArgs::pv_split, ACE_MI_ATTN_PV_SPLIT=1) asks for the same
-// three-product form there too: its errors are independent per key and
-// average over the row.  P is formed as exp2(s - m + 12) (scaled by
+// accumulate) -> ~22-bit operands.  P.V runs on single fp16 operands (P rounded to nearest, V hi)
+// unless PVS (AttnArgs::pv_split: ACE_MI_ATTN_PRECISION=f32, the condition / text encoders' default)
+// asks for the same three-product form there too.  P is formed as exp2(s - m + 12) (scaled by
 // 2^12 so its lo part stays a normal fp16; O and l carry the same factor).
 // Online softmax in f32 (exp2 domain) with a lazy running max: O and l are
 // rescaled only when a row's max grows by more than 2^RESCALE_LOG2 (P then

@@ -18,6 +18,7 @@
 // along M so co-resident tiles share weight panels in L2.
 #include <mutex>
 #include <map>
+#include <type_traits>
 #include <utility>
 
 #include "gemm_common.h"
@@ -30,8 +31,18 @@ namespace gemm_detail {
 //         a raw s_barrier, stage tile t+2 into it, compute the second half, then a COUNTED
 //         vmcnt(G) retires tile t+1 while t+2 stays in flight across the next barrier.
 // SK: split-K instance, held to 256 VGPRs (two blocks per CU where their LDS fits) with a chunked residual preload
+// (the residual-prefetch instances, XPF below, are held to 256 VGPRs too: two blocks per CU)
+template <int TBM, int TBN, int TWM, int TWN, int TEPI, int TPIPE, bool TSK>
+struct GemmTwoPerCU {
+    static constexpr bool value =
+        (TSK || ((TEPI == EPI_RESID || TEPI == EPI_RESID_GATED) && TPIPE == 1 && TWM * TWN == 4 &&
+                 (TBM / TWM / 16) * 4 * (TBN / TWN / 16) + (TEPI == EPI_RESID_GATED ? 2 * (TBN / TWN / 16) : 0) <= 63)) &&
+        (TBM + TBN) * 512 <= 160 * 1024;
+};
+
 template <int BM, int BN, int WM, int WN, bool F16, int EPI, int PIPE, bool SK = false>
-__global__ void __launch_bounds__(WM * WN * 64, SK && (BM + BN) * 512 <= 160 * 1024 ? 2 : 1) gemm_kernel(GemmParams p) {
+__global__ void __launch_bounds__(WM * WN * 64, (GemmTwoPerCU<BM, BN, WM, WN, EPI, PIPE, SK>::value ? 2 : 1))
+    gemm_kernel(GemmParams p) {
     constexpr int NW = WM * WN;
     constexpr int WTM = BM / WM;
     constexpr int WTN = BN / WN;
@@ -43,6 +54,10 @@ __global__ void __launch_bounds__(WM * WN * 64, SK && (BM + BN) * 512 <= 160 * 1
     constexpr int G_PER_WAVE = (BM + BN) / 8 / NW;
     static_assert((BM + BN) % (8 * NW) == 0, "staging split");
     static_assert(EPI != EPI_SWIGLU || (TN % 2 == 0), "swiglu needs column pairs");
+    // residual prefetch for the 4-wave pipelined tiles whose x (+ gate) loads fit one counted vmcnt
+    constexpr int NX = TM * 4 * TN + (EPI == EPI_RESID_GATED ? 2 * TN : 0);
+    constexpr bool XPF = (EPI == EPI_RESID || EPI == EPI_RESID_GATED) && PIPE == 1 && !SK && NW == 4 && NX <= 63;
+    constexpr int XW = NX;
 
     __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
 
@@ -185,7 +200,16 @@ __global__ void __launch_bounds__(WM * WN * 64, SK && (BM + BN) * 512 <= 160 * 1
         constexpr int I_EARLY = SK ? TM
                                    : (EPI == EPI_SWIGLU ||
                                       (WN == 4 && EPI != EPI_STORE_F32 && EPI != EPI_STORE_ACT)) ? TM / 2 : 0;
-        for (int kt = 0; kt < nk; ++kt) {
+        // Residual prefetch (XPF, the o / cross-o / down projections): the old x (and gate) values of the tile
+        // are requested right after the barrier of k-tile nk-2 -- no staging happens from there on, so the
+        // counted vmcnt(XW) at its end retires tile nk-1's LDS-DMA while the x loads stay in flight -- and land
+        // during the last two k-tiles' MFMAs.  The epilogue then only adds and stores: its read-modify-write of
+        // the f32 residual (96 x 128 x 4 B read + written per block, all blocks at once) no longer waits for
+        // HBM after the main loop.  The two peeled calls keep the prefetched registers out of any loop.
+        float xo[TM][4][TN];  // (dead unless XPF)
+        float g0[TN], g1[TN];
+        auto body = [&](int kt, auto pf_tag) {
+            constexpr bool PF = decltype(pf_tag)::value;
             const int cur = kt & 1;
             uint4 a[TM][2], b[TN][2];
             read_frags_asm(cur, a, b);
@@ -198,6 +222,7 @@ __global__ void __launch_bounds__(WM * WN * 64, SK && (BM + BN) * 512 <= 160 * 1
             __builtin_amdgcn_s_barrier();  // every wave has its fragments of tile kt: buffer `cur` is free
             const bool more = kt + 2 < nk;
             if (more) stage(cur, kt + 2);
+            if constexpr (PF) resid_prefetch<TM, TN, EPI>(p, m0 + wm0, n0 + wn0, lane, BM / WM, xo, g0, g1);
 #pragma unroll
             for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -207,10 +232,22 @@ __global__ void __launch_bounds__(WM * WN * 64, SK && (BM + BN) * 512 <= 160 * 1
             if (kt + 1 < nk) {
                 if (more)
                     wait_vmcnt<G_PER_WAVE>();  // tile kt+1 landed, kt+2 still in flight
+                else if constexpr (PF)
+                    wait_vmcnt<XW>();  // tile kt+1 landed, the residual prefetch still in flight
                 else
                     wait_vmcnt<0>();
                 __builtin_amdgcn_s_barrier();
             }
+        };
+        if constexpr (XPF) {
+            const int kp = nk >= 2 ? nk - 2 : 0;
+            for (int kt = 0; kt < kp; ++kt) body(kt, std::false_type{});
+            body(kp, std::true_type{});
+            if (kp + 1 < nk) body(kp + 1, std::false_type{});
+            resid_apply<TM, TN, EPI>(p, acc, m0 + wm0, n0 + wn0, lane, BM / WM, xo, g0, g1);
+            return;
+        } else {
+            for (int kt = 0; kt < nk; ++kt) body(kt, std::false_type{});
         }
     }
 
@@ -556,8 +593,8 @@ int g_forced_variant = -1;
 // o / cross 662 vs 569).
 double m_edge(int M, int bm) { return (double)M / (double)(((M + bm - 1) / bm) * bm); }
 
-// Quantized weights: the register-dequant kernel (gemm_qr_kernel, variants 20-24 [+ 100 S]); the round-1
-// LDS-dequant kernel (gemm_q_kernel, 0-7) only when forced.  Long sequences: 192-row tiles (8 waves where
+// Quantized weights: the LDS-staged dequant kernel (gemm_qr_kernel, variants 20-24 [+ 100 S]); the round-1
+// ds_write dequant kernel (gemm_q_kernel, 0-7) only when forced.  Long sequences: 192-row tiles (8 waves where
 // N % 256 == 0 leaves a full round of 256-column tiles); short ones: 128 / 64-row tiles, split over K until
 // the grid covers the 256 CUs.
 int pick_variant_q(int M, int N, int K) {
@@ -631,7 +668,7 @@ void launch_gemm(const uint16_t* A, int lda, const WeightView& W, int M, int N, 
         ACEMI_CHECK(epi.prep.q_col <= 0 && (epi.prep.k_col < 0 || epi.prep.k_col == 128 * nqc) &&
                         (epi.prep.v_col < 0 || epi.prep.v_col == 128 * (nqc + nkc)),
                     "gemm: fused attention prep expects the [q | k | v] head order");
-        v = v == 2 ? 3 : v == 5 ? 4 : v == 6 ? 1 : v == 9 ? 8 : v % 100 == 21 ? v - 1 : v;
+        v = v == 2 ? 3 : v == 5 ? 4 : v == 6 ? 1 : v == 9 ? 8 : v;
     }
     switch (W.fmt) {
         case WF_BF16:

@@ -235,6 +235,79 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
     }
 }
 
+// Residual epilogue in two halves (gemm_kernel's XPF path): resid_prefetch issues every load of the wave tile's old
+// x values (TM x 4 x TN, rows past M read as 0) and, for the gated form, the gate rows of the first and last item
+// the tile touches (2 x TN) -- exactly NX loads, issued early and consumed later by resid_apply, which adds and
+// stores with the arithmetic of gemm_epilogue (x + acc (* gate), each product / sum rounded once).  A wave tile
+// spanning more than two items (rows_per_item < wave rows) falls back to per-element gate loads in the apply.
+template <int TM, int TN, int EPI>
+__device__ __forceinline__ void resid_prefetch(const GemmParams& p, int mw, int nw, int lane, int wrows,
+                                               float (&xo)[TM][4][TN], float (&g0)[TN], float (&g1)[TN]) {
+    const GemmEpilogue& e = p.e;
+    const int ccol = lane & 15, crow = (lane >> 4) * 4;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int m = min(mw + i * 16 + crow + r, p.M - 1);  // rows past M: a valid row, never stored
+#pragma unroll
+            for (int j = 0; j < TN; ++j) xo[i][r][j] = e.c_f32[(int64_t)m * e.ldc + nw + j * 16 + ccol];
+        }
+    if constexpr (EPI == EPI_RESID_GATED) {
+        const int i0 = min(mw, p.M - 1) / e.rows_per_item, i1 = min(mw + wrows - 1, p.M - 1) / e.rows_per_item;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int n = nw + j * 16 + ccol;
+            g0[j] = e.gate[(int64_t)i0 * e.gate_stride + n];
+            g1[j] = e.gate[(int64_t)i1 * e.gate_stride + n];
+        }
+    }
+}
+
+template <int TM, int TN, int EPI>
+__device__ __forceinline__ void resid_apply(const GemmParams& p, f32x4 (&acc)[TM][TN], int mw, int nw, int lane,
+                                            int wrows, const float (&xo)[TM][4][TN], const float (&g0)[TN],
+                                            const float (&g1)[TN]) {
+    const GemmEpilogue& e = p.e;
+    const int ccol = lane & 15, crow = (lane >> 4) * 4;
+    const int i0 = min(mw, p.M - 1) / e.rows_per_item;
+    // the wave tile touches at most two items: gate rows from the prefetch (two separate arrays, so the select
+    // stays a v_cndmask -- a [2][TN] array indexed by the comparison went to scratch); otherwise (short items,
+    // tests) per-element gate loads.  The branch is uniform and outside the store loops, so the fast path
+    // issues its stores back to back (a load between stores makes hipcc wait for every store, vmcnt(0)).
+    if (EPI != EPI_RESID_GATED || e.rows_per_item >= wrows) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = mw + i * 16 + crow + r;
+                if (m >= p.M) continue;
+                const bool first = m / e.rows_per_item == i0;
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    float v = acc[i][j][r];
+                    if constexpr (EPI == EPI_RESID_GATED) v = __fmul_rn(v, first ? g0[j] : g1[j]);
+                    e.c_f32[(int64_t)m * e.ldc + nw + j * 16 + ccol] = __fadd_rn(xo[i][r][j], v);
+                }
+            }
+    } else {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = mw + i * 16 + crow + r;
+                if (m >= p.M) continue;
+                const int item = m / e.rows_per_item;
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const int n = nw + j * 16 + ccol;
+                    const float v = __fmul_rn(acc[i][j][r], e.gate[(int64_t)item * e.gate_stride + n]);
+                    e.c_f32[(int64_t)m * e.ldc + n] = __fadd_rn(xo[i][r][j], v);
+                }
+            }
+    }
+}
+
 // EPI_QKV_PREP: the block's BM x 128 f32 accumulator tile (one head of the [q | k | v] projection) goes
 // through LDS in row chunks (rows 144 floats apart: the 16x4 accumulator writes are conflict-free) and is
 // written straight into the attention operand layouts with attn_prep's arithmetic (prep_math.h): 16

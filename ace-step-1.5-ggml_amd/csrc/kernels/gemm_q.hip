@@ -316,84 +316,113 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_q_kernel(GemmParams p) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Register-dequant fused GEMM (the quantized default): NW waves side by side along N, each owning 32 columns
-// (two 16-wide MFMA column tiles) and ALL BM rows of a BM x (32 NW) output tile.  A [BM][64] k-tiles are
-// staged by LDS-DMA into a 3-slot ring of swizzled images shared by the NW waves (the dense kernel's A path);
-// W never touches LDS: each lane (column n = lane & 15, k group g = lane >> 4 of the 16x16x32 B operand) loads
-// its fragments' quantized bytes + scales straight from the resident planes two k-tiles ahead into registers
-// and forms the bf16 B fragments there with the staged dequant's arithmetic (deq_i8x4 / deq_u4x4: the same
-// f32 products, RNE to bf16).  The MFMA operands and the per-element k order therefore equal the staged
-// dequant + dense GEMM bit for bit, while the weights cross HBM / L2 at 1.0625 (Q8_0), 0.5625 (Q4_K) or
-// 1.125 (Q6_K) bytes each and no bf16 image exists.  One dequant per weight per block (the waves own
-// disjoint columns), reused by TM = BM / 16 MFMAs: ~20 VALU per 8-weight fragment against TM x 8 free issue
-// cycles per MFMA gap.  No ds_write anywhere (the LDS-DMA / ds_write hazard of DESIGN.md §10 cannot arise).
-// Pipeline per k-tile t: wait A(t) [vmcnt keeps A(t+1) and W(t+1) in flight], barrier, stage A(t+2) into the
-// slot last read at t-1, dequant W(t) -> B fragments, request W(t+2), then per kk: A fragments from LDS,
-// TM x 2 MFMAs.
-struct WFrag {  // one lane's quantized bytes of one k-tile: TN = 2 column tiles x 2 k halves
-    uint32_t q[2][2][2];  // [j][kk] 8 bytes (Q8_0 / Q6_K) or 4 bytes in q[..][0] (Q4_K)
-    float s[2][2][2];     // [j][kk] scale (Q8_0 / Q6_K: s[..][0]; Q4_K: d*sc, dmin*m)
+// Quantized-weight GEMM with both operands staged through LDS by LDS-DMA (the quantized default): the
+// BM x 64 activation k-tile (bf16, the dense kernels' swizzled image) AND the BN x 64 weight k-tile as its raw
+// ggml-format bytes + f32 scale planes (runtime/quant.h: 1.0625 B per Q8_0 weight, 0.5625 B Q4_K, 1.125 B
+// Q6_K) land in a 3-slot LDS ring; NW waves side by side along N, each owning 32 columns (two 16-wide MFMA
+// column tiles) and ALL BM rows, read their B fragments' bytes from LDS and form the bf16 fragments in
+// registers with the staged dequant's arithmetic (deq_i8x4 / deq_u4x4: one f32 product, RNE to bf16) -- so the
+// MFMA operands and the per-element k order equal the staged dequant + dense GEMM bit for bit, no bf16 image
+// exists, and each weight is expanded once per block and reused by TM = BM / 16 MFMAs.  Every LDS write is an
+// LDS-DMA (no ds_write: the DMA / ds_write hazard of DESIGN.md §10 cannot arise) and the per-wave DMA count per
+// k-tile is a compile-time constant, so one counted vmcnt per k-tile retires exactly the tile being consumed
+// while the next stays in flight (a register-held weight prefetch made hipcc drain every load, vmcnt(0), at
+// each k-tile: 0.62 of the dense kernel's rate).
+// Pipeline per k-tile t: vmcnt(G) retires A/W(t) [A/W(t+1) in flight], barrier, stage A/W(t+2) into the slot
+// last read at t-1, B bytes -> registers -> bf16 fragments, then per kk: A fragments from LDS, TM x 2 MFMAs.
+template <int WQ>
+struct QTile {  // bytes of one weight row per 64-wide k-tile (q plane, scale plane)
+    static constexpr int QB = WQ == WF_Q4_K ? 32 : 64;
+    static constexpr int SB = WQ == WF_Q8_0 ? 8 : 16;
+};
+
+template <int OFF>
+__device__ __forceinline__ uint2 ds_read_b64_off(uint32_t addr) {
+    uint2 v;
+    asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
+    return v;
+}
+template <int OFF>
+__device__ __forceinline__ uint32_t ds_read_b32_off(uint32_t addr) {
+    uint32_t v;
+    asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
+    return v;
+}
+
+// this lane's B fragment bytes (columns wn0 + j*16 + (lane & 15), k group g = lane >> 4) of the k-tile in the slot at
+// LDS byte address wq (q rows) / ws (scale rows): qd_read issues the LDS reads (the caller waits), qd_dequant forms
+// the bf16 fragments of one k half kk
+struct QRaw {
+    uint32_t q[2][2][2];  // [j][kk] 8 bytes (Q8_0 / Q6_K) or 4 bytes in [..][0] (Q4_K)
+    uint4 sc[2];          // [j] scales: Q8_0 (s_kk0, s_kk1, -, -); Q4_K (d0, m0, d1, m1); Q6_K (4 x d*sc per 16)
 };
 
 template <int WQ>
-__device__ __forceinline__ void qr_load(WFrag& f, const char* __restrict__ qrow0, const char* __restrict__ qrow1,
-                                        const float* __restrict__ srow0, const float* __restrict__ srow1, int kt,
-                                        int g) {
+__device__ __forceinline__ void qd_read(uint32_t wq, uint32_t ws, int row, int g, QRaw& r) {
+    constexpr int QB = QTile<WQ>::QB, SB = QTile<WQ>::SB;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-        const char* q = j ? qrow1 : qrow0;
-        const float* sr = j ? srow1 : srow0;
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-            const int blk = kt * 2 + kk;  // 32-value block index along the row
-            if constexpr (WQ == WF_Q4_K) {
-                f.q[j][kk][0] = *reinterpret_cast<const uint32_t*>(q + blk * 16 + g * 4);
-                const float2 dm = *reinterpret_cast<const float2*>(sr + 2 * blk);
-                f.s[j][kk][0] = dm.x;
-                f.s[j][kk][1] = dm.y;
+        const uint32_t qa = wq + (row + j * 16) * QB, sa = ws + (row + j * 16) * SB;
+        if constexpr (WQ == WF_Q4_K) {
+            r.q[j][0][0] = ds_read_b32_off<0>(qa + g * 4);
+            r.q[j][1][0] = ds_read_b32_off<16>(qa + g * 4);
+            r.sc[j] = ds_read_b128_off<0>(sa);
+        } else {
+            const uint2 q0 = ds_read_b64_off<0>(qa + g * 8), q1 = ds_read_b64_off<32>(qa + g * 8);
+            r.q[j][0][0] = q0.x;
+            r.q[j][0][1] = q0.y;
+            r.q[j][1][0] = q1.x;
+            r.q[j][1][1] = q1.y;
+            if constexpr (WQ == WF_Q8_0) {
+                const uint2 s2 = ds_read_b64_off<0>(sa);
+                r.sc[j] = make_uint4(s2.x, s2.y, 0u, 0u);
             } else {
-                const uint2 w = *reinterpret_cast<const uint2*>(q + blk * 32 + g * 8);
-                f.q[j][kk][0] = w.x;
-                f.q[j][kk][1] = w.y;
-                f.s[j][kk][0] = WQ == WF_Q8_0 ? sr[blk] : sr[2 * blk + (g >> 1)];  // Q6_K: one scale per 16
+                r.sc[j] = ds_read_b128_off<0>(sa);
             }
         }
     }
 }
 
 template <int WQ>
-__device__ __forceinline__ void qr_dequant(const WFrag& f, uint4 (&b)[2][2]) {
+__device__ __forceinline__ void qd_dequant(const QRaw& r, int g, int kk, uint4 (&b)[2][2]) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-            uint32_t o[4];
-            if constexpr (WQ == WF_Q4_K) {
-                const uint32_t w = f.q[j][kk][0];
-                const float d = f.s[j][kk][0], nm = -f.s[j][kk][1];
-                deq_u4x4(w & 0x0f0f0f0fu, d, nm, o[0], o[1]);
-                deq_u4x4((w >> 4) & 0x0f0f0f0fu, d, nm, o[2], o[3]);
-            } else {
-                const float d = f.s[j][kk][0];
-                deq_i8x4(f.q[j][kk][0], d, -128.0f * d, o[0], o[1]);
-                deq_i8x4(f.q[j][kk][1], d, -128.0f * d, o[2], o[3]);
-            }
-            b[j][kk] = make_uint4(o[0], o[1], o[2], o[3]);
+    for (int j = 0; j < 2; ++j) {
+        const float s[4] = {__uint_as_float(r.sc[j].x), __uint_as_float(r.sc[j].y), __uint_as_float(r.sc[j].z),
+                            __uint_as_float(r.sc[j].w)};
+        uint32_t o[4];
+        if constexpr (WQ == WF_Q4_K) {
+            const uint32_t w = r.q[j][kk][0];
+            const float d = s[2 * kk], nm = -s[2 * kk + 1];
+            deq_u4x4(w & 0x0f0f0f0fu, d, nm, o[0], o[1]);
+            deq_u4x4((w >> 4) & 0x0f0f0f0fu, d, nm, o[2], o[3]);
+        } else {
+            // Q8_0: one scale per 32 (block kk); Q6_K: one per 16 (k group g covers 16-half g >> 1)
+            const float d = WQ == WF_Q8_0 ? s[kk] : s[2 * kk + (g >> 1)];
+            deq_i8x4(r.q[j][kk][0], d, -128.0f * d, o[0], o[1]);
+            deq_i8x4(r.q[j][kk][1], d, -128.0f * d, o[2], o[3]);
         }
+        b[j][kk] = make_uint4(o[0], o[1], o[2], o[3]);
+    }
 }
 
-// two waves per SIMD (two 4-wave blocks or one 8-wave block per CU) where the LDS ring allows it
+// one workgroup of NW waves per CU where the ring allows two waves per SIMD
 template <int BM, int NW, int EPI, int WQ, bool SK = false>
-__global__ void __launch_bounds__(NW * 64, (NW == 8 || 2 * 3 * BM * 128 <= 160 * 1024) ? 2 : 1)
+__global__ void __launch_bounds__(NW * 64, (NW == 8 || 2 * 3 * (BM * 128 + 128 * (QTile<WQ>::QB + QTile<WQ>::SB)) <=
+                                                            160 * 1024) ? 2 : 1)
     gemm_qr_kernel(GemmParams p) {
     constexpr int BN = 32 * NW;
     constexpr int TM = BM / 16;
     constexpr int TN = 2;
     constexpr int BK = 64;
     constexpr int ROWB = BK * 2;
-    constexpr int SLOT = BM * ROWB;  // one A k-tile image
-    constexpr int G_A = BM / 8 / NW;  // 1 KiB LDS-DMA pieces per wave per k-tile
-    static_assert(BM % (8 * NW) == 0 && BM % 16 == 0, "A staging split");
+    constexpr int QB = QTile<WQ>::QB, SB = QTile<WQ>::SB;
+    constexpr int A_BYTES = BM * ROWB, WQ_BYTES = BN * QB, WS_BYTES = BN * SB;
+    constexpr int SLOT = A_BYTES + WQ_BYTES + WS_BYTES;
+    constexpr int PA = BM / 8;             // 1 KiB pieces (8 rows x 128 B)
+    constexpr int PQ = WQ_BYTES / 1024;    // 1 KiB pieces (64 lanes x 16 B)
+    constexpr int PS = WS_BYTES / 256;     // 256 B pieces (64 lanes x one f32)
+    static_assert(PA % NW == 0 && PQ % NW == 0 && PS % NW == 0, "LDS-DMA pieces must split evenly over the waves");
+    constexpr int G = (PA + PQ + PS) / NW;  // LDS-DMA instructions per wave per k-tile
     static_assert(EPI != EPI_SWIGLU || (TN % 2 == 0), "swiglu needs column pairs");
 
     __shared__ __attribute__((aligned(16))) char smem[3 * SLOT];
@@ -419,33 +448,47 @@ __global__ void __launch_bounds__(NW * 64, (NW == 8 || 2 * 3 * BM * 128 <= 160 *
     const int kt_begin = sk_part * nk_all / S;
     const int nk = (sk_part + 1) * nk_all / S - kt_begin;
 
-    // A staging sources (swizzled source chunk, as the dense kernel)
-    const uint16_t* src[G_A];
+    // LDS-DMA sources, fixed over k (+ kt * k-tile stride): A pieces (swizzled chunk as the dense kernel), W q
+    // pieces (QB / 16 lanes per row), W scale pieces (one f32 per lane, SB / 4 per row)
+    const uint16_t* srcA[PA / NW];
 #pragma unroll
-    for (int j = 0; j < G_A; ++j) {
+    for (int j = 0; j < PA / NW; ++j) {
         const int row = (wid + NW * j) * 8 + (lane >> 3);
         const int c = (lane & 7) ^ swz(row);
-        src[j] = p.A + (int64_t)min(m0 + row, M - 1) * p.lda + (int64_t)kt_begin * BK + c * 8;
+        srcA[j] = p.A + (int64_t)min(m0 + row, M - 1) * p.lda + (int64_t)kt_begin * BK + c * 8;
     }
-    auto stage = [&](int kt) {  // k-tile kt (relative) into slot kt % 3
-        char* base = smem + (kt % 3) * SLOT;
-#pragma unroll
-        for (int j = 0; j < G_A; ++j)
-            __builtin_amdgcn_global_load_lds((const void*)(src[j] + kt * BK), (lds_void*)(base + (wid + NW * j) * 1024),
-                                             16, 0, 0);
-    };
-
-    // this lane's two weight rows (column tiles j = 0, 1) and k group
-    const int g = lane >> 4;
-    const int64_t r0 = n0 + wn0 + (lane & 15), r1 = r0 + 16;
     const int qrow_bytes = WQ == WF_Q4_K ? K / 2 : K;
-    const int srow = WQ == WF_Q8_0 ? K / 32 : (WQ == WF_Q4_K ? K / 16 : K / 16);
-    const char* qb = static_cast<const char*>(p.Wq) + (int64_t)kt_begin * (WQ == WF_Q4_K ? 32 : 64);
-    const float* sb = p.Ws + (int64_t)kt_begin * (WQ == WF_Q8_0 ? 2 : 4);
-    const char* qrow0 = qb + r0 * qrow_bytes;
-    const char* qrow1 = qb + r1 * qrow_bytes;
-    const float* srow0 = sb + r0 * srow;
-    const float* srow1 = sb + r1 * srow;
+    const int srow_floats = WQ == WF_Q8_0 ? K / 32 : K / 16;
+    const char* srcQ[PQ / NW];
+#pragma unroll
+    for (int j = 0; j < PQ / NW; ++j) {
+        constexpr int LPR = QB / 16;  // lanes per row
+        const int e = (wid + NW * j) * 64 + lane;
+        srcQ[j] = static_cast<const char*>(p.Wq) + (int64_t)(n0 + e / LPR) * qrow_bytes + (int64_t)kt_begin * QB +
+                  (e % LPR) * 16;
+    }
+    const float* srcS[PS / NW];
+#pragma unroll
+    for (int j = 0; j < PS / NW; ++j) {
+        constexpr int FPR = SB / 4;  // floats per row
+        const int e = (wid + NW * j) * 64 + lane;
+        srcS[j] = p.Ws + (int64_t)(n0 + e / FPR) * srow_floats + (int64_t)kt_begin * FPR + (e % FPR);
+    }
+    auto stage = [&](int kt, int slot) {  // k-tile kt (relative) into ring slot `slot`
+        char* base = smem + slot * SLOT;
+#pragma unroll
+        for (int j = 0; j < PA / NW; ++j)
+            __builtin_amdgcn_global_load_lds((const void*)(srcA[j] + kt * BK), (lds_void*)(base + (wid + NW * j) * 1024),
+                                             16, 0, 0);
+#pragma unroll
+        for (int j = 0; j < PQ / NW; ++j)
+            __builtin_amdgcn_global_load_lds((const void*)(srcQ[j] + (int64_t)kt * QB),
+                                             (lds_void*)(base + A_BYTES + (wid + NW * j) * 1024), 16, 0, 0);
+#pragma unroll
+        for (int j = 0; j < PS / NW; ++j)
+            __builtin_amdgcn_global_load_lds((const void*)(srcS[j] + kt * (SB / 4)),
+                                             (lds_void*)(base + A_BYTES + WQ_BYTES + (wid + NW * j) * 256), 4, 0, 0);
+    };
 
     f32x4 acc[TM][TN];
 #pragma unroll
@@ -457,52 +500,64 @@ __global__ void __launch_bounds__(NW * 64, (NW == 8 || 2 * 3 * BM * 128 <= 160 *
     const int lrow = lane & 15, lchunk = lane >> 4;
     const int rsw = (lrow >> 1) & 7;
 
-    // prologue: A(0), W(0), A(1), W(1) in flight.  The two W register sets alternate by k-tile parity (a loop
-    // body per parity), so no copy of a register set with loads in flight forces an early vmcnt.
-    WFrag w0, w1;
-    stage(0);
-    qr_load<WQ>(w0, qrow0, qrow1, srow0, srow1, 0, g);
-    if (nk > 1) {
-        stage(1);
-        qr_load<WQ>(w1, qrow0, qrow1, srow0, srow1, 1, g);
+    // prologue: k-tiles 0 and 1 in flight.  The body is branch-free: past the last k-tile it re-stages the final
+    // one into the slot nobody reads again, so every iteration issues the same G DMA instructions per wave and
+    // the counted vmcnt(G) at its top always retires exactly the tile it consumes.
+    stage(0, 0);
+    stage(min(1, nk - 1), 1);
+    for (int kt = 0; kt < nk; ++kt) {
+        wait_vmcnt<G>();
+        __builtin_amdgcn_s_barrier();  // every wave's pieces of tile kt landed; slot (kt+2)%3 = (kt-1)%3 is free
+        stage(min(kt + 2, nk - 1), (kt + 2) % 3);
+        // W bytes and the kk = 0 A fragments in one LDS wait; the kk = 1 A reads are issued before the kk = 0
+        // MFMAs, and the kk = 1 dequant VALU sits between those MFMAs (no scheduling barrier in between), so the
+        // dequant of the second k half overlaps matrix work
+        const uint32_t sbase = lds0 + (kt % 3) * SLOT;
+        const uint32_t abase = sbase + lrow * ROWB;
+        QRaw raw;
+        qd_read<WQ>(sbase + A_BYTES, sbase + A_BYTES + WQ_BYTES, wn0 + lrow, lchunk, raw);
+        uint4 a0[TM][2], a1[TM][2], b[TN][2];
+        ReadRows<0, TM, 16 * ROWB>::run(abase + (((0 * 4 + lchunk) ^ rsw) * 16), a0, 0);
+        lds_wait_all();
+        qd_dequant<WQ>(raw, lchunk, 0, b);
+        ReadRows<0, TM, 16 * ROWB>::run(abase + (((1 * 4 + lchunk) ^ rsw) * 16), a1, 1);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<false>(a0[i][0], b[j][0], acc[i][j]);
+        qd_dequant<WQ>(raw, lchunk, 1, b);
+        lds_wait_all();
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<false>(a1[i][1], b[j][1], acc[i][j]);
     }
-    // VMEM instructions younger than A(kt)'s pieces that may stay in flight at the top of k-tile kt: W(kt) and
-    // A(kt+1) (W(kt+1) too, so this is conservative): >= 4 W loads per k-tile whatever the compiler merges
-    constexpr int KEEP = G_A + 4;
-    auto step = [&](int kt, WFrag& w) {
-        if (kt + 1 < nk)
-            wait_vmcnt<KEEP>();
-        else
-            wait_vmcnt<0>();
-        __builtin_amdgcn_s_barrier();  // every wave's pieces of A(kt) landed; slot (kt+2)%3 = (kt-1)%3 is free
-        if (kt + 2 < nk) stage(kt + 2);
-        uint4 b[TN][2];
-        qr_dequant<WQ>(w, b);
-        if (kt + 2 < nk) qr_load<WQ>(w, qrow0, qrow1, srow0, srow1, kt + 2, g);
-        const uint32_t sbase = lds0 + (kt % 3) * SLOT + lrow * ROWB;
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-            uint4 a[TM][2];
-            ReadRows<0, TM, 16 * ROWB>::run(sbase + (((kk * 4 + lchunk) ^ rsw) * 16), a, kk);
-            lds_wait_all();
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<false>(a[i][kk], b[j][kk], acc[i][j]);
-        }
-    };
-    for (int kt = 0; kt < nk; kt += 2) {
-        step(kt, w0);
-        if (kt + 1 < nk) step(kt + 1, w1);
-    }
+    wait_vmcnt<0>();  // the dummy stages past the end land before the epilogue reuses the ring
     __syncthreads();  // LDS reads done before the epilogue reuses the ring
 
     if constexpr (SK)
         if (!splitk_join<TM, TN, NW, 4, 3 * SLOT>(p, acc, S, sk_tile, sk_part, tid, smem, ticket0)) return;
-    if constexpr (EPI == EPI_QKV_PREP)
-        qkv_prep_tile<BM, NW, TM, TN, 3 * SLOT>(p, acc, m0, n0, 0, wn0, tid, smem);
-    else
+    if constexpr (EPI == EPI_QKV_PREP) {
+        // one head per 128 columns: waves [4 hb, 4 hb + 4) hold head (n0 >> 7) + hb
+        const int ccol = lane & 15, crow = (lane >> 4) * 4;
+#pragma unroll
+        for (int hb = 0; hb < BN / 128; ++hb)
+            qkv_prep_head<BM, NW, 3 * SLOT>(p, m0, (n0 >> 7) + hb, tid, smem, [&](float* tile, int c0, int CH) {
+                if ((wn0 >> 7) != hb) return;
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    const int rb = i * 16 - c0;
+                    if (rb < 0 || rb >= CH) continue;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+#pragma unroll
+                        for (int j = 0; j < TN; ++j)
+                            tile[(rb + crow + r) * PREP_LD + (wn0 & 127) + j * 16 + ccol] = acc[i][j][r];
+                }
+            });
+    } else {
         gemm_epilogue<TM, TN, false, EPI, (SK ? 32 : 64)>(p, acc, m0, n0 + wn0, lane);
+    }
 }
 
 template <int BM, int BN, int WM, int WN, int EPI, int WQ>
@@ -515,28 +570,23 @@ void launch_q_cfg(const GemmParams& p, hipStream_t s) {
         hipLaunchKernelGGL((gemm_q_kernel<BM, BN, WM, WN, EPI, WQ>), dim3(nbm * nbn), dim3(WM * WN * 64), 0, s, p);
 }
 
-// register-dequant kernel (gemm_qr_kernel): BM x (32 NW) tiles, split-K over S blocks per tile for the short ones
+// LDS-dequant kernel (gemm_qr_kernel): BM x (32 NW) tiles, split-K over S blocks per tile for the short ones
 template <int BM, int NW, int EPI, int WQ>
 void launch_qr_cfg(GemmParams p, int S, hipStream_t s) {
     constexpr int BN = 32 * NW;
-    if (p.N % BN != 0) throw std::runtime_error("gemm: register-dequant tile needs N % (32 * waves) == 0");
+    if (p.N % BN != 0) throw std::runtime_error("gemm: quantized tile needs N % (32 * waves) == 0");
     const int nbm = (p.M + BM - 1) / BM;
     const int nbn = p.N / BN;
-    if constexpr (EPI == EPI_QKV_PREP && NW != 4) {
-        throw std::runtime_error("gemm: the fused attention prep needs 128-wide column tiles");
-    } else {
-        if (S > 1) {
-            if constexpr (BM <= 128 && NW == 4) {
-                if (p.K / 64 < 2 * S || S > 4) throw std::runtime_error("gemm: bad split-K factor");
-                splitk_setup(p, nbm * nbn, S, (size_t)BM * BN * 4, s);
-                hipLaunchKernelGGL((gemm_qr_kernel<BM, NW, EPI, WQ, true>), dim3(nbm * nbn * S), dim3(NW * 64), 0, s,
-                                   p);
-            } else {
-                throw std::runtime_error("gemm: split-K is for the 64 / 128-row register-dequant tiles");
-            }
+    if (S > 1) {
+        if constexpr (BM <= 128 && NW == 4) {
+            if (p.K / 64 < 2 * S || S > 4) throw std::runtime_error("gemm: bad split-K factor");
+            splitk_setup(p, nbm * nbn, S, (size_t)BM * BN * 4, s);
+            hipLaunchKernelGGL((gemm_qr_kernel<BM, NW, EPI, WQ, true>), dim3(nbm * nbn * S), dim3(NW * 64), 0, s, p);
         } else {
-            hipLaunchKernelGGL((gemm_qr_kernel<BM, NW, EPI, WQ>), dim3(nbm * nbn), dim3(NW * 64), 0, s, p);
+            throw std::runtime_error("gemm: split-K is for the 64 / 128-row quantized tiles");
         }
+    } else {
+        hipLaunchKernelGGL((gemm_qr_kernel<BM, NW, EPI, WQ>), dim3(nbm * nbn), dim3(NW * 64), 0, s, p);
     }
 }
 

@@ -22,6 +22,7 @@ DitEngine::DitEngine(int device) : device_(device) {
     staged_quant_ = !(q && q[0] == '0');
     const char* h = std::getenv("ACE_MI_QUANT_STAGE_SCOPE");
     stage_per_call_ = !(h && std::strcmp(h, "layer") == 0);
+    stage_model_ = h && std::strcmp(h, "model") == 0;
     // TEST ONLY: ACE_MI_TEST_FAULT="layer,row,col,amp" adds amp to one 16 x 128 tile of the residual right after
     // that layer's o-projection GEMM (the parity negative control of tests/test_gpu_parity_strict.py)
     if (const char* f = std::getenv("ACE_MI_TEST_FAULT")) {
@@ -391,7 +392,9 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
         ensure(wring_, stage_slot_bytes_ * (stage_per_call_ ? n_layers : 1));
         // per-call scope: the images written by the first forward of a sampling call serve its later steps
         // (the weights are loop-invariant); any other forward expands them again
-        restage = !(stage_per_call_ && io.reuse_stage && stage_layers_ >= n_layers);
+        // "model" scope: the images stay valid across calls (the weights never change after load), so the
+        // reference's per-step decoder.forward hook does not re-expand them either
+        restage = !(stage_per_call_ && (io.reuse_stage || stage_model_) && stage_layers_ >= n_layers);
         stage_layers_ = stage_per_call_ ? n_layers : 0;
     }
 

@@ -128,12 +128,14 @@ class DitEngine {
     struct LayerViews {
         WeightView qkv, o, cq, co, gu, down;
     };
-    // Scope of the staged images (ACE_MI_QUANT_STAGE_SCOPE): "call" (default) keeps one slot per layer, so
+    // Scope of the staged images (ACE_MI_QUANT_STAGE_SCOPE): "model" keeps them across calls; "call" keeps one slot
+    // per layer, so
     // the dequant runs once per sampling call (step 0) instead of once per step, at the cost of a bf16
     // image of the block weights as workspace (2.8 GB for the 24-layer DiT: 1 % of HBM); "layer" = the
     // single shared slot, expanded before every layer of every forward.
     bool staged_quant_ = true;
     bool stage_per_call_ = true;
+    bool stage_model_ = false;  // ACE_MI_QUANT_STAGE_SCOPE=model: images kept across calls while the weights are loaded
     size_t stage_slot_bytes_ = 0;
     int stage_layers_ = 0;  // layers whose images wring_ holds (per-call scope)
     Buf wring_;

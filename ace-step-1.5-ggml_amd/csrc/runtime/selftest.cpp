@@ -1,9 +1,11 @@
-// Kernel self-test entries (include/acestep_mi355x.h): run one gfx950 kernel on host
-// buffers so the GPU parity tests can compare it with an fp32 reference of the same op.
+// Kernel self-test entries (include/acestep_mi355x.h, "test library"): run one gfx950 kernel on host buffers so
+// the GPU parity tests can compare it with an fp64 / fp32 reference of the same op, and the kernel
+// micro-benchmarks of tools/.  Built only into libacestep_mi355x_selftest.so (the product objects + this
+// file, Makefile target `selftest`); the product library libacestep_mi355x.so does not contain them.
 #include <cstring>
 #include <vector>
 
-#include "../../../include/acestep_mi355x.h"
+#include "../../../include/acestep_mi355x_selftest.h"
 #include "../kernels.h"
 #include "quant.h"
 
@@ -285,42 +287,9 @@ ace_ggml_status ace_mi_bench_gemm(int32_t act_type, int32_t epi, int32_t variant
     return ACE_GGML_OK;
 }
 
-// Force a GEMM kernel variant for subsequent launches (-1 = automatic).
-ace_ggml_status ace_mi_gemm_variant(int32_t variant) {
-    if (variant < -1 || variant % 100 > 24 || variant > 424) return ACE_GGML_ERR_INVALID_ARG;
-    acemi::gemm_force_variant(variant);
-    return ACE_GGML_OK;
-}
-
 }  // extern "C"
 
 extern "C" {
-
-// ggml block quantization of rows (the loader's encoders): returns bytes written, or -1.
-int64_t ace_mi_quantize(int32_t qtype, const float* src, int64_t rows, int64_t cols, uint8_t* dst, size_t dst_size) {
-    using namespace acemi;
-    const auto t = static_cast<quant::QType>(qtype);
-    if (!src || !dst || rows <= 0 || (t != quant::Q8_0 && t != quant::Q4_K && t != quant::Q6_K)) return -1;
-    if (!quant::applies(t, cols)) return -1;
-    const size_t need = (size_t)rows * quant::row_bytes(t, cols);
-    if (dst_size < need) return -1;
-    try {
-        quant::quantize_rows(t, src, rows, cols, dst);
-    } catch (const std::exception&) {
-        return -1;
-    }
-    return (int64_t)need;
-}
-
-ace_ggml_status ace_mi_dequantize(int32_t qtype, const uint8_t* src, int64_t rows, int64_t cols, float* dst) {
-    using namespace acemi;
-    const auto t = static_cast<quant::QType>(qtype);
-    if (!src || !dst || rows <= 0 || (t != quant::Q8_0 && t != quant::Q4_K && t != quant::Q6_K) ||
-        !quant::applies(t, cols))
-        return ACE_GGML_ERR_INVALID_ARG;
-    quant::dequantize_rows(t, src, rows, cols, dst);
-    return ACE_GGML_OK;
-}
 
 // Staged dequant kernel on ggml block rows W [N][K]: out = bf16 bits of bf16(dequant(W)) [N][K].
 ace_ggml_status ace_mi_kernel_dequant(int32_t qtype, int32_t N, int32_t K, const uint8_t* W_blocks, uint16_t* out) {

@@ -98,35 +98,9 @@ ACE_GGML_API ace_ggml_status ace_mi_probe_gemm(ace_ggml_context* ctx, int32_t wh
 /* Synchronise the context stream. */
 ACE_GGML_API ace_ggml_status ace_mi_synchronize(ace_ggml_context* ctx);
 
-/* ---- kernel self-test entries (blocking, host buffers; used by the -m gpu parity tests) ----
- * GEMM: C = A[M][K] . W[N][K]^T with A, W raw 16-bit words of act_type (0 bf16, 1 fp16).
- * epi 0: out_f32[M][N] = C (+ bias[N] if bias != NULL);
- * epi 4: SwiGLU on 16-column interleaved gate|up weights, out_u16[M][N/2] raw act words;
- * epi 3 / 2: residual update in place, out_f32[M][N] holds x on entry: x += C (epi 3) or
- * x += C * gate[N] (epi 2, the gate passed in `bias`). */
-ACE_GGML_API ace_ggml_status ace_mi_kernel_gemm(int32_t act_type, int32_t epi, int32_t M, int32_t N, int32_t K,
-                                                const uint16_t* A, const uint16_t* W, const float* bias,
-                                                float* out_f32, uint16_t* out_u16);
-/* Attention core only (no norm/RoPE): q [B][nq][Hq*128] f32, kv [B][nk][2*Hkv*128] f32 (K then V),
- * kmask [B][nk] int32 or NULL, window > 0 = sliding |q-k| <= window; `split` is a flag word: bit 0 =
- * hi/lo fp16 operands (default engine mode; clear = single fp16), bit 1 = causal (key k > query q
- * masked); out [B][nq][Hq*128] f32 (the kernel's bf16 output widened). */
-ACE_GGML_API ace_ggml_status ace_mi_kernel_attention(int32_t B, int32_t Hq, int32_t Hkv, int32_t nq, int32_t nk,
-                                                     int32_t window, float scale, int32_t split, const float* q,
-                                                     const float* kv, const int32_t* kmask, float* out);
-
-/* Attention micro-benchmark on pseudo-random device operands (fixed seed): average ms per launch (HIP
- * events) of the engine's attention kernel; flags bit 0 = hi/lo operands, bit 1 = causal, bit 2 = a
- * key-padding mask (every 7th key masked). */
-ACE_GGML_API ace_ggml_status ace_mi_bench_attention(int32_t B, int32_t Hq, int32_t Hkv, int32_t nq, int32_t nk,
-                                                    int32_t window, int32_t flags, int32_t iters, float* avg_ms);
-
-/* GEMM micro-benchmark on random device operands: average ms per launch (HIP events) of the
- * engine's GEMM for act_type (0 bf16, 1 fp16), epilogue `epi` (0 f32 store, 2 gated residual,
- * 4 SwiGLU), kernel `variant` (-1 automatic, 0..9 forced: 128x128 two pipelines, 256x256, 256x128, 192x128, 192x256, 192x64, 96x128, 64x128, 64x64). */
-ACE_GGML_API ace_ggml_status ace_mi_bench_gemm(int32_t act_type, int32_t epi, int32_t variant, int32_t M, int32_t N,
-                                               int32_t K, int32_t iters, float* avg_ms);
-/* Force the GEMM kernel variant of all later launches in this process (-1 = automatic). */
+/* Force the GEMM kernel variant of all later launches in this process (-1 = automatic; dense 0..11, quantized
+ * 20..24, + 100 S for split-K over S blocks per tile; A/B measurements).  The kernel self-test and
+ * micro-benchmark entries live in the separate test library (include/acestep_mi355x_selftest.h). */
 ACE_GGML_API ace_ggml_status ace_mi_gemm_variant(int32_t variant);
 
 /* VAE decode on device pointers, stream-ordered: latents [n_frames][latent_channels] f32 ->
@@ -147,19 +121,6 @@ ACE_GGML_API int64_t ace_mi_quantize(int32_t qtype, const float* src, int64_t ro
 /* ggml dequantize_row_* of block rows to f32. */
 ACE_GGML_API ace_ggml_status ace_mi_dequantize(int32_t qtype, const uint8_t* src, int64_t rows, int64_t cols,
                                                float* dst);
-/* Dequant-fused GEMM on ggml block rows W [N][K]: out = A . bf16(dequant(W))^T (+ bias), A bf16 [M][K];
- * epi 0 (f32 store) or 4 (SwiGLU, bf16 out [M][N/2]); variant -1 automatic, 0..7 forced (6 dense only; 8..11 are dense-only tiles). */
-ACE_GGML_API ace_ggml_status ace_mi_kernel_gemm_q(int32_t qtype, int32_t epi, int32_t variant, int32_t M, int32_t N,
-                                                  int32_t K, const uint16_t* A, const uint8_t* W_blocks,
-                                                  const float* bias, float* out_f32, uint16_t* out_u16);
-/* Staged dequant kernel (the bf16 weight image the DiT's staged-dequant ring multiplies): out = bf16 bits of
- * bf16(dequant(W)) [N][K] for ggml block rows W [N][K]. */
-ACE_GGML_API ace_ggml_status ace_mi_kernel_dequant(int32_t qtype, int32_t N, int32_t K, const uint8_t* W_blocks,
-                                                   uint16_t* out);
-/* Dequant-fused GEMM micro-benchmark: average ms per launch (HIP events). */
-ACE_GGML_API ace_ggml_status ace_mi_bench_gemm_q(int32_t qtype, int32_t epi, int32_t variant, int32_t M, int32_t N,
-                                                 int32_t K, int32_t iters, float* avg_ms);
-
 /* ---- condition encoders: the conditioning half of
  * ace_generate_audio_style_lyric_timbre_impl (acestep_ggml.cpp:2324-2556) on the GPU.  Host buffers,
  * blocking, like the reference's internal functions they expose. ---- */

@@ -13,21 +13,30 @@ from acestep_mi355x import LIB_PATH
 from acestep_mi355x import capi
 
 
-def header_symbols():
+def header_symbols(headers=("acestep_ggml.h", "acestep_mi355x.h")):
     syms = set()
-    for h in ("acestep_ggml.h", "acestep_mi355x.h"):
+    for h in headers:
         text = open(os.path.join(ROOT, "include", h), encoding="utf-8").read()
         syms |= set(re.findall(r"ACE_GGML_API\s+[\w\s\*]*?\b(ace_\w+)\s*\(", text))
     return syms
 
 
 def test_library_exists_and_exports_header_symbols():
+    """The product library exports exactly the public headers' symbols and none of the kernel self-tests; the
+    test library (product objects + self-tests) exports both."""
     assert os.path.exists(LIB_PATH), "build the library first (__graft_entry__.build())"
     lib = ctypes.CDLL(LIB_PATH)
     declared = header_symbols()
     assert declared == set(capi.EXPORTED_SYMBOLS)
     for s in declared:
         assert hasattr(lib, s), s
+    tests_only = header_symbols(("acestep_mi355x_selftest.h",))
+    assert tests_only == set(capi.SELFTEST_SYMBOLS) and not (tests_only & declared)
+    for s in tests_only:
+        assert not hasattr(lib, s), f"{s}: self-test entry in the product library"
+    st = capi.load_selftest_library()
+    for s in declared | tests_only:
+        assert hasattr(st, s), s
 
 
 def test_reference_abi_signatures_present():

@@ -47,7 +47,8 @@ def check(got, ref, floor, tag, floor_max=None):
                  f" maxabs_bound={MAXABS_K * floor_max:.3e}")
     print(f"{tag}: rel_l2={l2:.3e} floor={floor:.3e} ratio={l2 / max(floor, 1e-12):.2f} cos={cos:.7f} "
           f"rel_max={mx:.3e} bound={bound:.3e}{extra}")
-    assert np.isfinite(l2) and l2 <= bound and cos >= COS_MIN, (tag, l2, floor, cos)
+    # cosine: 1 - cos ~ rel_l2^2 / 2, so it is held to the same bound (with 2x slack), never looser than 1e-5
+    assert np.isfinite(l2) and l2 <= bound and 1.0 - cos <= max(1.0 - COS_MIN, bound * bound), (tag, l2, floor, cos)
     if floor_max is not None:
         assert ma <= MAXABS_K * floor_max, (tag, ma, floor_max)
     return l2

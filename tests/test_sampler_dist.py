@@ -166,10 +166,12 @@ def test_sharded_flow_equals_single_process(tiny_ckpt, tiny_vae, world, B, metho
 
 
 def test_sde_noise_is_independent_per_item():
-    """Whole-batch SDE draws: items differ from each other, and a rank's slice equals the single-process slice."""
+    """Per-item SDE draws: items differ from each other, and a rank's slice (only its own items drawn) equals the
+    single-process slice of the same items."""
     from acestep_mi355x.sampler import sde_noise
-    a = sde_noise(3, 4, 5, 2, 7, "cpu")
-    b = sde_noise(3, 4, 5, 2, 7, "cpu")
+    a = sde_noise(3, [0, 1, 2, 3], 5, 2, 7, "cpu")
+    b = sde_noise(3, [0, 1, 2, 3], 5, 2, 7, "cpu")
     torch.testing.assert_close(a, b)
     assert not torch.allclose(a[:, 0], a[:, 1])
-    assert not torch.allclose(sde_noise(3, 4, 5, 2, None, "cpu"), sde_noise(3, 4, 5, 2, None, "cpu"))
+    torch.testing.assert_close(sde_noise(3, [1, 3], 5, 2, 7, "cpu"), a[:, [1, 3]])
+    assert not torch.allclose(sde_noise(3, [0, 1], 5, 2, None, "cpu"), sde_noise(3, [0, 1], 5, 2, None, "cpu"))

@@ -20,11 +20,13 @@ e = rng.standard_normal((1, L, 2048)).astype(np.float32)
 dev = torch.device("cuda:0")
 x0, dc, de = (torch.from_numpy(a).to(dev) for a in (h, c, e))
 d = cached_checkpoint(make_config(num_hidden_layers=2), seed=0, backend="torch")
-for qt in ("", "q8_0"):
+for qt, staged in (("", "1"), ("q8_0", "1"), ("q8_0", "0")):
+    os.environ["ACE_MI_QUANT_STAGED"] = staged
     if qt:
         os.environ["ACE_GGML_DIT_WEIGHT_QTYPE"] = qt
     else:
         os.environ.pop("ACE_GGML_DIT_WEIGHT_QTYPE", None)
+    qt = qt + ("" if staged == "1" else "-fused")
     br = GGMLCAPIBridge()
     br.load_dit(d)
 
@@ -53,8 +55,14 @@ for qt in ("", "q8_0"):
     print(qt or "bf16", "1-step loop == forward + euler:", bool(torch.equal(a1, ref1)),
           "max|d|", float((a1 - ref1).abs().max()), flush=True)
     a3 = loop([1.0, 0.9])
+    print(qt or "bf16", "2-step loop twice identical:", bool(torch.equal(a3, loop([1.0, 0.9]))), flush=True)
     x = x0 - v1 * float(np.float32(1.0) - np.float32(0.9))
+    # the torch Euler update against IEEE f32 mul-then-sub on the host
+    xh = (x0.cpu().numpy() - (v1.cpu().numpy() * np.float32(np.float32(1.0) - np.float32(0.9))).astype(np.float32))
+    print(qt or "bf16", "torch euler == host f32 euler:", bool(np.array_equal(xh, x.cpu().numpy())), flush=True)
     va = fwd(x, np.float32(0.9))
+    print(qt or "bf16", "forward of the step-1 input twice identical:", bool(torch.equal(va, fwd(x, np.float32(0.9)))),
+          flush=True)
     ref3 = x - va * float(np.float32(0.9))
     print(qt or "bf16", "2-step loop == per-step:", bool(torch.equal(a3, ref3)), "max|d|", float((a3 - ref3).abs().max()),
           flush=True)
