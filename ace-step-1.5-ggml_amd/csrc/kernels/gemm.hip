@@ -35,9 +35,9 @@ namespace gemm_detail {
 template <int TBM, int TBN, int TWM, int TWN, int TEPI, int TPIPE, bool TSK>
 struct GemmTwoPerCU {
     static constexpr bool value =
-        (TSK || ((TEPI == EPI_RESID || TEPI == EPI_RESID_GATED) && TPIPE == 1 && TWM * TWN == 4 &&
+        (TSK || ((TEPI == EPI_RESID || TEPI == EPI_RESID_GATED) && TPIPE >= 1 && TWM * TWN == 4 &&
                  (TBM / TWM / 16) * 4 * (TBN / TWN / 16) + (TEPI == EPI_RESID_GATED ? 2 * (TBN / TWN / 16) : 0) <= 63)) &&
-        (TBM + TBN) * 512 <= 160 * 1024;
+        (TBM + TBN) * 256 * (TPIPE >= 3 ? TPIPE : 2) <= 160 * 1024;
 };
 
 template <int BM, int BN, int WM, int WN, bool F16, int EPI, int PIPE, bool SK = false>
@@ -56,10 +56,13 @@ __global__ void __launch_bounds__(WM * WN * 64, (GemmTwoPerCU<BM, BN, WM, WN, EP
     static_assert(EPI != EPI_SWIGLU || (TN % 2 == 0), "swiglu needs column pairs");
     // residual prefetch for the 4-wave pipelined tiles whose x (+ gate) loads fit one counted vmcnt
     constexpr int NX = TM * 4 * TN + (EPI == EPI_RESID_GATED ? 2 * TN : 0);
-    constexpr bool XPF = (EPI == EPI_RESID || EPI == EPI_RESID_GATED) && PIPE == 1 && !SK && NW == 4 && NX <= 63;
+    constexpr bool XPF = (EPI == EPI_RESID || EPI == EPI_RESID_GATED) && PIPE >= 1 && !SK && NW == 4 && NX <= 63;
     constexpr int XW = NX;
 
-    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+    // LDS stages: PIPE 0 / 1 double-buffer; PIPE 3 / 4 keep 3 / 4 k-tiles in the ring (short-sequence tiles, whose
+    // few MFMAs per k-tile cannot cover an L2 / Infinity Cache round trip with one tile in flight)
+    constexpr int NS = PIPE >= 3 ? PIPE : 2;
+    __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -125,6 +128,17 @@ __global__ void __launch_bounds__(WM * WN * 64, (GemmTwoPerCU<BM, BN, WM, WN, EP
     const int nk = kt_end - kt_begin;
     const int lrow = lane & 15;
     const int lchunk = lane >> 4;
+    // wait until at most `younger` k-tiles' LDS-DMA (G_PER_WAVE instructions each) of this wave are in flight
+    auto wait_retire = [&](int younger) {
+        if (NS >= 4 && younger >= 3)
+            wait_vmcnt<(NS >= 4 ? 3 : 0) * G_PER_WAVE>();
+        else if (NS >= 3 && younger >= 2)
+            wait_vmcnt<(NS >= 3 ? 2 : 0) * G_PER_WAVE>();
+        else if (younger >= 1)
+            wait_vmcnt<G_PER_WAVE>();
+        else
+            wait_vmcnt<0>();
+    };
 
     auto read_frags = [&](int buf, uint4 (&a)[TM][2], uint4 (&b)[TN][2]) {
         const char* As = smem + buf * STAGE;
@@ -180,13 +194,11 @@ __global__ void __launch_bounds__(WM * WN * 64, (GemmTwoPerCU<BM, BN, WM, WN, EP
             __syncthreads();
         }
     } else {
-        stage(0, 0);
-        if (nk > 1) {
-            stage(1, 1);
-            wait_vmcnt<G_PER_WAVE>();
-        } else {
-            wait_vmcnt<0>();
-        }
+        // prologue: k-tiles 0 .. NS-1 requested, tile 0 retired
+#pragma unroll
+        for (int t = 0; t < NS; ++t)
+            if (t < nk) stage(t, t);
+        wait_retire(min(nk, NS) - 1);
         __builtin_amdgcn_s_barrier();
         // MFMAs issued before the buffer-release barrier: the first half of the tile for the SwiGLU
         // (gate|up) instances, none elsewhere (240 s step, tools/ab_multi.sh: qkv with the fused prep 66.5
@@ -210,7 +222,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (GemmTwoPerCU<BM, BN, WM, WN, EP
         float g0[TN], g1[TN];
         auto body = [&](int kt, auto pf_tag) {
             constexpr bool PF = decltype(pf_tag)::value;
-            const int cur = kt & 1;
+            const int cur = kt % NS;
             uint4 a[TM][2], b[TN][2];
             read_frags_asm(cur, a, b);
 #pragma unroll
@@ -220,8 +232,8 @@ __global__ void __launch_bounds__(WM * WN * 64, (GemmTwoPerCU<BM, BN, WM, WN, EP
 #pragma unroll
                     for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<F16>(a[i][kk], b[j][kk], acc[i][j]);
             __builtin_amdgcn_s_barrier();  // every wave has its fragments of tile kt: buffer `cur` is free
-            const bool more = kt + 2 < nk;
-            if (more) stage(cur, kt + 2);
+            const bool more = kt + NS < nk;
+            if (more) stage(cur, kt + NS);
             if constexpr (PF) resid_prefetch<TM, TN, EPI>(p, m0 + wm0, n0 + wn0, lane, BM / WM, xo, g0, g1);
 #pragma unroll
             for (int kk = 0; kk < 2; ++kk)
@@ -230,17 +242,15 @@ __global__ void __launch_bounds__(WM * WN * 64, (GemmTwoPerCU<BM, BN, WM, WN, EP
 #pragma unroll
                     for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<F16>(a[i][kk], b[j][kk], acc[i][j]);
             if (kt + 1 < nk) {
-                if (more)
-                    wait_vmcnt<G_PER_WAVE>();  // tile kt+1 landed, kt+2 still in flight
-                else if constexpr (PF)
-                    wait_vmcnt<XW>();  // tile kt+1 landed, the residual prefetch still in flight
+                if constexpr (PF)
+                    wait_vmcnt<XW>();  // tile kt+1 (the last) landed, the residual prefetch still in flight
                 else
-                    wait_vmcnt<0>();
+                    wait_retire(min(kt + NS, nk - 1) - (kt + 1));  // tile kt+1 landed, the younger ones in flight
                 __builtin_amdgcn_s_barrier();
             }
         };
         if constexpr (XPF) {
-            const int kp = nk >= 2 ? nk - 2 : 0;
+            const int kp = nk >= 2 ? nk - 2 : 0;  // no staging from here on (kp + NS >= nk)
             for (int kt = 0; kt < kp; ++kt) body(kt, std::false_type{});
             body(kp, std::true_type{});
             if (kp + 1 < nk) body(kp + 1, std::false_type{});
@@ -252,11 +262,11 @@ __global__ void __launch_bounds__(WM * WN * 64, (GemmTwoPerCU<BM, BN, WM, WN, EP
     }
 
     if constexpr (SK)
-        if (!splitk_join<TM, TN, NW, SplitKMax<BM, BN>::value, 2 * STAGE>(p, acc, S, sk_tile, sk_part, tid, smem,
+        if (!splitk_join<TM, TN, NW, SplitKMax<BM, BN>::value, NS * STAGE>(p, acc, S, sk_tile, sk_part, tid, smem,
                                                                                 ticket0))
             return;
     if constexpr (EPI == EPI_QKV_PREP)
-        qkv_prep_tile<BM, NW, TM, TN, 2 * STAGE>(p, acc, m0, n0, wm0, wn0, tid, smem);
+        qkv_prep_tile<BM, NW, TM, TN, NS * STAGE>(p, acc, m0, n0, wm0, wn0, tid, smem);
     else
         // residual preload chunk: whole tile for the 4-wave tiles; the 8-wave (2x4) tiles keep the round-1
         // one-row-group chunks (a whole-tile preload spilled 796 B per lane in the 256x256 gated residual)
@@ -514,7 +524,7 @@ void launch_cfg(GemmParams p, int S, hipStream_t s) {
     const dim3 block(WM * WN * 64);
     if constexpr (EPI == EPI_QKV_PREP && BN != 128) {
         throw std::runtime_error("gemm: the fused attention prep needs 128-wide column tiles");
-    } else if constexpr (WM * WN == 4 && PIPE == 1) {  // split-K instances: the 4-wave pipelined tiles
+    } else if constexpr (WM * WN == 4 && PIPE >= 1) {  // split-K instances: the 4-wave pipelined tiles
         if (S > 1)
             hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, F16, EPI, PIPE, true>), grid, block, 0, s, p);
         else
@@ -554,6 +564,8 @@ void launch_variant(int variant, const GemmParams& p, hipStream_t s) {
         case 9: launch_cfg<64, 64, 2, 2, F16, EPI, 1>(p, S, s); break;
         case 10: launch_cfg8<256, F16, EPI>(p, s); break;
         case 11: launch_cfg8<192, F16, EPI>(p, s); break;
+        case 12: launch_cfg<64, 64, 2, 2, F16, EPI, 4>(p, S, s); break;
+        case 13: launch_cfg<64, 128, 2, 2, F16, EPI, 3>(p, S, s); break;
         default: throw std::runtime_error("gemm: bad variant");
     }
 }
@@ -614,11 +626,12 @@ int pick_variant_q(int M, int N, int K) {
 int pick_variant(int M, int N, int K, bool quant) {
     if (g_forced_variant >= 0) {  // forced (tests / micro-benchmarks), where that tile supports the shape
         const int f = g_forced_variant % 100, S = g_forced_variant / 100;
-        const bool wide = f == 2 || f == 5 || f == 10 || f == 11 || f == 21;
+        const bool wide = f == 2 || f == 5 || f == 10 || f == 11 || f == 21;  // (12, 13: 64-row multi-stage tiles)
         const bool qr = f >= 20 && f <= 24;
         const bool dense_only = (f == 6 || (f >= 8 && f < 20) || S > 1) && !qr;
         const bool sk_ok = S <= 1 || (qr ? (f == 22 || f == 23) && S <= 4 && K / 64 >= 2 * S
-                                         : ((f == 1 || f == 3 || f == 4 ? S <= 2 : (f >= 6 && f <= 9 && S <= 4)) &&
+                                         : ((f == 1 || f == 3 || f == 4 ? S <= 2
+                                                                       : (((f >= 6 && f <= 9) || f == 12 || f == 13) && S <= 4)) &&
                                             K / 64 >= 2 * S));
         if (!(wide && N % 256 != 0) && !(quant && dense_only) && !(!quant && qr) && sk_ok) return g_forced_variant;
     }

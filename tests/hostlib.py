@@ -9,12 +9,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "ace-step-1.5-ggml_amd", "csrc")
 CLANG = "/opt/rocm/llvm/bin/clang++"
 RUNTIME = ("json.cpp", "gguf.cpp", "quant.cpp", "model.cpp", "blocks.cpp", "engine.cpp", "text_encoder.cpp", "vae.cpp",
-           "abi.cpp", "cond.cpp", "text.cpp", "generate.cpp", "selftest.cpp")
+           "abi.cpp", "cond.cpp", "text.cpp", "generate.cpp", "util_abi.cpp", "selftest.cpp")
 
 
 def build_host_lib() -> str:
     srcs = [os.path.join(CSRC, "runtime", f) for f in RUNTIME] + [os.path.join(ROOT, "tests", "host", "kernel_emul.cpp")]
-    h = hashlib.sha1()
+    h = hashlib.sha1(" ".join(RUNTIME).encode())
     for d in (os.path.join(CSRC, "runtime"), CSRC, os.path.join(ROOT, "include"), os.path.join(ROOT, "tests", "host")):
         for f in sorted(os.listdir(d)):
             if f.endswith((".cpp", ".h")):
