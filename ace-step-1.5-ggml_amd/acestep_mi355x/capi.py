@@ -666,8 +666,9 @@ def kernel_dequant(w_blocks: np.ndarray, qtype: str) -> np.ndarray:
 
 
 def kernel_gemm_q(a_bits: np.ndarray, w_blocks: np.ndarray, qtype: str, epi: int = 0, variant: int = -1,
-                  bias: Optional[np.ndarray] = None) -> np.ndarray:
-    """Dequant-fused GEMM: a_bits bf16 words [M][K], w_blocks ggml block bytes [N][nb][bb]."""
+                  bias: Optional[np.ndarray] = None, x: Optional[np.ndarray] = None) -> np.ndarray:
+    """Dequant-fused GEMM: a_bits bf16 words [M][K], w_blocks ggml block bytes [N][nb][bb].  epi 2 / 3: returns
+    x + acc (* bias as the per-column gate for 2)."""
     lib = load_selftest_library()
     a = np.ascontiguousarray(a_bits, dtype=np.uint16)
     w = np.ascontiguousarray(w_blocks, dtype=np.uint8)
@@ -676,8 +677,8 @@ def kernel_gemm_q(a_bits: np.ndarray, w_blocks: np.ndarray, qtype: str, epi: int
     u16p = ctypes.POINTER(ctypes.c_uint16)
     u8p = ctypes.POINTER(ctypes.c_uint8)
     b = None if bias is None else np.ascontiguousarray(bias, dtype=np.float32)
-    if epi == 0:
-        out = np.empty((M, N), dtype=np.float32)
+    if epi in (0, 2, 3):
+        out = np.ascontiguousarray(x, dtype=np.float32).copy() if epi in (2, 3) else np.empty((M, N), np.float32)
         st = lib.ace_mi_kernel_gemm_q(QTYPES[qtype], epi, variant, M, N, K, a.ctypes.data_as(u16p),
                                       w.ctypes.data_as(u8p), _fptr(b), _fptr(out), None)
     else:

@@ -182,8 +182,8 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
                     for (int j = 0; j < TN; ++j) {
                         const int n = nw + j * 16 + ccol;
                         float v = acc[i0 + ii][j][r];
-                        if constexpr (EPI == EPI_RESID_GATED) v = __fmul_rn(v, gt[ii][r][j]);
-                        e.c_f32[(int64_t)m * e.ldc + n] = __fadd_rn(xo[ii][r][j], v);
+                        if constexpr (EPI == EPI_RESID_GATED) v = rn_mul(v, gt[ii][r][j]);
+                        e.c_f32[(int64_t)m * e.ldc + n] = rn_add(xo[ii][r][j], v);
                     }
                 }
             }
@@ -226,7 +226,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
                         const int c = n - kpos * e.out_ch;
                         const int t = pp * e.patch + kpos;
                         if (t < e.out_T) {
-                            e.c_f32[((int64_t)item * e.out_T + t) * e.out_ch + c] = __fadd_rn(v, e.bias[c]);
+                            e.c_f32[((int64_t)item * e.out_T + t) * e.out_ch + c] = rn_add(v, e.bias[c]);
                         }
                     }
                 }
@@ -286,8 +286,8 @@ __device__ __forceinline__ void resid_apply(const GemmParams& p, f32x4 (&acc)[TM
 #pragma unroll
                 for (int j = 0; j < TN; ++j) {
                     float v = acc[i][j][r];
-                    if constexpr (EPI == EPI_RESID_GATED) v = __fmul_rn(v, first ? g0[j] : g1[j]);
-                    e.c_f32[(int64_t)m * e.ldc + nw + j * 16 + ccol] = __fadd_rn(xo[i][r][j], v);
+                    if constexpr (EPI == EPI_RESID_GATED) v = rn_mul(v, first ? g0[j] : g1[j]);
+                    e.c_f32[(int64_t)m * e.ldc + nw + j * 16 + ccol] = rn_add(xo[i][r][j], v);
                 }
             }
     } else {
@@ -301,8 +301,8 @@ __device__ __forceinline__ void resid_apply(const GemmParams& p, f32x4 (&acc)[TM
 #pragma unroll
                 for (int j = 0; j < TN; ++j) {
                     const int n = nw + j * 16 + ccol;
-                    const float v = __fmul_rn(acc[i][j][r], e.gate[(int64_t)item * e.gate_stride + n]);
-                    e.c_f32[(int64_t)m * e.ldc + n] = __fadd_rn(xo[i][r][j], v);
+                    const float v = rn_mul(acc[i][j][r], e.gate[(int64_t)item * e.gate_stride + n]);
+                    e.c_f32[(int64_t)m * e.ldc + n] = rn_add(xo[i][r][j], v);
                 }
             }
     }

@@ -329,8 +329,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_q_kernel(GemmParams p) {
 // while the next stays in flight (a register-held weight prefetch made hipcc drain every load, vmcnt(0), at
 // each k-tile: 0.62 of the dense kernel's rate).
 // Pipeline per k-tile t: vmcnt(G) retires A/W(t) [A/W(t+1) in flight], barrier, stage A/W(t+2) into the slot
-// last read at t-1, W bytes + kk = 0 A fragments of t from LDS under the kk = 1 MFMAs of t-1, bf16 fragments,
-// kk = 1 A reads under the kk = 0 MFMAs of t (the MFMA order per accumulator stays k order).
+// last read at t-1, B bytes -> registers -> bf16 fragments, then per kk: A fragments from LDS, TM x 2 MFMAs.
 template <int WQ>
 struct QTile {  // bytes of one weight row per 64-wide k-tile (q plane, scale plane)
     static constexpr int QB = WQ == WF_Q4_K ? 32 : 64;
@@ -406,10 +405,10 @@ __device__ __forceinline__ void qd_dequant(const QRaw& r, int g, int kk, uint4 (
     }
 }
 
-// one workgroup of NW waves per CU where the ring allows two waves per SIMD
+// two workgroups per CU where the ring allows it (not for split-K: its join needs the registers)
 template <int BM, int NW, int EPI, int WQ, bool SK = false>
-__global__ void __launch_bounds__(NW * 64, (NW == 8 || 2 * 3 * (BM * 128 + 128 * (QTile<WQ>::QB + QTile<WQ>::SB)) <=
-                                                            160 * 1024) ? 2 : 1)
+__global__ void __launch_bounds__(NW * 64, (!SK && (NW == 8 || 2 * 3 * (BM * 128 + 128 * (QTile<WQ>::QB + QTile<WQ>::SB)) <=
+                                                                     160 * 1024)) ? 2 : 1)
     gemm_qr_kernel(GemmParams p) {
     constexpr int BN = 32 * NW;
     constexpr int TM = BM / 16;
@@ -506,46 +505,33 @@ __global__ void __launch_bounds__(NW * 64, (NW == 8 || 2 * 3 * (BM * 128 + 128 *
     // the counted vmcnt(G) at its top always retires exactly the tile it consumes.
     stage(0, 0);
     stage(min(1, nk - 1), 1);
-    // Skewed by half a k-tile: the kk = 1 MFMAs of tile kt-1 (operands a[.][1], b[.][1] kept in registers) run
-    // right after the barrier of tile kt, under the latency of tile kt's W / A reads, and the dequant VALU of
-    // tile kt is interleaved with them and with tile kt's kk = 0 MFMAs -- the barrier / LDS / dequant phase is
-    // no longer exposed once per k-tile (with one workgroup per CU both waves of a SIMD reach it together).
-    uint4 a[TM][2], b[TN][2];
     for (int kt = 0; kt < nk; ++kt) {
         wait_vmcnt<G>();
         __builtin_amdgcn_s_barrier();  // every wave's pieces of tile kt landed; slot (kt+2)%3 = (kt-1)%3 is free
         stage(min(kt + 2, nk - 1), (kt + 2) % 3);
+        // W bytes and the kk = 0 A fragments in one LDS wait; the kk = 1 A reads are issued before the kk = 0
+        // MFMAs, and the kk = 1 dequant VALU sits between those MFMAs (no scheduling barrier in between), so the
+        // dequant of the second k half overlaps matrix work
         const uint32_t sbase = lds0 + (kt % 3) * SLOT;
         const uint32_t abase = sbase + lrow * ROWB;
         QRaw raw;
         qd_read<WQ>(sbase + A_BYTES, sbase + A_BYTES + WQ_BYTES, wn0 + lrow, lchunk, raw);
-        ReadRows<0, TM, 16 * ROWB>::run(abase + (((0 * 4 + lchunk) ^ rsw) * 16), a, 0);
-        if (kt > 0) {
-#pragma unroll
-            for (int i = 0; i < TM / 2; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<false>(a[i][1], b[j][1], acc[i][j]);
-        }
+        uint4 a0[TM][2], a1[TM][2], b[TN][2];
+        ReadRows<0, TM, 16 * ROWB>::run(abase + (((0 * 4 + lchunk) ^ rsw) * 16), a0, 0);
         lds_wait_all();
-        qd_dequant<WQ>(raw, lchunk, 0, b);  // b[.][0]: not read by the kk = 1 MFMAs
-        if (kt > 0) {
-#pragma unroll
-            for (int i = TM / 2; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<false>(a[i][1], b[j][1], acc[i][j]);
-        }
-        qd_dequant<WQ>(raw, lchunk, 1, b);
-        ReadRows<0, TM, 16 * ROWB>::run(abase + (((1 * 4 + lchunk) ^ rsw) * 16), a, 1);
+        qd_dequant<WQ>(raw, lchunk, 0, b);
+        ReadRows<0, TM, 16 * ROWB>::run(abase + (((1 * 4 + lchunk) ^ rsw) * 16), a1, 1);
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<false>(a[i][0], b[j][0], acc[i][j]);
-        lds_wait_all();  // a[.][1] landed: this wave's reads of slot kt are done before the next barrier
+            for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<false>(a0[i][0], b[j][0], acc[i][j]);
+        qd_dequant<WQ>(raw, lchunk, 1, b);
+        lds_wait_all();
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<false>(a1[i][1], b[j][1], acc[i][j]);
     }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<false>(a[i][1], b[j][1], acc[i][j]);
     wait_vmcnt<0>();  // the dummy stages past the end land before the epilogue reuses the ring
     __syncthreads();  // LDS reads done before the epilogue reuses the ring
 

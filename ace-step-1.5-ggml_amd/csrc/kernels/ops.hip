@@ -121,8 +121,8 @@ __global__ void __launch_bounds__(256) rmsnorm_mod_kernel(const float* __restric
         uint16_t o[4], lo[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            float t = __fmul_rn(__fmul_rn(y[j], sc), ww[j]);
-            if (scp) t = __fadd_rn(__fmul_rn(t, __fadd_rn(s4[j], 1.0f)), h4[j]);
+            float t = rn_mul(rn_mul(y[j], sc), ww[j]);
+            if (scp) t = rn_add(rn_mul(t, rn_add(s4[j], 1.0f)), h4[j]);
             o[j] = (F16 || X3) ? f32_to_f16(t) : f32_to_bf16_rne(t);
             if (X3) lo[j] = f32_to_f16(t - (float)__builtin_bit_cast(_Float16, o[j]));
         }
@@ -193,15 +193,104 @@ __global__ void __launch_bounds__(256) rmsnorm_mod_rows_kernel(const float* __re
         uint32_t pk[4];
 #pragma unroll
         for (int j = 0; j < 8; j += 2) {
-            float t0 = __fmul_rn(__fmul_rn(y[j], sc), ww[j]);
-            float t1 = __fmul_rn(__fmul_rn(y[j + 1], sc), ww[j + 1]);
+            float t0 = rn_mul(rn_mul(y[j], sc), ww[j]);
+            float t1 = rn_mul(rn_mul(y[j + 1], sc), ww[j + 1]);
             if (scp) {
-                t0 = __fadd_rn(__fmul_rn(t0, __fadd_rn(s8[j], 1.0f)), h8[j]);
-                t1 = __fadd_rn(__fmul_rn(t1, __fadd_rn(s8[j + 1], 1.0f)), h8[j + 1]);
+                t0 = rn_add(rn_mul(t0, rn_add(s8[j], 1.0f)), h8[j]);
+                t1 = rn_add(rn_mul(t1, rn_add(s8[j + 1], 1.0f)), h8[j + 1]);
             }
             pk[j / 2] = (uint32_t)to_act(F16, t0) | ((uint32_t)to_act(F16, t1) << 16);
         }
         *(uint4*)(orow + i) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+    }
+}
+
+// Same operator, persistent: a fixed grid of waves strides over the rows, each wave holding w (and the
+// current item's 1 + scale, shift) in registers across its rows and loading the next row while it finishes
+// this one.  The one-row-per-wave kernels re-read w / scale / shift from L2 for every row (3x the bytes of
+// x itself) and run as one ramp-and-tail round of short-lived waves.
+template <bool F16, int NC>
+__global__ void __launch_bounds__(256) rmsnorm_mod_persist_kernel(const float* __restrict__ x, int M, int H,
+                                                                  const float* __restrict__ w,
+                                                                  const float* __restrict__ scale,
+                                                                  const float* __restrict__ shift, int64_t mod_stride,
+                                                                  int rows_per_item, float eps,
+                                                                  uint16_t* __restrict__ out) {
+    const int nwaves = gridDim.x * 4;
+    int m = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (m >= M) return;
+    const int lane = threadIdx.x & 63;
+    float4 wv[2 * NC], s1[2 * NC], hv[2 * NC], v[2 * NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const int i = c * 512 + lane * 8;
+        v[2 * c] = *(const float4*)(x + (int64_t)m * H + i);
+        v[2 * c + 1] = *(const float4*)(x + (int64_t)m * H + i + 4);
+        wv[2 * c] = *(const float4*)(w + i);
+        wv[2 * c + 1] = *(const float4*)(w + i + 4);
+    }
+    int item = -1;
+    for (;;) {
+        const int nxt = m + nwaves;
+        float4 vn[2 * NC];
+        if (nxt < M) {  // wave-uniform
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                const int i = c * 512 + lane * 8;
+                vn[2 * c] = *(const float4*)(x + (int64_t)nxt * H + i);
+                vn[2 * c + 1] = *(const float4*)(x + (int64_t)nxt * H + i + 4);
+            }
+        }
+        const int it = m / rows_per_item;
+        if (scale && it != item) {  // wave-uniform: a new batch item's modulation vectors
+            item = it;
+            const float* scp = scale + (int64_t)it * mod_stride;
+            const float* shp = shift + (int64_t)it * mod_stride;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                const int i = c * 512 + lane * 8;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const float4 a = *(const float4*)(scp + i + 4 * h);
+                    s1[2 * c + h] = make_float4(rn_add(a.x, 1.0f), rn_add(a.y, 1.0f), rn_add(a.z, 1.0f), rn_add(a.w, 1.0f));
+                    hv[2 * c + h] = *(const float4*)(shp + i + 4 * h);
+                }
+            }
+        }
+        float ss = 0.f;
+#pragma unroll
+        for (int k = 0; k < 2 * NC; ++k) ss += v[k].x * v[k].x + v[k].y * v[k].y + v[k].z * v[k].z + v[k].w * v[k].w;
+        ss = wave_sum(ss);
+        const float sc = 1.0f / sqrtf(ss / (float)H + eps);
+        uint16_t* orow = out + (int64_t)m * H;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const int i = c * 512 + lane * 8;
+            const float y[8] = {v[2 * c].x, v[2 * c].y, v[2 * c].z, v[2 * c].w,
+                                v[2 * c + 1].x, v[2 * c + 1].y, v[2 * c + 1].z, v[2 * c + 1].w};
+            const float ww[8] = {wv[2 * c].x, wv[2 * c].y, wv[2 * c].z, wv[2 * c].w,
+                                 wv[2 * c + 1].x, wv[2 * c + 1].y, wv[2 * c + 1].z, wv[2 * c + 1].w};
+            const float sp[8] = {s1[2 * c].x, s1[2 * c].y, s1[2 * c].z, s1[2 * c].w,
+                                 s1[2 * c + 1].x, s1[2 * c + 1].y, s1[2 * c + 1].z, s1[2 * c + 1].w};
+            const float hh[8] = {hv[2 * c].x, hv[2 * c].y, hv[2 * c].z, hv[2 * c].w,
+                                 hv[2 * c + 1].x, hv[2 * c + 1].y, hv[2 * c + 1].z, hv[2 * c + 1].w};
+            uint32_t pk[4];
+#pragma unroll
+            for (int j = 0; j < 8; j += 2) {
+                float t0 = rn_mul(rn_mul(y[j], sc), ww[j]);
+                float t1 = rn_mul(rn_mul(y[j + 1], sc), ww[j + 1]);
+                if (scale) {
+                    t0 = rn_add(rn_mul(t0, sp[j]), hh[j]);
+                    t1 = rn_add(rn_mul(t1, sp[j + 1]), hh[j + 1]);
+                }
+                pk[j / 2] = (uint32_t)to_act(F16, t0) | ((uint32_t)to_act(F16, t1) << 16);
+            }
+            *(uint4*)(orow + i) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+        }
+        if (nxt >= M) break;
+        m = nxt;
+#pragma unroll
+        for (int k = 0; k < 2 * NC; ++k) v[k] = vn[k];
     }
 }
 
@@ -233,10 +322,10 @@ __global__ void __launch_bounds__(256) rmsnorm_f32_kernel(const float* __restric
         if (i >= H) break;
         const float4 wv = *(const float4*)(w + i);
         float4 o;
-        o.x = __fmul_rn(__fmul_rn(v[k].x, sc), wv.x);
-        o.y = __fmul_rn(__fmul_rn(v[k].y, sc), wv.y);
-        o.z = __fmul_rn(__fmul_rn(v[k].z, sc), wv.z);
-        o.w = __fmul_rn(__fmul_rn(v[k].w, sc), wv.w);
+        o.x = rn_mul(rn_mul(v[k].x, sc), wv.x);
+        o.y = rn_mul(rn_mul(v[k].y, sc), wv.y);
+        o.z = rn_mul(rn_mul(v[k].z, sc), wv.z);
+        o.w = rn_mul(rn_mul(v[k].w, sc), wv.w);
         *(float4*)(orow + i) = o;
     }
 }
@@ -376,16 +465,16 @@ __global__ void timestep_freq_kernel(const float* __restrict__ t, const float* _
     const int b = blockIdx.x;
     const int half = dim / 2;
     float tv = t[b];
-    if (r) tv = __fsub_rn(tv, r[b]);
-    const float ts = __fmul_rn(tv, scale);
+    if (r) tv = rn_sub(tv, r[b]);
+    const float ts = rn_mul(tv, scale);
     // exp / cos / sin evaluated in double and rounded once: the correctly rounded f32 results, i.e. the values
     // any accurate f32 libm gives.  The sinusoid is the most ill-conditioned spot of the graph: arg reaches
     // ~1000, so one ulp of fr moves arg by ~6e-5 and the feature by as much; a 1-2 ulp device expf / cosf
     // put the timestep features ~1e-4 away from an accurate evaluation.
     for (int i = threadIdx.x; i < half; i += blockDim.x) {
-        const float expo = __fdiv_rn(__fmul_rn(-log_max, (float)i), (float)half);
+        const float expo = rn_div(rn_mul(-log_max, (float)i), (float)half);
         const float fr = (float)exp((double)expo);
-        const float arg = __fmul_rn(ts, fr);
+        const float arg = rn_mul(ts, fr);
         f[(int64_t)b * dim + i] = (float)cos((double)arg);
         f[(int64_t)b * dim + i + half] = (float)sin((double)arg);
     }
@@ -451,10 +540,10 @@ __global__ void __launch_bounds__(256) gemv_kernel(const void* __restrict__ xv_,
             for (int c = 0; c < 4; ++c) {
                 float v = wave_sum(acc[m][c]);
                 if (lane == 0) {
-                    if (bias) v = __fadd_rn(v, bias[n0 + c]);
+                    if (bias) v = rn_add(v, bias[n0 + c]);
                     if (silu_out) v = silu_f(v);
                     float* yp = y + (int64_t)m * N + n0 + c;
-                    *yp = accumulate ? __fadd_rn(*yp, v) : v;
+                    *yp = accumulate ? rn_add(*yp, v) : v;
                 }
             }
         }
@@ -472,7 +561,7 @@ __global__ void layer_mods_kernel(const float* __restrict__ tables, const float*
         r /= 6;
         const int b = (int)(r % B);
         const int l = (int)(r / B);
-        mod[i] = __fadd_rn(tables[((int64_t)l * 6 + j) * H + c], proj[((int64_t)b * 6 + j) * H + c]);
+        mod[i] = rn_add(tables[((int64_t)l * 6 + j) * H + c], proj[((int64_t)b * 6 + j) * H + c]);
     }
 }
 
@@ -484,24 +573,24 @@ __global__ void out_mods_kernel(const float* __restrict__ table, const float* __
         const int c = (int)(i % H);
         const int j = (int)((i / H) % 2);
         const int b = (int)(i / (2 * H));
-        const float temb = __fadd_rn(tt[(int64_t)b * H + c], tr[(int64_t)b * H + c]);
-        om[i] = __fadd_rn(table[(int64_t)j * H + c], temb);
+        const float temb = rn_add(tt[(int64_t)b * H + c], tr[(int64_t)b * H + c]);
+        om[i] = rn_add(table[(int64_t)j * H + c], temb);
     }
 }
 
 __global__ void euler_kernel(float* __restrict__ xt, const float* __restrict__ v, int64_t n, float dt) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        xt[i] = __fsub_rn(xt[i], __fmul_rn(v[i], dt));
+        xt[i] = rn_sub(xt[i], rn_mul(v[i], dt));
 }
 
 // SDE step of the reference generation loop (acestep/mlx_dit/generate.py:183-192):
 // x0 = xt - v*t ; xt = t_next*noise + (1 - t_next)*x0
 __global__ void sde_kernel(float* __restrict__ xt, const float* __restrict__ v, const float* __restrict__ noise,
                            int64_t n, float t, float t_next) {
-    const float keep = __fsub_rn(1.0f, t_next);
+    const float keep = rn_sub(1.0f, t_next);
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const float x0 = __fsub_rn(xt[i], __fmul_rn(v[i], t));
-        xt[i] = __fadd_rn(__fmul_rn(t_next, noise[i]), __fmul_rn(keep, x0));
+        const float x0 = rn_sub(xt[i], rn_mul(v[i], t));
+        xt[i] = rn_add(rn_mul(t_next, noise[i]), rn_mul(keep, x0));
     }
 }
 
@@ -510,7 +599,7 @@ __global__ void sde_kernel(float* __restrict__ xt, const float* __restrict__ v, 
 // localised error (tests/test_gpu_parity_strict.py); never launched unless that variable is set.
 __global__ void fault_tile_kernel(float* __restrict__ x, int ld, int rows, int row0, int col0, float amp) {
     const int r = row0 + (int)(blockIdx.x * 8 + (threadIdx.x >> 7)), c = col0 + (int)(threadIdx.x & 127);
-    if (r < rows) x[(int64_t)r * ld + c] = __fadd_rn(x[(int64_t)r * ld + c], amp);
+    if (r < rows) x[(int64_t)r * ld + c] = rn_add(x[(int64_t)r * ld + c], amp);
 }
 
 inline dim3 grid_for(int64_t n, int block = 256) {
@@ -551,6 +640,34 @@ void launch_rmsnorm_mod(ActType t, const float* x, int M, int H, const float* w,
         const char* e = std::getenv("ACE_MI_RMSNORM_ROWS");
         return e && e[0] == '1';
     }();
+    // persistent kernel (default for H = 512 * NC, NC <= 4): ACE_MI_RMSNORM_PERSIST = workgroups per CU
+    // (default 2; 0 = off)
+    static const int persist = [] {
+        const char* e = std::getenv("ACE_MI_RMSNORM_PERSIST");
+        const int v = e ? std::atoi(e) : 2;
+        return v < 0 ? 0 : std::min(v, 16);
+    }();
+    if (!x3 && persist > 0 && H % 512 == 0 && H <= 2048) {
+        static int n_cu = 0;
+        if (n_cu == 0) {
+            int dev = 0;
+            ACEMI_HIP(hipGetDevice(&dev));
+            ACEMI_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+        }
+        const dim3 g((unsigned)std::min<int64_t>((M + 3) / 4, (int64_t)n_cu * persist));
+#define ACEMI_RMSP(F, NC)                                                                                         \
+    hipLaunchKernelGGL((rmsnorm_mod_persist_kernel<F, NC>), g, dim3(256), 0, s, x, M, H, w, scale, shift, mod_stride, \
+                       rows_per_item, eps, out)
+        switch (H / 512) {
+            case 1: if (f16) ACEMI_RMSP(true, 1); else ACEMI_RMSP(false, 1); break;
+            case 2: if (f16) ACEMI_RMSP(true, 2); else ACEMI_RMSP(false, 2); break;
+            case 3: if (f16) ACEMI_RMSP(true, 3); else ACEMI_RMSP(false, 3); break;
+            default: if (f16) ACEMI_RMSP(true, 4); else ACEMI_RMSP(false, 4); break;
+        }
+#undef ACEMI_RMSP
+        ACEMI_HIP(hipGetLastError());
+        return;
+    }
     if (!x3 && rows && H % 512 == 0 && H <= 4096) {
         const dim3 g((M + 3) / 4);
 #define ACEMI_RMSR(F, NC) \

@@ -10,6 +10,28 @@
 #include <cstdint>
 
 namespace acemi {
+
+// Separately rounded f32 operations (the reference's ggml ops round after every op).  HIP's __fmul_rn /
+// __fadd_rn are plain operators, and hipcc's default -ffp-contract=fast fuses a product into a following add
+// even across them (one rounding instead of two: the device Euler update x - v*dt came out 1 ulp off torch's
+// and the oracle's).  The kernels build with -ffp-contract=fast-honor-pragmas, so contract(off) here holds.
+__device__ __forceinline__ float rn_mul(float a, float b) {
+#pragma clang fp contract(off)
+    return a * b;
+}
+__device__ __forceinline__ float rn_add(float a, float b) {
+#pragma clang fp contract(off)
+    return a + b;
+}
+__device__ __forceinline__ float rn_sub(float a, float b) {
+#pragma clang fp contract(off)
+    return a - b;
+}
+__device__ __forceinline__ float rn_div(float a, float b) {
+#pragma clang fp contract(off)
+    return a / b;
+}
+
 namespace prep {
 
 __device__ __forceinline__ uint16_t f16_bits(float f) {
@@ -47,15 +69,15 @@ __device__ __forceinline__ void head_row_v(float (&y)[8], bool has_w, const floa
         const float sc = 1.0f / sqrtf(ss / 128.0f + eps);
         const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
 #pragma unroll
-        for (int j = 0; j < 8; ++j) y[j] = __fmul_rn(__fmul_rn(y[j], sc), wv[j]);
+        for (int j = 0; j < 8; ++j) y[j] = rn_mul(rn_mul(y[j], sc), wv[j]);
     }
     float r[8];
     if (has_rope) {
         const float c[4] = {c4.x, c4.y, c4.z, c4.w}, s[4] = {s4.x, s4.y, s4.z, s4.w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            r[j] = __fsub_rn(__fmul_rn(y[j], c[j]), __fmul_rn(y[4 + j], s[j]));
-            r[4 + j] = __fadd_rn(__fmul_rn(y[j], s[j]), __fmul_rn(y[4 + j], c[j]));
+            r[j] = rn_sub(rn_mul(y[j], c[j]), rn_mul(y[4 + j], s[j]));
+            r[4 + j] = rn_add(rn_mul(y[j], s[j]), rn_mul(y[4 + j], c[j]));
         }
     } else {
 #pragma unroll

@@ -18,6 +18,7 @@
 
 #include "../kernels.h"
 #include "lds_asm.h"
+#include "prep_math.h"
 
 namespace acemi {
 namespace {
@@ -38,10 +39,10 @@ __device__ __forceinline__ uint16_t f32_to_f16(float f) {
 // more than the tile's MFMAs at 128 channels.  Their results differ from libm's by ~1e-6 relative,
 // far below the fp16 rounding of the next conv's operand that follows.
 __device__ __forceinline__ float snake_f(float x, float ea, float rcp_eb) {
-    float s = __sinf(__fmul_rn(ea, x));
-    s = __fmul_rn(s, s);
-    s = __fmul_rn(s, rcp_eb);  // / e^beta as a multiply by the (1-ulp) hardware reciprocal
-    return __fadd_rn(x, s);
+    float s = __sinf(rn_mul(ea, x));
+    s = rn_mul(s, s);
+    s = rn_mul(s, rcp_eb);  // / e^beta as a multiply by the (1-ulp) hardware reciprocal
+    return rn_add(x, s);
 }
 
 template <int I, int N, int STRIDE>
@@ -213,7 +214,7 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(ConvGemmArgs p) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int row = wm0 + i * 16 + crow2 + r;
-                    const float v = __fadd_rn(acc[i][j][r], b1);
+                    const float v = rn_add(acc[i][j][r], b1);
                     *reinterpret_cast<uint16_t*>(ytile + row * 256 + (((col >> 3) ^ (row & 15)) << 4) + (col & 7) * 2) =
                         f32_to_f16(snake_f(v, ea, reb));
                 }
@@ -289,8 +290,8 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(ConvGemmArgs p) {
                 if (u < 0 || u >= p.T_out) continue;
                 const int64_t o = (obase + u) * p.Cout + co_j[j];
                 float v = acc[i][j][r];
-                if (bias_e) v = __fadd_rn(v, bias_j[j]);
-                if (p.resid) v = __fadd_rn(xo[r][j], v);
+                if (bias_e) v = rn_add(v, bias_j[j]);
+                if (p.resid) v = rn_add(xo[r][j], v);
                 if (p.store_x) p.X[o] = v;
                 if (p.S_out) p.S_out[o] = f32_to_f16(p.snake_ea ? snake_f(v, ea_j[j], reb_j[j]) : v);
             }

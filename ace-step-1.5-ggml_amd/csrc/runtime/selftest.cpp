@@ -328,8 +328,11 @@ ace_ggml_status ace_mi_kernel_gemm_q(int32_t qtype, int32_t epi, int32_t variant
     if (!A || !W_blocks || M <= 0 || N % 128 != 0 || K % 64 != 0) return ACE_GGML_ERR_INVALID_ARG;
     if (t != quant::Q8_0 && t != quant::Q4_K && t != quant::Q6_K) return ACE_GGML_ERR_INVALID_ARG;
     if (!quant::applies(t, K)) return ACE_GGML_ERR_INVALID_ARG;
-    if (epi != EPI_STORE_F32 && epi != EPI_SWIGLU) return ACE_GGML_ERR_UNSUPPORTED;
-    if ((epi == EPI_STORE_F32 && !out_f32) || (epi == EPI_SWIGLU && !out_u16)) return ACE_GGML_ERR_INVALID_ARG;
+    const bool resid = epi == EPI_RESID || epi == EPI_RESID_GATED;
+    if (epi != EPI_STORE_F32 && epi != EPI_SWIGLU && !resid) return ACE_GGML_ERR_UNSUPPORTED;
+    if (((epi == EPI_STORE_F32 || resid) && !out_f32) || (epi == EPI_SWIGLU && !out_u16))
+        return ACE_GGML_ERR_INVALID_ARG;
+    if (epi == EPI_RESID_GATED && !bias) return ACE_GGML_ERR_INVALID_ARG;
     if (variant < -1 || variant % 100 > 24 || variant > 424) return ACE_GGML_ERR_INVALID_ARG;
     try {
         std::vector<uint8_t> qp(quant::q_plane_bytes(t, N, K));
@@ -342,8 +345,15 @@ ace_ggml_status ace_mi_kernel_gemm_q(int32_t qtype, int32_t epi, int32_t variant
         if (bias) ACEMI_HIP(hipMemcpy(dB.p, bias, (size_t)N * 4, hipMemcpyHostToDevice));
         GemmEpilogue e;
         e.kind = epi;
-        e.bias = bias ? dB.as<float>() : nullptr;
-        if (epi == EPI_STORE_F32) {
+        e.bias = bias && !resid ? dB.as<float>() : nullptr;
+        if (resid) {  // out_f32 holds x on entry: x += acc (* gate[n], the gate passed as `bias`)
+            ACEMI_HIP(hipMemcpy(dC.p, out_f32, (size_t)M * N * 4, hipMemcpyHostToDevice));
+            e.c_f32 = dC.as<float>();
+            e.ldc = N;
+            e.gate = epi == EPI_RESID_GATED ? dB.as<float>() : nullptr;
+            e.gate_stride = 0;
+            e.rows_per_item = M;
+        } else if (epi == EPI_STORE_F32) {
             e.c_f32 = dC.as<float>();
             e.ldc = N;
         } else {
@@ -358,7 +368,7 @@ ace_ggml_status ace_mi_kernel_gemm_q(int32_t qtype, int32_t epi, int32_t variant
         launch_gemm(dA.as<uint16_t>(), K, w, M, N, K, e, nullptr);
         gemm_force_variant(-1);
         ACEMI_HIP(hipDeviceSynchronize());
-        if (epi == EPI_STORE_F32)
+        if (epi == EPI_STORE_F32 || resid)
             ACEMI_HIP(hipMemcpy(out_f32, dC.p, (size_t)M * N * 4, hipMemcpyDeviceToHost));
         else
             ACEMI_HIP(hipMemcpy(out_u16, dC.p, (size_t)M * (N / 2) * 2, hipMemcpyDeviceToHost));

@@ -55,6 +55,8 @@ def test_gemm_q_matches_dequantized_product(qtype, variant, M, N, K):
     capi = _capi()
     if variant in (2, 5, 21) and N % 256:
         pytest.skip("256-wide tiles need N % 256 == 0")
+    if variant == 21 and qtype == "q4_k":
+        pytest.skip("the 8-wave tile is not used for Q4_K (wrong columns, round 3): forcing it runs the automatic one")
     if variant >= 100 and K // 64 < 2 * (variant // 100):
         pytest.skip("split-K needs two k-tiles per part")
     rng = np.random.default_rng(M + K + variant)
@@ -66,6 +68,32 @@ def test_gemm_q_matches_dequantized_product(qtype, variant, M, N, K):
     ref, scale = _q_ref(a, blocks, qtype)
     ref = ref + bias
     assert np.all(np.abs(got - ref) <= 2e-6 * scale + 1e-6), np.max(np.abs(got - ref) / (scale + 1e-6))
+
+
+@pytest.mark.parametrize("qtype", ["q8_0", "q4_k", "q6_k"])
+@pytest.mark.parametrize("variant", [-1, 20, 21, 22, 23, 24, 222, 423])
+@pytest.mark.parametrize("epi", [2, 3])
+def test_gemm_q_residual_epilogues(qtype, variant, epi):
+    """x += A.bf16(dequant(W))^T (* gate[n]) in place (the o / cross-o / down projections) through the
+    register-dequant tiles, M edges included."""
+    capi = _capi()
+    M, N, K = 300, 512, 512
+    if variant in (21,) and N % 256:
+        pytest.skip("256-wide tiles need N % 256 == 0")
+    if variant == 21 and qtype == "q4_k":
+        pytest.skip("the 8-wave tile is not used for Q4_K (round 3)")
+    rng = np.random.default_rng(7 * epi + variant + 100)
+    a = f32_to_bf16_bits(rng.standard_normal((M, K)).astype(np.float32))
+    w = (rng.standard_normal((N, K)) * 0.02).astype(np.float32)
+    blocks = capi.quantize(w, qtype)
+    x = rng.standard_normal((M, N)).astype(np.float32)
+    gate = rng.standard_normal(N).astype(np.float32) if epi == 2 else None
+    got = capi.kernel_gemm_q(a, blocks, qtype, epi=epi, variant=variant, bias=gate, x=x)
+    acc, scale = _q_ref(a, blocks, qtype)
+    g = gate.astype(np.float64) if epi == 2 else np.ones(N)
+    ref = x.astype(np.float64) + acc * g
+    assert np.all(np.abs(got - ref) <= (2e-6 * scale + 1e-6) * np.abs(g) + 2e-7 * np.abs(ref)), \
+        np.max(np.abs(got - ref))
 
 
 @pytest.mark.parametrize("qtype", ["q8_0", "q4_k"])
