@@ -22,7 +22,7 @@ DitEngine::DitEngine(int device) : device_(device) {
     staged_quant_ = !(q && q[0] == '0');
     const char* h = std::getenv("ACE_MI_QUANT_STAGE_SCOPE");
     stage_per_call_ = !(h && std::strcmp(h, "layer") == 0);
-    stage_model_ = h && std::strcmp(h, "model") == 0;
+    stage_model_ = !(h && (std::strcmp(h, "call") == 0 || std::strcmp(h, "layer") == 0));  // default: model
     // TEST ONLY: ACE_MI_TEST_FAULT="layer,row,col,amp" adds amp to one 16 x 128 tile of the residual right after
     // that layer's o-projection GEMM (the parity negative control of tests/test_gpu_parity_strict.py)
     if (const char* f = std::getenv("ACE_MI_TEST_FAULT")) {

@@ -128,14 +128,15 @@ class DitEngine {
     struct LayerViews {
         WeightView qkv, o, cq, co, gu, down;
     };
-    // Scope of the staged images (ACE_MI_QUANT_STAGE_SCOPE): "model" keeps them across calls; "call" keeps one slot
-    // per layer, so
-    // the dequant runs once per sampling call (step 0) instead of once per step, at the cost of a bf16
-    // image of the block weights as workspace (2.8 GB for the 24-layer DiT: 1 % of HBM); "layer" = the
-    // single shared slot, expanded before every layer of every forward.
+    // Scope of the staged images (ACE_MI_QUANT_STAGE_SCOPE): "model" (default since round 3) expands every layer's
+    // image once, at the first forward after the load, and keeps it while the weights are loaded (they never change),
+    // so the per-step decoder.forward hook and the ABI forward do not re-expand them either; "call" keeps one
+    // slot per layer for one sampling call (expanded at its step 0); both cost a bf16 image of the block weights
+    // as workspace (2.8 GB for the 24-layer DiT: 1 % of HBM); "layer" = the single shared 117 MB slot, expanded
+    // before every layer of every forward (the low-memory mode: weights + one slot).
     bool staged_quant_ = true;
     bool stage_per_call_ = true;
-    bool stage_model_ = false;  // ACE_MI_QUANT_STAGE_SCOPE=model: images kept across calls while the weights are loaded
+    bool stage_model_ = true;  // images kept across calls while the weights are loaded (ACE_MI_QUANT_STAGE_SCOPE)
     size_t stage_slot_bytes_ = 0;
     int stage_layers_ = 0;  // layers whose images wring_ holds (per-call scope)
     Buf wring_;

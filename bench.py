@@ -28,6 +28,10 @@ Extra lines beside the headline (one GPU only; each the same 27-step schedule, t
   bf16_line        the same workload with bf16 weights (+ its own hook_line)
   line_60s         BASELINE configs[1]: 60 s (T = 1500), bs = 1, bf16 weights
   line_10s         10 s (T = 250, configs[0]'s shape) forward rate with the headline weights and with bf16
+  lowmem_line      quantized weights with ACE_MI_QUANT_STAGE_SCOPE=layer (planes + one 117 MB bf16 slot,
+                   expanded before every layer of every step) and its device-memory footprint
+`memory` reports the device bytes taken by the weights (after load_dit) and by the workspace (after the timed
+run; with the default `model` scope it holds the bf16 images of the quantized block weights).
 """
 import argparse
 import json
@@ -121,10 +125,24 @@ def main():
 
     if args.qtype == "bf16":
         args.qtype = ""
+    def dev_used():
+        if args.emulate:
+            return 0
+        free, total = torch.cuda.mem_get_info(dev)
+        return total - free
+
     set_weights(args.qtype)
+    mem0 = dev_used()
     br = GGMLCAPIBridge(device=local, lib_path=lib_path) if lib_path else GGMLCAPIBridge(device=local)
     br.load_dit(ckpt)
-    wdesc = f"{args.qtype.upper()} dequant-fused (bf16 MFMA)" if args.qtype else "bf16"
+    mem_weights = dev_used() - mem0
+    stage_scope = os.environ.get("ACE_MI_QUANT_STAGE_SCOPE", "model")
+    if not args.qtype:
+        wdesc = "bf16"
+    elif os.environ.get("ACE_MI_QUANT_STAGED", "1") == "0":
+        wdesc = f"{args.qtype.upper()} dequant-fused GEMM (bf16 MFMA)"
+    else:
+        wdesc = (f"{args.qtype.upper()} (staged dequant to bf16 images, scope {stage_scope}; bf16 MFMA)")
     info = br.info
 
     T = int(round(args.seconds * 25))        # 25 Hz latent frames
@@ -230,6 +248,8 @@ def main():
     # conditioning broadcast to every rank before the timed region (f32 noise, context, encoder states)
     bcast_bytes = 4 * B * (T * audio + T * ctxd + L * H)
     finite = bool(torch.isfinite(xt).all().item())
+    memory = {"weights_bytes": mem_weights, "workspace_bytes": dev_used() - mem0 - mem_weights,
+              "stage_scope": stage_scope if args.qtype else None}
 
     # ---- per-kernel timing (HIP events on the launch stream, one event pair per launch)
     breakdown = {}
@@ -285,15 +305,32 @@ def main():
                                                                        "10 s (T = 250, N = 125 tokens, L = 512), bs = 1:"
                                                                        " DiT forwards + Euler per s")}
 
+    # ---- low-memory quantized mode: one shared 117 MB bf16 slot expanded before every layer of every step
+    if args.qtype and single and not args.no_extra_lines and stage_scope != "layer":
+        br.close()
+        os.environ["ACE_MI_QUANT_STAGE_SCOPE"] = "layer"
+        m0 = dev_used()
+        br = GGMLCAPIBridge(device=local, lib_path=lib_path) if lib_path else GGMLCAPIBridge(device=local)
+        br.load_dit(ckpt)
+        mw = dev_used() - m0
+        el_lm = timed(run)
+        extras["lowmem_line"] = {**line(B * args.steps, el_lm,
+                                        "the headline loop with ACE_MI_QUANT_STAGE_SCOPE=layer: quantized planes + one "
+                                        "shared bf16 slot expanded before every layer of every step"),
+                                 "weights_bytes": mw, "workspace_bytes": dev_used() - m0 - mw}
+        os.environ.pop("ACE_MI_QUANT_STAGE_SCOPE", None)
     # ---- the same workload with bf16 weights, reported beside a quantized line (single GPU only)
     bf16_line = None
     if args.qtype and single and not args.no_bf16_line:
         br.close()
         set_weights("")
         br = GGMLCAPIBridge(device=local, lib_path=lib_path) if lib_path else GGMLCAPIBridge(device=local)
+        m0 = dev_used()
         br.load_dit(ckpt)
+        mw = dev_used() - m0
         el_bf16 = timed(run)
         bf16_line = line(B * args.steps, el_bf16, "the same 240 s bs=1 sampling loop with bf16 weights (no quantization)")
+        bf16_line["weights_bytes"] = mw
         if not args.no_profile:
             br.profile_enable(True)
             br.profile_reset()
@@ -320,6 +357,16 @@ def main():
         in60 = small_inputs(1500)
         extras["line_60s"] = line(args.steps, timed(lambda f, k: run(f, k, in60)),
                                   "BASELINE configs[1]: DiT 27-step sample, 60 s (T = 1500, N = 750), bs = 1, bf16")
+        if not args.no_profile:
+            br.profile_enable(True)
+            br.profile_reset()
+            run(0, args.steps, in60)
+            sync()
+            prof60 = br.profile_get()
+            br.profile_enable(False)
+            extras["line_60s"]["dit_block_linears_frac_of_bf16_peak"] = block_linear_frac(prof60, args.steps, 1500, 1,
+                                                                                           info)
+            extras["line_60s"]["breakdown_ms_per_step"] = {n: round(ms / args.steps, 4) for n, ms, _ in prof60}
 
     # ---- CPU baseline: the C++/OpenMP restatement of ggml's CPU forward_dit on the host cores
     cpu = None
@@ -360,6 +407,7 @@ def main():
                 "parallelism": f"dp{world} (batch-sharded, RCCL broadcast of conditioning)",
             },
             "finite": finite,
+            "memory": memory,
             "ranks": {"elapsed_s": [round(v, 5) for v in rank_elapsed], "broadcast_bytes_per_rank": bcast_bytes,
                       "items_per_rank": [len(shard_indices(B, world, r)) for r in range(world)]},
             "roofline": roofline,

@@ -263,8 +263,8 @@ def test_staged_dequant_equals_fused(tiny_ckpt, monkeypatch, qtype, width):
 
 @pytest.mark.parametrize("qtype", ["q8_0", "q4_k"])
 def test_sampling_call_scope_staging_equals_per_layer(tiny_ckpt, monkeypatch, qtype):
-    """ace_mi_dit_sample_ex with quantized weights: the bf16 images expanded once per sampling call
-    (ACE_MI_QUANT_STAGE_SCOPE=call, default; steps 1.. reuse them) give the same bits as expanding them
+    """ace_mi_dit_sample_ex with quantized weights: the bf16 images kept for the model (ACE_MI_QUANT_STAGE_SCOPE=
+    model, default) or expanded once per sampling call (=call; steps 1.. reuse them) give the same bits as expanding them
     before every layer of every step (=layer) and as the dequant-fused GEMMs (ACE_MI_QUANT_STAGED=0).
     A first call on fewer layers (ACE_GGML_DIT_MAX_LAYERS) must not leave images a later call reuses."""
     import torch
@@ -278,7 +278,7 @@ def test_sampling_call_scope_staging_equals_per_layer(tiny_ckpt, monkeypatch, qt
     sched = [1.0, 0.75, 0.5, 0.25]
     dc, de = (torch.from_numpy(a).cuda() for a in (c, e))
     outs = []
-    for scope, staged in (("call", "1"), ("layer", "1"), ("call", "0")):
+    for scope, staged in (("model", "1"), ("call", "1"), ("layer", "1"), ("call", "0")):
         monkeypatch.setenv("ACE_MI_QUANT_STAGE_SCOPE", scope)
         monkeypatch.setenv("ACE_MI_QUANT_STAGED", staged)
         br = GGMLCAPIBridge()

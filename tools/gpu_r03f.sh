@@ -7,4 +7,5 @@ timeout -k 10 300 python tools/gemm_msweep.py 7,14,15,4 3000 > gpurun_out/msweep
 timeout -k 10 300 python tools/diag_det.py > gpurun_out/diag_det2.log 2>&1 || exit $?
 timeout -k 10 900 $T tests/test_gpu_quant.py tests/test_gpu_kernels.py > gpurun_out/quant_f.log 2>&1; rc=$?
 [ $rc -gt 1 ] && exit $rc
+timeout -k 10 600 python bench.py --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/bench_r03f.json 2> gpurun_out/bench_r03f.err || exit $?
 exit 0
