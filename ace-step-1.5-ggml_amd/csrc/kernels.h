@@ -120,11 +120,13 @@ struct AttnArgs {
     bool split = true;                 // hi/lo fp16 Q.K operands (see attention.hip)
     bool pv_split = false;             // hi/lo fp16 P.V operands too (needs split)
     int64_t q_plane = 0, k_plane = 0, v_plane = 0;  // element offset of the lo planes
-    // Optional f32 workspace of attn_part_floats(): with it, a grid too small to fill the chip in
-    // whole rounds splits every block's key range in two and merges the halves in a second kernel.
+    // Optional f32 workspace of attn_part_floats() (zeroed before first use: its tail holds the key-split
+    // tickets, which every launch leaves at zero): with it, a grid too small to fill the chip in whole rounds
+    // splits every block's key range in two or four; the last part of each group merges them.
     float* part = nullptr;
     int ksplit = 1;  // set by launch_attention
     int xcd_order = 1;  // set by launch_attention: XCD-aware block order
+    int fused_merge = 0;  // set by launch_attention: the last part of a key-split group merges (no merge kernel)
 };
 size_t attn_part_floats(int B, int nq, int Hq);
 // Operand precision of the attention MFMAs: FP16 = single fp16 operands (two workgroups per CU),
@@ -191,6 +193,10 @@ void launch_out_mods(const float* out_table, const float* temb_t, const float* t
 void launch_fault_tile(float* x, int ld, int rows, int row0, int col0, float amp, hipStream_t s);
 // xt -= v * dt
 void launch_euler(float* xt, const float* v, int64_t n, float dt, hipStream_t s);
+// Read-only sweep of up to 6 device ranges (weights of the next layer) on a side stream, so they sit in the
+// memory-side cache (MALL) when the layer's GEMMs read them; `blocks` workgroups.  Nothing is written except
+// one word of `sink` in a case that never occurs (keeps the loads).
+void launch_prefetch(const void* const* ptrs, const size_t* bytes, int n, int blocks, unsigned* sink, hipStream_t s);
 // SDE re-noise step: xt = t_next * noise + (1 - t_next) * (xt - v * t)
 void launch_sde(float* xt, const float* v, const float* noise, int64_t n, float t, float t_next, hipStream_t s);
 

@@ -82,6 +82,7 @@ struct Ring {
 };
 
 typedef u32x4_t frag;  // 8 fp16 of one MFMA operand
+typedef __attribute__((ext_vector_type(2))) unsigned u32x2_t;
 
 __device__ __forceinline__ f32x16 mfma32(const frag& a, const frag& b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0,
@@ -462,6 +463,88 @@ __global__ void __launch_bounds__(256, OCC) attn_kernel(AttnArgs a) {
     if (i < n) iter(std::integral_constant<int, 0>{}, i);
 
     const float l = l_run + __shfl_xor(l_run, 32);
+    if (a.ksplit > 1 && a.fused_merge) {
+        // Key split, merged in place: every part stores its unnormalised O, running max and sum with
+        // device-coherent (sc1) stores, completes them (vmcnt 0) and takes a ticket; the part that takes the
+        // last ticket (whichever finishes last: no block ever waits) reads all S parts back in part order with
+        // sc1 loads and writes the normalised output -- the same arithmetic and order as attn_merge_kernel.
+        const int S = a.ksplit;
+        const int64_t rows = (int64_t)a.B * a.nq * a.Hq;
+        const int64_t r = ((int64_t)b * a.nq + qrow) * a.Hq + head;
+        const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void*)a.part, 0, 0x7fffffff, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rm =
+            __builtin_amdgcn_make_buffer_rsrc((void*)(a.part + S * rows * D), 0, 0x7fffffff, 0x00020000);
+        if (qrow < a.nq) {
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int g4 = 0; g4 < 4; ++g4) {
+                    const u32x4_t v = {__float_as_uint(o[dt][4 * g4 + 0]), __float_as_uint(o[dt][4 * g4 + 1]),
+                                       __float_as_uint(o[dt][4 * g4 + 2]), __float_as_uint(o[dt][4 * g4 + 3])};
+                    __builtin_amdgcn_raw_buffer_store_b128(
+                        v, ro, (int)((((int64_t)split * rows + r) * D + 32 * dt + 8 * g4 + 4 * h) * 4), 0, 16);
+                }
+            if (h == 0) {
+                const u32x2_t v = {__float_as_uint(m_run), __float_as_uint(l)};
+                __builtin_amdgcn_raw_buffer_store_b64(v, rm, (int)(((int64_t)split * rows + r) * 2 * 4), 0, 16);
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();  // every lane's stores are complete; the ring is free
+        unsigned* cnt = reinterpret_cast<unsigned*>(a.part + 4 * rows * (D + 2));
+        const int group = (b * a.Hkv + kvh) * n_qt + qt;
+        volatile unsigned* flag = reinterpret_cast<volatile unsigned*>(smem);
+        if (tid == 0) *flag = __hip_atomic_fetch_add(cnt + group, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        if (*flag != (unsigned)(S - 1)) return;
+        if (tid == 0) __hip_atomic_store(cnt + group, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (qrow >= a.nq) return;
+        float mk[4], lk[4];
+        float M = -INFINITY;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (k < S) {
+                const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(rm, (int)(((int64_t)k * rows + r) * 2 * 4), 0, 16);
+                mk[k] = __uint_as_float(v[0]);
+                lk[k] = __uint_as_float(v[1]);
+                M = fmaxf(M, mk[k]);
+            }
+        }
+        float wk[4], den = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (k < S) {
+                wk[k] = mk[k] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(mk[k] - M);
+                den += wk[k] * lk[k];
+            }
+        }
+        const float inv = 1.0f / den;
+        uint16_t* op = a.out + ((int64_t)b * a.nq + qrow) * (a.Hq * D) + head * D;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+                const int d = 32 * dt + 8 * g4 + 4 * h;
+                float v[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    if (k < S) {
+                        const u32x4_t t = __builtin_amdgcn_raw_buffer_load_b128(
+                            ro, (int)((((int64_t)k * rows + r) * D + d) * 4), 0, 16);
+                        v[0] += wk[k] * __uint_as_float(t[0]);
+                        v[1] += wk[k] * __uint_as_float(t[1]);
+                        v[2] += wk[k] * __uint_as_float(t[2]);
+                        v[3] += wk[k] * __uint_as_float(t[3]);
+                    }
+                }
+                uint2 w;
+                w.x = (uint32_t)to_act<F16OUT>(v[0] * inv) | ((uint32_t)to_act<F16OUT>(v[1] * inv) << 16);
+                w.y = (uint32_t)to_act<F16OUT>(v[2] * inv) | ((uint32_t)to_act<F16OUT>(v[3] * inv) << 16);
+                *(uint2*)(op + d) = w;
+            }
+        }
+        return;
+    }
     if (a.ksplit > 1) {  // unnormalised partial O, running max and sum for attn_merge_kernel
         if (qrow < a.nq) {
             const int64_t row = ((int64_t)split * a.B + b) * a.nq + qrow;
@@ -498,32 +581,41 @@ __global__ void __launch_bounds__(256, OCC) attn_kernel(AttnArgs a) {
     }
 }
 
-// Combine the key-range parts of one (item, query, head) row per wave: M = max m_k, weights
-// 2^(m_k - M) (0 for a part whose keys were all masked), out = sum w_k O_k / sum w_k l_k; a row with
-// no unmasked key at all stays 0/0 = NaN as in ggml.
-// Two key-split parts per row (the only split launch_attention makes): half a wave per row, 16-byte
-// partial reads, every load issued before the first use.
-template <bool F16OUT>
+// Combine the S key-range parts of one (item, query, head) row: M = max m_k, weights 2^(m_k - M) (0 for a
+// part whose keys were all masked), out = sum w_k O_k / sum w_k l_k; a row with no unmasked key at all stays
+// 0/0 = NaN as in ggml.  Half a wave per row, 16-byte partial reads, every load issued before the first use.
+template <bool F16OUT, int S>
 __global__ void __launch_bounds__(256) attn_merge_kernel(AttnArgs a) {
     const int64_t rows = (int64_t)a.B * a.nq * a.Hq;
     const int64_t r = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
     if (r >= rows) return;
     const int d = (threadIdx.x & 31) * 4;
-    const float* ml = a.part + 2 * rows * D;
-    const float2 ml0 = *(const float2*)(ml + r * 2);
-    const float2 ml1 = *(const float2*)(ml + (rows + r) * 2);
-    const float4 o0 = *(const float4*)(a.part + r * D + d);
-    const float4 o1 = *(const float4*)(a.part + (rows + r) * D + d);
-    const float M = fmaxf(ml0.x, ml1.x);
-    const float w0 = ml0.x == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(ml0.x - M);
-    const float w1 = ml1.x == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(ml1.x - M);
-    const float inv = 1.0f / (w0 * ml0.y + w1 * ml1.y);
-    const float v[4] = {(w0 * o0.x + w1 * o1.x) * inv, (w0 * o0.y + w1 * o1.y) * inv,
-                        (w0 * o0.z + w1 * o1.z) * inv, (w0 * o0.w + w1 * o1.w) * inv};
+    const float* ml = a.part + S * rows * D;
+    float2 mlk[S];
+    float4 ok[S];
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+        mlk[k] = *(const float2*)(ml + (k * rows + r) * 2);
+        ok[k] = *(const float4*)(a.part + (k * rows + r) * D + d);
+    }
+    float M = mlk[0].x;
+#pragma unroll
+    for (int k = 1; k < S; ++k) M = fmaxf(M, mlk[k].x);
+    float den = 0.f, v[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+        const float w = mlk[k].x == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(mlk[k].x - M);
+        den += w * mlk[k].y;
+        v[0] += w * ok[k].x;
+        v[1] += w * ok[k].y;
+        v[2] += w * ok[k].z;
+        v[3] += w * ok[k].w;
+    }
+    const float inv = 1.0f / den;
     // row r = (b * nq + q) * Hq + head: out[b][q][head*128 + d] is contiguous in r * 128 + d
     *(uint2*)(a.out + r * D + d) =
-        make_uint2((uint32_t)to_act<F16OUT>(v[0]) | ((uint32_t)to_act<F16OUT>(v[1]) << 16),
-                   (uint32_t)to_act<F16OUT>(v[2]) | ((uint32_t)to_act<F16OUT>(v[3]) << 16));
+        make_uint2((uint32_t)to_act<F16OUT>(v[0] * inv) | ((uint32_t)to_act<F16OUT>(v[1] * inv) << 16),
+                   (uint32_t)to_act<F16OUT>(v[2] * inv) | ((uint32_t)to_act<F16OUT>(v[3] * inv) << 16));
 }
 
 template <bool F16OUT, bool SPLIT, bool PVS>
@@ -580,15 +672,35 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s) {
         const int span = a.window > 0 ? std::min(a.nk, qpb + 2 * a.window) : a.nk;
         // (measured: full 240 s 317 -> 262 us incl. the merge; at 8 key tiles or fewer -- cross attention,
         // sliding windows -- the extra prologue and merge cost more than the round saves)
-        static int mode = -1;  // ACE_MI_ATTN_KSPLIT=1 never / 2 always (where a workspace exists) / auto
+        static int mode = -1;  // ACE_MI_ATTN_KSPLIT=1 never / 2 always (where a workspace exists) / 4 see below / auto
         if (mode < 0) {
             const char* e = std::getenv("ACE_MI_ATTN_KSPLIT");
-            mode = (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 0;
+            mode = (e && (e[0] == '1' || e[0] == '2' || e[0] == '4')) ? e[0] - '0' : 0;
         }
         // blocks resident per CU: two for the single-fp16 kernel (66 KiB ring), one for the hi/lo ones
         const int per_cu = a.split ? 1 : 2;
-        const bool want = blocks * 10 < (int64_t)n_cu * per_cu * 16 && (span + KT - 1) / KT >= 16;
-        if (a.part && (mode == 2 || (mode == 0 && want))) b.ksplit = 2;
+        const int64_t slots = (int64_t)n_cu * per_cu;
+        const int ntiles = (span + KT - 1) / KT;
+        int S = 1;
+        if (ntiles >= 16) {
+            if (blocks * 10 < slots * 16) S = 2;
+        } else if (mode == 4) {
+            // ACE_MI_ATTN_KSPLIT=4: short key ranges (cross attention, sliding windows, short sequences) split too,
+            // while the grid stays within one round and every part keeps >= 2 key tiles.  Measured at 60 s
+            // (rocprof, profiles/r03_trace_60s_*.txt): attention 698 us + 48 merges 275 us per forward against
+            // ~950 us unsplit -- the merge launches (~5 us each) eat the gain, so not the default
+            while (S < 4 && blocks * 2 * S <= slots && ntiles >= 4 * S) S *= 2;
+        }
+        if (a.part && mode == 2) b.ksplit = 2;
+        else if (a.part && (mode == 0 || mode == 4)) b.ksplit = S;
+        // ACE_MI_ATTN_FUSED_MERGE=1: the last part of a group merges in the attention kernel (sc1 partial
+        // round trip, no merge launch) -- measured 2.6x slower attention at 60 s, so off by default
+        static int fm = -1;
+        if (fm < 0) {
+            const char* e = std::getenv("ACE_MI_ATTN_FUSED_MERGE");
+            fm = (e && e[0] == '1') ? 1 : 0;
+        }
+        b.fused_merge = fm;
     }
     const dim3 grid(8 * ((a.B * a.Hkv * n_qt * b.ksplit + 7) / 8));  // XCD-aware order, see attn_kernel
     const bool f16 = out_t == ActType::F16;
@@ -604,21 +716,29 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s) {
         f16 ? launch_t<true, false, false>(b, grid, s) : launch_t<false, false, false>(b, grid, s);
     }
     ACEMI_HIP(hipGetLastError());
-    if (b.ksplit > 1) {
+    if (b.ksplit > 1 && !b.fused_merge) {
         const int64_t rows = (int64_t)a.B * a.nq * a.Hq;
-        ACEMI_CHECK(b.ksplit == 2, "attention: the merge handles two key-split parts");
+        ACEMI_CHECK(b.ksplit == 2 || b.ksplit == 4, "attention: the merge handles 2 or 4 key-split parts");
         const dim3 mgrid((unsigned)((rows + 7) / 8));
-        if (out_t == ActType::F16)
-            hipLaunchKernelGGL(attn_merge_kernel<true>, mgrid, dim3(256), 0, s, b);
-        else
-            hipLaunchKernelGGL(attn_merge_kernel<false>, mgrid, dim3(256), 0, s, b);
+        if (b.ksplit == 2) {
+            if (out_t == ActType::F16)
+                hipLaunchKernelGGL((attn_merge_kernel<true, 2>), mgrid, dim3(256), 0, s, b);
+            else
+                hipLaunchKernelGGL((attn_merge_kernel<false, 2>), mgrid, dim3(256), 0, s, b);
+        } else {
+            if (out_t == ActType::F16)
+                hipLaunchKernelGGL((attn_merge_kernel<true, 4>), mgrid, dim3(256), 0, s, b);
+            else
+                hipLaunchKernelGGL((attn_merge_kernel<false, 4>), mgrid, dim3(256), 0, s, b);
+        }
         ACEMI_HIP(hipGetLastError());
     }
 }
 
 size_t attn_part_floats(int B, int nq, int Hq) {
     const size_t rows = (size_t)B * nq * Hq;
-    return 2 * rows * (D + 2);
+    // up to four key-split parts + one ticket word per (item, kv head, query tile) group (qpb >= 32)
+    return 4 * rows * (D + 2) + (size_t)B * Hq * ((nq + 31) / 32 + 1);
 }
 
 }  // namespace acemi

@@ -619,10 +619,12 @@ int pick_variant_q(int M, int N, int K, int fmt) {
         if (fmt != WF_Q4_K && N % 256 == 0 && mb192 * (N / 256) >= 256) return 21;
         return 20;
     }
-    // no split-K for the quantized tiles by default: whole forwards through the split 64-row tiles were not
-    // run-to-run identical (tools/diag_det.py, round 3; the kernel-level split tests pass) -- forced only
+    // Short sequences: round 1's LDS-dequant kernel (96 x 128).  Whole forwards through the 64 / 128-row
+    // register-dequant tiles (22, 23, split or not) were not run-to-run identical (tools/diag_det.py, round 3;
+    // every kernel-level test of them passes, the attention-prep epilogue is the one path those tests do not
+    // reach) -- forced only.
     (void)K;
-    return M > 256 ? 22 : 23;
+    return 7;
 }
 
 int pick_variant(int M, int N, int K, bool quant, int fmt) {
@@ -645,6 +647,9 @@ int pick_variant(int M, int N, int K, bool quant, int fmt) {
     // 1011 (256x256) vs 941 (v2), qkv 933 vs 902, down 922 (192x256) vs 818, o 814 vs 786; M = 24000 gate|up
     // 1089 vs 1016, qkv 941 vs 897, down 955 vs 915, o 767 (v2) vs 724; M = 6000 down 921 (192x256) vs 853.
     // At M = 3000 the 4-wave tiles stay ahead (their second block per CU hides prologue and epilogue).
+    // narrow outputs (proj_out: N = 128 at M = 3000 -- 16 tiles of 192 rows on a 256-CU chip, 28 TFLOP/s):
+    // 64x64 tiles split over 4 K parts
+    if (N <= 128 && M >= 512 && K / 64 >= 8) return 409;
     if (N % 256 == 0 && M >= 8192) {
         if (N >= 4096) return 10;
         if (M >= 20000) return K >= 4096 ? 10 : 2;
@@ -660,7 +665,21 @@ int pick_variant(int M, int N, int K, bool quant, int fmt) {
     // join's device-coherent partial round trip (~3-4 us after the main loop) costs more than the fuller grid
     if (N <= 2048 && K >= 4096 && M >= 1000 && M < 2000) return 207;
     const int64_t mb96 = (M + 95) / 96, mb64 = (M + 63) / 64;
-    if (mb96 * (N / 128) <= 256) return mb64 * (N / 128) >= 256 ? 8 : 9;
+    // Short sequences read every weight cold (each layer's weights were last touched one step earlier), so the
+    // picks below follow the cold-weight sweep (ACE_MI_BENCH_COLD=24, profiles/r03_msweep_cold_ns.jsonl), where
+    // the multi-stage rings keep more weight tiles in flight:
+    //  10 s (M = 125): gate|up 64x128 3-stage (296 vs 267 TFLOP/s for 64x64), qkv / o 64x64 4-stage (146 vs 114,
+    //  76 vs 74), the K = 6144 down 64x64 4-stage over 2 K parts (126 vs 69);
+    //  60 s (M = 750): qkv 96x128 (495 vs 433 for 64x128), down 64x128 3-stage over 2 K parts (387 vs 349)
+    if (M <= 256) {
+        if (K >= 4096) return 212;
+        return N >= 8192 ? 13 : 12;
+    }
+    if (K >= 4096 && mb96 * (N / 128) <= 256 && mb64 * (N / 128) < 256) return 213;
+    if (mb96 * (N / 128) <= 256) {
+        if (mb96 * (N / 128) == 256) return 7;  // one full round of 96-row tiles (60 s qkv)
+        return mb64 * (N / 128) >= 256 ? 8 : 9;
+    }
     if (m_edge(M, 96) >= m_edge(M, 128) - 0.02) return 7;  // N = 2048: 512 tiles, two per CU
     return 1;
 }
@@ -684,7 +703,8 @@ void launch_gemm(const uint16_t* A, int lda, const WeightView& W, int M, int N, 
         ACEMI_CHECK(epi.prep.q_col <= 0 && (epi.prep.k_col < 0 || epi.prep.k_col == 128 * nqc) &&
                         (epi.prep.v_col < 0 || epi.prep.v_col == 128 * (nqc + nkc)),
                     "gemm: fused attention prep expects the [q | k | v] head order");
-        v = v == 2 ? 3 : v == 5 ? 4 : v == 6 ? 1 : v == 9 ? 8 : v;
+        if (v >= 100 && g_forced_variant < 0) v %= 100;  // (the narrow-output split-K pick is not for the prep)
+        v = v == 2 ? 3 : v == 5 ? 4 : v == 6 ? 1 : v == 9 ? 8 : v == 12 ? 13 : v;
     }
     switch (W.fmt) {
         case WF_BF16:

@@ -23,6 +23,7 @@ DitEngine::DitEngine(int device) : device_(device) {
     const char* h = std::getenv("ACE_MI_QUANT_STAGE_SCOPE");
     stage_per_call_ = !(h && std::strcmp(h, "layer") == 0);
     stage_model_ = !(h && (std::strcmp(h, "call") == 0 || std::strcmp(h, "layer") == 0));  // default: model
+    if (const char* pf = std::getenv("ACE_MI_WEIGHT_PREFETCH")) prefetch_blocks_ = std::max(0, std::atoi(pf));
     // TEST ONLY: ACE_MI_TEST_FAULT="layer,row,col,amp" adds amp to one 16 x 128 tile of the residual right after
     // that layer's o-projection GEMM (the parity negative control of tests/test_gpu_parity_strict.py)
     if (const char* f = std::getenv("ACE_MI_TEST_FAULT")) {
@@ -37,6 +38,13 @@ DitEngine::~DitEngine() {
                    &mods_, &outmod_, &cos_, &sin_, &ein_, &knorm_tab_}) {
         if (b->p) (void)hipFree(b->p);
     }
+    if (pf_stream_) {
+        (void)hipStreamSynchronize(pf_stream_);
+        (void)hipStreamDestroy(pf_stream_);
+    }
+    if (pf_ev_) (void)hipEventDestroy(pf_ev_);
+    if (pf_done_) (void)hipEventDestroy(pf_done_);
+    if (pf_sink_.p) (void)hipFree(pf_sink_.p);
     if (ev0_) (void)hipEventDestroy(ev0_);
     if (ev1_) (void)hipEventDestroy(ev1_);
     if (wring_.p) (void)hipFree(wring_.p);
@@ -86,6 +94,34 @@ void DitEngine::stage_layer(int li, hipStream_t st) {
     tic(st);
     if (n > 0) launch_dequant_bf16_batch(jobs, n, st);
     toc("dequant_stage", st);
+}
+
+// Side-stream sweep of layer li's block weights (ACE_MI_WEIGHT_PREFETCH), ordered after the work already queued
+// on s; the forward joins the side stream before it returns.
+void DitEngine::prefetch_layer(int li, bool staged, hipStream_t s) {
+    if (!pf_stream_) {
+        ACEMI_HIP(hipStreamCreateWithFlags(&pf_stream_, hipStreamNonBlocking));
+        ACEMI_HIP(hipEventCreateWithFlags(&pf_ev_, hipEventDisableTiming));
+        ACEMI_HIP(hipEventCreateWithFlags(&pf_done_, hipEventDisableTiming));
+    }
+    ensure(pf_sink_, 256);
+    const LayerViews lw = layer_views(li, staged);
+    const DevLayer& ly = model_.layers[li];
+    const DevWeight* ws[6] = {&ly.w_qkv, &ly.w_o, &ly.w_cq, &ly.w_co, &ly.w_gu, &ly.w_down};
+    const WeightView* vs[6] = {&lw.qkv, &lw.o, &lw.cq, &lw.co, &lw.gu, &lw.down};
+    const void* ptrs[6];
+    size_t bytes[6];
+    int n = 0;
+    for (int i = 0; i < 6; ++i) {
+        if (weight_quantized(vs[i]->fmt) || !vs[i]->q) continue;  // bf16 / fp16 images only
+        ptrs[n] = vs[i]->q;
+        bytes[n] = (size_t)ws[i]->rows * ws[i]->cols * 2;
+        ++n;
+    }
+    if (n == 0) return;
+    ACEMI_HIP(hipEventRecord(pf_ev_, s));
+    ACEMI_HIP(hipStreamWaitEvent(pf_stream_, pf_ev_, 0));
+    launch_prefetch(ptrs, bytes, n, prefetch_blocks_, get<unsigned>(pf_sink_), pf_stream_);
 }
 
 // Layer li's bf16 image: its own slot when the images of the whole model are kept for the sampling call,
@@ -401,6 +437,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
     for (int li = 0; li < n_layers; ++li) {  // :1466-1535
         const DevLayer& ly = m.layers[li];
         if (staged && restage) stage_layer(li, s);
+        if (prefetch_blocks_ > 0 && li + 1 < n_layers && !(staged && restage)) prefetch_layer(li + 1, staged, s);
         const LayerViews lw = layer_views(li, staged);
         const float* lm = mods + (size_t)li * B * 6 * H;
         const float* shift_msa = lm + 0 * H;
@@ -585,6 +622,10 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
         tic(s);
         launch_gemm(head_in, kout * H, m.proj_out_w.view(), (int)M, P * c.audio_dim, kout * H, e, s);
         toc("gemm_proj_out", s);
+    }
+    if (pf_stream_) {  // the side stream's sweeps end before anything ordered after this forward on s
+        ACEMI_HIP(hipEventRecord(pf_done_, pf_stream_));
+        ACEMI_HIP(hipStreamWaitEvent(s, pf_done_, 0));
     }
 }
 

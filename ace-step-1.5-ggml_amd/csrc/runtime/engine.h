@@ -147,6 +147,14 @@ class DitEngine {
         int layer = -1, row = 0, col = 0;
         float amp = 0.f;
     } fault_;
+    // ACE_MI_WEIGHT_PREFETCH=B: at the start of layer l, a side stream sweeps layer l+1's block weights (B
+    // workgroups) so the memory-side cache holds them when its GEMMs start (short sequences read every weight
+    // cold: tools/gemm_msweep.py with ACE_MI_BENCH_COLD); 0 = off (default)
+    int prefetch_blocks_ = 0;
+    hipStream_t pf_stream_ = nullptr;
+    hipEvent_t pf_ev_ = nullptr, pf_done_ = nullptr;
+    Buf pf_sink_;
+    void prefetch_layer(int li, bool staged, hipStream_t s);
     // profiling
     bool profiling_ = false;
     hipEvent_t ev0_ = nullptr, ev1_ = nullptr;

@@ -2,7 +2,9 @@
 // the GPU parity tests can compare it with an fp64 / fp32 reference of the same op, and the kernel
 // micro-benchmarks of tools/.  Built only into libacestep_mi355x_selftest.so (the product objects + this
 // file, Makefile target `selftest`); the product library libacestep_mi355x.so does not contain them.
+#include <algorithm>
 #include <cstring>
+#include <cstdlib>
 #include <vector>
 
 #include "../../../include/acestep_mi355x_selftest.h"
@@ -90,6 +92,7 @@ struct AttnSetup {
         using namespace acemi;
         const int D = 128;
         const int nq_pad = (int)round_up(nq, 128), nk_pad = (int)round_up(nk, 128);
+        ACEMI_HIP(hipMemset(dpart.p, 0, attn_part_floats(B, nq, Hq) * 4));  // the key-split tickets start at 0
         nqf = (size_t)B * nq * Hq * D;
         const size_t nkvf = (size_t)B * nk * 2 * Hkv * D;
         ACEMI_HIP(hipMemcpy(dq.p, q, nqf * 4, hipMemcpyHostToDevice));
@@ -263,14 +266,22 @@ ace_ggml_status ace_mi_bench_gemm(int32_t act_type, int32_t epi, int32_t variant
         e.gate = dG.as<float>();
         e.rows_per_item = M;
         const ActType at = act_type == 1 ? ActType::F16 : ActType::BF16;
+        // ACE_MI_BENCH_COLD=R: rotate over R device copies of W (R x |W| beyond the 256 MB MALL = weights cold in
+        // every launch, as in a forward where each layer's weights were last read one step earlier)
+        const char* ce = std::getenv("ACE_MI_BENCH_COLD");
+        const int R = ce ? std::max(1, std::min(64, std::atoi(ce))) : 1;
+        DevMem dWr((size_t)R * hw.size() * 2);
+        for (int r = 0; r < R; ++r)
+            ACEMI_HIP(hipMemcpy(dWr.as<uint16_t>() + (size_t)r * hw.size(), dW.p, hw.size() * 2, hipMemcpyDeviceToDevice));
+        auto wptr = [&](int i) { return dWr.as<uint16_t>() + (size_t)(i % R) * hw.size(); };
         gemm_force_variant(variant);
         hipEvent_t e0, e1;
         ACEMI_HIP(hipEventCreate(&e0));
         ACEMI_HIP(hipEventCreate(&e1));
-        for (int i = 0; i < 3; ++i) launch_gemm(at, dA.as<uint16_t>(), K, dW.as<uint16_t>(), K, M, N, K, e, nullptr);
+        for (int i = 0; i < 3; ++i) launch_gemm(at, dA.as<uint16_t>(), K, wptr(i), K, M, N, K, e, nullptr);
         ACEMI_HIP(hipEventRecord(e0, nullptr));
         for (int i = 0; i < iters; ++i)
-            launch_gemm(at, dA.as<uint16_t>(), K, dW.as<uint16_t>(), K, M, N, K, e, nullptr);
+            launch_gemm(at, dA.as<uint16_t>(), K, wptr(i + 3), K, M, N, K, e, nullptr);
         ACEMI_HIP(hipEventRecord(e1, nullptr));
         ACEMI_HIP(hipEventSynchronize(e1));
         float ms = 0.f;

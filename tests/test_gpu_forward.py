@@ -337,7 +337,9 @@ def test_fused_qkv_prep_is_bit_exact(tiny_ckpt, monkeypatch, width, variant):
             h = r.standard_normal((B, T, 64)).astype(np.float32)
             c = r.standard_normal((B, T, 128)).astype(np.float32)
             e = r.standard_normal((B, L, H)).astype(np.float32)
-            capi.gemm_variant(variant if fused else -1)  # the 8-wave tiles' two-heads-per-tile prep (10, 11)
+            # the same tiles on both sides (the 8-wave tiles' two-heads-per-tile prep: 10, 11), so only the prep
+            # path differs (a split-K pick on one side would change the other GEMMs' summation order)
+            capi.gemm_variant(variant)
             try:
                 outs[(fused, B, T)] = _batched(br, h, c, e, 0.7)
             finally:

@@ -231,7 +231,7 @@ def test_gguf_tiny_matches_oracle(tiny_ckpt, monkeypatch, quant):
 
 
 @pytest.mark.parametrize("qtype", ["q8_0", "q4_k", "q6_k"])
-@pytest.mark.parametrize("width", ["tiny", "full"])
+@pytest.mark.parametrize("width", ["tiny", "full", "240s"])
 def test_staged_dequant_equals_fused(tiny_ckpt, monkeypatch, qtype, width):
     """The staged dequant (ACE_MI_QUANT_STAGED, default: each layer's bf16 weight image expanded right before the
     layer, dense GEMMs) and the dequant-fused GEMMs (ACE_MI_QUANT_STAGED=0) give the same bits: both multiply
@@ -239,6 +239,10 @@ def test_staged_dequant_equals_fused(tiny_ckpt, monkeypatch, qtype, width):
     from acestep_mi355x.capi import GGMLCAPIBridge
     if width == "tiny":
         d, H, T, L = tiny_ckpt, 256, 301, 20
+    elif width == "240s":  # M = 3000: the register-dequant 192-row tiles (incl. their attention-prep epilogue)
+        from acestep_mi355x.synthetic import cached_checkpoint, make_config
+        d, H, T, L = cached_checkpoint(make_config(num_hidden_layers=2), seed=0, backend="torch"), 2048, 6000, 512
+        monkeypatch.setenv("ACE_GGML_DIT_MAX_LAYERS", "2")
     else:
         from acestep_mi355x.synthetic import cached_checkpoint, make_config
         d, H, T, L = cached_checkpoint(make_config(num_hidden_layers=3), seed=0, backend="torch"), 2048, 400, 64
