@@ -252,13 +252,21 @@ def test_staged_dequant_equals_fused(tiny_ckpt, monkeypatch, qtype, width):
     h = rng.standard_normal((T, 64)).astype(np.float32)
     c = rng.standard_normal((T, 128)).astype(np.float32)
     e = rng.standard_normal((L, H)).astype(np.float32)
+    # short sequences: the same 96 x 128 tiles on both paths (the automatic dense pick there splits the K = 6144
+    # down projection over two blocks, a different summation order from the unsplit fused tile); at 240 s both
+    # paths run their automatic tiles (staged: dense 192 / 96-row; fused: the register-dequant 192-row tiles)
+    from acestep_mi355x import capi
     outs = []
     for staged in ("1", "0"):
         monkeypatch.setenv("ACE_MI_QUANT_STAGED", staged)
         br = GGMLCAPIBridge()
         br.load_dit(d)
-        outs.append(br.dit_forward_tfirst(h, c, e, None, None, 0.6, 0.6))
-        outs.append(br.dit_forward_tfirst(h, c, e, None, None, 0.6, 0.6))  # slot reused by a second forward
+        capi.gemm_variant(-1 if width == "240s" else 7)
+        try:
+            outs.append(br.dit_forward_tfirst(h, c, e, None, None, 0.6, 0.6))
+            outs.append(br.dit_forward_tfirst(h, c, e, None, None, 0.6, 0.6))  # slot reused by a second forward
+        finally:
+            capi.gemm_variant(-1)
         br.close()
     assert np.isfinite(outs[0]).all()
     for o in outs[1:]:
