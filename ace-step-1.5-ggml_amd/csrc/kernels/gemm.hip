@@ -543,7 +543,8 @@ void launch_cfg8(const GemmParams& p, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Skinny GEMM (variant 30) for very short sequences (M <= 128: 10 s of audio is M = 125): every output
+// Skinny GEMM (variant 30, forced only: measured 2x slower than the tiled kernels at 10 s, see pick_variant)
+// for very short sequences (M <= 128: 10 s of audio is M = 125): every output
 // column slice of 16 * TN columns is one workgroup over ALL M rows, its four waves split K four ways and the
 // partial tiles are summed in wave order through LDS (no global join) before the shared epilogue.  Operands
 // come straight from global memory into registers (A is L2-resident: 125 x 2048 bf16 = 0.5 MB; each W
@@ -740,8 +741,8 @@ int pick_variant(int M, int N, int K, bool quant, int fmt) {
     const int64_t mb192 = (M + 191) / 192;
     const bool edge_ok = m_edge(M, 192) >= m_edge(M, 128) - 0.02;
     if (quant) return pick_variant_q(M, N, K, fmt);
-    // very short sequences (10 s: M = 125): the skinny weight-stream kernel (launch_skinny checks the shape)
-    if (M <= 128 && K % 1024 == 0) return 30;
+    // (variant 30, the skinny weight-stream kernel, is forced-only: at 10 s it ran the block linears 2x slower
+    // than the tiles below -- every 16-column workgroup re-reads all of A with 16-byte row-scattered loads)
     // 8-wave ping-pong tiles for batched sequences (tools/gemm_msweep.py on MI355X, TFLOP/s): M = 12000 gate|up
     // 1011 (256x256) vs 941 (v2), qkv 933 vs 902, down 922 (192x256) vs 818, o 814 vs 786; M = 24000 gate|up
     // 1089 vs 1016, qkv 941 vs 897, down 955 vs 915, o 767 (v2) vs 724; M = 6000 down 921 (192x256) vs 853.

@@ -48,6 +48,8 @@ DitEngine::~DitEngine() {
     if (ev0_) (void)hipEventDestroy(ev0_);
     if (ev1_) (void)hipEventDestroy(ev1_);
     if (wring_.p) (void)hipFree(wring_.p);
+    for (auto& kv : img_)
+        if (kv.second.p) (void)hipFree(kv.second.p);
 }
 
 namespace {
@@ -94,6 +96,21 @@ void DitEngine::stage_layer(int li, hipStream_t st) {
     tic(st);
     if (n > 0) launch_dequant_bf16_batch(jobs, n, st);
     toc("dequant_stage", st);
+}
+
+WeightView DitEngine::dense_view(const DevWeight& w, hipStream_t s) {
+    WeightView v = w.view();
+    if (!staged_quant_ || !stage_per_call_ || !weight_quantized(v.fmt) || !v.q) return v;
+    Buf& b = img_[v.q];
+    if (!b.p) {
+        ensure(b, (size_t)w.rows * w.cols * 2);
+        launch_dequant_bf16(v, w.rows, w.cols, static_cast<uint16_t*>(b.p), s);
+    }
+    v.fmt = WF_BF16;
+    v.q = b.p;
+    v.s = nullptr;
+    v.ld = w.cols;
+    return v;
 }
 
 // Side-stream sweep of layer li's block weights (ACE_MI_WEIGHT_PREFETCH), ordered after the work already queued
@@ -311,7 +328,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
         e.c_f32 = x;
         e.ldc = H;
         tic(s);
-        launch_gemm(a0, kin * P * c.in_channels, m.proj_in_w.view(), (int)M, H, kin * P * c.in_channels, e, s);
+        launch_gemm(a0, kin * P * c.in_channels, dense_view(m.proj_in_w, s), (int)M, H, kin * P * c.in_channels, e, s);
         toc("gemm_proj_in", s);
     }
 
@@ -357,7 +374,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
         e.bias = m.cond_b;
         e.c_act = encp;
         e.ldc = H;
-        launch_gemm(enc_act, H, m.cond_w.view(), (int)Me, H, H, e, s);
+        launch_gemm(enc_act, H, dense_view(m.cond_w, s), (int)Me, H, H, e, s);
         toc("gemm_condition", s);
         // one GEMM for every layer's cross k|v when the weights are fused: ckv [Me][n_layers*2kd]
         const bool fused = m.w_ckv_all.q != nullptr;
@@ -368,7 +385,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
             ek.c_f32 = get<float>(ckv_);
             ek.ldc = ld_ckv;
             tic(s);
-            launch_gemm(encp, H, m.w_ckv_all.view(), (int)Me, ld_ckv, H, ek, s);  // first n_layers layers
+            launch_gemm(encp, H, dense_view(m.w_ckv_all, s), (int)Me, ld_ckv, H, ek, s);  // first n_layers layers
             toc("gemm_cross_kv", s);
         }
         for (int li = 0; li < n_layers; ++li) {
@@ -379,7 +396,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
                 ek.c_f32 = get<float>(ckv_);
                 ek.ldc = 2 * kd;
                 tic(s);
-                launch_gemm(encp, H, ly.w_ckv.view(), (int)Me, 2 * kd, H, ek, s);
+                launch_gemm(encp, H, dense_view(ly.w_ckv, s), (int)Me, 2 * kd, H, ek, s);
                 toc("gemm_cross_kv", s);
             }
             PrepArgs pa{};
@@ -620,7 +637,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
         e.out_ch = c.audio_dim;
         e.patch = P;
         tic(s);
-        launch_gemm(head_in, kout * H, m.proj_out_w.view(), (int)M, P * c.audio_dim, kout * H, e, s);
+        launch_gemm(head_in, kout * H, dense_view(m.proj_out_w, s), (int)M, P * c.audio_dim, kout * H, e, s);
         toc("gemm_proj_out", s);
     }
     if (pf_stream_) {  // the side stream's sweeps end before anything ordered after this forward on s

@@ -7,6 +7,7 @@
 // issues serially per item (scripts/run_non_ggml_real_case.py:518-527).
 #pragma once
 
+#include <map>
 #include <memory>
 #include <vector>
 
@@ -140,6 +141,11 @@ class DitEngine {
     size_t stage_slot_bytes_ = 0;
     int stage_layers_ = 0;  // layers whose images wring_ holds (per-call scope)
     Buf wring_;
+    // bf16 images of the quantized weights outside the six block matrices (condition embedder, every layer's
+    // cross k|v, proj in / out), expanded at their first use and kept while the weights are loaded (model and
+    // call scope; the layer scope runs them through the dequant-fused GEMM)
+    std::map<const void*, Buf> img_;
+    WeightView dense_view(const DevWeight& w, hipStream_t s);
     char* stage_slot(int li);
     LayerViews layer_views(int li, bool staged);
     void stage_layer(int li, hipStream_t st);
