@@ -748,8 +748,9 @@ int pick_variant(int M, int N, int K, bool quant, int fmt) {
     // 1089 vs 1016, qkv 941 vs 897, down 955 vs 915, o 767 (v2) vs 724; M = 6000 down 921 (192x256) vs 853.
     // At M = 3000 the 4-wave tiles stay ahead (their second block per CU hides prologue and epilogue).
     // narrow outputs (proj_out: N = 128 at M = 3000 -- 16 tiles of 192 rows on a 256-CU chip, 28 TFLOP/s):
-    // 64x64 tiles split over 4 K parts
-    if (N <= 128 && M >= 512 && K / 64 >= 8) return 409;
+    // 64x64 tiles (94 workgroups).  Not split over K: the summation order then stays the one every other tile
+    // (and the dequant-fused kernels) uses, which the staged == fused test relies on
+    if (N <= 128 && M >= 512) return 9;
     if (N % 256 == 0 && M >= 8192) {
         if (N >= 4096) return 10;
         if (M >= 20000) return K >= 4096 ? 10 : 2;
