@@ -61,7 +61,7 @@ struct ReadRows<N, N, STRIDE> {
 };
 
 template <bool FUSE2>
-__global__ void __launch_bounds__(256) conv_gemm_kernel(ConvGemmArgs p) {
+__global__ void __launch_bounds__(256, 2) conv_gemm_kernel(ConvGemmArgs p) {
     constexpr int BM = 128, BN = 128, WM = 2, WN = 2, NW = 4;
     constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
     constexpr int BK = 64, ROWB = BK * 2, STAGE = (BM + BN) * ROWB;
@@ -246,54 +246,82 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(ConvGemmArgs p) {
     }
     const float* bias_e = FUSE2 ? p.bias2 : p.bias;
 
-    // epilogue: (m, n) -> output time u and channel co; bias, residual, store, next Snake
-    // A thread's TN output columns are fixed, so their channel, transposed-conv phase, bias and Snake
-    // parameters are loaded once (not per element); the sequence split is one division per row.
-    const int ccol = lane & 15, crow = (lane >> 4) * 4;
-    int co_j[TN], rr_j[TN];
-    float bias_j[TN], ea_j[TN], reb_j[TN];
+    // Epilogue through LDS: the bias-added tile goes to LDS as f32 [BM][BN] (64 KB = both stage buffers), then
+    // every wave sweeps two whole tile rows per instruction (lane = 4 consecutive columns), so the residual read,
+    // the f32 store and the fp16 Snake store are 16 / 16 / 8-byte accesses over 512 contiguous bytes of a row.
+    // (From the accumulator layout each wave instruction touched 4 rows x 64 B, with 4-byte accesses; at 128
+    // channels the read-modify-write of x cost as much as the MFMAs.)  Same arithmetic per element: acc + bias,
+    // then x + that, then the Snake of the sum.
+    static_assert(BM * BN * 4 <= 2 * STAGE, "epilogue tile must fit the stage buffers");
+    float* zt = reinterpret_cast<float*>(smem);
+    {
+        const int ccol = lane & 15, crow = (lane >> 4) * 4;
+        __syncthreads();  // every wave is done with the stage buffers / the fused conv's y tile
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-        const int n = n0 + wn0 + j * 16 + ccol;
-        rr_j[j] = p.up > 1 ? n / p.Cout : 0;
-        co_j[j] = n - rr_j[j] * p.Cout;
-        bias_j[j] = bias_e ? bias_e[co_j[j]] : 0.f;
-        ea_j[j] = p.snake_ea ? p.snake_ea[co_j[j]] : 0.f;
-        reb_j[j] = p.snake_eb ? __builtin_amdgcn_rcpf(p.snake_eb[co_j[j]]) : 0.f;
+        for (int j = 0; j < TN; ++j) {
+            const int col = wn0 + j * 16 + ccol;
+            int co = n0 + col;
+            if (p.up > 1) co -= (co / p.Cout) * p.Cout;
+            const float b = bias_e ? bias_e[co] : 0.f;
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    zt[(wm0 + i * 16 + crow + r) * BN + col] = bias_e ? rn_add(acc[i][j][r], b) : acc[i][j][r];
+        }
+        __syncthreads();
     }
-    // Per 16-row group i: (sequence, row within it) of its 4 rows, then the residual's 16 old values
-    // loaded before the group's first store (interleaved, every load waited for the store before it;
-    // a whole-tile preload held 64 more registers and halved the occupancy).
+    const int c4 = (lane & 31) * 4;
+    const int n = n0 + c4;
+    const int rr = p.up > 1 ? n / p.Cout : 0;
+    const int co = n - rr * p.Cout;
+    float ea[4], reb[4];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-        int it_r[4], ml_r[4];
-        float xo[4][TN];
+    for (int e = 0; e < 4; ++e) {
+        ea[e] = p.snake_ea ? p.snake_ea[co + e] : 0.f;
+        reb[e] = p.snake_eb ? __builtin_amdgcn_rcpf(p.snake_eb[co + e]) : 0.f;
+    }
+    constexpr int RPI = NW * 2;  // tile rows per sweep iteration
+    constexpr int UNR = 4;       // iterations whose residual loads are issued together
+    static_assert((BM / RPI) % UNR == 0, "epilogue sweep");
+#pragma unroll 1
+    for (int it0 = 0; it0 < BM / RPI; it0 += UNR) {
+        int64_t o[UNR];
+        float4 xo[UNR];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int m = m0 + wm0 + i * 16 + crow + r;
-            it_r[r] = m < p.M ? m / Mi : -1;
-            ml_r[r] = m - it_r[r] * Mi;
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                const int u = p.up > 1 ? ml_r[r] * p.up + rr_j[j] - p.crop : ml_r[r];
-                const bool ok = it_r[r] >= 0 && u >= 0 && u < p.T_out;
-                xo[r][j] = (ok && p.resid) ? p.X[((int64_t)it_r[r] * p.T_out + u) * p.Cout + co_j[j]] : 0.f;
+        for (int q = 0; q < UNR; ++q) {
+            const int row = (it0 + q) * RPI + wid * 2 + (lane >> 5);
+            const int m = m0 + row;
+            o[q] = -1;
+            xo[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (m < p.M) {
+                const int item = m / Mi, ml = m - item * Mi;
+                const int u = p.up > 1 ? ml * p.up + rr - p.crop : ml;
+                if (u >= 0 && u < p.T_out) {
+                    o[q] = ((int64_t)item * p.T_out + u) * p.Cout + co;
+                    if (p.resid) xo[q] = *reinterpret_cast<const float4*>(p.X + o[q]);
+                }
             }
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            if (it_r[r] < 0) continue;
-            const int64_t obase = (int64_t)it_r[r] * p.T_out;
+        for (int q = 0; q < UNR; ++q) {
+            if (o[q] < 0) continue;
+            const int row = (it0 + q) * RPI + wid * 2 + (lane >> 5);
+            float4 v = *reinterpret_cast<const float4*>(zt + row * BN + c4);
+            if (p.resid) {
+                v.x = rn_add(xo[q].x, v.x);
+                v.y = rn_add(xo[q].y, v.y);
+                v.z = rn_add(xo[q].z, v.z);
+                v.w = rn_add(xo[q].w, v.w);
+            }
+            if (p.store_x) *reinterpret_cast<float4*>(p.X + o[q]) = v;
+            if (p.S_out) {
+                const float vv[4] = {v.x, v.y, v.z, v.w};
+                uint16_t h[4];
 #pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                const int u = p.up > 1 ? ml_r[r] * p.up + rr_j[j] - p.crop : ml_r[r];
-                if (u < 0 || u >= p.T_out) continue;
-                const int64_t o = (obase + u) * p.Cout + co_j[j];
-                float v = acc[i][j][r];
-                if (bias_e) v = rn_add(v, bias_j[j]);
-                if (p.resid) v = rn_add(xo[r][j], v);
-                if (p.store_x) p.X[o] = v;
-                if (p.S_out) p.S_out[o] = f32_to_f16(p.snake_ea ? snake_f(v, ea_j[j], reb_j[j]) : v);
+                for (int e = 0; e < 4; ++e) h[e] = f32_to_f16(p.snake_ea ? snake_f(vv[e], ea[e], reb[e]) : vv[e]);
+                *reinterpret_cast<uint2*>(p.S_out + o[q]) =
+                    make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16));
             }
         }
     }
@@ -403,6 +431,7 @@ void launch_conv_gemm(const ConvGemmArgs& a, hipStream_t s) {
     ACEMI_CHECK(a.up > 1 || a.N == a.Cout, "conv_gemm: N must equal Cout");
     ACEMI_CHECK(!(a.resid || a.store_x) || a.X, "conv_gemm: null X");
     ACEMI_CHECK(a.items >= 1 && a.M % a.items == 0, "conv_gemm: rows must split evenly into the sequences");
+    ACEMI_CHECK(a.Cout % 4 == 0, "conv_gemm: output channels must be a multiple of 4");
     const int nbm = (a.M + 127) / 128, nbn = a.N / 128;
     if (a.W2) {
         ACEMI_CHECK(a.N == 128 && a.Cout == 128 && a.up <= 1 && a.snake2_ea && a.snake2_eb,
