@@ -15,6 +15,9 @@
 // the running activation, and the NEXT Snake (x + sin^2(e^a x)/e^b, f32) written as the fp16
 // operand of the next conv.
 #include <cmath>
+#include <algorithm>
+#include <cstdlib>
+#include <type_traits>
 
 #include "../kernels.h"
 #include "lds_asm.h"
@@ -60,45 +63,68 @@ struct ReadRows<N, N, STRIDE> {
     __device__ __forceinline__ static void run(uint32_t, uint4 (&)[N][2], int) {}
 };
 
-template <bool FUSE2>
+// HD > 0: the 128-channel k7 conv of a residual unit with dilation HD (Cin = Cout = 128, pad 3*HD).  Its A
+// operand is staged ONCE per tile: the BM + 6*HD input rows the tile's seven taps read (the halo) land in LDS
+// as 256-byte rows (16-byte chunks XOR-swizzled by row & 15), and tap k reads its fragments at a shift of
+// k*HD rows; only the weights stream through the two-buffer ring (4 instead of 8 LDS-DMA pieces per wave per
+// k-tile, A read from HBM / L2 once instead of seven times).  Tiles do not cross sequences (block -> (item,
+// tile of that item)).  HD = 0: the generic implicit-GEMM staging (A rows re-gathered per k-tile).
+template <bool FUSE2, int HD>
 __global__ void __launch_bounds__(256, 2) conv_gemm_kernel(ConvGemmArgs p) {
     constexpr int BM = 128, BN = 128, WM = 2, WN = 2, NW = 4;
     constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
     constexpr int BK = 64, ROWB = BK * 2, STAGE = (BM + BN) * ROWB;
-    constexpr int G_PER_WAVE = (BM + BN) / 8 / NW;  // 8
+    constexpr int WSTAGE = BN * ROWB;                      // weight k-tile (halo mode)
+    constexpr int HR = BM + 6 * HD;                        // halo rows
+    constexpr int HP = (HR + 3) / 4;                       // 1 KiB halo pieces (4 rows of 256 B)
+    constexpr int HPW = (HP + NW - 1) / NW;                // pieces per wave (the last clamped: duplicates)
+    constexpr int HALO = HP * 1024;
+    constexpr int G_PER_WAVE = HD ? BN / 8 / NW : (BM + BN) / 8 / NW;  // LDS-DMA pieces per wave per k-tile
+    constexpr int SMEM = HD ? HALO + 2 * WSTAGE : 2 * STAGE;
+    static_assert(BM * BN * 4 <= SMEM, "epilogue tile must fit the LDS image");
 
-    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+    __shared__ __attribute__((aligned(16))) char smem[SMEM];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
 
-    // block -> tile: XCD-aware bijective remap, then M-grouped order
-    const int nbm = (p.M + BM - 1) / BM;
-    const int nbn = p.N / BN;
+    // block -> tile: XCD-aware bijective remap (consecutive tiles on one XCD), then M-grouped order
+    const int Mi = p.M / p.items;  // rows per sequence
     int bid = blockIdx.x;
     {
         const int nwg = gridDim.x, xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
         bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
     }
-    constexpr int GM = 8;
-    const int group = bid / (GM * nbn);
-    const int first_m = group * GM;
-    const int gm = min(nbm - first_m, GM);
-    const int m0 = (first_m + (bid % (GM * nbn)) % gm) * BM;
-    const int n0 = ((bid % (GM * nbn)) / gm) * BN;
+    int m0, n0, mlim;
+    if constexpr (HD > 0) {
+        const int nt = (Mi + BM - 1) / BM;
+        const int item = bid / nt;
+        m0 = item * Mi + (bid - item * nt) * BM;
+        mlim = item * Mi + Mi;
+        n0 = 0;
+    } else {
+        const int nbm = (p.M + BM - 1) / BM;
+        const int nbn = p.N / BN;
+        constexpr int GM = 8;
+        const int group = bid / (GM * nbn);
+        const int first_m = group * GM;
+        const int gm = min(nbm - first_m, GM);
+        m0 = (first_m + (bid % (GM * nbn)) % gm) * BM;
+        n0 = ((bid % (GM * nbn)) / gm) * BN;
+        mlim = p.M;
+    }
     const int wm0 = (wid / WN) * WTM, wn0 = (wid % WN) * WTN;
 
     const int cblocks = p.Cin / BK;
-    const int nk = p.taps * cblocks;
+    const int nk = (p.dbg & 1) ? min(2, p.taps * cblocks) : p.taps * cblocks;
     const int K = p.taps * p.Cin;
 
     // per-lane staging rows (fixed) and swizzled 16-byte chunk
-    const int Mi = p.M / p.items;  // rows per sequence
     int srow[G_PER_WAVE];
     int schunk[G_PER_WAVE];
     int sml[G_PER_WAVE];           // row within its sequence (A rows)
     int64_t sbase[G_PER_WAVE];     // first input row of its sequence
 #pragma unroll
     for (int j = 0; j < G_PER_WAVE; ++j) {
-        const int row = (wid + NW * j) * 8 + (lane >> 3);
+        const int row = (wid + NW * j) * 8 + (lane >> 3) + (HD ? BM : 0);  // halo mode: weight rows only
         srow[j] = row;
         schunk[j] = (lane & 7) ^ swz(row);
         const int m = m0 + row, item = m / Mi;
@@ -106,7 +132,7 @@ __global__ void __launch_bounds__(256, 2) conv_gemm_kernel(ConvGemmArgs p) {
         sbase[j] = (int64_t)item * p.T_in;
     }
     auto stage = [&](int buf, int kt) {
-        char* base = smem + buf * STAGE;
+        char* base = HD ? smem + HALO + buf * WSTAGE - BM * ROWB : smem + buf * STAGE;
         const int tap = kt / cblocks;
         const int c0 = (kt - tap * cblocks) * BK;
         const int shift = tap * p.dil - p.pad;
@@ -115,7 +141,7 @@ __global__ void __launch_bounds__(256, 2) conv_gemm_kernel(ConvGemmArgs p) {
         for (int j = 0; j < G_PER_WAVE; ++j) {
             const int row = srow[j];
             const uint16_t* src;
-            if (row < BM) {
+            if (!HD && row < BM) {
                 const int m = m0 + row;
                 const int t = sml[j] * istr + shift;
                 src = (m < p.M && t >= 0 && t < p.T_in) ? p.S + (sbase[j] + t) * p.Cin + c0 + schunk[j] * 8
@@ -124,8 +150,24 @@ __global__ void __launch_bounds__(256, 2) conv_gemm_kernel(ConvGemmArgs p) {
                 src = p.W + (int64_t)(n0 + row - BM) * K + kt * BK + schunk[j] * 8;
             }
             __builtin_amdgcn_global_load_lds((const void*)src,
-                                             (__attribute__((address_space(3))) void*)(base + (wid + NW * j) * 1024),
+                                             (__attribute__((address_space(3))) void*)(base + (wid + NW * j + (HD ? BM / 8 : 0)) * 1024),
                                              16, 0, 0);
+        }
+    };
+    // halo mode: input rows t0 - 3*HD .. t0 + BM - 1 + 3*HD of the tile's sequence (zero rows outside it)
+    auto stage_halo = [&]() {
+        const int item = m0 / Mi, t0 = m0 - item * Mi;
+        const int hc = lane & 15;
+#pragma unroll
+        for (int j = 0; j < HPW; ++j) {
+            const int pc = min(wid + NW * j, HP - 1);
+            const int hr = pc * 4 + (lane >> 4);
+            const int t = t0 - 3 * HD + hr;
+            const int cl = hc ^ (hr & 15);
+            const uint16_t* src = (hr < HR && t >= 0 && t < p.T_in) ? p.S + ((int64_t)item * p.T_in + t) * 128 + cl * 8
+                                                                     : p.zero + hc * 8;
+            __builtin_amdgcn_global_load_lds((const void*)src,
+                                             (__attribute__((address_space(3))) void*)(smem + pc * 1024), 16, 0, 0);
         }
     };
 
@@ -137,13 +179,21 @@ __global__ void __launch_bounds__(256, 2) conv_gemm_kernel(ConvGemmArgs p) {
 
     const uint32_t lds0 = lds_addr(smem);
     const int lrow = lane & 15, lchunk = lane >> 4;
-    auto read_frags = [&](int buf, uint4 (&a)[TM][2], uint4 (&b)[TN][2]) {
-        const uint32_t sb = lds0 + buf * STAGE;
+    auto read_frags = [&](int kt, uint4 (&a)[TM][2], uint4 (&b)[TN][2]) {
+        const int buf = kt & 1;
+        const uint32_t sbB = HD ? lds0 + HALO + buf * WSTAGE : lds0 + buf * STAGE + BM * ROWB;
+        const int tap = kt >> 1, half = kt & 1;                 // (halo mode: Cin = 128, two k-tiles per tap)
+        const int hrow = wm0 + lrow + tap * HD;                 // halo row of fragment 0 (+16 per fragment)
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
             const int ch = (kk * 4 + lchunk) ^ ((lrow >> 1) & 7);
-            ReadRows<0, TN, 16 * ROWB>::run(sb + BM * ROWB + (wn0 + lrow) * ROWB + ch * 16, b, kk);
-            ReadRows<0, TM, 16 * ROWB>::run(sb + (wm0 + lrow) * ROWB + ch * 16, a, kk);
+            ReadRows<0, TN, 16 * ROWB>::run(sbB + (wn0 + lrow) * ROWB + ch * 16, b, kk);
+            if constexpr (HD > 0) {
+                const int hch = (half * 8 + kk * 4 + lchunk) ^ (hrow & 15);
+                ReadRows<0, TM, 16 * 256>::run(lds0 + hrow * 256 + hch * 16, a, kk);
+            } else {
+                ReadRows<0, TM, 16 * ROWB>::run(lds0 + buf * STAGE + (wm0 + lrow) * ROWB + ch * 16, a, kk);
+            }
         }
         lds_wait_all();
     };
@@ -161,6 +211,7 @@ __global__ void __launch_bounds__(256, 2) conv_gemm_kernel(ConvGemmArgs p) {
 
     // PIPE-1 schedule of the DiT GEMM (gemm.hip): fragments read up front, raw barrier frees the
     // buffer, tile kt+2 staged while the MFMAs run, counted vmcnt retires kt+1.
+    if constexpr (HD > 0) stage_halo();  // retired together with k-tile 0
     stage(0, 0);
     if (nk > 1) {
         stage(1, 1);
@@ -174,7 +225,7 @@ __global__ void __launch_bounds__(256, 2) conv_gemm_kernel(ConvGemmArgs p) {
     for (int kt = 0; kt < nk; ++kt) {
         const int cur = kt & 1;
         uint4 a[TM][2], b[TN][2];
-        read_frags(cur, a, b);
+        read_frags(kt, a, b);
         __builtin_amdgcn_s_barrier();
         const bool more = kt + 2 < nk;
         if (more) stage(cur, kt + 2);
@@ -189,7 +240,7 @@ __global__ void __launch_bounds__(256, 2) conv_gemm_kernel(ConvGemmArgs p) {
         }
     }
 
-    if constexpr (FUSE2) {
+    if (FUSE2 && !(p.dbg & 2)) {
         // k1 conv of the residual unit on this tile (N = Cout = 128: the tile holds every channel).
         // W2 fragments straight from global memory (32 KB, L2-resident), issued before the LDS round trip.
         const int lrow2 = lane & 15, lch2 = lane >> 4;
@@ -271,6 +322,7 @@ __global__ void __launch_bounds__(256, 2) conv_gemm_kernel(ConvGemmArgs p) {
         }
         __syncthreads();
     }
+    if (p.dbg & 4) return;
     const int c4 = (lane & 31) * 4;
     const int n = n0 + c4;
     const int rr = p.up > 1 ? n / p.Cout : 0;
@@ -294,7 +346,7 @@ __global__ void __launch_bounds__(256, 2) conv_gemm_kernel(ConvGemmArgs p) {
             const int m = m0 + row;
             o[q] = -1;
             xo[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (m < p.M) {
+            if (m < mlim) {
                 const int item = m / Mi, ml = m - item * Mi;
                 const int u = p.up > 1 ? ml * p.up + rr - p.crop : ml;
                 if (u >= 0 && u < p.T_out) {
@@ -424,7 +476,15 @@ __global__ void __launch_bounds__(256) conv_out_kernel(const uint16_t* __restric
 
 }  // namespace
 
-void launch_conv_gemm(const ConvGemmArgs& a, hipStream_t s) {
+// ACE_MI_VAE_HALO=0: the residual units' k7 convs through the generic staging (A/B switch, read per launch)
+static bool vae_halo_on() {
+    const char* e = std::getenv("ACE_MI_VAE_HALO");
+    return !(e && e[0] == '0');
+}
+
+void launch_conv_gemm(const ConvGemmArgs& a_in, hipStream_t s) {
+    ConvGemmArgs a = a_in;
+    if (const char* e = std::getenv("ACE_MI_VAE_DBG")) a.dbg = std::atoi(e);
     ACEMI_CHECK(a.Cin % 64 == 0 && a.N % 128 == 0 && a.M >= 1 && a.taps >= 1, "conv_gemm: unsupported shape");
     ACEMI_CHECK(a.S && a.W && a.zero, "conv_gemm: null operand");
     ACEMI_CHECK(a.up <= 1 || a.N == a.up * a.Cout, "conv_gemm: transposed conv needs N = stride * Cout");
@@ -433,12 +493,30 @@ void launch_conv_gemm(const ConvGemmArgs& a, hipStream_t s) {
     ACEMI_CHECK(a.items >= 1 && a.M % a.items == 0, "conv_gemm: rows must split evenly into the sequences");
     ACEMI_CHECK(a.Cout % 4 == 0, "conv_gemm: output channels must be a multiple of 4");
     const int nbm = (a.M + 127) / 128, nbn = a.N / 128;
-    if (a.W2) {
+    if (a.W2)
         ACEMI_CHECK(a.N == 128 && a.Cout == 128 && a.up <= 1 && a.snake2_ea && a.snake2_eb,
                     "conv_gemm: the fused k1 conv needs Cout = N = 128 and a Snake between the convs");
-        hipLaunchKernelGGL(conv_gemm_kernel<true>, dim3(nbm * nbn), dim3(256), 0, s, a);
+    // the residual unit's dilated k7 conv at 128 channels: halo-staged A (one LDS image per tile)
+    const int hd = (a.taps == 7 && a.Cin == 128 && a.N == 128 && a.Cout == 128 && a.up <= 1 &&
+                    a.in_stride == 1 && a.T_in * a.items == a.M && a.pad == 3 * a.dil &&
+                    (a.dil == 1 || a.dil == 3 || a.dil == 9) && vae_halo_on())
+                       ? a.dil
+                       : 0;
+    const dim3 blk(256);
+    if (hd) {
+        const dim3 grid((unsigned)(a.items * ((a.M / a.items + 127) / 128)));
+        auto go = [&](auto fuse) {
+            constexpr bool F = decltype(fuse)::value;
+            if (hd == 1) hipLaunchKernelGGL((conv_gemm_kernel<F, 1>), grid, blk, 0, s, a);
+            else if (hd == 3) hipLaunchKernelGGL((conv_gemm_kernel<F, 3>), grid, blk, 0, s, a);
+            else hipLaunchKernelGGL((conv_gemm_kernel<F, 9>), grid, blk, 0, s, a);
+        };
+        if (a.W2) go(std::true_type{});
+        else go(std::false_type{});
+    } else if (a.W2) {
+        hipLaunchKernelGGL((conv_gemm_kernel<true, 0>), dim3(nbm * nbn), blk, 0, s, a);
     } else {
-        hipLaunchKernelGGL(conv_gemm_kernel<false>, dim3(nbm * nbn), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((conv_gemm_kernel<false, 0>), dim3(nbm * nbn), blk, 0, s, a);
     }
     ACEMI_HIP(hipGetLastError());
 }

@@ -116,21 +116,40 @@ def test_tiled_decode_hook_matches_windowed_oracle(tiny_vae):
         assert l2 < 5e-3
 
 
+@pytest.mark.parametrize("T", [37, 61])
+def test_halo_staged_residual_convs_equal_generic(tiny_vae, T, monkeypatch):
+    """The 128-channel residual units' k7 convs with the halo-staged A operand (default) give the same bits as
+    the generic per-k-tile staging (ACE_MI_VAE_HALO=0): same products, same k order.  Odd T: ragged tiles at
+    every stage.  Decode and encode (the encoder's 128-channel units run the unfused k7 conv)."""
+    d, br = tiny_vae
+    lat = np.random.default_rng(100 + T).standard_normal((T, 64)).astype(np.float32)
+    audio = np.random.default_rng(200 + T).standard_normal((T * 6, 2)).astype(np.float32)
+    n = br.vae_out_len(T)  # (the samples past n of the [T*hop] host buffer are not written)
+    halo = br.vae_decode_tfirst(lat)[:n], br.vae_encode_tfirst(audio)
+    monkeypatch.setenv("ACE_MI_VAE_HALO", "0")
+    generic = br.vae_decode_tfirst(lat)[:n], br.vae_encode_tfirst(audio)
+    for i, what in enumerate(("decode", "encode")):
+        d = np.abs(halo[i].astype(np.float64) - generic[i])
+        print(f"halo vs generic {what} T={T}: {int((d > 0).sum())} of {d.size} differ, max {d.max():.3e}")
+        np.testing.assert_array_equal(halo[i], generic[i])
+
+
 @pytest.mark.slow
-def test_full_size_vae_decode():
+@pytest.mark.parametrize("T", [6, 5])
+def test_full_size_vae_decode(T):
     """The real ACE-Step 1.5 decoder shape (128 x [1,2,4,8,16] channels, strides 10,6,4,4,2,
-    hop 1920) on 6 latent frames (11520 samples)."""
+    hop 1920) on 6 / 5 latent frames (11520 / 9600 samples; 5: ragged 128-row tiles in the 128-channel blocks)."""
     from acestep_mi355x.capi import GGMLCAPIBridge
     from acestep_mi355x.synthetic import VAE_FULL_CONFIG
     from oracle.vae_oracle import VaeWeights, decode_with_floor
     d = _ckpt(VAE_FULL_CONFIG)
     br = GGMLCAPIBridge()
     br.load_vae(d)
-    lat = np.random.default_rng(11).standard_normal((6, 64)).astype(np.float32)
+    lat = np.random.default_rng(11).standard_normal((T, 64)).astype(np.float32)
     got = br.vae_decode_tfirst(lat)
     br.close()
     ref, floor = decode_with_floor(VaeWeights(d), lat)
-    _check(got, ref, floor, "full VAE T=6")
+    _check(got, ref, floor, f"full VAE T={T}")
 
 
 @pytest.mark.parametrize("n", [120, 126, 600])
