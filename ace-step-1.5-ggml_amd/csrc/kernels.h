@@ -230,7 +230,6 @@ struct ConvGemmArgs {
     const float* bias2 = nullptr;
     const float* snake2_ea = nullptr;
     const float* snake2_eb = nullptr;
-    int dbg = 0;  // timing experiments only (ACE_MI_VAE_DBG): 1 = two k-tiles, 2 = no fused k1 conv, 4 = no stores
 };
 void launch_conv_gemm(const ConvGemmArgs& a, hipStream_t s);
 void launch_to_f16(const float* x, int64_t n, uint16_t* y, hipStream_t s);

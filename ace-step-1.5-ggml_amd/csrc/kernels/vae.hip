@@ -114,7 +114,7 @@ __global__ void __launch_bounds__(256, 2) conv_gemm_kernel(ConvGemmArgs p) {
     const int wm0 = (wid / WN) * WTM, wn0 = (wid % WN) * WTN;
 
     const int cblocks = p.Cin / BK;
-    const int nk = (p.dbg & 1) ? min(2, p.taps * cblocks) : p.taps * cblocks;
+    const int nk = p.taps * cblocks;
     const int K = p.taps * p.Cin;
 
     // per-lane staging rows (fixed) and swizzled 16-byte chunk
@@ -240,7 +240,7 @@ __global__ void __launch_bounds__(256, 2) conv_gemm_kernel(ConvGemmArgs p) {
         }
     }
 
-    if (FUSE2 && !(p.dbg & 2)) {
+    if constexpr (FUSE2) {
         // k1 conv of the residual unit on this tile (N = Cout = 128: the tile holds every channel).
         // W2 fragments straight from global memory (32 KB, L2-resident), issued before the LDS round trip.
         const int lrow2 = lane & 15, lch2 = lane >> 4;
@@ -305,76 +305,91 @@ __global__ void __launch_bounds__(256, 2) conv_gemm_kernel(ConvGemmArgs p) {
     // then x + that, then the Snake of the sum.
     static_assert(BM * BN * 4 <= 2 * STAGE, "epilogue tile must fit the stage buffers");
     float* zt = reinterpret_cast<float*>(smem);
-    {
-        const int ccol = lane & 15, crow = (lane >> 4) * 4;
-        __syncthreads();  // every wave is done with the stage buffers / the fused conv's y tile
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const int col = wn0 + j * 16 + ccol;
-            int co = n0 + col;
-            if (p.up > 1) co -= (co / p.Cout) * p.Cout;
-            const float b = bias_e ? bias_e[co] : 0.f;
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    zt[(wm0 + i * 16 + crow + r) * BN + col] = bias_e ? rn_add(acc[i][j][r], b) : acc[i][j][r];
-        }
-        __syncthreads();
-    }
-    if (p.dbg & 4) return;
     const int c4 = (lane & 31) * 4;
     const int n = n0 + c4;
     const int rr = p.up > 1 ? n / p.Cout : 0;
     const int co = n - rr * p.Cout;
+    constexpr int RPI = NW * 2;  // tile rows per sweep iteration
+    constexpr int NIT = BM / RPI;
+    // output offset of sweep iteration `it` (this lane's 4 columns), or -1 outside the sequence / the crop
+    // (branch-free: the residual loads below are issued unconditionally from a clamped offset -- behind a branch,
+    // hipcc waited for every earlier load before the next one)
+    auto out_off = [&](int it) -> int64_t {
+        const int m = m0 + it * RPI + wid * 2 + (lane >> 5);
+        const int item = m / Mi, ml = m - item * Mi;
+        const int u = p.up > 1 ? ml * p.up + rr - p.crop : ml;
+        const bool ok = m < mlim && u >= 0 && u < p.T_out;
+        return ok ? ((int64_t)item * p.T_out + u) * p.Cout + co : (int64_t)-1;
+    };
+    // per-column bias and Snake parameters first: a wait for any load issued after the residual loads below would
+    // also wait for those (vmcnt retires in issue order)
+    const int ccol = lane & 15, crow = (lane >> 4) * 4;
+    float bz[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        int cz = n0 + wn0 + j * 16 + ccol;
+        if (p.up > 1) cz -= (cz / p.Cout) * p.Cout;
+        bz[j] = bias_e ? bias_e[cz] : 0.f;
+    }
     float ea[4], reb[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
         ea[e] = p.snake_ea ? p.snake_ea[co + e] : 0.f;
         reb[e] = p.snake_eb ? __builtin_amdgcn_rcpf(p.snake_eb[co + e]) : 0.f;
     }
-    constexpr int RPI = NW * 2;  // tile rows per sweep iteration
-    constexpr int UNR = 4;       // iterations whose residual loads are issued together
-    static_assert((BM / RPI) % UNR == 0, "epilogue sweep");
-#pragma unroll 1
-    for (int it0 = 0; it0 < BM / RPI; it0 += UNR) {
-        int64_t o[UNR];
-        float4 xo[UNR];
+    // the residual's old values for the whole sweep are requested here, before the tile goes through LDS, so one
+    // HBM round trip (under the z writes and the barriers) replaces one per group of iterations
+    // (no resid: the loads read the zero buffer -- a branch around them made hipcc wait vmcnt(0) at the first use
+    // of the bias loads, i.e. for all of them)
+    // (the asm uses make hipcc retire the bias / Snake loads here: its wait at their first later use was vmcnt(0),
+    // i.e. for every residual load too)
 #pragma unroll
-        for (int q = 0; q < UNR; ++q) {
-            const int row = (it0 + q) * RPI + wid * 2 + (lane >> 5);
-            const int m = m0 + row;
-            o[q] = -1;
-            xo[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (m < mlim) {
-                const int item = m / Mi, ml = m - item * Mi;
-                const int u = p.up > 1 ? ml * p.up + rr - p.crop : ml;
-                if (u >= 0 && u < p.T_out) {
-                    o[q] = ((int64_t)item * p.T_out + u) * p.Cout + co;
-                    if (p.resid) xo[q] = *reinterpret_cast<const float4*>(p.X + o[q]);
-                }
-            }
+    for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(bz[j]));
+#pragma unroll
+    for (int e = 0; e < 4; ++e) asm volatile("" ::"v"(ea[e]), "v"(reb[e]));
+    __builtin_amdgcn_sched_barrier(0);
+    const float* xsrc = p.resid ? p.X : reinterpret_cast<const float*>(p.zero);
+    float4 xo[NIT];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+        const int64_t o = out_off(it);
+        xo[it] = *reinterpret_cast<const float4*>(xsrc + (p.resid && o >= 0 ? o : 0));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    {
+        __builtin_amdgcn_s_barrier();  // every wave is done with the stage buffers / the fused conv's y tile
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int col = wn0 + j * 16 + ccol;
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    zt[(wm0 + i * 16 + crow + r) * BN + col] = bias_e ? rn_add(acc[i][j][r], bz[j]) : acc[i][j][r];
         }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    }
 #pragma unroll
-        for (int q = 0; q < UNR; ++q) {
-            if (o[q] < 0) continue;
-            const int row = (it0 + q) * RPI + wid * 2 + (lane >> 5);
-            float4 v = *reinterpret_cast<const float4*>(zt + row * BN + c4);
-            if (p.resid) {
-                v.x = rn_add(xo[q].x, v.x);
-                v.y = rn_add(xo[q].y, v.y);
-                v.z = rn_add(xo[q].z, v.z);
-                v.w = rn_add(xo[q].w, v.w);
-            }
-            if (p.store_x) *reinterpret_cast<float4*>(p.X + o[q]) = v;
-            if (p.S_out) {
-                const float vv[4] = {v.x, v.y, v.z, v.w};
-                uint16_t h[4];
+    for (int it = 0; it < NIT; ++it) {
+        const int64_t o = out_off(it);
+        if (o < 0) continue;
+        const int row = it * RPI + wid * 2 + (lane >> 5);
+        float4 v = *reinterpret_cast<const float4*>(zt + row * BN + c4);
+        if (p.resid) {
+            v.x = rn_add(xo[it].x, v.x);
+            v.y = rn_add(xo[it].y, v.y);
+            v.z = rn_add(xo[it].z, v.z);
+            v.w = rn_add(xo[it].w, v.w);
+        }
+        if (p.store_x) *reinterpret_cast<float4*>(p.X + o) = v;
+        if (p.S_out) {
+            const float vv[4] = {v.x, v.y, v.z, v.w};
+            uint16_t h[4];
 #pragma unroll
-                for (int e = 0; e < 4; ++e) h[e] = f32_to_f16(p.snake_ea ? snake_f(vv[e], ea[e], reb[e]) : vv[e]);
-                *reinterpret_cast<uint2*>(p.S_out + o[q]) =
-                    make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16));
-            }
+            for (int e = 0; e < 4; ++e) h[e] = f32_to_f16(p.snake_ea ? snake_f(vv[e], ea[e], reb[e]) : vv[e]);
+            *reinterpret_cast<uint2*>(p.S_out + o) =
+                make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16));
         }
     }
 }
@@ -482,9 +497,7 @@ static bool vae_halo_on() {
     return !(e && e[0] == '0');
 }
 
-void launch_conv_gemm(const ConvGemmArgs& a_in, hipStream_t s) {
-    ConvGemmArgs a = a_in;
-    if (const char* e = std::getenv("ACE_MI_VAE_DBG")) a.dbg = std::atoi(e);
+void launch_conv_gemm(const ConvGemmArgs& a, hipStream_t s) {
     ACEMI_CHECK(a.Cin % 64 == 0 && a.N % 128 == 0 && a.M >= 1 && a.taps >= 1, "conv_gemm: unsupported shape");
     ACEMI_CHECK(a.S && a.W && a.zero, "conv_gemm: null operand");
     ACEMI_CHECK(a.up <= 1 || a.N == a.up * a.Cout, "conv_gemm: transposed conv needs N = stride * Cout");
@@ -503,8 +516,9 @@ void launch_conv_gemm(const ConvGemmArgs& a_in, hipStream_t s) {
                        ? a.dil
                        : 0;
     const dim3 blk(256);
+    const int ntiles = hd ? a.items * ((a.M / a.items + 127) / 128) : nbm * nbn;
     if (hd) {
-        const dim3 grid((unsigned)(a.items * ((a.M / a.items + 127) / 128)));
+        const dim3 grid((unsigned)ntiles);
         auto go = [&](auto fuse) {
             constexpr bool F = decltype(fuse)::value;
             if (hd == 1) hipLaunchKernelGGL((conv_gemm_kernel<F, 1>), grid, blk, 0, s, a);
