@@ -666,6 +666,9 @@ void launch_variant(int variant, const GemmParams& p, hipStream_t s) {
         case 13: launch_cfg<64, 128, 2, 2, F16, EPI, 3>(p, S, s); break;
         case 14: launch_cfg<96, 128, 2, 2, F16, EPI, 3>(p, S, s); break;
         case 15: launch_cfg<128, 128, 2, 2, F16, EPI, 3>(p, S, s); break;
+        // 8 waves (4 x 2) on a 192x128 tile: one tile per CU at M = 3000, N = 2048 (256 tiles), two waves per SIMD
+        case 16: launch_cfg<192, 128, 4, 2, F16, EPI, 1>(p, S, s); break;
+        case 17: launch_cfg<192, 128, 4, 2, F16, EPI, 3>(p, S, s); break;
         default: throw std::runtime_error("gemm: bad variant");
     }
 }

@@ -190,7 +190,7 @@ def test_attention_running_max_moves_mid_sequence(nk, mode):
     _check_attn(got, q, kv, hq, hkv, 0, None, scale, mode)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 204, 207, 208, 212, 307, 409, 413, 414])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 204, 207, 208, 212, 307, 409, 413, 414])
 @pytest.mark.parametrize("M,N,K", [(1, 256, 64), (300, 512, 128), (1000, 768, 2048), (513, 256, 6144)])
 def test_gemm_all_variants(variant, M, N, K):
     """Every GEMM kernel variant (128x128 / 256x256 / 256x128 / 192x128 / 192x256 / 64x64 / 64x128, the
@@ -253,7 +253,7 @@ def test_gemm_skinny(M, N, K, epi):
         assert np.all(np.abs(got - ref) <= (2e-6 * scale + 1e-6) * np.abs(gg) + 2e-7 * np.abs(ref))
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 204, 207, 213, 215, 408])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 204, 207, 213, 215, 408])
 @pytest.mark.parametrize("epi", [2, 3])
 @pytest.mark.parametrize("M,N,K", [(300, 512, 128), (1000, 768, 2048), (9001, 512, 256)])
 def test_gemm_residual_epilogues(variant, epi, M, N, K):

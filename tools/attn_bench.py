@@ -19,13 +19,14 @@ CASES = [  # name, B, hq, hkv, nq, nk, window, masked
 
 
 def main():
-    only = os.environ.get("ATTN_CASE")  # e.g. "self_full 240s" (split mode only) for a PMC pass
+    only = os.environ.get("ATTN_CASE")  # e.g. "self_full 240s" (one mode, ATTN_MODE or split) for a PMC pass
+    only_mode = os.environ.get("ATTN_MODE", "split")
     for name, B, hq, hkv, nq, nk, win, masked in CASES:
         if only and name != only:
             continue
         modes = {"split": (True, False), "pvsplit": (True, True), "fast": (False, False)}
         for mode, (split, pvs) in modes.items():
-            if only and mode != "split":
+            if only and mode != only_mode:
                 continue
             ms = capi.bench_attention(B, hq, hkv, nq, nk, win, split=split, masked=masked, iters=10, pv_split=pvs)
             nk_eff = min(nk, 2 * win + 1) if win else nk
