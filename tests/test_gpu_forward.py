@@ -309,13 +309,14 @@ def _batched(br, h, c, e, t):
     return out.cpu().numpy()
 
 
-@pytest.mark.parametrize("variant", [-1, 10, 11])
+@pytest.mark.parametrize("variant", [-1, 10, 11, 16])
 @pytest.mark.parametrize("width", ["tiny", "full"])
 def test_fused_qkv_prep_is_bit_exact(tiny_ckpt, monkeypatch, width, variant):
     """The QKV / cross-q GEMMs with QK-norm, RoPE and the attention re-layout fused into their epilogue
     (EPI_QKV_PREP) give the same bits as the f32 store + attn_prep pair (ACE_MI_UNFUSED_PREP=1): batched
     items whose token counts are not multiples of 16 or of the GEMM's row tile, so V^T key groups are cut
-    by chunk and item edges; the automatic tile choice and the forced 8-wave 256-column tiles."""
+    by chunk and item edges; the automatic tile choice, the forced 8-wave 256-column tiles and the 8-wave
+    (4 x 2) 192x128 tiles."""
     from acestep_mi355x.capi import GGMLCAPIBridge
     if width == "tiny":
         d, H, cases = tiny_ckpt, 256, [(1, 37, 5), (2, 301, 9), (3, 1001, 17)]
