@@ -27,6 +27,7 @@ Extra lines beside the headline (one GPU only; each the same 27-step schedule, t
   attn_split_line  the headline loop with f32-faithful `split` attention (hi/lo fp16 Q.K operands)
   bf16_line        the same workload with bf16 weights (+ its own hook_line)
   line_60s         BASELINE configs[1]: 60 s (T = 1500), bs = 1, bf16 weights
+  line_600s        BASELINE configs[4]'s DiT sequence on one GPU: 600 s (T = 15000, N = 7500), bs = 1, bf16 weights
   line_10s         10 s (T = 250, configs[0]'s shape) forward rate with the headline weights and with bf16
   lowmem_line      quantized weights with ACE_MI_QUANT_STAGE_SCOPE=layer (planes + one 117 MB bf16 slot,
                    expanded before every layer of every step) and its device-memory footprint
@@ -367,6 +368,12 @@ def main():
             extras["line_60s"]["dit_block_linears_frac_of_bf16_peak"] = block_linear_frac(prof60, args.steps, 1500, 1,
                                                                                            info)
             extras["line_60s"]["breakdown_ms_per_step"] = {n: round(ms / args.steps, 4) for n, ms, _ in prof60}
+        # ---- BASELINE configs[4]'s DiT sequence (its 4 items sharded one per GPU): 600 s, bs = 1, bf16
+        in600 = small_inputs(15000)
+        extras["line_600s"] = line(args.steps, timed(lambda f, k: run(f, k, in600)),
+                                   "configs[4]'s DiT sequence on one GPU: 27-step sample, 600 s (T = 15000, N = 7500), "
+                                   "bs = 1, bf16 (configs[4] itself: 60 steps, Q4_K, one item per GPU)")
+        del in600
 
     # ---- CPU baseline: the C++/OpenMP restatement of ggml's CPU forward_dit on the host cores
     cpu = None
