@@ -50,11 +50,6 @@
 #include "../kernels.h"
 #include "lds_asm.h"
 
-// wave priority experiment (build define): 1 = s_setprio 1 around the MFMA blocks, 2 = around the softmax VALU
-#ifndef ACEMI_ATTN_PRIO
-#define ACEMI_ATTN_PRIO 0
-#endif
-
 namespace acemi {
 namespace {
 
@@ -388,10 +383,7 @@ __global__ void __launch_bounds__(256, OCC) attn_kernel(AttnArgs a) {
 
         // S(i+1) from K slot NXT (on the last tile: a discarded product of the slot's stale but
         // finite contents, which keeps this block branch-free) || P(i) = exp2(S(i) - m + 12)
-        if (ACEMI_ATTN_PRIO == 1) __builtin_amdgcn_s_setprio(1);
         s_tile(std::integral_constant<int, NXT>{}, s_nxt);
-        if (ACEMI_ATTN_PRIO == 1) __builtin_amdgcn_s_setprio(0);
-        if (ACEMI_ATTN_PRIO == 2) __builtin_amdgcn_s_setprio(1);
         const float m_use = ((m_run == -INFINITY) ? 0.f : m_run) - PSCALE_LOG2;
         float lsum = 0.f;
         frag pf[4], pfl[4];
@@ -424,7 +416,6 @@ __global__ void __launch_bounds__(256, OCC) attn_kernel(AttnArgs a) {
             }
         }
         l_run += lsum;
-        if (ACEMI_ATTN_PRIO == 2) __builtin_amdgcn_s_setprio(0);
 
         // O^T += V^T(i) . P^T(i) ; PVS: Vh.Ph + Vh.Pl + Vl.Ph  ||  scale / mask / max of S(i+1)
         static_for<0, 2>([&](auto dp_c) {  // two 32-row d-tiles per LDS round trip
@@ -440,7 +431,6 @@ __global__ void __launch_bounds__(256, OCC) attn_kernel(AttnArgs a) {
                 }
             });
             lds_wait_tie(vf);
-            if (ACEMI_ATTN_PRIO == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
             for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -451,7 +441,6 @@ __global__ void __launch_bounds__(256, OCC) attn_kernel(AttnArgs a) {
                         o[dp + u] = mfma32(vf[8 + 4 * u + g], pf[g], o[dp + u]);
                     }
                 }
-            if (ACEMI_ATTN_PRIO == 1) __builtin_amdgcn_s_setprio(0);
         });
         const float mnx = prep(std::integral_constant<int, NXT>{}, s_nxt, i + 1);
         if (more) {
