@@ -754,22 +754,23 @@ int pick_variant(int M, int N, int K, bool quant, int fmt) {
     // 64x64 tiles (94 workgroups).  Not split over K: the summation order then stays the one every other tile
     // (and the dequant-fused kernels) uses, which the staged == fused test relies on
     if (N <= 128 && M >= 512) return 9;
-    // Long single sequences and two-item batches, 4000 <= M < 8192 (600 s: M = 7500; tools/gemm_msweep.py,
-    // profiles/r03_msweep_v16_*.jsonl, TFLOP/s): the 8-wave 192x128 tiles (v16) -- M = 4500 o 795 vs 490 (v4), down
-    // 904 vs 813 (v11), qkv 959 vs 920; M = 6000 o 950 vs 605, down 1078 vs ~920, qkv 1053 vs 1040 -- until the
-    // 256x256 ping-pong tiles fit one round: M = 7500 o 816 (v10) vs 536 (v4) / 760 (v16), down 1010 vs 706 (v11) /
-    // 797, gate|up 936 vs 892 (v4); qkv stays on v16 there (987 vs 970).
-    if (M >= 4000 && M < 8192) {
-        const bool wide_fit = M >= 6800 && N % 256 == 0;
-        if (N <= 2048) return wide_fit ? 10 : 16;
+    // 600 s single sequences (M = 7500) and similar, 6800 <= M < 8192: the 256x256 ping-pong tiles (one round of
+    // 240 tiles for the N = 2048 projections) and the 8-wave 192x128 tiles for qkv.  Measured in the sampling loop
+    // (bench.py --seconds 600, same-box A/B against the previous picks, profiles/r03_pick_ab_600s/): 29.75 -> 33.25
+    // steps/s.  The isolated-GEMM sweep (profiles/r03_msweep_v16_*.jsonl) also favoured the 192x128 8-wave tiles at
+    // M = 4500..12000, but inside the loop (cold weights, fresh activations) they were neutral at M = 6000 and 2 %
+    // slower at M = 12000 (profiles/r03_bs_ab/), so the picks below 6800 and from 8192 stay as they were.
+    if (M >= 6800 && M < 8192) {
+        if (N <= 2048 && N % 256 == 0) return 10;
         if (N <= 4096) return 16;
-        if (wide_fit) return 10;
+        if (N % 256 == 0) return 10;
     }
     if (N % 256 == 0 && M >= 8192) {
         if (N >= 4096) return 10;
         if (M >= 20000) return K >= 4096 ? 10 : 2;
-        return 16;  // M = 12000: o 952 vs 806 (v11), down 960 vs 928
+        return 11;
     }
+    if (N % 256 == 0 && M >= 4500 && N <= 2048 && K >= 4096) return 11;
     if (edge_ok && mb192 * (N / 128) >= 384) return 4;
     // short sequences (60 s: M = 750): too few 96-row tiles to cover the CUs -> 64-row tiles, and
     // 64x64 when even those leave CUs idle (M = 750: N = 2048 projections 273-337 -> 364-453 TFLOP/s,
