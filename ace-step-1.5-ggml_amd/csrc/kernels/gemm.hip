@@ -16,8 +16,12 @@
 // ds_read, which makes every ds_read_b128 lane group conflict-free.
 // Blocks are remapped XCD-aware (blocks b, b+8 share an XCD) and grouped
 // along M so co-resident tiles share weight panels in L2.
+#include <array>
+#include <cstdio>
+#include <cstdlib>
 #include <mutex>
 #include <map>
+#include <vector>
 #include <type_traits>
 #include <utility>
 
@@ -728,9 +732,30 @@ int pick_variant_q(int M, int N, int K, int fmt) {
     return 7;
 }
 
+// Per-shape overrides for in-loop A/B runs (ACE_MI_GEMM_OVERRIDE="N:K:variant[,N:K:variant...]", dense weights,
+// any M; read once): the isolated-GEMM sweeps mispredicted the sampling loop at some shapes (cold weights, fresh
+// activations), so tile picks are confirmed with whole bench lines.
+static int gemm_override(int N, int K) {
+    static const std::vector<std::array<int, 3>> table = [] {
+        std::vector<std::array<int, 3>> t;
+        const char* e = std::getenv("ACE_MI_GEMM_OVERRIDE");
+        while (e && *e) {
+            int n = 0, k = 0, v = 0, used = 0;
+            if (std::sscanf(e, "%d:%d:%d%n", &n, &k, &v, &used) != 3) break;
+            t.push_back({n, k, v});
+            e += used;
+            if (*e == ',') ++e;
+        }
+        return t;
+    }();
+    for (const auto& x : table)
+        if (x[0] == N && x[1] == K) return x[2];
+    return -1;
+}
+
 int pick_variant(int M, int N, int K, bool quant, int fmt) {
-    if (g_forced_variant >= 0) {  // forced (tests / micro-benchmarks), where that tile supports the shape
-        const int f = g_forced_variant % 100, S = g_forced_variant / 100;
+    auto supports = [&](int v) {  // the tile / split-K factor handles this shape (and weight format)
+        const int f = v % 100, S = v / 100;
         const bool wide = f == 2 || f == 5 || f == 10 || f == 11 || f == 21;  // (12-15: multi-stage rings)
         const bool qr = f >= 20 && f <= 24;
         const bool dense_only = (f == 6 || (f >= 8 && f < 20) || f == 30 || S > 1) && !qr;
@@ -738,8 +763,13 @@ int pick_variant(int M, int N, int K, bool quant, int fmt) {
                                          : ((f == 1 || f == 3 || f == 4 ? S <= 2
                                                                        : (((f >= 6 && f <= 9) || (f >= 12 && f <= 15)) && S <= 4)) &&
                                             K / 64 >= 2 * S));
-        if (!(wide && N % 256 != 0) && !(quant && dense_only) && !(!quant && qr) && sk_ok && !(f == 21 && fmt == WF_Q4_K))
-            return g_forced_variant;
+        return !(wide && N % 256 != 0) && !(quant && dense_only) && !(!quant && qr) && sk_ok &&
+               !(f == 21 && fmt == WF_Q4_K);
+    };
+    if (g_forced_variant >= 0 && supports(g_forced_variant)) return g_forced_variant;  // tests / micro-benchmarks
+    if (!quant) {
+        const int ov = gemm_override(N, K);
+        if (ov >= 0 && supports(ov)) return ov;
     }
     const int64_t mb192 = (M + 191) / 192;
     const bool edge_ok = m_edge(M, 192) >= m_edge(M, 128) - 0.02;
