@@ -88,9 +88,11 @@ void launch_gemm(ActType t, const uint16_t* A, int lda, const uint16_t* W, int l
 // -1 = automatic tile choice; 0..11 force a kernel variant, + 100 * S (S = 2..4) split-K over S blocks per
 // tile for the 4-wave tiles (micro-benchmarks / tests)
 void gemm_force_variant(int v);
-// Throws if any split-K GEMM join on the current device timed out since the workspace was created (synchronizes
-// the streams that ran split-K GEMMs; called at the library's synchronisation points).
+// Throws (once) if a split-K GEMM join on the current device timed out since the last check: reads a per-device
+// host-pinned error word, no stream is synchronised (called at the library's synchronisation points and on entry).
 void gemm_splitk_check();
+// free the split-K workspace of stream s on the current device (before the owner destroys s)
+void gemm_splitk_release(hipStream_t s);
 // bf16 image [N][K] (ld K) of a quantized weight: bit-identical to what the dequant-fused GEMM feeds its MFMAs
 void launch_dequant_bf16(const WeightView& W, int N, int K, uint16_t* out, hipStream_t s);
 // the same for 1..8 matrices of one format in one launch

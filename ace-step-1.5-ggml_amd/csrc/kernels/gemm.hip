@@ -473,17 +473,30 @@ __global__ void __launch_bounds__(512) gemm8_kernel(GemmParams p) {
 }
 
 // split-K workspace of one (device, stream): partial tiles + per-tile ticket / ready counters (zeroed once;
-// each launch leaves them zero, see splitk_join) + an error word.  Launches on one stream are ordered, so one
-// set per stream suffices; keyed by the device too, since the null stream has the same handle on every
-// device.  It only grows (a grow waits for the stream before freeing the old buffers).
+// each launch leaves them zero, see splitk_join).  Launches on one stream are ordered, so one set per stream
+// suffices; keyed by the device too, since the null stream has the same handle on every device.  It only grows
+// (a grow waits for the stream before freeing the old buffers) and is freed by gemm_splitk_release when the
+// owning context destroys its stream.  The join's timeout error word is per device, in pinned host memory:
+// gemm_splitk_check reads it without touching any stream (no sync of another context's, possibly destroyed,
+// stream) and clears it once reported.
 struct SplitKWs {
     void* ws = nullptr;
     size_t ws_bytes = 0;
-    unsigned* cnt = nullptr;  // [2][tiles] tickets, ready counts; then the error word
+    unsigned* cnt = nullptr;  // [2][tiles] tickets, ready counts
     size_t tiles = 0;
 };
 std::mutex g_sk_mu;
 std::map<std::pair<int, hipStream_t>, SplitKWs> g_sk;
+std::map<int, unsigned*> g_sk_err;  // per device: host-pinned, device-mapped error word
+
+unsigned* splitk_err_word(int dev) {  // (g_sk_mu held)
+    unsigned*& e = g_sk_err[dev];
+    if (!e) {
+        ACEMI_HIP(hipHostMalloc(reinterpret_cast<void**>(&e), sizeof(unsigned), hipHostMallocMapped));
+        *reinterpret_cast<volatile unsigned*>(e) = 0u;
+    }
+    return e;
+}
 
 void splitk_setup(GemmParams& p, int ntiles, int S, size_t tile_bytes, hipStream_t s) {
     int dev = 0;
@@ -504,15 +517,18 @@ void splitk_setup(GemmParams& p, int ntiles, int S, size_t tile_bytes, hipStream
         w.cnt = nullptr;
         w.tiles = 0;
         const size_t t = std::max<size_t>((size_t)ntiles, 4096);
-        ACEMI_HIP(hipMalloc(&w.cnt, (2 * t + 1) * sizeof(unsigned)));
-        ACEMI_HIP(hipMemsetAsync(w.cnt, 0, (2 * t + 1) * sizeof(unsigned), s));
+        ACEMI_HIP(hipMalloc(&w.cnt, 2 * t * sizeof(unsigned)));
+        ACEMI_HIP(hipMemsetAsync(w.cnt, 0, 2 * t * sizeof(unsigned), s));
         w.tiles = t;
     }
+    unsigned* err = splitk_err_word(dev);
+    unsigned* err_dev = nullptr;
+    ACEMI_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&err_dev), err, 0));
     p.ksplit = S;
     p.sk_ws = static_cast<f32x4*>(w.ws);
     p.sk_cnt = w.cnt;
     p.sk_ready = w.cnt + w.tiles;
-    p.sk_err = w.cnt + 2 * w.tiles;
+    p.sk_err = err_dev;
 }
 
 template <int BM, int BN, int WM, int WN, bool F16, int EPI, int PIPE>
@@ -892,14 +908,25 @@ void gemm_splitk_check() {
     std::lock_guard<std::mutex> lk(g_sk_mu);
     int cur = 0;
     ACEMI_HIP(hipGetDevice(&cur));
-    for (auto& kv : g_sk) {
-        if (kv.first.first != cur || !kv.second.cnt) continue;
-        unsigned err = 0;
-        ACEMI_HIP(hipStreamSynchronize(kv.first.second));
-        ACEMI_HIP(hipMemcpy(&err, kv.second.cnt + 2 * kv.second.tiles, sizeof(unsigned), hipMemcpyDeviceToHost));
-        if (err) throw std::runtime_error("gemm: a split-K join timed out waiting for its partial tiles (results invalid)");
+    auto it = g_sk_err.find(cur);
+    if (it == g_sk_err.end() || !it->second) return;
+    volatile unsigned* e = it->second;
+    if (*e) {
+        *e = 0u;  // reported once: later calls start clean
+        throw std::runtime_error("gemm: a split-K join timed out waiting for its partial tiles (results invalid)");
     }
 }
 
+void gemm_splitk_release(hipStream_t s) {
+    std::lock_guard<std::mutex> lk(g_sk_mu);
+    int cur = 0;
+    ACEMI_HIP(hipGetDevice(&cur));
+    auto it = g_sk.find(std::make_pair(cur, s));
+    if (it == g_sk.end()) return;
+    (void)hipStreamSynchronize(s);  // the stream is still alive here: its last joins are done with the buffers
+    if (it->second.ws) (void)hipFree(it->second.ws);
+    if (it->second.cnt) (void)hipFree(it->second.cnt);
+    g_sk.erase(it);
+}
 
 }  // namespace acemi

@@ -34,7 +34,7 @@ struct GemmParams {
     f32x4* sk_ws;
     unsigned* sk_cnt;
     unsigned* sk_ready;
-    unsigned* sk_err;  // set to 1 when a join's bounded wait timed out (checked by gemm_splitk_check)
+    unsigned* sk_err;  // per-device host-pinned word, set to 1 when a join's bounded wait timed out (gemm_splitk_check)
 };
 
 __device__ __forceinline__ uint16_t f32_to_bf16_rne(float f) {
@@ -534,7 +534,7 @@ __device__ __forceinline__ bool splitk_join(const GemmParams& p, f32x4 (&acc)[TM
             __hip_atomic_store(p.sk_cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(p.sk_ready + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
-            __hip_atomic_store(p.sk_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(p.sk_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // host-pinned word
         }
     }
     __syncthreads();

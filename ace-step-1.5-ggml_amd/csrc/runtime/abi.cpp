@@ -56,7 +56,13 @@ void ace_ggml_destroy(ace_ggml_context* ctx) {
     if (ctx->d_in) (void)hipFree(ctx->d_in);
     if (ctx->d_v) (void)hipFree(ctx->d_v);
     if (ctx->d_sched) (void)hipFree(ctx->d_sched);
-    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    if (ctx->stream) {
+        try {
+            acemi::gemm_splitk_release(ctx->stream);
+        } catch (const std::exception&) {
+        }
+        (void)hipStreamDestroy(ctx->stream);
+    }
     delete ctx;
 }
 
@@ -196,6 +202,7 @@ ace_ggml_status ace_mi_dit_forward_batched(ace_ggml_context* ctx, int32_t batch,
     if (enc_len > 0 && !d_enc) return set_error(ctx, ACE_GGML_ERR_INVALID_ARG, "encoder_hidden_states is null");
     try {
         bind_device(ctx);
+        acemi::gemm_splitk_check();  // a failure of an earlier asynchronous call surfaces here
         hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
         acemi::ForwardIO io;
         io.B = batch;
@@ -231,6 +238,7 @@ ace_ggml_status run_sampler(ace_ggml_context* ctx, int32_t batch, float* d_xt, c
     if (sde && n_steps > 1 && !d_noise) return set_error(ctx, ACE_GGML_ERR_INVALID_ARG, "sde needs noise");
     try {
         bind_device(ctx);
+        acemi::gemm_splitk_check();  // a failure of an earlier asynchronous call surfaces here
         hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
         const auto& c = ctx->dit->model().cfg;
         const size_t n = (size_t)batch * seq_len * c.audio_dim;

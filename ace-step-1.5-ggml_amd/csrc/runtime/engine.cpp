@@ -45,6 +45,7 @@ DitEngine::~DitEngine() {
     if (pf_ev_) (void)hipEventDestroy(pf_ev_);
     if (pf_done_) (void)hipEventDestroy(pf_done_);
     if (pf_sink_.p) (void)hipFree(pf_sink_.p);
+    if (stage_ev_) (void)hipEventDestroy(stage_ev_);
     if (ev0_) (void)hipEventDestroy(ev0_);
     if (ev1_) (void)hipEventDestroy(ev1_);
     if (wring_.p) (void)hipFree(wring_.p);
@@ -96,6 +97,7 @@ void DitEngine::stage_layer(int li, hipStream_t st) {
     tic(st);
     if (n > 0) launch_dequant_bf16_batch(jobs, n, st);
     toc("dequant_stage", st);
+    images_written_ = true;
 }
 
 WeightView DitEngine::dense_view(const DevWeight& w, hipStream_t s) {
@@ -105,6 +107,7 @@ WeightView DitEngine::dense_view(const DevWeight& w, hipStream_t s) {
     if (!b.p) {
         ensure(b, (size_t)w.rows * w.cols * 2);
         launch_dequant_bf16(v, w.rows, w.cols, static_cast<uint16_t*>(b.p), s);
+        images_written_ = true;
     }
     v.fmt = WF_BF16;
     v.q = b.p;
@@ -304,6 +307,9 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
     ACEMI_CHECK(L == 0 || io.enc != nullptr, "encoder_hidden_states required when enc_len > 0");
     prepare_shape(B, Np, L);
     rope_for(Np, s);
+    // bf16 images written by an earlier forward (possibly on another stream) are complete before this one reads them
+    if (stage_ev_set_) ACEMI_HIP(hipStreamWaitEvent(s, stage_ev_, 0));
+    images_written_ = false;
 
     int n_layers = c.layers;
     if (io.max_layers > 0) n_layers = std::min(n_layers, io.max_layers);
@@ -639,6 +645,11 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
         tic(s);
         launch_gemm(head_in, kout * H, dense_view(m.proj_out_w, s), (int)M, P * c.audio_dim, kout * H, e, s);
         toc("gemm_proj_out", s);
+    }
+    if (images_written_) {
+        if (!stage_ev_) ACEMI_HIP(hipEventCreateWithFlags(&stage_ev_, hipEventDisableTiming));
+        ACEMI_HIP(hipEventRecord(stage_ev_, s));
+        stage_ev_set_ = true;
     }
     if (pf_stream_) {  // the side stream's sweeps end before anything ordered after this forward on s
         ACEMI_HIP(hipEventRecord(pf_done_, pf_stream_));

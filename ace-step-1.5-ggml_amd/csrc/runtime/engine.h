@@ -145,6 +145,11 @@ class DitEngine {
     // cross k|v, proj in / out), expanded at their first use and kept while the weights are loaded (model and
     // call scope; the layer scope runs them through the dequant-fused GEMM)
     std::map<const void*, Buf> img_;
+    // recorded after a forward that wrote bf16 images (staged slots or dense_view images); every later forward's
+    // stream waits on it, so a forward on another stream never reads an image still being expanded
+    hipEvent_t stage_ev_ = nullptr;
+    bool stage_ev_set_ = false;
+    bool images_written_ = false;
     WeightView dense_view(const DevWeight& w, hipStream_t s);
     char* stage_slot(int li);
     LayerViews layer_views(int li, bool staged);

@@ -24,7 +24,10 @@ Extra lines beside the headline (one GPU only; each the same 27-step schedule, t
   hook_line        the reference pipeline's drop-in path: a Python Euler loop over torch ROCm tensors calling
                    the installed `decoder.forward` (acestep_mi355x.hook, scripts/run_non_ggml_real_case.py:
                    460-533) once per step, as model.generate_audio does
-  attn_split_line  the headline loop with f32-faithful `split` attention (hi/lo fp16 Q.K operands)
+  attn_{fp16,split,f32}_line  the headline loop in each attention precision (fp16 operands; hi/lo Q.K; hi/lo Q.K and
+                   P.V = ggml's F32 kq / kqv), each with its per-kernel attention time per step
+  line_bs          the metric's bs = 2, 4, 8 per GPU at 240 s (item-steps/s, block-linear fraction of peak)
+  line_config4     BASELINE configs[4] per GPU: Q4_K 60-step 600 s sample + windowed VAE decode of the result
   bf16_line        the same workload with bf16 weights (+ its own hook_line)
   line_60s         BASELINE configs[1]: 60 s (T = 1500), bs = 1, bf16 weights
   line_600s        BASELINE configs[4]'s DiT sequence on one GPU: 600 s (T = 15000, N = 7500), bs = 1, bf16 weights
@@ -45,6 +48,13 @@ sys.path.insert(0, os.path.join(ROOT, "ace-step-1.5-ggml_amd"))
 sys.path.insert(0, ROOT)
 
 METRIC = "DiT denoising steps/sec (240s@5Hz latent, bs=1..8) + single-step ms; 1/2/4/8 GPU"
+# DiT attention operand precision of the headline (the engine's default; ACE_MI_BENCH_ATTN overrides for A/B runs):
+# "fp16" single fp16 operands, "split" hi/lo fp16 Q.K, "f32" hi/lo Q.K and P.V (ggml's F32 kq / kqv,
+# acestep_dit_model.cpp:1238-1251)
+HEADLINE_ATTN = os.environ.get("ACE_MI_BENCH_ATTN", "fp16")
+ATTN_DESC = {"fp16": "fp16-operand f32-accumulate attention",
+             "split": "split attention (hi/lo fp16 Q.K, fp16 P.V, f32 accumulate)",
+             "f32": "f32-faithful attention (hi/lo fp16 Q.K and P.V, f32 accumulate)"}
 BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16/fp16 MFMA (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
 
@@ -136,6 +146,7 @@ def main():
     mem0 = dev_used()
     br = GGMLCAPIBridge(device=local, lib_path=lib_path) if lib_path else GGMLCAPIBridge(device=local)
     br.load_dit(ckpt)
+    br.set_attn_precision(HEADLINE_ATTN)
     mem_weights = dev_used() - mem0
     stage_scope = os.environ.get("ACE_MI_QUANT_STAGE_SCOPE", "model")
     if not args.qtype:
@@ -295,11 +306,19 @@ def main():
         extras["hook_line"] = line(B * args.steps, timed(hook_runner(br, xt, ctx, enc, T)),
                                    "the headline workload through the installed decoder.forward hook: a Python "
                                    "Euler loop on torch tensors, one hook call per step (model.generate_audio)")
-        # ---- f32-faithful attention operands
-        br.set_attn_precision("split")
-        extras["attn_split_line"] = line(B * args.steps, timed(run),
-                                         "the headline loop with split (hi/lo fp16 Q.K) attention operands")
-        br.set_attn_precision("fp16")
+        # ---- every attention precision: steps/s of the headline loop + per-kernel attention time per step
+        modes = {}
+        for mode in ("fp16", "split", "f32"):
+            br.set_attn_precision(mode)
+            el_m = elapsed if mode == HEADLINE_ATTN else timed(run)
+            entry = line(B * args.steps, el_m, f"the headline loop with {ATTN_DESC[mode]}")
+            if not args.no_profile:
+                entry["attention"] = attention_breakdown(br, run, args.steps, sync)
+            modes[mode] = entry
+        br.set_attn_precision(HEADLINE_ATTN)
+        extras["attn_split_line"] = modes["split"]
+        extras["attn_f32_line"] = modes["f32"]
+        extras["attn_fp16_line"] = modes["fp16"]
         # ---- 10 s forward rate (configs[0]'s shape) with the headline weights
         in10 = small_inputs(250)
         extras["line_10s"] = {"weights": args.qtype or "bf16", **line(args.steps, timed(lambda f, k: run(f, k, in10)),
@@ -375,6 +394,20 @@ def main():
                                    "bs = 1, bf16 (configs[4] itself: 60 steps, Q4_K, one item per GPU)")
         del in600
 
+    if single and not args.no_extra_lines:
+        # ---- the metric's bs = 2, 4, 8 per GPU at 240 s with the headline weights (reload them: the bridge above
+        # may hold bf16 weights now)
+        br.close()
+        set_weights(args.qtype)
+        br = GGMLCAPIBridge(device=local, lib_path=lib_path) if lib_path else GGMLCAPIBridge(device=local)
+        br.load_dit(ckpt)
+        br.set_attn_precision(HEADLINE_ATTN)
+        extras["line_bs"] = batch_lines(br, run, timed, torch, dev, T, L, audio, ctxd, H, args, info, sync)
+        br.close()
+        # ---- BASELINE configs[4]'s per-GPU work: Q4_K, 60-step DiT sample of 600 s + windowed VAE decode
+        extras["line_config4"] = config4_line(ckpt, lib_path, local, torch, dev, L, audio, ctxd, H, sync)
+        br = GGMLCAPIBridge(device=local, lib_path=lib_path) if lib_path else GGMLCAPIBridge(device=local)
+
     # ---- CPU baseline: the C++/OpenMP restatement of ggml's CPU forward_dit on the host cores
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and os.environ.get("ACE_MI_CPU_BASELINE", "1") != "0":
@@ -404,7 +437,8 @@ def main():
                 "workload": ("BASELINE configs[2]: " if (args.qtype == "q8_0" and args.seconds == 240.0 and b_loc == 1)
                              else "") + f"DiT {args.sample_steps}-step sample, {args.seconds:g} s audio "
                             f"(T={T} latent frames @25 Hz, N={(T + 1) // 2} tokens), enc_len={L}, "
-                            f"bs={b_loc}/GPU, {wdesc} weights, fp16-operand f32-accumulate attention",
+                            f"bs={b_loc}/GPU, {wdesc} weights, {ATTN_DESC[HEADLINE_ATTN]}",
+                "attention_precision": HEADLINE_ATTN,
                 "weights": args.qtype or "bf16",
                 "sampler": "ace_mi_dit_sample_ex (device loop: batched DiT forward + Euler kernel per step)",
                 "cross_attention_cache": bool(args.cross_cache),
@@ -427,6 +461,111 @@ def main():
     br.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def attention_breakdown(br, run, steps, sync):
+    """per-kernel attention time of one generation-loop call (HIP events on the launch stream), per step"""
+    br.profile_enable(True)
+    br.profile_reset()
+    run(0, steps)
+    sync()
+    prof = br.profile_get()
+    br.profile_enable(False)
+    out = {}
+    tot = 0.0
+    for name, ms, cnt in prof:
+        if name.startswith("attn_"):
+            out[name] = {"avg_us": round(1000.0 * ms / max(cnt, 1), 2), "ms_per_step": round(ms / steps, 4)}
+            tot += ms / steps
+    out["total_ms_per_step"] = round(tot, 4)
+    return out
+
+
+def batch_lines(br, run, timed, torch, dev, T, L, audio, ctxd, H, args, info, sync):
+    """item-steps/s of the 240 s loop at bs = 2, 4, 8 items per GPU (one batched forward per step) with the DiT
+    block linears' fraction of the bf16 MFMA peak"""
+    out = {}
+    for b in (2, 4, 8):
+        g = torch.Generator(device=dev).manual_seed(100 + b)
+        x_ = torch.randn((b, T, audio), generator=g, device=dev)
+        c_ = torch.cat([torch.randn((b, T, audio), generator=g, device=dev),
+                        torch.ones((b, T, ctxd - audio), device=dev)], dim=-1).contiguous()
+        e_ = torch.randn((b, L, H), generator=g, device=dev)
+        sync()
+        inp = (x_, c_, e_, T)
+        el = timed(lambda f, k: run(f, k, inp))
+        ent = {"value": round(b * args.steps / el, 3), "unit": "item-steps/s", "ms_per_step": round(1000.0 * el / args.steps, 3),
+               "batch_per_gpu": b, "workload": f"240 s (T = {T}), bs = {b} per GPU, headline weights and attention"}
+        if not args.no_profile:
+            br.profile_enable(True)
+            br.profile_reset()
+            run(0, args.steps, inp)
+            sync()
+            prof = br.profile_get()
+            br.profile_enable(False)
+            ent["dit_block_linears_frac_of_bf16_peak"] = block_linear_frac(prof, args.steps, T, b, info)
+        out[f"bs{b}"] = ent
+        del x_, c_, e_, inp
+    return out
+
+
+def config4_line(ckpt, lib_path, local, torch, dev, L, audio, ctxd, H, sync):
+    """BASELINE configs[4] per GPU (its bs = 4 over 4 GPUs is one item per GPU): Q4_K DiT weights, a 60-step
+    shifted-linear (shift 3) sample of 600 s (T = 15000 frames, N = 7500 tokens) in one device-loop call, then
+    the reference's windowed VAE decode of the result (ACE_GGML_VAE_CHUNK_FRAMES default 128, overlap 32,
+    acestep_ggml.cpp:2114-2229) through the installed tiled_decode hook on the same GPU.  Synthetic weights
+    (DiT N(0, 0.02), VAE weight-normed N(0, 1)); wall time of each stage with the stream synchronised around it."""
+    import tempfile
+    import types
+    from acestep_mi355x.capi import GGMLCAPIBridge
+    from acestep_mi355x.hook import install_vae_backend
+    from acestep_mi355x.schedule import shifted_linear_schedule
+    from acestep_mi355x.synthetic import VAE_FULL_CONFIG, write_vae_checkpoint
+    T, steps = 15000, 60
+    set_weights("q4_k")
+    br = GGMLCAPIBridge(device=local, lib_path=lib_path) if lib_path else GGMLCAPIBridge(device=local)
+    try:
+        br.load_dit(ckpt)
+        br.set_attn_precision(HEADLINE_ATTN)
+        vdir = os.path.join(tempfile.gettempdir(), "acestep_mi355x_synth", "vae_full_f32_seed0")
+        if not os.path.exists(os.path.join(vdir, "diffusion_pytorch_model.safetensors")):
+            write_vae_checkpoint(vdir, VAE_FULL_CONFIG, seed=0)
+        br.load_vae(vdir)
+        g = torch.Generator(device=dev).manual_seed(4)
+        x_ = torch.randn((1, T, audio), generator=g, device=dev)
+        c_ = torch.cat([torch.randn((1, T, audio), generator=g, device=dev),
+                        torch.ones((1, T, ctxd - audio), device=dev)], dim=-1).contiguous()
+        e_ = torch.randn((1, L, H), generator=g, device=dev)
+        sched = shifted_linear_schedule(steps, 3.0)
+        stream = torch.cuda.current_stream().cuda_stream
+        x_w = x_.clone()
+        br.dit_sample_ex_device(1, T, L, x_w.data_ptr(), c_.data_ptr(), e_.data_ptr(), 0, 0, sched[:2], stream=stream)
+        sync()
+        t0 = time.perf_counter()
+        br.dit_sample_ex_device(1, T, L, x_.data_ptr(), c_.data_ptr(), e_.data_ptr(), 0, 0, sched, stream=stream)
+        sync()
+        t_dit = time.perf_counter() - t0
+        handler = types.SimpleNamespace()
+        install_vae_backend(handler, br, chunk_size_default=128, overlap_default=32)
+        lat = x_.transpose(1, 2).contiguous()                       # [1, 64, T]
+        handler.tiled_decode(lat[:, :, :256], offload_wav_to_cpu=False)  # warm the decoder's workspace
+        sync()
+        t0 = time.perf_counter()
+        wav = handler.tiled_decode(lat, offload_wav_to_cpu=False)
+        sync()
+        t_vae = time.perf_counter() - t0
+        finite = bool(torch.isfinite(wav).all().item()) and bool(torch.isfinite(x_).all().item())
+        n_samples = int(wav.shape[-1])
+        total = t_dit + t_vae
+        return {"value": round(1.0 / total, 4), "unit": "items/s", "seconds_per_item": round(total, 3),
+                "dit_s": round(t_dit, 3), "dit_steps_per_s": round(steps / t_dit, 3), "vae_decode_s": round(t_vae, 3),
+                "audio_samples": n_samples, "audio_seconds": round(n_samples / 48000.0, 2),
+                "realtime_factor": round(n_samples / 48000.0 / total, 1), "finite": finite, "weights": "q4_k",
+                "workload": "configs[4] per GPU: Q4_K DiT 60-step sample of 600 s (T = 15000, N = 7500, L = 512, bs 1) "
+                            "+ windowed VAE decode (128-frame windows, 32-frame overlap) through the tiled_decode hook"}
+    finally:
+        br.close()
+        set_weights("")
 
 
 def set_weights(qtype):

@@ -497,6 +497,7 @@ void launch_out_mods(const float* table, const float* tt, const float* tr, int B
 }
 
 void gemm_splitk_check() {}
+void gemm_splitk_release(hipStream_t) {}
 
 void launch_fault_tile(float* x, int ld, int rows, int row0, int col0, float amp, hipStream_t) {
     for (int r = row0; r < row0 + 16 && r < rows; ++r)

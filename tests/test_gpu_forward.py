@@ -217,6 +217,30 @@ def test_full_width_two_layers_240s(monkeypatch):
     check(got, ref, floor, "full-width 2-layer 240s", fmax)
 
 
+def test_context_destroy_then_new_context_60s(monkeypatch):
+    """ADVICE r3: a context whose stream ran split-K GEMMs (the 60 s down projection, variant 213) is destroyed;
+    a forward in a new context on the same device must still run (no sync of the dead stream, no stale error
+    word) and give the same bits as the first context's forward."""
+    from acestep_mi355x.capi import GGMLCAPIBridge
+    from acestep_mi355x.synthetic import cached_checkpoint, make_config
+    d = cached_checkpoint(make_config(num_hidden_layers=2), seed=0, backend="torch")
+    monkeypatch.setenv("ACE_GGML_DIT_MAX_LAYERS", "2")
+    rng = np.random.default_rng(60)
+    T, L = 1500, 512
+    h = rng.standard_normal((T, 64)).astype(np.float32)
+    c = np.concatenate([rng.standard_normal((T, 64)), np.ones((T, 64))], axis=1).astype(np.float32)
+    e = rng.standard_normal((L, 2048)).astype(np.float32)
+    outs = []
+    for _ in range(2):
+        br = GGMLCAPIBridge()
+        br.load_dit(d)
+        outs.append(br.dit_forward_tfirst(h, c, e, None, None, 0.7, 0.7))
+        br.synchronize()
+        br.close()
+    assert np.isfinite(outs[0]).all()
+    assert np.array_equal(outs[0], outs[1])
+
+
 @pytest.mark.slow
 def test_full_width_two_layers_600s(monkeypatch):
     """The largest BASELINE config's sequence (C5: 600 s, T = 15000 frames, N = 7500 tokens, L = 512)

@@ -125,7 +125,7 @@ def test_peaked_attention_240s_two_layers(monkeypatch, precision):
     check(got, ref, floor, f"peaked 240 s 2 layers, attention {precision}", fmax)
 
 
-@pytest.mark.parametrize("precision", ["fp16", "f32"])
+@pytest.mark.parametrize("precision", ["fp16", "split", "f32"])
 @pytest.mark.parametrize("peaked", [False, True], ids=["default", "peaked"])
 @pytest.mark.parametrize("first", ["sliding_attention", "full_attention"])
 def test_one_layer_literal_bound(monkeypatch, first, peaked, precision):
