@@ -581,6 +581,407 @@ __global__ void __launch_bounds__(256, OCC) attn_kernel(AttnArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// attn2_kernel (round 4): the same operands, layouts, block decomposition and online softmax as attn_kernel, with
+// the per-tile instruction stream laid out by hand for one wave per SIMD (the hi/lo modes run one workgroup per CU):
+//   phase B  S(i+1) = K(i+1) Q^T  (16 k-steps of (k-slice, 32-key half), 1 or 3 MFMAs each)  interleaved step by
+//            step with the softmax finish of tile i: p = exp2(s * c - m'), the row sum and the fp16 packing of
+//            one pair of scores (one v_cvt_pk_f16_f32), the K fragments read two steps ahead (counted lgkmcnt) and
+//            the next tiles' LDS-DMA pieces spread over the first steps;
+//   phase C  O^T += V^T(i) P^T(i)  (16 steps of (d-tile, 16-key group), 1 or 3 MFMAs) interleaved with the
+//            softmax start of tile i+1: the running max over raw scores (c > 0, so max(s) * c = max(s * c)
+//            exactly), V fragments read two steps ahead.
+// The score scale c = scale * log2(e) is folded into the exp2 argument (one FMA per score instead of a multiply
+// and a subtract); every MFMA accumulator chain starts from an inline zero; scores are consumed in place (no
+// copy of S between iterations: the two tile buffers alternate by name in the 2-unrolled loop).  A
+// sched_barrier after each step keeps the step's MFMAs and its VALU / LDS slice together (the compiler otherwise
+// clusters all MFMAs of a phase and leaves the VALU work exposed after them).
+template <bool F16OUT, bool SPLIT, bool PVS, bool KBIAS, int OCC>
+__global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
+    static_assert(SPLIT || !PVS, "hi/lo P.V needs hi/lo operands");
+    using RG = Ring<SPLIT, PVS>;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int h = lane >> 5;
+    const int lq = lane & 31;
+
+    const int rep = a.Hq / a.Hkv;
+    const int qpb = 128 / rep;
+    const int n_qt = (a.nq + qpb - 1) / qpb;
+    const int n_blocks = a.B * a.Hkv * n_qt * a.ksplit;
+    const int per = (n_blocks + 7) >> 3;
+    int bid = a.xcd_order ? (blockIdx.x & 7) * per + (blockIdx.x >> 3) : blockIdx.x;
+    if (bid >= n_blocks) return;
+    const int split = bid % a.ksplit;
+    bid /= a.ksplit;
+    const int qt = bid % n_qt;
+    bid /= n_qt;
+    const int kvh = bid % a.Hkv;
+    const int b = bid / a.Hkv;
+    const int waves_per_head = 4 / rep;
+    const int head = kvh * rep + wid / waves_per_head;
+    const int q0 = qt * qpb;
+    const int qw0 = q0 + (wid % waves_per_head) * 32;
+    const int qrow = qw0 + lq;
+
+    int klo = 0, khi = a.nk;
+    if (a.window > 0) {
+        klo = max(0, q0 - a.window);
+        khi = min(a.nk, q0 + qpb - 1 + a.window + 1);
+    }
+    if (a.causal) khi = min(khi, q0 + qpb);
+    const int n_all = max(0, (khi + KT - 1) / KT - klo / KT);
+    const int chunk = (n_all + a.ksplit - 1) / a.ksplit;
+    const int kt_begin = klo / KT + split * chunk;
+    const int n = max(0, min(chunk, n_all - split * chunk));
+
+    int lo_abs = 0, hi_abs = a.nk;
+    if (a.window > 0) {
+        lo_abs = max(lo_abs, qrow - a.window);
+        hi_abs = min(hi_abs, qrow + a.window + 1);
+    }
+    if (a.causal) hi_abs = min(hi_abs, qrow + 1);
+    lo_abs -= 4 * h;
+    hi_abs -= 4 * h;
+
+    const uint16_t* qptr = a.q + (((int64_t)b * a.Hq + head) * a.nq_pad + qrow) * D + 8 * h;
+    frag qf[8], qfl[8];
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) qf[ks] = *(const frag*)(qptr + 16 * ks);
+    if constexpr (SPLIT) {
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) qfl[ks] = *(const frag*)(qptr + a.q_plane + 16 * ks);
+    }
+
+    const uint16_t* kbase = a.k + ((int64_t)b * a.Hkv + kvh) * a.nk_pad * D;
+    const uint16_t* vbase = a.vt + ((int64_t)b * a.Hkv + kvh) * D * a.nk_pad;
+    const float* kb = KBIAS ? a.kbias + (int64_t)b * a.nk_pad : nullptr;
+
+    // LDS-DMA pieces of one K / V^T tile (1 KiB per wave instruction) as buffer loads: the lane part of the source
+    // offset is the same for every piece (the XOR swizzle depends on the row mod 16 / d mod 16 only), so one voffset
+    // register per operand; the piece and tile parts go to the scalar offset.  K piece p: hi rows
+    // 4 (wid + 4 (p & 3)) + lane / 16, p >= 4 the lo plane (SPLIT); V piece p: V^T d-rows 8 (wid + 4 (p & 3)) + lane / 8,
+    // p >= 4 the lo plane (PVS); the key bias: wave 0, 4 bytes per lane.
+    constexpr int NPK = SPLIT ? 8 : 4;
+    constexpr int NPV = PVS ? 8 : 4;
+    const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc((void*)kbase, 0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc((void*)vbase, 0, 0x7fffffff, 0x00020000);
+    const int krow = 4 * wid + (lane >> 4);
+    const int kvoff = krow * 256 + (((lane & 15) ^ (krow & 15)) << 4);
+    const int vrow = 8 * wid + (lane >> 3);
+    const int vvoff = vrow * a.nk_pad * 2 + (((lane & 7) ^ ((vrow >> 1) & 7)) << 4);
+    const int kplane_b = SPLIT ? (int)(a.k_plane * 2) : 0;
+    const int vplane_b = PVS ? (int)(a.v_plane * 2) : 0;
+    auto k_piece = [&](int slot, int kt, int p) {
+        const int so = kt * (KT * D * 2) + (p & 3) * 4096 + (p >= 4 ? kplane_b : 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            krs, (lds_void*)(smem + slot * RG::KS + (p >= 4 ? RG::K_LO : RG::K_HI) + (wid + 4 * (p & 3)) * 1024), 16, kvoff,
+            so, 0, 0);
+    };
+    auto v_piece = [&](int slot, int kt, int p) {
+        const int so = kt * (KT * 2) + (p & 3) * (64 * a.nk_pad) + (p >= 4 ? vplane_b : 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            vrs, (lds_void*)(smem + RG::V0 + slot * RG::VS + (p >= 4 ? RG::V_LO : 0) + (wid + 4 * (p & 3)) * 1024), 16,
+            vvoff, so, 0, 0);
+    };
+    auto bias_piece = [&](int slot, int kt) {
+        if constexpr (KBIAS) {
+            if (wid == 0)
+                __builtin_amdgcn_global_load_lds((const void*)(kb + kt * KT + lane), (lds_void*)(smem + slot * RG::KS + RG::KB),
+                                                 4, 0, 0);
+        }
+    };
+
+    const int cK = h ^ (lq & 15);
+    const int cV = h ^ ((lq >> 1) & 7);
+    const uint32_t smem_l = lds_addr(smem);
+    uint32_t kaddr[8], vaddr[4];
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) kaddr[ks] = smem_l + RG::K_HI + lq * 256 + (((2 * ks) ^ cK) << 4);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) vaddr[g] = smem_l + RG::V0 + lq * 128 + (((2 * g) ^ cV) << 4);
+    const uint32_t kbaddr = smem_l + RG::KB + 16 * h;
+
+    const float c_log2 = a.scale * 1.4426950408889634f;
+    constexpr int RK = SPLIT ? 2 : 1;   // LDS reads per QK step
+    constexpr int RV = PVS ? 2 : 1;     // LDS reads per PV step
+
+    // ---- phase B building blocks: K fragments of QK step j (k-slice ks = j / 2, half t = j % 2) from K slot SLOT
+    auto k_read = [&](auto slot_c, auto j_c, frag& hi, frag& lo) {
+        constexpr int SLOT = decltype(slot_c)::value, j = decltype(j_c)::value;
+        constexpr int t = j & 1, ks = j >> 1;
+        hi = lds_frag<SLOT * RG::KS + t * 32 * 256>(kaddr[ks]);
+        if constexpr (SPLIT) lo = lds_frag<SLOT * RG::KS + t * 32 * 256 + RG::K_LO - RG::K_HI>(kaddr[ks]);
+    };
+    // S(tile in K slot SLOT) into sn, interleaved with fin(j) (the softmax-finish slice of step j) and dma(j)
+    auto qk_phase = [&](auto slot_c, f32x16 (&sn)[2], auto&& fin, auto&& dma) {
+        frag kh[3], kl[3];
+        k_read(slot_c, std::integral_constant<int, 0>{}, kh[0], kl[0]);
+        k_read(slot_c, std::integral_constant<int, 1>{}, kh[1], kl[1]);
+        static_for<0, 16>([&](auto j_c) {
+            constexpr int j = decltype(j_c)::value;
+            constexpr int t = j & 1, ks = j >> 1;
+            if constexpr (j + 2 < 16) k_read(slot_c, std::integral_constant<int, j + 2>{}, kh[(j + 2) % 3], kl[(j + 2) % 3]);
+            // reads issued after step j's: those of steps j+1, j+2 (when issued)
+            constexpr int after = RK * ((j + 2 < 16 ? 2 : 15 - j));
+            asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(after) : "memory");
+            asm volatile("" : "+v"(kh[j % 3]));
+            if constexpr (SPLIT) asm volatile("" : "+v"(kl[j % 3]));
+            if constexpr (ks == 0) {
+                sn[t] = mfma32(kh[j % 3], qf[0], f32x16{});
+            } else {
+                sn[t] = mfma32(kh[j % 3], qf[ks], sn[t]);
+            }
+            if constexpr (SPLIT) {
+                sn[t] = mfma32(kh[j % 3], qfl[ks], sn[t]);
+                sn[t] = mfma32(kl[j % 3], qf[ks], sn[t]);
+            }
+            dma(j_c);
+            fin(j_c);
+            __builtin_amdgcn_sched_barrier(0);
+        });
+    };
+
+    float m_run = -INFINITY;
+    float l_run = 0.f;
+    f32x16 o[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
+
+    // softmax start of a tile (S in sn, its key bias in K slot SLOT, relative index i): KBIAS folds scale and bias
+    // into sn (x = s * c + bias); masks (tiles crossing a bound only) set -inf; returns the lane's max over its 64
+    // keys in the exp2 domain, combined across the two lane halves
+    auto mask_tile = [&](f32x16 (&sn)[2], int i) {
+        const int k0 = (kt_begin + i) * KT;
+        const int lo = lo_abs - k0, hi = hi_abs - k0;
+        if (__builtin_amdgcn_ballot_w64(lo > 0 || hi < 60) != 0) {
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int kr = key_of(t, r);
+                    sn[t][r] = (kr >= lo && kr < hi) ? sn[t][r] : -INFINITY;
+                }
+        }
+    };
+    auto bias_tile = [&](auto slot_c, f32x16 (&sn)[2]) {
+        if constexpr (KBIAS) {
+            constexpr int SLOT = decltype(slot_c)::value;
+            frag kbv[8];
+            static_for<0, 8>([&](auto j_c) {
+                constexpr int j = decltype(j_c)::value;
+                kbv[j] = lds_frag<SLOT * RG::KS + (32 * (j / 4) + 8 * (j % 4)) * 4>(kbaddr);
+            });
+            lds_wait_tie(kbv);
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    sn[t][r] = __builtin_fmaf(sn[t][r], c_log2, __uint_as_float(kbv[4 * t + (r >> 2)][r & 3]));
+        }
+    };
+    auto finish_max = [&](float mraw) -> float {
+        const float mx = KBIAS ? mraw : (mraw == -INFINITY ? -INFINITY : mraw * c_log2);
+        return fmaxf(mx, __shfl_xor(mx, 32));
+    };
+
+    float alpha = 1.f;
+    bool rescale = false;
+    auto update_max = [&](float mloc) {
+        const bool move = mloc > m_run + RESCALE_LOG2;
+        alpha = move ? __builtin_amdgcn_exp2f(m_run - mloc) : 1.f;
+        m_run = move ? mloc : m_run;
+        rescale = __builtin_amdgcn_ballot_w64(move) != 0;
+    };
+    auto apply_rescale = [&]() {
+        if (rescale) {
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+            l_run *= alpha;
+        }
+    };
+
+    f32x16 sA[2], sB[2];
+    auto no_fin = [](auto) {};
+    auto no_dma = [](auto) {};
+    if (n > 0) {
+#pragma unroll
+        for (int p = 0; p < NPK; ++p) k_piece(0, kt_begin, p);
+        bias_piece(0, kt_begin);
+#pragma unroll
+        for (int p = 0; p < NPV; ++p) v_piece(0, kt_begin, p);
+        if (n > 1) {
+#pragma unroll
+            for (int p = 0; p < NPK; ++p) k_piece(1, kt_begin + 1, p);
+            bias_piece(1, kt_begin + 1);
+        }
+        wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        qk_phase(std::integral_constant<int, 0>{}, sA, no_fin, no_dma);
+        bias_tile(std::integral_constant<int, 0>{}, sA);
+        mask_tile(sA, 0);
+        float mr = -INFINITY;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) mr = fmaxf(mr, sA[t][r]);
+        update_max(finish_max(mr));
+        apply_rescale();
+        __builtin_amdgcn_s_barrier();  // every wave has read K slot 0: iteration 0 restages it
+    }
+
+    // one pipeline iteration for relative tile i: S(i) in sc (from K slot SLOT), V(i) in V slot SLOT; computes
+    // S(i+1) into sn from K slot NXT
+    auto iter = [&](auto slot_c, f32x16 (&sc)[2], f32x16 (&sn)[2], int i) {
+        constexpr int SLOT = decltype(slot_c)::value;
+        constexpr int NXT = SLOT ^ 1;
+        const bool more = i + 1 < n;
+        const bool more2 = i + 2 < n;
+        const int ktk = kt_begin + i + 2, ktv = kt_begin + i + 1;
+        const float m_use = ((m_run == -INFINITY) ? 0.f : m_run) - PSCALE_LOG2;
+        const float nm = -m_use;
+        float lsum = 0.f;
+        frag pf[4], pfl[4];
+        // softmax finish of tile i, pair j (elements 2j, 2j + 1 of the flattened [t][r] scores)
+        auto fin = [&](auto j_c) {
+            constexpr int j = decltype(j_c)::value;
+            constexpr int t = j >> 3, r = 2 * (j & 7);
+            float p0, p1;
+            if constexpr (KBIAS) {
+                p0 = __builtin_amdgcn_exp2f(sc[t][r] + nm);
+                p1 = __builtin_amdgcn_exp2f(sc[t][r + 1] + nm);
+            } else {
+                p0 = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[t][r], c_log2, nm));
+                p1 = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[t][r + 1], c_log2, nm));
+            }
+            lsum += p0;
+            lsum += p1;
+            constexpr int fi = 2 * t + (r >> 3), fj = (r & 7) >> 1;
+            // (the empty asm pins each result to its step: without it the IR passes sink the whole softmax finish
+            // to the P.V MFMAs that consume it, i.e. after every MFMA of this phase)
+            if constexpr (PVS) {
+                const auto h2 = __builtin_amdgcn_cvt_pkrtz(p0, p1);
+                uint32_t w = __builtin_bit_cast(uint32_t, h2);
+                uint32_t wl = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(p0 - (float)h2[0], p1 - (float)h2[1]));
+                asm volatile("" : "+v"(w), "+v"(wl), "+v"(lsum));
+                pf[fi][fj] = w;
+                pfl[fi][fj] = wl;
+            } else {
+                typedef float f2 __attribute__((ext_vector_type(2)));
+                typedef _Float16 h2t __attribute__((ext_vector_type(2)));
+                const h2t hv = __builtin_convertvector((f2){p0, p1}, h2t);
+                uint32_t w = __builtin_bit_cast(uint32_t, hv);
+                asm volatile("" : "+v"(w), "+v"(lsum));
+                pf[fi][fj] = w;
+            }
+        };
+        auto dma = [&](auto j_c) {
+            constexpr int j = decltype(j_c)::value;
+            static_assert(NPK + NPV <= 16, "one DMA piece per QK step");
+            if constexpr (j < NPK) {
+                if (more2) {
+                    k_piece(SLOT, ktk, j);
+                    if constexpr (j == 0) bias_piece(SLOT, ktk);
+                }
+            } else if constexpr (j < NPK + NPV) {
+                if (more) v_piece(NXT, ktv, j - NPK);
+            }
+        };
+        qk_phase(std::integral_constant<int, NXT>{}, sn, [&](auto j_c) { fin(j_c); }, [&](auto j_c) { dma(j_c); });
+        l_run += lsum;
+
+        // phase C: O^T += V^T(i) P^T(i) || softmax start of tile i+1
+        bias_tile(std::integral_constant<int, NXT>{}, sn);
+        mask_tile(sn, i + 1);
+        float mr = -INFINITY;
+        {
+            frag vh[3], vl[3];
+            auto v_read = [&](auto j_c, frag& hi, frag& lo) {
+                constexpr int j = decltype(j_c)::value;
+                constexpr int dt = j >> 2, g = j & 3;
+                hi = lds_frag<SLOT * RG::VS + dt * 32 * 128>(vaddr[g]);
+                if constexpr (PVS) lo = lds_frag<SLOT * RG::VS + dt * 32 * 128 + RG::V_LO>(vaddr[g]);
+            };
+            v_read(std::integral_constant<int, 0>{}, vh[0], vl[0]);
+            v_read(std::integral_constant<int, 1>{}, vh[1], vl[1]);
+            static_for<0, 16>([&](auto j_c) {
+                constexpr int j = decltype(j_c)::value;
+                constexpr int dt = j >> 2, g = j & 3;
+                if constexpr (j + 2 < 16) v_read(std::integral_constant<int, j + 2>{}, vh[(j + 2) % 3], vl[(j + 2) % 3]);
+                constexpr int after = RV * ((j + 2 < 16 ? 2 : 15 - j));
+                asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(after) : "memory");
+                asm volatile("" : "+v"(vh[j % 3]));
+                if constexpr (PVS) asm volatile("" : "+v"(vl[j % 3]));
+                o[dt] = mfma32(vh[j % 3], pf[g], o[dt]);
+                if constexpr (PVS) {
+                    o[dt] = mfma32(vh[j % 3], pfl[g], o[dt]);
+                    o[dt] = mfma32(vl[j % 3], pf[g], o[dt]);
+                }
+                // running max of tile i+1: two scores per step
+                constexpr int t = j >> 3, r = 2 * (j & 7);
+                mr = fmaxf(mr, fmaxf(sn[t][r], sn[t][r + 1]));
+                asm volatile("" : "+v"(mr));
+                __builtin_amdgcn_sched_barrier(0);
+            });
+        }
+        const float mnx = finish_max(mr);
+        if (more) {
+            update_max(mnx);
+            apply_rescale();
+            wait_vmcnt<0>();
+            __builtin_amdgcn_s_barrier();
+        }
+    };
+
+    int i = 0;
+    for (; i + 1 < n; i += 2) {
+        iter(std::integral_constant<int, 0>{}, sA, sB, i);
+        iter(std::integral_constant<int, 1>{}, sB, sA, i + 1);
+    }
+    if (i < n) iter(std::integral_constant<int, 0>{}, sA, sB, i);
+
+    const float l = l_run + __shfl_xor(l_run, 32);
+    if (a.ksplit > 1) {
+        if (qrow < a.nq) {
+            const int64_t row = ((int64_t)split * a.B + b) * a.nq + qrow;
+            float* po = a.part + row * (a.Hq * D) + head * D;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int g4 = 0; g4 < 4; ++g4)
+                    *(float4*)(po + 32 * dt + 8 * g4 + 4 * h) =
+                        make_float4(o[dt][4 * g4 + 0], o[dt][4 * g4 + 1], o[dt][4 * g4 + 2], o[dt][4 * g4 + 3]);
+            if (h == 0)
+                *(float2*)(a.part + (int64_t)a.ksplit * a.B * a.nq * a.Hq * D + (row * a.Hq + head) * 2) =
+                    make_float2(m_run, l);
+        }
+        return;
+    }
+    const float inv = 1.0f / l;
+    if (qrow < a.nq) {
+        uint16_t* op = a.out + ((int64_t)b * a.nq + qrow) * (a.Hq * D) + head * D;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+                const int d = 32 * dt + 8 * g4 + 4 * h;
+                uint2 w;
+                w.x = (uint32_t)to_act<F16OUT>(o[dt][4 * g4 + 0] * inv) |
+                      ((uint32_t)to_act<F16OUT>(o[dt][4 * g4 + 1] * inv) << 16);
+                w.y = (uint32_t)to_act<F16OUT>(o[dt][4 * g4 + 2] * inv) |
+                      ((uint32_t)to_act<F16OUT>(o[dt][4 * g4 + 3] * inv) << 16);
+                *(uint2*)(op + d) = w;
+            }
+        }
+    }
+}
+
 // Combine the S key-range parts of one (item, query, head) row: M = max m_k, weights 2^(m_k - M) (0 for a
 // part whose keys were all masked), out = sum w_k O_k / sum w_k l_k; a row with no unmasked key at all stays
 // 0/0 = NaN as in ggml.  Half a wave per row, 16-byte partial reads, every load issued before the first use.
@@ -621,6 +1022,19 @@ __global__ void __launch_bounds__(256) attn_merge_kernel(AttnArgs a) {
 template <bool F16OUT, bool SPLIT, bool PVS>
 void launch_t(const AttnArgs& a, dim3 grid, hipStream_t s) {
     const size_t lds = Ring<SPLIT, PVS>::BYTES;
+    static int v2 = -1;  // ACE_MI_ATTN_V1=1: round 3's kernel (A/B)
+    if (v2 < 0) {
+        const char* e = std::getenv("ACE_MI_ATTN_V1");
+        v2 = (e && e[0] == '1') ? 0 : 1;
+    }
+    if (v2 && a.fused_merge == 0) {
+        constexpr int OCC = SPLIT ? 1 : 2;
+        if (a.kbias)
+            hipLaunchKernelGGL((attn2_kernel<F16OUT, SPLIT, PVS, true, OCC>), grid, dim3(256), lds, s, a);
+        else
+            hipLaunchKernelGGL((attn2_kernel<F16OUT, SPLIT, PVS, false, OCC>), grid, dim3(256), lds, s, a);
+        return;
+    }
     static int occ = 0;  // ACE_MI_ATTN_OCC=1: one workgroup per CU for the single-fp16 kernel too (A/B)
     if (occ == 0) {
         const char* e = std::getenv("ACE_MI_ATTN_OCC");

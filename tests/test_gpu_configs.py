@@ -233,3 +233,53 @@ def test_config4_vae_decode_192_frames_windowed():
     floor = float(np.linalg.norm(pert.astype(np.float64) - ref) / np.linalg.norm(ref.astype(np.float64)))
     assert got.shape == ref.shape, (got.shape, ref.shape)
     check(got, ref, floor, "full VAE, 192 frames windowed")
+
+
+def test_config4_vae_decode_full_600s_windowed():
+    """configs[4]'s whole decode: the 600 s latent (T = 15000 frames) through the installed tiled_decode hook with
+    the reference C path's default plan (ACE_GGML_VAE_CHUNK_FRAMES 128, overlap 32: acestep_ggml.cpp:2114-2151)
+    -- 235 windows.  Exact length (the hook's plan length and T x hop), finite everywhere, and three interior
+    windows (first, middle, last) equal the oracle decoding the same window frames, trimmed the same way."""
+    import torch
+    import types
+    from acestep_mi355x.capi import GGMLCAPIBridge
+    from acestep_mi355x.hook import install_vae_backend, tiled_out_len
+    from acestep_mi355x.synthetic import VAE_FULL_CONFIG
+    from oracle import vae_oracle as V
+    from test_gpu_vae import _ckpt
+    d = _ckpt(VAE_FULL_CONFIG)
+    br = GGMLCAPIBridge()
+    br.load_vae(d)
+    handler = types.SimpleNamespace()
+    install_vae_backend(handler, br, chunk_size_default=128, overlap_default=32)
+    T = 15000
+    lat = np.random.default_rng(600).standard_normal((1, 64, T)).astype(np.float32)
+    got = handler.tiled_decode(torch.from_numpy(lat).cuda(), offload_wav_to_cpu=True).numpy()[0].T  # [samples, ch]
+    n_expect = tiled_out_len(br, T, 128, 32)
+    hop = br.vae_out_len(1)
+    br.close()
+    assert got.shape == (n_expect, 2), (got.shape, n_expect)
+    assert n_expect == T * hop, (n_expect, T, hop)
+    assert np.isfinite(got).all()
+    W = V.VaeWeights(d)
+    plan = _python_plan(T, 128, 32)
+    offs = np.cumsum([0] + [(ce - cs) * hop for cs, ce, _, _ in plan])
+
+    def window(idx):
+        cs, ce, ws, we = plan[idx]
+        wav = V.decode(W, lat[0, :, ws:we].T)
+        up = wav.shape[0] / max(1, we - ws)
+        ts, te = int(round((cs - ws) * up)), int(round((we - ce) * up))
+        return wav[ts:wav.shape[0] - te if te > 0 else wav.shape[0]]
+
+    for idx in (0, len(plan) // 2, len(plan) - 1):
+        ref = window(idx)
+        V.CONV_PERTURB = 1e-6
+        try:
+            pert = window(idx)
+        finally:
+            V.CONV_PERTURB = 0.0
+        floor = float(np.linalg.norm(pert.astype(np.float64) - ref) / np.linalg.norm(ref.astype(np.float64)))
+        seg = got[offs[idx]:offs[idx + 1]]
+        assert seg.shape == ref.shape, (idx, seg.shape, ref.shape)
+        check(seg, ref, floor, f"600 s VAE decode, window {idx} of {len(plan)}")

@@ -1,0 +1,108 @@
+"""Static issue-cost model of a kernel's loops (one wave alone on its SIMD, MI355X_MICROARCH.md cycle constants):
+an MFMA occupies the matrix pipe 32 (32x32x16) / 16 (16x16x32) cycles and holds vector issue for 8; VALU issue 4
+(transcendentals 8), LDS reads 4, LDS writes 13, LDS-DMA pieces 60 (guide: 'among bare MFMAs'), scalar 2.  Data
+dependences and waits are ignored, so the estimate is a lower bound; the interesting number is its ratio to the
+MFMA-only time.  Usage: python tools/isa_cost.py file.s [kernel-name-substring]"""
+import os
+import re
+import sys
+
+TRANS = ("v_exp_", "v_log_", "v_rcp_", "v_rsq_", "v_sqrt_", "v_sin_", "v_cos_")
+
+
+def cost(op):
+    if op.startswith("v_mfma"):
+        return ("M", 16 if "16x16" in op else 32)
+    if op.startswith(TRANS):
+        return ("E", 8)
+    if op.startswith("v_"):
+        return ("v", 4)
+    if op.startswith("ds_read") or op.startswith("ds_bpermute") or op.startswith("ds_permute"):
+        return ("R", 4)
+    if op.startswith("ds_"):
+        return ("W", 13)
+    if op.startswith("global_load_lds") or (op.startswith("buffer_load") and "lds" in op):
+        return ("D", 60)
+    if op.startswith("global_") or op.startswith("buffer_") or op.startswith("scratch_"):
+        return ("G", 8)
+    if op.startswith("s_waitcnt"):
+        return ("w", 0)
+    if op.startswith("s_barrier"):
+        return ("B", 0)
+    if op.startswith("s_nop"):
+        return ("n", 4)
+    if op.startswith("s_"):
+        return ("s", 2)
+    return ("?", 4)
+
+
+def simulate(ops):
+    t = 0
+    pipe = 0
+    mf = 0
+    for op in ops:
+        c, k = cost(op)
+        if c == "M":
+            start = max(t, pipe)
+            pipe = start + k
+            t = start + 8
+            mf += k
+        else:
+            t += k
+    return max(t, pipe), mf
+
+
+def main(path, pat=""):
+    cur = None
+    funcs = {}
+    for line in open(path):
+        m = re.match(r"^(_Z\S+):", line)
+        if m:
+            cur = m.group(1)
+            funcs[cur] = []
+            continue
+        if cur:
+            funcs[cur].append(line)
+    for name, text in funcs.items():
+        if pat and pat not in name:
+            continue
+        labels = {}
+        for i, l in enumerate(text):
+            m = re.match(r"^(\.LBB\d+_\d+):", l)
+            if m:
+                labels[m.group(1)] = i
+        for j, l in enumerate(text):
+            m = re.search(r"s_c?branch\w*\s+(\.LBB\d+_\d+)", l)
+            if not m or labels.get(m.group(1), 1 << 30) >= j:
+                continue
+            body = text[labels[m.group(1)]:j + 1]
+            if os.environ.get("ISA_SKIP_FWD") == "1":
+                # drop forward-skipped regions (rare branches: masks, rescales): from a conditional forward branch to
+                # its target label
+                kept, skip_to = [], None
+                for b in body:
+                    lm = re.match(r"^(\.LBB\d+_\d+):", b)
+                    if skip_to and lm and lm.group(1) == skip_to:
+                        skip_to = None
+                    if skip_to:
+                        continue
+                    fm = re.search(r"s_cbranch_(?:vccz|vccnz|execz|scc0|scc1)\s+(\.LBB\d+_\d+)", b)
+                    if fm and labels.get(fm.group(1), -1) > labels[m.group(1)] and labels.get(fm.group(1), 1 << 30) <= j:
+                        skip_to = fm.group(1)
+                    kept.append(b)
+                body = kept
+            ops = [b.split()[0] for b in body if b.strip() and not b.strip().startswith((";", ".")) and not b.startswith(".")]
+            if sum(1 for o in ops if o.startswith("v_mfma")) < 8:
+                continue
+            cyc, mf = simulate(ops)
+            cnt = {}
+            for o in ops:
+                c, _ = cost(o)
+                cnt[c] = cnt.get(c, 0) + 1
+            acc = sum(1 for o in ops if o.startswith("v_accvgpr"))
+            print(f"{name[:100]} {m.group(1)}: ops={len(ops)} mfma_cyc={mf} est_cyc={cyc} util={mf / max(cyc, 1):.2f} "
+                  f"counts={dict(sorted(cnt.items()))} accvgpr={acc}")
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
