@@ -523,8 +523,9 @@ class GGMLCAPIBridge:
         self._ensure_ok(self.lib.ace_mi_synchronize(self.ctx), "ace_mi_synchronize")
 
     def set_attn_precision(self, mode: str) -> None:
-        """DiT attention operand precision for subsequent forwards: "fp16", "split" or "f32"."""
-        code = {"fp16": 0, "split": 1, "f32": 2}[mode]
+        """DiT attention operand precision for subsequent forwards: "fp16", "split", "f32" or "f8c"
+        (include/acestep_mi355x.h, ace_mi_dit_set_attn_precision)."""
+        code = {"fp16": 0, "split": 1, "f32": 2, "f8c": 3}[mode]
         self._ensure_ok(self.lib.ace_mi_dit_set_attn_precision(self.ctx, code), "ace_mi_dit_set_attn_precision")
 
     def profile_enable(self, on: bool) -> None:
@@ -580,9 +581,10 @@ def kernel_gemm(a_bits: np.ndarray, w_bits: np.ndarray, act_type: int = 0, epi: 
 
 def kernel_attention(q: np.ndarray, kv: np.ndarray, hq: int, hkv: int, window: int = 0,
                      kmask: Optional[np.ndarray] = None, scale: Optional[float] = None,
-                     split: bool = True, causal: bool = False, pv_split: bool = False) -> np.ndarray:
+                     split: bool = True, causal: bool = False, pv_split: bool = False, f8: bool = False) -> np.ndarray:
     """q [B][nq][hq*128] f32, kv [B][nk][2*hkv*128] f32 -> out [B][nq][hq*128] f32 (bf16-rounded).
-    split: hi/lo fp16 Q.K; pv_split: hi/lo fp16 P.V too (both = the fully f32-faithful mode)."""
+    split: hi/lo fp16 Q.K; pv_split: hi/lo fp16 P.V too (both = the fully f32-faithful mode); f8 (with both):
+    the f8c mode (fp8 correction products)."""
     lib = load_selftest_library()
     q = np.ascontiguousarray(q, dtype=np.float32)
     kv = np.ascontiguousarray(kv, dtype=np.float32)
@@ -592,7 +594,7 @@ def kernel_attention(q: np.ndarray, kv: np.ndarray, hq: int, hkv: int, window: i
     out = np.empty_like(q)
     sc = float(scale) if scale is not None else 1.0 / np.sqrt(128.0)
     st = lib.ace_mi_kernel_attention(B, hq, hkv, nq, nk, int(window), sc, (1 if split else 0) | (2 if causal else 0)
-                                     | (8 if pv_split else 0), _fptr(q), _fptr(kv),
+                                     | (8 if pv_split else 0) | (16 if f8 else 0), _fptr(q), _fptr(kv),
                                      _iptr(km), _fptr(out))
     if st != ACE_GGML_OK:
         raise RuntimeError(f"ace_mi_kernel_attention failed (status={st})")
@@ -600,11 +602,13 @@ def kernel_attention(q: np.ndarray, kv: np.ndarray, hq: int, hkv: int, window: i
 
 
 def bench_attention(B: int, hq: int, hkv: int, nq: int, nk: int, window: int = 0, split: bool = True,
-                    causal: bool = False, masked: bool = False, iters: int = 20, pv_split: bool = False) -> float:
+                    causal: bool = False, masked: bool = False, iters: int = 20, pv_split: bool = False,
+                    f8: bool = False) -> float:
     """Average ms per launch of the engine's attention kernel on pseudo-random operands (GPU)."""
     lib = load_selftest_library()
     ms = ctypes.c_float(0.0)
-    flags = (1 if split else 0) | (2 if causal else 0) | (4 if masked else 0) | (8 if pv_split else 0)
+    flags = (1 if split else 0) | (2 if causal else 0) | (4 if masked else 0) | (8 if pv_split else 0) | \
+        (16 if f8 else 0)
     st = lib.ace_mi_bench_attention(B, hq, hkv, nq, nk, int(window), flags, iters, ctypes.byref(ms))
     if st != ACE_GGML_OK:
         raise RuntimeError(f"ace_mi_bench_attention failed (status={st})")

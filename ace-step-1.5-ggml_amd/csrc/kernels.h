@@ -26,6 +26,7 @@ struct PrepArgs {
     uint16_t* kh;
     uint16_t* vt;
     int64_t q_plane = 0, k_plane = 0, v_plane = 0;  // >0: also write lo = f16(x - f16(x)) planes
+    int f8 = 0;  // 1: the lo planes hold the fp8 operands of the f8c attention mode instead (prep_math.h)
     // > 1 (k / v sections only): one launch for `layers` consecutive layers, layer l reading src + l*src_layer,
     // writing kh + l*kh_layer / vt + l*vt_layer, normalising by k_norm_layers[l] (a device table)
     int layers = 1;
@@ -129,13 +130,17 @@ struct AttnArgs {
     int ksplit = 1;  // set by launch_attention
     int xcd_order = 1;  // set by launch_attention: XCD-aware block order
     int fused_merge = 0;  // set by launch_attention: the last part of a key-split group merges (no merge kernel)
+    bool f8 = false;  // f8c mode (needs split + pv_split): the lo planes hold fp8 hi / lo operands (prep_math.h), the
+                      // correction products Kl.Qh + Kh.Ql and Vl.Ph + Vh.Pl run as block-scaled fp8 MFMAs
 };
 size_t attn_part_floats(int B, int nq, int Hq);
 // Operand precision of the attention MFMAs: FP16 = single fp16 operands (two workgroups per CU),
 // SPLIT = hi/lo fp16 Q.K (three MFMAs per product) with fp16 P.V, F32 = hi/lo fp16 for both products
-// (~22-bit operands, the f32-faithful mode).  ACE_MI_ATTN_PRECISION=fp16|split|f32 overrides `dflt`;
+// (~22-bit operands, the f32-faithful mode), F8C = hi/lo for both products with the two correction products as
+// block-scaled e4m3 MFMAs (hi x hi in fp16, Kl.Qh + Kh.Ql and Vl.Ph + Vh.Pl at e4m3 precision: ~2^-15 relative
+// per product instead of F32's ~2^-22, at 2/3 of F32's matrix-core time).  ACE_MI_ATTN_PRECISION=fp16|split|f32 overrides `dflt`;
 // the legacy ACE_MI_ATTN_FAST=1 means fp16.
-enum class AttnPrecision { FP16, SPLIT, F32 };
+enum class AttnPrecision { FP16, SPLIT, F32, F8C };
 inline AttnPrecision attn_precision_from_env(AttnPrecision dflt) {
     const char* f = std::getenv("ACE_MI_ATTN_FAST");
     if (f && f[0] && f[0] != '0') return AttnPrecision::FP16;
@@ -145,7 +150,8 @@ inline AttnPrecision attn_precision_from_env(AttnPrecision dflt) {
     if (v == "fp16") return AttnPrecision::FP16;
     if (v == "split") return AttnPrecision::SPLIT;
     if (v == "f32") return AttnPrecision::F32;
-    throw std::runtime_error("ACE_MI_ATTN_PRECISION must be fp16, split or f32");
+    if (v == "f8c") return AttnPrecision::F8C;
+    throw std::runtime_error("ACE_MI_ATTN_PRECISION must be fp16, split, f32 or f8c");
 }
 void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s);
 

@@ -89,6 +89,21 @@ __device__ __forceinline__ f32x16 mfma32(const frag& a, const frag& b, f32x16 c)
                                                   0, 0);
 }
 
+typedef __attribute__((ext_vector_type(8))) int v8i;
+__device__ __forceinline__ v8i cat8(const frag& x, const frag& y) {
+    return v8i{(int)x[0], (int)x[1], (int)x[2], (int)x[3], (int)y[0], (int)y[1], (int)y[2], (int)y[3]};
+}
+__device__ __forceinline__ v8i cat8(const uint32_t (&w)[8]) {
+    return v8i{(int)w[0], (int)w[1], (int)w[2], (int)w[3], (int)w[4], (int)w[5], (int)w[6], (int)w[7]};
+}
+// f8c mode: block-scaled e4m3 x e4m3 MFMA, K = 64, with E8M0 scales (127 = 1, 116 = 2^-11) on A and B
+constexpr int F8_SCALE_1 = 127;
+constexpr int F8_SCALE_LO = 127 - 11;
+constexpr float PSCALE_F8_LOG2 = 5.0f;  // f8c: P <= 2^(5 + RESCALE_LOG2) = 256, inside e4m3 (max 448)
+__device__ __forceinline__ f32x16 mfma_f8(const v8i& a, const v8i& b, f32x16 c, int sa, int sb) {
+    return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 0, 0, 0, sa, 0, sb);
+}
+
 template <int OFF>
 __device__ __forceinline__ frag lds_frag(uint32_t addr) {
     frag v;
@@ -596,9 +611,10 @@ __global__ void __launch_bounds__(256, OCC) attn_kernel(AttnArgs a) {
 // copy of S between iterations: the two tile buffers alternate by name in the 2-unrolled loop).  A
 // sched_barrier after each step keeps the step's MFMAs and its VALU / LDS slice together (the compiler otherwise
 // clusters all MFMAs of a phase and leaves the VALU work exposed after them).
-template <bool F16OUT, bool SPLIT, bool PVS, bool KBIAS, int OCC>
+template <bool F16OUT, bool SPLIT, bool PVS, bool KBIAS, int OCC, bool F8 = false>
 __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
     static_assert(SPLIT || !PVS, "hi/lo P.V needs hi/lo operands");
+    static_assert(!F8 || (SPLIT && PVS), "f8c stages both lo planes");
     using RG = Ring<SPLIT, PVS>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x;
@@ -648,9 +664,14 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
 
     const uint16_t* qptr = a.q + (((int64_t)b * a.Hq + head) * a.nq_pad + qrow) * D + 8 * h;
     frag qf[8], qfl[8];
+    v8i q8[4];  // F8: B operands of the correction chain, bytes [64 c + 32 h, +32) of the [hi8 | lo8] q row
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) qf[ks] = *(const frag*)(qptr + 16 * ks);
-    if constexpr (SPLIT) {
+    if constexpr (F8) {
+        const char* q8row = reinterpret_cast<const char*>(qptr - 8 * h + a.q_plane) + 32 * h;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) q8[c] = cat8(*(const frag*)(q8row + 64 * c), *(const frag*)(q8row + 64 * c + 16));
+    } else if constexpr (SPLIT) {
 #pragma unroll
         for (int ks = 0; ks < 8; ++ks) qfl[ks] = *(const frag*)(qptr + a.q_plane + 16 * ks);
     }
@@ -703,38 +724,69 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
 #pragma unroll
     for (int g = 0; g < 4; ++g) vaddr[g] = smem_l + RG::V0 + lq * 128 + (((2 * g) ^ cV) << 4);
     const uint32_t kbaddr = smem_l + RG::KB + 16 * h;
+    // F8: fp8 K row (key 32 t + lq) chunks 4 c + 2 h + e, fp8 V^T row (d = 32 dt + lq) chunks 4 i + 2 h + e, swizzled
+    // like the fp16 images (the same LDS-DMA pieces fill them)
+    uint32_t k8a[4][2], v8a[2][2];
+    if constexpr (F8) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int e = 0; e < 2; ++e) k8a[c][e] = smem_l + RG::K_LO + lq * 256 + (((4 * c + 2 * h + e) ^ (lq & 15)) << 4);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int e = 0; e < 2; ++e)
+                v8a[i][e] = smem_l + RG::V0 + RG::V_LO + lq * 128 + (((4 * i + 2 * h + e) ^ ((lq >> 1) & 7)) << 4);
+    }
+    constexpr float PSC = F8 ? PSCALE_F8_LOG2 : PSCALE_LOG2;
 
     const float c_log2 = a.scale * 1.4426950408889634f;
     constexpr int RK = SPLIT ? 2 : 1;   // LDS reads per QK step
     constexpr int RV = PVS ? 2 : 1;     // LDS reads per PV step
 
-    // ---- phase B building blocks: K fragments of QK step j (k-slice ks = j / 2, half t = j % 2) from K slot SLOT
-    auto k_read = [&](auto slot_c, auto j_c, frag& hi, frag& lo) {
+    // ---- phase B building blocks: K fragments of QK step j from K slot SLOT.  Steps j < 16: k-slice ks = j / 2 of
+    // half t = j % 2 (fp16 hi, + lo for SPLIT); F8 steps j = 16..23: correction chunk c = (j - 16) / 2 of half t
+    // (two 16-byte reads of the fp8 row)
+    constexpr int NB = F8 ? 24 : 16;
+    auto k_read = [&](auto slot_c, auto j_c, frag& x, frag& y) {
         constexpr int SLOT = decltype(slot_c)::value, j = decltype(j_c)::value;
-        constexpr int t = j & 1, ks = j >> 1;
-        hi = lds_frag<SLOT * RG::KS + t * 32 * 256>(kaddr[ks]);
-        if constexpr (SPLIT) lo = lds_frag<SLOT * RG::KS + t * 32 * 256 + RG::K_LO - RG::K_HI>(kaddr[ks]);
+        constexpr int t = j & 1;
+        if constexpr (j < 16) {
+            constexpr int ks = j >> 1;
+            x = lds_frag<SLOT * RG::KS + t * 32 * 256>(kaddr[ks]);
+            if constexpr (SPLIT && !F8) y = lds_frag<SLOT * RG::KS + t * 32 * 256 + RG::K_LO - RG::K_HI>(kaddr[ks]);
+        } else {
+            constexpr int c = (j - 16) >> 1;
+            x = lds_frag<SLOT * RG::KS + t * 32 * 256>(k8a[c][0]);
+            y = lds_frag<SLOT * RG::KS + t * 32 * 256>(k8a[c][1]);
+        }
     };
+    // LDS reads of QK step j, and of the reads issued after step j's own (steps j+1, j+2)
+    auto rk = [](int j) constexpr { return F8 ? (j < 16 ? 1 : 2) : (SPLIT ? 2 : 1); };
     // S(tile in K slot SLOT) into sn, interleaved with fin(j) (the softmax-finish slice of step j) and dma(j)
     auto qk_phase = [&](auto slot_c, f32x16 (&sn)[2], auto&& fin, auto&& dma) {
         frag kh[3], kl[3];
         k_read(slot_c, std::integral_constant<int, 0>{}, kh[0], kl[0]);
         k_read(slot_c, std::integral_constant<int, 1>{}, kh[1], kl[1]);
-        static_for<0, 16>([&](auto j_c) {
+        static_for<0, NB>([&](auto j_c) {
             constexpr int j = decltype(j_c)::value;
             constexpr int t = j & 1, ks = j >> 1;
-            if constexpr (j + 2 < 16) k_read(slot_c, std::integral_constant<int, j + 2>{}, kh[(j + 2) % 3], kl[(j + 2) % 3]);
-            // reads issued after step j's: those of steps j+1, j+2 (when issued)
-            constexpr int after = RK * ((j + 2 < 16 ? 2 : 15 - j));
+            if constexpr (j + 2 < NB) k_read(slot_c, std::integral_constant<int, j + 2>{}, kh[(j + 2) % 3], kl[(j + 2) % 3]);
+            constexpr int after = (j + 1 < NB ? rk(j + 1) : 0) + (j + 2 < NB ? rk(j + 2) : 0);
             asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(after) : "memory");
             asm volatile("" : "+v"(kh[j % 3]));
-            if constexpr (SPLIT) asm volatile("" : "+v"(kl[j % 3]));
-            if constexpr (ks == 0) {
+            if constexpr (rk(j) == 2) asm volatile("" : "+v"(kl[j % 3]));
+            if constexpr (j >= 16) {
+                // Kl.Qh (c = 0, 1: the 2^-11 on A) + Kh.Ql (c = 2, 3: on B), e4m3 x e4m3, K = 64 per MFMA
+                constexpr int c = (j - 16) >> 1;
+                sn[t] = mfma_f8(cat8(kh[j % 3], kl[j % 3]), q8[c], sn[t], c < 2 ? F8_SCALE_LO : F8_SCALE_1,
+                                c < 2 ? F8_SCALE_1 : F8_SCALE_LO);
+            } else if constexpr (ks == 0) {
                 sn[t] = mfma32(kh[j % 3], qf[0], f32x16{});
             } else {
                 sn[t] = mfma32(kh[j % 3], qf[ks], sn[t]);
             }
-            if constexpr (SPLIT) {
+            if constexpr (SPLIT && !F8 && j < 16) {
                 sn[t] = mfma32(kh[j % 3], qfl[ks], sn[t]);
                 sn[t] = mfma32(kl[j % 3], qf[ks], sn[t]);
             }
@@ -844,46 +896,61 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
         const bool more = i + 1 < n;
         const bool more2 = i + 2 < n;
         const int ktk = kt_begin + i + 2, ktv = kt_begin + i + 1;
-        const float m_use = ((m_run == -INFINITY) ? 0.f : m_run) - PSCALE_LOG2;
+        const float m_use = ((m_run == -INFINITY) ? 0.f : m_run) - PSC;
         const float nm = -m_use;
         float lsum = 0.f;
         frag pf[4], pfl[4];
+        uint32_t ph8[8], pl8[8];  // F8: fp8 P (hi) and P - f16(P) (lo), byte c = 16 t + r of the lane's 32 keys
         // softmax finish of tile i, pair j (elements 2j, 2j + 1 of the flattened [t][r] scores)
         auto fin = [&](auto j_c) {
             constexpr int j = decltype(j_c)::value;
-            constexpr int t = j >> 3, r = 2 * (j & 7);
-            float p0, p1;
-            if constexpr (KBIAS) {
-                p0 = __builtin_amdgcn_exp2f(sc[t][r] + nm);
-                p1 = __builtin_amdgcn_exp2f(sc[t][r + 1] + nm);
-            } else {
-                p0 = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[t][r], c_log2, nm));
-                p1 = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[t][r + 1], c_log2, nm));
-            }
-            lsum += p0;
-            lsum += p1;
-            constexpr int fi = 2 * t + (r >> 3), fj = (r & 7) >> 1;
-            // (the empty asm pins each result to its step: without it the IR passes sink the whole softmax finish
-            // to the P.V MFMAs that consume it, i.e. after every MFMA of this phase)
-            if constexpr (PVS) {
-                const auto h2 = __builtin_amdgcn_cvt_pkrtz(p0, p1);
-                uint32_t w = __builtin_bit_cast(uint32_t, h2);
-                uint32_t wl = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(p0 - (float)h2[0], p1 - (float)h2[1]));
-                asm volatile("" : "+v"(w), "+v"(wl), "+v"(lsum));
-                pf[fi][fj] = w;
-                pfl[fi][fj] = wl;
-            } else {
-                typedef float f2 __attribute__((ext_vector_type(2)));
-                typedef _Float16 h2t __attribute__((ext_vector_type(2)));
-                const h2t hv = __builtin_convertvector((f2){p0, p1}, h2t);
-                uint32_t w = __builtin_bit_cast(uint32_t, hv);
-                asm volatile("" : "+v"(w), "+v"(lsum));
-                pf[fi][fj] = w;
+            if constexpr (j < 16) {
+                constexpr int t = j >> 3, r = 2 * (j & 7);
+                float p0, p1;
+                if constexpr (KBIAS) {
+                    p0 = __builtin_amdgcn_exp2f(sc[t][r] + nm);
+                    p1 = __builtin_amdgcn_exp2f(sc[t][r + 1] + nm);
+                } else {
+                    p0 = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[t][r], c_log2, nm));
+                    p1 = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[t][r + 1], c_log2, nm));
+                }
+                lsum += p0;
+                lsum += p1;
+                constexpr int fi = 2 * t + (r >> 3), fj = (r & 7) >> 1;
+                // (the empty asm pins each result to its step: without it the IR passes sink the whole softmax
+                // finish to the P.V MFMAs that consume it, i.e. after every MFMA of this phase)
+                if constexpr (F8) {
+                    typedef float f2 __attribute__((ext_vector_type(2)));
+                    typedef _Float16 h2t __attribute__((ext_vector_type(2)));
+                    const h2t hv = __builtin_convertvector((f2){p0, p1}, h2t);
+                    uint32_t w = __builtin_bit_cast(uint32_t, hv);
+                    int w8 = (j & 1) ? (int)ph8[j >> 1] : 0;
+                    w8 = __builtin_amdgcn_cvt_pk_fp8_f32(p0, p1, w8, (j & 1) != 0);
+                    asm volatile("" : "+v"(w), "+v"(w8), "+v"(lsum), "+v"(p0), "+v"(p1));
+                    pf[fi][fj] = w;
+                    ph8[j >> 1] = (uint32_t)w8;
+                    sc[t][r] = p0;  // P itself, for the lo part formed in phase C
+                    sc[t][r + 1] = p1;
+                } else if constexpr (PVS) {
+                    const auto h2 = __builtin_amdgcn_cvt_pkrtz(p0, p1);
+                    uint32_t w = __builtin_bit_cast(uint32_t, h2);
+                    uint32_t wl = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(p0 - (float)h2[0], p1 - (float)h2[1]));
+                    asm volatile("" : "+v"(w), "+v"(wl), "+v"(lsum));
+                    pf[fi][fj] = w;
+                    pfl[fi][fj] = wl;
+                } else {
+                    typedef float f2 __attribute__((ext_vector_type(2)));
+                    typedef _Float16 h2t __attribute__((ext_vector_type(2)));
+                    const h2t hv = __builtin_convertvector((f2){p0, p1}, h2t);
+                    uint32_t w = __builtin_bit_cast(uint32_t, hv);
+                    asm volatile("" : "+v"(w), "+v"(lsum));
+                    pf[fi][fj] = w;
+                }
             }
         };
         auto dma = [&](auto j_c) {
             constexpr int j = decltype(j_c)::value;
-            static_assert(NPK + NPV <= 16, "one DMA piece per QK step");
+            static_assert(NPK + NPV <= NB, "one DMA piece per QK step");
             if constexpr (j < NPK) {
                 if (more2) {
                     k_piece(SLOT, ktk, j);
@@ -896,37 +963,62 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
         qk_phase(std::integral_constant<int, NXT>{}, sn, [&](auto j_c) { fin(j_c); }, [&](auto j_c) { dma(j_c); });
         l_run += lsum;
 
-        // phase C: O^T += V^T(i) P^T(i) || softmax start of tile i+1
+        // phase C: O^T += V^T(i) P^T(i) || softmax start of tile i+1.  Steps j < 16: d-tile dt = j / 4, 16-key group
+        // g = j % 4 (fp16 hi, + lo for PVS); F8 steps 16..23: d-tile (j - 16) / 2, correction i = j % 2 (Vl.Ph, Vh.Pl)
         bias_tile(std::integral_constant<int, NXT>{}, sn);
         mask_tile(sn, i + 1);
         float mr = -INFINITY;
         {
+            constexpr int NC = F8 ? 24 : 16;
             frag vh[3], vl[3];
-            auto v_read = [&](auto j_c, frag& hi, frag& lo) {
+            auto v_read = [&](auto j_c, frag& x, frag& y) {
                 constexpr int j = decltype(j_c)::value;
-                constexpr int dt = j >> 2, g = j & 3;
-                hi = lds_frag<SLOT * RG::VS + dt * 32 * 128>(vaddr[g]);
-                if constexpr (PVS) lo = lds_frag<SLOT * RG::VS + dt * 32 * 128 + RG::V_LO>(vaddr[g]);
+                if constexpr (j < 16) {
+                    constexpr int dt = j >> 2, g = j & 3;
+                    x = lds_frag<SLOT * RG::VS + dt * 32 * 128>(vaddr[g]);
+                    if constexpr (PVS && !F8) y = lds_frag<SLOT * RG::VS + dt * 32 * 128 + RG::V_LO>(vaddr[g]);
+                } else {
+                    constexpr int dt = (j - 16) >> 1, ii = j & 1;
+                    x = lds_frag<SLOT * RG::VS + dt * 32 * 128>(v8a[ii][0]);
+                    y = lds_frag<SLOT * RG::VS + dt * 32 * 128>(v8a[ii][1]);
+                }
             };
+            auto rv = [](int j) constexpr { return F8 ? (j < 16 ? 1 : 2) : (PVS ? 2 : 1); };
             v_read(std::integral_constant<int, 0>{}, vh[0], vl[0]);
             v_read(std::integral_constant<int, 1>{}, vh[1], vl[1]);
-            static_for<0, 16>([&](auto j_c) {
+            static_for<0, NC>([&](auto j_c) {
                 constexpr int j = decltype(j_c)::value;
-                constexpr int dt = j >> 2, g = j & 3;
-                if constexpr (j + 2 < 16) v_read(std::integral_constant<int, j + 2>{}, vh[(j + 2) % 3], vl[(j + 2) % 3]);
-                constexpr int after = RV * ((j + 2 < 16 ? 2 : 15 - j));
+                if constexpr (j + 2 < NC) v_read(std::integral_constant<int, j + 2>{}, vh[(j + 2) % 3], vl[(j + 2) % 3]);
+                constexpr int after = (j + 1 < NC ? rv(j + 1) : 0) + (j + 2 < NC ? rv(j + 2) : 0);
                 asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(after) : "memory");
                 asm volatile("" : "+v"(vh[j % 3]));
-                if constexpr (PVS) asm volatile("" : "+v"(vl[j % 3]));
-                o[dt] = mfma32(vh[j % 3], pf[g], o[dt]);
-                if constexpr (PVS) {
-                    o[dt] = mfma32(vh[j % 3], pfl[g], o[dt]);
-                    o[dt] = mfma32(vl[j % 3], pf[g], o[dt]);
+                if constexpr (rv(j) == 2) asm volatile("" : "+v"(vl[j % 3]));
+                if constexpr (j < 16) {
+                    constexpr int dt = j >> 2, g = j & 3;
+                    o[dt] = mfma32(vh[j % 3], pf[g], o[dt]);
+                    if constexpr (PVS && !F8) {
+                        o[dt] = mfma32(vh[j % 3], pfl[g], o[dt]);
+                        o[dt] = mfma32(vl[j % 3], pf[g], o[dt]);
+                    }
+                    // running max of tile i+1: two scores per step
+                    constexpr int t = j >> 3, r = 2 * (j & 7);
+                    mr = fmaxf(mr, fmaxf(sn[t][r], sn[t][r + 1]));
+                    asm volatile("" : "+v"(mr));
+                    if constexpr (F8) {  // fp8 lo part of P pair j: P - f16(P) (exact in f32)
+                        constexpr int fi = 2 * t + (r >> 3), fj = (r & 7) >> 1;
+                        typedef _Float16 h2t __attribute__((ext_vector_type(2)));
+                        const h2t hv = __builtin_bit_cast(h2t, (uint32_t)pf[fi][fj]);
+                        int w8 = (j & 1) ? (int)pl8[j >> 1] : 0;
+                        w8 = __builtin_amdgcn_cvt_pk_fp8_f32(sc[t][r] - (float)hv[0], sc[t][r + 1] - (float)hv[1], w8,
+                                                             (j & 1) != 0);
+                        asm volatile("" : "+v"(w8));
+                        pl8[j >> 1] = (uint32_t)w8;
+                    }
+                } else {
+                    constexpr int dt = (j - 16) >> 1, ii = j & 1;
+                    const v8i pb = ii == 0 ? cat8(ph8) : cat8(pl8);
+                    o[dt] = mfma_f8(cat8(vh[j % 3], vl[j % 3]), pb, o[dt], ii == 0 ? F8_SCALE_LO : F8_SCALE_1, F8_SCALE_1);
                 }
-                // running max of tile i+1: two scores per step
-                constexpr int t = j >> 3, r = 2 * (j & 7);
-                mr = fmaxf(mr, fmaxf(sn[t][r], sn[t][r + 1]));
-                asm volatile("" : "+v"(mr));
                 __builtin_amdgcn_sched_barrier(0);
             });
         }
@@ -1027,6 +1119,15 @@ void launch_t(const AttnArgs& a, dim3 grid, hipStream_t s) {
         const char* e = std::getenv("ACE_MI_ATTN_V1");
         v2 = (e && e[0] == '1') ? 0 : 1;
     }
+    if constexpr (SPLIT && PVS) {
+        if (a.f8) {
+            if (a.kbias)
+                hipLaunchKernelGGL((attn2_kernel<F16OUT, true, true, true, 1, true>), grid, dim3(256), lds, s, a);
+            else
+                hipLaunchKernelGGL((attn2_kernel<F16OUT, true, true, false, 1, true>), grid, dim3(256), lds, s, a);
+            return;
+        }
+    }
     if (v2 && a.fused_merge == 0) {
         constexpr int OCC = SPLIT ? 1 : 2;
         if (a.kbias)
@@ -1118,6 +1219,7 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s) {
     }
     const dim3 grid(8 * ((a.B * a.Hkv * n_qt * b.ksplit + 7) / 8));  // XCD-aware order, see attn_kernel
     const bool f16 = out_t == ActType::F16;
+    ACEMI_CHECK(!a.f8 || (a.split && a.pv_split && !b.fused_merge), "attention: f8c mode needs split + pv_split");
     if (a.split) {
         ACEMI_CHECK(a.q_plane > 0 && a.k_plane > 0, "attention: split mode needs lo planes");
         if (a.pv_split) {

@@ -782,6 +782,7 @@ int pick_variant(int M, int N, int K, bool quant, int fmt) {
         return !(wide && N % 256 != 0) && !(quant && dense_only) && !(!quant && qr) && sk_ok &&
                !(f == 21 && fmt == WF_Q4_K);
     };
+    if (g_forced_variant >= 0x10000) return g_forced_variant & 0xffff;  // diagnostics (selftest): no support check
     if (g_forced_variant >= 0 && supports(g_forced_variant)) return g_forced_variant;  // tests / micro-benchmarks
     if (!quant) {
         const int ov = gemm_override(N, K);

@@ -349,7 +349,7 @@ __device__ __forceinline__ void qkv_prep_head(const GemmParams& p, int m0, int h
                 float y[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
                 prep::head_row(y, w, d, a.eps, a.rope_cos ? a.rope_cos + (int64_t)n * 64 + d : nullptr,
                                a.rope_cos ? a.rope_sin + (int64_t)n * 64 + d : nullptr,
-                               base + b * bstride + (int64_t)n * 128, plane);
+                               base + b * bstride + (int64_t)n * 128, plane, a.f8 ? (isq ? 1 : 2) : 0);
             }
         } else {
             // V^T: groups of 16 keys of one item; a group cut by the chunk edge is written key by key
@@ -375,10 +375,20 @@ __device__ __forceinline__ void qkv_prep_head(const GemmParams& p, int m0, int h
                     }
                     uint32_t wv[8], wl[8];
                     prep::v_words(v, wv, wl);
+                    if (a.f8 && a.v_plane > 0) {  // natural key order for the fp8 plane (vperm is an involution)
+                        float vn[16];
+                        uint32_t hn = 0;
+#pragma unroll
+                        for (int w = 0; w < 16; ++w) {
+                            vn[w] = v[prep::vperm(w)];
+                            hn |= ((have >> prep::vperm(w)) & 1u) << w;
+                        }
+                        prep::v_store8(vn, vdst, a.v_plane, g0, hn);
+                    }
                     if (have == 0xffffu) {
                         *(uint4*)(vdst + g0) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
                         *(uint4*)(vdst + g0 + 8) = make_uint4(wv[4], wv[5], wv[6], wv[7]);
-                        if (a.v_plane > 0) {
+                        if (a.v_plane > 0 && !a.f8) {
                             *(uint4*)(vdst + a.v_plane + g0) = make_uint4(wl[0], wl[1], wl[2], wl[3]);
                             *(uint4*)(vdst + a.v_plane + g0 + 8) = make_uint4(wl[4], wl[5], wl[6], wl[7]);
                         }
@@ -387,7 +397,7 @@ __device__ __forceinline__ void qkv_prep_head(const GemmParams& p, int m0, int h
                         for (int k = 0; k < 16; ++k) {
                             if (!((have >> k) & 1u)) continue;
                             vdst[g0 + k] = (uint16_t)(wv[k >> 1] >> (16 * (k & 1)));
-                            if (a.v_plane > 0) vdst[a.v_plane + g0 + k] = (uint16_t)(wl[k >> 1] >> (16 * (k & 1)));
+                            if (a.v_plane > 0 && !a.f8) vdst[a.v_plane + g0 + k] = (uint16_t)(wl[k >> 1] >> (16 * (k & 1)));
                         }
                     }
                 }

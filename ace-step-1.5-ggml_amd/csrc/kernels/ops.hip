@@ -404,7 +404,8 @@ __global__ void __launch_bounds__(256) attn_prep_kernel(PrepArgs a) {
             float y[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
             const bool rope = a.rope_cos && n < a.n_tok;
             prep::head_row(y, w, d, a.eps, rope ? a.rope_cos + (int64_t)n * 64 + d : nullptr,
-                           rope ? a.rope_sin + (int64_t)n * 64 + d : nullptr, base + (int64_t)n * 128, plane);
+                           rope ? a.rope_sin + (int64_t)n * 64 + d : nullptr, base + (int64_t)n * 128, plane,
+                           a.f8 ? (isq ? 1 : 2) : 0);
         }
         return;
     }
@@ -429,7 +430,12 @@ __global__ void __launch_bounds__(256) attn_prep_kernel(PrepArgs a) {
         prep::v_words(v, wv, wl);
         *(uint4*)(vdst + g0) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
         *(uint4*)(vdst + g0 + 8) = make_uint4(wv[4], wv[5], wv[6], wv[7]);
-        if (a.v_plane > 0) {
+        if (a.f8 && a.v_plane > 0) {
+            float vn[16];
+#pragma unroll
+            for (int w = 0; w < 16; ++w) vn[w] = v[prep::vperm(w)];
+            prep::v_store8(vn, vdst, a.v_plane, g0, 0xffffu);
+        } else if (a.v_plane > 0) {
             *(uint4*)(vdst + a.v_plane + g0) = make_uint4(wl[0], wl[1], wl[2], wl[3]);
             *(uint4*)(vdst + a.v_plane + g0 + 8) = make_uint4(wl[4], wl[5], wl[6], wl[7]);
         }

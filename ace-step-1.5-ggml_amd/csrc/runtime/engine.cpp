@@ -15,7 +15,8 @@ DitEngine::DitEngine(int device) : device_(device) {
     // DESIGN.md "Parity"); the condition / text encoders keep the f32-faithful default
     const AttnPrecision prec = attn_precision_from_env(AttnPrecision::FP16);
     attn_split_ = prec != AttnPrecision::FP16;
-    attn_pv_split_ = prec == AttnPrecision::F32;
+    attn_pv_split_ = prec == AttnPrecision::F32 || prec == AttnPrecision::F8C;
+    attn_f8_ = prec == AttnPrecision::F8C;
     const char* u = std::getenv("ACE_MI_UNFUSED_PREP");
     fused_prep_ = !(u && u[0] && u[0] != '0');
     const char* q = std::getenv("ACE_MI_QUANT_STAGED");
@@ -422,6 +423,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
             pa.vt = get<uint16_t>(vc_) + (size_t)li * B * c.hkv * D * Lpad;
             pa.k_plane = split ? kc_plane : 0;
             pa.v_plane = attn_pv_split_ ? kc_plane : 0;
+            pa.f8 = attn_f8_ ? 1 : 0;
             if (fused) {  // every layer's cross K/V re-layout in one launch (PrepArgs::layers)
                 pa.layers = n_layers;
                 pa.src_layer = 2 * kd;
@@ -497,6 +499,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
             pa.q_plane = split ? q_plane : 0;
             pa.k_plane = split ? k_plane : 0;
             pa.v_plane = attn_pv_split_ ? k_plane : 0;
+            pa.f8 = attn_f8_ ? 1 : 0;
             qkv_gemm(act, lw.qkv, (int)M, qd + 2 * kd, pa, qkv, "gemm_qkv", s);
         }
         {
@@ -519,6 +522,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
             aa.scale = scale;
             aa.split = split;
             aa.pv_split = attn_pv_split_;
+            aa.f8 = attn_f8_;
             aa.q_plane = q_plane;
             aa.k_plane = k_plane;
             aa.v_plane = k_plane;
@@ -559,6 +563,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
                 pa.eps = c.eps;
                 pa.qh = get<uint16_t>(qh_);
                 pa.q_plane = split ? q_plane : 0;
+                pa.f8 = attn_f8_ ? 1 : 0;
                 qkv_gemm(act, lw.cq, (int)M, qd, pa, qkv, "gemm_cross_q", s);
             }
             {
@@ -580,6 +585,7 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
                 aa.scale = scale;
                 aa.split = split;
                 aa.pv_split = attn_pv_split_;
+            aa.f8 = attn_f8_;
                 aa.q_plane = q_plane;
                 aa.k_plane = kc_plane;
                 aa.v_plane = kc_plane;

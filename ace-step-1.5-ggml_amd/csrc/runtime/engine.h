@@ -72,7 +72,9 @@ class DitEngine {
     // attention operand precision of subsequent forwards (DiT blocks; the encoders keep their own)
     void set_attn_precision(AttnPrecision p) {
         attn_split_ = p != AttnPrecision::FP16;
-        attn_pv_split_ = p == AttnPrecision::F32;
+        attn_pv_split_ = p == AttnPrecision::F32 || p == AttnPrecision::F8C;
+        attn_f8_ = p == AttnPrecision::F8C;
+        cross_key_.valid = false;  // cached cross K/V planes are in the previous mode's encoding
     }
     // enable per-kernel-class event timing for subsequent forwards
     void set_profiling(bool on);
@@ -116,6 +118,7 @@ class DitEngine {
     void rope_table(int n, Buf& cs, Buf& sn, hipStream_t s);
     bool attn_split_ = false;  // hi/lo fp16 Q.K operands (ACE_MI_ATTN_PRECISION)
     bool attn_pv_split_ = false;  // hi/lo fp16 P.V operands too
+    bool attn_f8_ = false;        // f8c: the lo planes hold fp8 operands (AttnArgs::f8)
     bool fused_prep_ = true;      // EPI_QKV_PREP (ACE_MI_UNFUSED_PREP=1: f32 store + attn_prep)
     void qkv_gemm(const uint16_t* act, const WeightView& w, int M, int N, PrepArgs pa, float* scratch,
                   const char* name, hipStream_t s);

@@ -113,6 +113,8 @@ struct AttnSetup {
         pq.qh = dqh.as<uint16_t>();
         const int64_t qpl = (int64_t)B * Hq * nq_pad * D, kpl = (int64_t)B * Hkv * nk_pad * D;
         pq.q_plane = split ? qpl : 0;
+        const bool f8 = split && (flags & 8) && (flags & 16);
+        pq.f8 = f8 ? 1 : 0;
         launch_attn_prep(pq, nullptr);
         PrepArgs pk{};
         pk.src = dkv.as<float>();
@@ -129,6 +131,7 @@ struct AttnSetup {
         pk.vt = dvt.as<uint16_t>();
         pk.k_plane = split ? kpl : 0;
         pk.v_plane = split ? kpl : 0;
+        pk.f8 = f8 ? 1 : 0;
         launch_attn_prep(pk, nullptr);
         launch_key_bias(kmask ? dm.as<int32_t>() : nullptr, B, nk, 1, nk, nk_pad, dkb.as<float>(), nullptr);
         a.q = dqh.as<uint16_t>();
@@ -149,6 +152,7 @@ struct AttnSetup {
         a.split = split;
         a.causal = (flags & 2) != 0;
         a.pv_split = split && (flags & 8) != 0;
+        a.f8 = f8;
         a.q_plane = qpl;
         a.k_plane = kpl;
         a.v_plane = kpl;
@@ -183,7 +187,7 @@ ace_ggml_status ace_mi_kernel_attention(int32_t B, int32_t Hq, int32_t Hkv, int3
 
 // Attention micro-benchmark: pseudo-random N(0,1)-like q / kv (fixed seed), average ms per launch over
 // `iters` launches timed with hipEvents.  flags: bit 0 split (hi/lo) operands, bit 1 causal, bit 3 hi/lo P.V,
-// bit 2 a key-padding mask (every 7th key masked).
+// bit 2 a key-padding mask (every 7th key masked), bit 4 the f8c operand encoding (with bits 0 and 3).
 ace_ggml_status ace_mi_bench_attention(int32_t B, int32_t Hq, int32_t Hkv, int32_t nq, int32_t nk, int32_t window,
                                        int32_t flags, int32_t iters, float* avg_ms) {
     using namespace acemi;
@@ -203,7 +207,7 @@ ace_ggml_status ace_mi_bench_attention(int32_t B, int32_t Hq, int32_t Hkv, int32
         for (auto& v : q) v = 2.0f * rnd();
         for (auto& v : kv) v = rnd();
         for (size_t i = 0; i < km.size(); ++i) km[i] = (i % 7) != 6;
-        AttnSetup st(B, Hq, Hkv, nq, nk, window, 1.0f / std::sqrt(128.0f), flags & 11, q.data(), kv.data(),
+        AttnSetup st(B, Hq, Hkv, nq, nk, window, 1.0f / std::sqrt(128.0f), flags & 27, q.data(), kv.data(),
                      (flags & 4) ? km.data() : nullptr);
         hipEvent_t e0, e1;
         ACEMI_HIP(hipEventCreate(&e0));

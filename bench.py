@@ -54,7 +54,9 @@ METRIC = "DiT denoising steps/sec (240s@5Hz latent, bs=1..8) + single-step ms; 1
 HEADLINE_ATTN = os.environ.get("ACE_MI_BENCH_ATTN", "fp16")
 ATTN_DESC = {"fp16": "fp16-operand f32-accumulate attention",
              "split": "split attention (hi/lo fp16 Q.K, fp16 P.V, f32 accumulate)",
-             "f32": "f32-faithful attention (hi/lo fp16 Q.K and P.V, f32 accumulate)"}
+             "f32": "f32-faithful attention (hi/lo fp16 Q.K and P.V, f32 accumulate)",
+             "f8c": "f32-class attention (hi/lo Q.K and P.V: hi x hi fp16, correction products block-scaled e4m3, "
+                    "f32 accumulate)"}
 BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16/fp16 MFMA (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
 
@@ -308,7 +310,7 @@ def main():
                                    "Euler loop on torch tensors, one hook call per step (model.generate_audio)")
         # ---- every attention precision: steps/s of the headline loop + per-kernel attention time per step
         modes = {}
-        for mode in ("fp16", "split", "f32"):
+        for mode in ("fp16", "split", "f32", "f8c"):
             br.set_attn_precision(mode)
             el_m = elapsed if mode == HEADLINE_ATTN else timed(run)
             entry = line(B * args.steps, el_m, f"the headline loop with {ATTN_DESC[mode]}")
@@ -319,6 +321,7 @@ def main():
         extras["attn_split_line"] = modes["split"]
         extras["attn_f32_line"] = modes["f32"]
         extras["attn_fp16_line"] = modes["fp16"]
+        extras["attn_f8c_line"] = modes["f8c"]
         # ---- 10 s forward rate (configs[0]'s shape) with the headline weights
         in10 = small_inputs(250)
         extras["line_10s"] = {"weights": args.qtype or "bf16", **line(args.steps, timed(lambda f, k: run(f, k, in10)),

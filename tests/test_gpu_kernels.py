@@ -95,7 +95,8 @@ def _attn_ref(q, kv, hq, hkv, window, kmask, scale, rnd=round_f16):
     return out.reshape(B, nq, hq * D)
 
 
-MODES = {"split": dict(split=True), "pvsplit": dict(split=True, pv_split=True), "fast": dict(split=False)}
+MODES = {"split": dict(split=True), "pvsplit": dict(split=True, pv_split=True), "fast": dict(split=False),
+         "f8c": dict(split=True, pv_split=True, f8=True)}
 
 
 def _check_attn(got, q, kv, hq, hkv, window, kmask, scale, mode):
@@ -111,11 +112,12 @@ def _check_attn(got, q, kv, hq, hkv, window, kmask, scale, mode):
     ref = _attn_ref(q, kv, hq, hkv, window, kmask, scale, rnd=f32)
     err = np.abs(got - ref)
     vmax = float(np.abs(kv[:, :, hkv * 128:]).max())
-    tol = 2.0 ** -8 * np.abs(ref) + (1e-5 if mode == "pvsplit" else 2.0 ** -10 * vmax)
+    # f8c: the correction products at e4m3 precision leave ~2^-15 relative per product (2^-13 of max|v| is slack)
+    tol = 2.0 ** -8 * np.abs(ref) + {"pvsplit": 1e-5, "f8c": 2.0 ** -13 * vmax}.get(mode, 2.0 ** -10 * vmax)
     assert np.all(err <= tol), float((err - tol).max())
     mism = np.mean(got != bf16_bits_to_f32(f32_to_bf16_bits(ref.astype(np.float32))))
-    # pvsplit is much closer to the f32 reference than a single-fp16 evaluation would be
-    assert mism < (0.01 if mode == "pvsplit" else 0.25), mism
+    # pvsplit / f8c are much closer to the f32 reference than a single-fp16 evaluation would be
+    assert mism < {"pvsplit": 0.01, "f8c": 0.03}.get(mode, 0.25), mism
     return ref
 
 

@@ -24,11 +24,13 @@ def main():
     for name, B, hq, hkv, nq, nk, win, masked in CASES:
         if only and name != only:
             continue
-        modes = {"split": (True, False), "pvsplit": (True, True), "fast": (False, False)}
-        for mode, (split, pvs) in modes.items():
+        modes = {"split": (True, False, False), "pvsplit": (True, True, False), "fast": (False, False, False),
+                 "f8c": (True, True, True)}
+        for mode, (split, pvs, f8) in modes.items():
             if only and mode != only_mode:
                 continue
-            ms = capi.bench_attention(B, hq, hkv, nq, nk, win, split=split, masked=masked, iters=10, pv_split=pvs)
+            ms = capi.bench_attention(B, hq, hkv, nq, nk, win, split=split, masked=masked, iters=10, pv_split=pvs,
+                                      f8=f8)
             nk_eff = min(nk, 2 * win + 1) if win else nk
             flop = 4.0 * B * nq * nk_eff * 128 * hq
             print(json.dumps({"case": name, "mode": mode, "ms": round(ms, 4),

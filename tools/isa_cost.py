@@ -12,6 +12,8 @@ TRANS = ("v_exp_", "v_log_", "v_rcp_", "v_rsq_", "v_sqrt_", "v_sin_", "v_cos_")
 
 def cost(op):
     if op.startswith("v_mfma"):
+        if "scale" in op and "f8f6f4" in op:  # block-scaled K=64 / K=128 forms: twice the bf16 form's cycles
+            return ("M", 32 if "16x16" in op else 64)
         return ("M", 16 if "16x16" in op else 32)
     if op.startswith(TRANS):
         return ("E", 8)
