@@ -265,6 +265,9 @@ ace_ggml_status run_sampler(ace_ggml_context* ctx, int32_t batch, float* d_xt, c
         io.enc_mask = d_enc_mask;
         io.out = ctx->d_v;
         io.max_layers = max_layers_env();
+        // every step's timestep is known now: the timestep MLPs of all steps in one pass (r = t in the sampler)
+        const auto ts = ctx->dit->precompute_timesteps(ctx->d_sched, ctx->d_sched, n_steps * batch, s);
+        const int H = c.hidden;
         bool switched = false;
         for (int i = 0; i < n_steps; ++i) {
             bool fresh = (i == 0);
@@ -281,6 +284,9 @@ ace_ggml_status run_sampler(ace_ggml_context* ctx, int32_t batch, float* d_xt, c
             io.reuse_stage = i > 0;  // quantized weights: dequantized once per call (engine.h)
             io.t = ctx->d_sched + (size_t)i * batch;
             io.r = io.t;
+            io.ts_proj = ts.proj + (size_t)i * batch * 6 * H;
+            io.ts_temb_t = ts.temb_t + (size_t)i * batch * H;
+            io.ts_temb_r = ts.temb_r + (size_t)i * batch * H;
             ctx->dit->forward(io, s);
             if (i + 1 == n_steps) {  // final step: x0 = xt - v * t
                 acemi::launch_euler(d_xt, ctx->d_v, (int64_t)n, schedule[i], s);

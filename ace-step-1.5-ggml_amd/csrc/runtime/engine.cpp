@@ -36,7 +36,7 @@ DitEngine::DitEngine(int device) : device_(device) {
 DitEngine::~DitEngine() {
     for (Buf* b : {&a0_, &x_, &act_, &attn_, &act2_, &qkv_, &qh_, &kh_, &vt_, &kbias_, &enc_act_, &encp_, &ckv_, &kc_,
                    &vc_, &kbias_c_, &attn_part_, &freq_, &freq_act_, &th_, &th_act_, &temb_t_, &temb_r_, &temb_act_, &proj_,
-                   &mods_, &outmod_, &cos_, &sin_, &ein_, &knorm_tab_}) {
+                   &mods_, &outmod_, &cos_, &sin_, &ein_, &knorm_tab_, &ts_proj_, &ts_temb_t_, &ts_temb_r_}) {
         if (b->p) (void)hipFree(b->p);
     }
     if (pf_stream_) {
@@ -339,24 +339,20 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
         toc("gemm_proj_in", s);
     }
 
-    // ---- timestep embeddings (:1416-1424, timestep_forward :1286-1308)
+    // ---- timestep embeddings (:1416-1424, timestep_forward :1286-1308), or the sampler's precomputed rows
     {
-        const float log_max = std::log(10000.0f);
-        float* freq = get<float>(freq_);
-        float* th = get<float>(th_);
-        float* proj = get<float>(proj_);
         tic(s);
-        for (int e = 0; e < 2; ++e) {
-            float* temb = get<float>(e == 0 ? temb_t_ : temb_r_);
-            launch_timestep_freq(io.t, e == 0 ? nullptr : io.r, B, 256, 1000.0f, log_max, freq, s);
-            const ActType ta = m.te[e].act;
-            // each linear rounds its f32 input to the weight type itself (launch_gemv_f32 = to_act + gemv)
-            launch_gemv_f32(ta, freq, false, B, m.te[e].w1, H, 256, m.te[e].b1, true, false, th, s);
-            launch_gemv_f32(ta, th, false, B, m.te[e].w2, H, H, m.te[e].b2, false, false, temb, s);
-            launch_gemv_f32(ta, temb, true, B, m.te[e].wp, 6 * H, H, m.te[e].bp, false, e == 1, proj, s);
+        const float* proj = io.ts_proj;
+        const float* temb_t = io.ts_temb_t;
+        const float* temb_r = io.ts_temb_r;
+        if (!proj) {
+            timestep_embed(io.t, io.r, B, get<float>(proj_), get<float>(temb_t_), get<float>(temb_r_), s);
+            proj = get<float>(proj_);
+            temb_t = get<float>(temb_t_);
+            temb_r = get<float>(temb_r_);
         }
         launch_layer_mods(m.tables, proj, n_layers, B, H, get<float>(mods_), s);
-        launch_out_mods(m.out_table, get<float>(temb_t_), get<float>(temb_r_), B, H, get<float>(outmod_), s);
+        launch_out_mods(m.out_table, temb_t, temb_r, B, H, get<float>(outmod_), s);
         toc("timestep", s);
     }
 
@@ -661,6 +657,42 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
         ACEMI_HIP(hipEventRecord(pf_done_, pf_stream_));
         ACEMI_HIP(hipStreamWaitEvent(s, pf_done_, 0));
     }
+}
+
+void DitEngine::timestep_embed(const float* t, const float* r, int rows, float* proj, float* temb_t, float* temb_r,
+                               hipStream_t s) {
+    const DitModel& m = model_;
+    const int H = m.cfg.hidden;
+    const float log_max = std::log(10000.0f);
+    ensure(freq_, (size_t)8 * 256 * 4);
+    ensure(th_, (size_t)8 * H * 4);
+    float* freq = get<float>(freq_);
+    float* th = get<float>(th_);
+    // rows are independent: chunks of up to 8 (the GEMV kernel's row limit), the same arithmetic per row
+    for (int r0 = 0; r0 < rows; r0 += 8) {
+        const int n = std::min(8, rows - r0);
+        float* pr = proj + (size_t)r0 * 6 * H;
+        for (int e = 0; e < 2; ++e) {
+            float* temb = (e == 0 ? temb_t : temb_r) + (size_t)r0 * H;
+            launch_timestep_freq(t + r0, e == 0 ? nullptr : r + r0, n, 256, 1000.0f, log_max, freq, s);
+            const ActType ta = m.te[e].act;
+            // each linear rounds its f32 input to the weight type itself (launch_gemv_f32 = to_act + gemv)
+            launch_gemv_f32(ta, freq, false, n, m.te[e].w1, H, 256, m.te[e].b1, true, false, th, s);
+            launch_gemv_f32(ta, th, false, n, m.te[e].w2, H, H, m.te[e].b2, false, false, temb, s);
+            launch_gemv_f32(ta, temb, true, n, m.te[e].wp, 6 * H, H, m.te[e].bp, false, e == 1, pr, s);
+        }
+    }
+}
+
+DitEngine::TimestepRows DitEngine::precompute_timesteps(const float* t, const float* r, int rows, hipStream_t s) {
+    const int H = model_.cfg.hidden;
+    ensure(ts_proj_, (size_t)rows * 6 * H * 4);
+    ensure(ts_temb_t_, (size_t)rows * H * 4);
+    ensure(ts_temb_r_, (size_t)rows * H * 4);
+    tic(s);
+    timestep_embed(t, r, rows, get<float>(ts_proj_), get<float>(ts_temb_t_), get<float>(ts_temb_r_), s);
+    toc("timestep_precompute", s);
+    return TimestepRows{get<float>(ts_proj_), get<float>(ts_temb_t_), get<float>(ts_temb_r_)};
 }
 
 // A projection feeding attention: with EPI_QKV_PREP the GEMM epilogue writes the attention operands of

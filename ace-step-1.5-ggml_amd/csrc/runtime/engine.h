@@ -37,6 +37,12 @@ struct ForwardIO {
     // Reuse the bf16 images of the quantized block weights written by the previous forward of this engine
     // (staged dequant at sampling-call scope): set by the sampler entry for steps 1.. of one call.
     bool reuse_stage = false;
+    // Timestep embeddings precomputed for this forward's B items (DitEngine::precompute_timesteps, the sampler
+    // entry: every step's t is known when the sampling call starts): proj [B][6H] = the summed AdaLN projections
+    // of t and t - r, temb_t / temb_r [B][H].  Null: computed from t / r inside the forward.
+    const float* ts_proj = nullptr;
+    const float* ts_temb_t = nullptr;
+    const float* ts_temb_r = nullptr;
 };
 
 // One condition-encoder pass for B items of n tokens each (forward_lyric_encoder /
@@ -68,6 +74,15 @@ class DitEngine {
     DitModel& model() { return model_; }
     int device() const { return device_; }
     void forward(const ForwardIO& io, hipStream_t s);
+    // The timestep embeddings of `rows` (t, r) pairs in one pass (the weights read once per 8 rows instead of once
+    // per forward): into engine buffers, returned as [rows][6H] proj and [rows][H] temb_t / temb_r pointers
+    // (valid until the next call), bit-identical to what forward() computes for each row.
+    struct TimestepRows {
+        const float* proj;
+        const float* temb_t;
+        const float* temb_r;
+    };
+    TimestepRows precompute_timesteps(const float* t, const float* r, int rows, hipStream_t s);
     void encode(const EncodeIO& io, hipStream_t s);
     // attention operand precision of subsequent forwards (DiT blocks; the encoders keep their own)
     void set_attn_precision(AttnPrecision p) {
@@ -109,6 +124,11 @@ class DitEngine {
         const float* enc = nullptr;
     } cross_key_;
     Buf freq_, freq_act_, th_, th_act_, temb_t_, temb_r_, temb_act_, proj_, mods_, outmod_, cos_, sin_;
+    Buf ts_proj_, ts_temb_t_, ts_temb_r_;  // precompute_timesteps outputs
+    // timestep MLPs for rows items (t, r pointers per row): proj [rows][6H] (t and t - r summed), temb_t / temb_r
+    // [rows][H]; freq_ / th_ serve as scratch for up to 8 rows at a time
+    void timestep_embed(const float* t, const float* r, int rows, float* proj, float* temb_t, float* temb_r,
+                        hipStream_t s);
     int rope_np_ = -1;
     Buf knorm_tab_;  // [layers] device pointers to the cross k-norm weights
     size_t knorm_tab_n_ = 0;
