@@ -189,6 +189,12 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
 _SELFTEST = None
 
 
+def selftest_library_path() -> str:
+    """Path of the TEST library (a superset of the product ABI that also reads the test-only environment hooks,
+    runtime/test_hooks.cpp)."""
+    return os.environ.get("ACE_MI_SELFTEST_LIB") or os.path.join(os.path.dirname(LIB_PATH), "libacestep_mi355x_selftest.so")
+
+
 def load_selftest_library() -> ctypes.CDLL:
     """The TEST library (kernel self-tests / micro-benchmarks, include/acestep_mi355x_selftest.h), built beside the
     product library by the same make; the product library is loaded first (one HIP runtime per process)."""
@@ -196,7 +202,7 @@ def load_selftest_library() -> ctypes.CDLL:
     if _SELFTEST is not None:
         return _SELFTEST
     load_library()
-    p = os.environ.get("ACE_MI_SELFTEST_LIB") or os.path.join(os.path.dirname(LIB_PATH), "libacestep_mi355x_selftest.so")
+    p = selftest_library_path()
     if not os.path.exists(p):
         raise RuntimeError(f"libacestep_mi355x_selftest.so not found at {p}: make -C ace-step-1.5-ggml_amd/csrc")
     lib = ctypes.CDLL(p)

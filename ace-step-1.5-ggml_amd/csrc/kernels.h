@@ -199,6 +199,10 @@ void launch_out_mods(const float* out_table, const float* temb_t, const float* t
 // TEST ONLY (fault injection for the parity negative control): x[r][c] += amp for r in [row0, row0 + 16),
 // c in [col0, col0 + 128)
 void launch_fault_tile(float* x, int ld, int rows, int row0, int col0, float amp, hipStream_t s);
+// Test-only hooks (runtime/test_hooks.cpp): read from the environment in the self-test library only; the product
+// library's versions return "off"
+bool test_fault_from_env(int& layer, int& row, int& col, float& amp);
+int gemm_override_from_env(int N, int K);
 // xt -= v * dt
 void launch_euler(float* xt, const float* v, int64_t n, float dt, hipStream_t s);
 // Read-only sweep of up to 6 device ranges (weights of the next layer) on a side stream, so they sit in the

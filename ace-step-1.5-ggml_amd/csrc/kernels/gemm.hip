@@ -748,26 +748,10 @@ int pick_variant_q(int M, int N, int K, int fmt) {
     return 7;
 }
 
-// Per-shape overrides for in-loop A/B runs (ACE_MI_GEMM_OVERRIDE="N:K:variant[,N:K:variant...]", dense weights,
-// any M; read once): the isolated-GEMM sweeps mispredicted the sampling loop at some shapes (cold weights, fresh
-// activations), so tile picks are confirmed with whole bench lines.
-static int gemm_override(int N, int K) {
-    static const std::vector<std::array<int, 3>> table = [] {
-        std::vector<std::array<int, 3>> t;
-        const char* e = std::getenv("ACE_MI_GEMM_OVERRIDE");
-        while (e && *e) {
-            int n = 0, k = 0, v = 0, used = 0;
-            if (std::sscanf(e, "%d:%d:%d%n", &n, &k, &v, &used) != 3) break;
-            t.push_back({n, k, v});
-            e += used;
-            if (*e == ',') ++e;
-        }
-        return t;
-    }();
-    for (const auto& x : table)
-        if (x[0] == N && x[1] == K) return x[2];
-    return -1;
-}
+// Per-shape overrides for in-loop A/B runs (ACE_MI_GEMM_OVERRIDE, read by the self-test library only:
+// runtime/test_hooks.cpp): the isolated-GEMM sweeps mispredicted the sampling loop at some shapes (cold weights,
+// fresh activations), so tile picks are confirmed with whole bench lines.
+static int gemm_override(int N, int K) { return gemm_override_from_env(N, K); }
 
 int pick_variant(int M, int N, int K, bool quant, int fmt) {
     auto supports = [&](int v) {  // the tile / split-K factor handles this shape (and weight format)

@@ -25,12 +25,8 @@ DitEngine::DitEngine(int device) : device_(device) {
     stage_per_call_ = !(h && std::strcmp(h, "layer") == 0);
     stage_model_ = !(h && (std::strcmp(h, "call") == 0 || std::strcmp(h, "layer") == 0));  // default: model
     if (const char* pf = std::getenv("ACE_MI_WEIGHT_PREFETCH")) prefetch_blocks_ = std::max(0, std::atoi(pf));
-    // TEST ONLY: ACE_MI_TEST_FAULT="layer,row,col,amp" adds amp to one 16 x 128 tile of the residual right after
-    // that layer's o-projection GEMM (the parity negative control of tests/test_gpu_parity_strict.py)
-    if (const char* f = std::getenv("ACE_MI_TEST_FAULT")) {
-        if (f[0] && std::sscanf(f, "%d,%d,%d,%f", &fault_.layer, &fault_.row, &fault_.col, &fault_.amp) != 4)
-            throw std::runtime_error("ACE_MI_TEST_FAULT must be layer,row,col,amp");
-    }
+    // TEST ONLY (self-test library builds): ACE_MI_TEST_FAULT, runtime/test_hooks.cpp
+    if (!test_fault_from_env(fault_.layer, fault_.row, fault_.col, fault_.amp)) fault_.layer = -1;
 }
 
 DitEngine::~DitEngine() {

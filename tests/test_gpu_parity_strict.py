@@ -12,7 +12,7 @@
   it has not accumulated yet, so the north-star bound is asserted literally there wherever the oracle's own
   floor leaves room for it (rel-L2 <= max(1e-3, floor)), for a sliding and a full-attention first layer, with
   and without peaked logits, in the fp16 (default) and f32 attention modes.
-* Negative control.  ACE_MI_TEST_FAULT (test-only engine hook, restated in the oracle as
+* Negative control.  ACE_MI_TEST_FAULT (test-only engine hook of the self-test library, restated in the oracle as
   dit_oracle.FAULT) adds 0.015 to one 16 x 128 tile of the residual after layer 1's o-projection -- one row
   group of one GEMM output tile, a ~4 % error on 16 of 3000 tokens.  The rel-L2 bound absorbs it (the test
   asserts that it does); the element-wise bound max|d| / rms <= 2.5 x its floor must catch it.
@@ -61,7 +61,7 @@ def _oracle(d, layers, t=0.9):
 
 
 def _gpu(d, layers, monkeypatch, precision=None, fault=None, t=0.9):
-    from acestep_mi355x.capi import GGMLCAPIBridge
+    from acestep_mi355x.capi import GGMLCAPIBridge, selftest_library_path
     monkeypatch.setenv("ACE_GGML_DIT_MAX_LAYERS", str(layers))
     if precision:
         monkeypatch.setenv("ACE_MI_ATTN_PRECISION", precision)
@@ -72,7 +72,8 @@ def _gpu(d, layers, monkeypatch, precision=None, fault=None, t=0.9):
     else:
         monkeypatch.delenv("ACE_MI_TEST_FAULT", raising=False)
     h, c, e = _inputs()
-    br = GGMLCAPIBridge()
+    # the fault hook is read by the self-test library only (runtime/test_hooks.cpp)
+    br = GGMLCAPIBridge(lib_path=selftest_library_path()) if fault else GGMLCAPIBridge()
     try:
         br.load_dit(d)
         return br.dit_forward_tfirst(h, c, e, None, None, t, t)
