@@ -123,7 +123,9 @@ def sde_noise(n_draws: int, items: Sequence[int], T: int, C: int, seed: Optional
     (bsz, T, C) normal per step) that does not depend on the world size or on which rank owns it, and a rank
     draws and moves nothing but its own slice.  Drawn on the CPU (the same stream on every backend) and moved
     to `device`.  seed None -> fresh nondeterministic seeds (every rank must then be given an explicit seed to
-    agree)."""
+    agree).  Intentional deviation: the reference draws one (bsz, T, C) normal per step from MLX's generator
+    (generate.py:187), which cannot be reproduced here; this per-item mapping (seed * 1000003 + b) is pinned by
+    tests/golden/sde_noise_seed7.json."""
     out = torch.empty((n_draws, len(items), T, C), dtype=torch.float32)
     for k, b in enumerate(items):
         g = torch.Generator()

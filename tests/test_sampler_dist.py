@@ -175,3 +175,18 @@ def test_sde_noise_is_independent_per_item():
     assert not torch.allclose(a[:, 0], a[:, 1])
     torch.testing.assert_close(sde_noise(3, [1, 3], 5, 2, 7, "cpu"), a[:, [1, 3]])
     assert not torch.allclose(sde_noise(3, [0, 1], 5, 2, None, "cpu"), sde_noise(3, [0, 1], 5, 2, None, "cpu"))
+
+
+def test_sde_noise_seed_mapping_is_pinned():
+    """The seed -> noise mapping (item b: torch CPU generator seeded with seed * 1000003 + b) is an intentional
+    deviation from the reference's single (bsz, T, C) MLX draw per step (generate.py:187, not reproducible without
+    MLX); the committed fixture (tests/golden/make_sde_noise_fixture.py) catches any change to the stream."""
+    import json
+    import os
+    import torch
+    from acestep_mi355x.sampler import sde_noise
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "sde_noise_seed7.json"),
+              encoding="utf-8") as f:
+        g = json.load(f)
+    x = sde_noise(g["n_draws"], g["items"], g["T"], g["C"], g["seed"], "cpu")
+    torch.testing.assert_close(x.reshape(-1), torch.tensor(g["values"], dtype=torch.float32), rtol=0, atol=0)
