@@ -687,6 +687,9 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
     // p >= 4 the lo plane (PVS); the key bias: wave 0, 4 bytes per lane.
     constexpr int NPK = SPLIT ? 8 : 4;
     constexpr int NPV = PVS ? 8 : 4;
+    // VL: V(i+1) is requested in phase C of iteration i and waited for before phase C of iteration i+1 (a second
+    // barrier per tile), so its pieces can sit behind the phase's long MFMAs; the fp16 mode keeps one barrier
+    constexpr bool VL = SPLIT;
     const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc((void*)kbase, 0, 0x7fffffff, 0x00020000);
     const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc((void*)vbase, 0, 0x7fffffff, 0x00020000);
     const int krow = 4 * wid + (lane >> 4);
@@ -744,54 +747,67 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
     constexpr int RK = SPLIT ? 2 : 1;   // LDS reads per QK step
     constexpr int RV = PVS ? 2 : 1;     // LDS reads per PV step
 
-    // ---- phase B building blocks: K fragments of QK step j from K slot SLOT.  Steps j < 16: k-slice ks = j / 2 of
-    // half t = j % 2 (fp16 hi, + lo for SPLIT); F8 steps j = 16..23: correction chunk c = (j - 16) / 2 of half t
-    // (two 16-byte reads of the fp8 row)
+    // ---- phase B: QK of the next tile in NB steps.  Position p runs the hi step h (k-slice ks = h / 2 of half
+    // t = h % 2: fp16 hi, + lo for SPLIT) or, for F8, every third position (p % 3 == 2) the correction step
+    // k = p / 3 (chunk c = k / 2 of half t = k % 2: two 16-byte reads of the fp8 row, one K = 64 fp8 MFMA)
     constexpr int NB = F8 ? 24 : 16;
-    auto k_read = [&](auto slot_c, auto j_c, frag& x, frag& y) {
-        constexpr int SLOT = decltype(slot_c)::value, j = decltype(j_c)::value;
-        constexpr int t = j & 1;
-        if constexpr (j < 16) {
-            constexpr int ks = j >> 1;
+    struct BStep {
+        bool corr;
+        int idx;  // h or k
+    };
+    auto bstep = [](int p) constexpr -> BStep {
+        if (!F8) return BStep{false, p};
+        return p % 3 == 2 ? BStep{true, p / 3} : BStep{false, p - p / 3};
+    };
+    auto k_read = [&](auto slot_c, auto p_c, frag& x, frag& y) {
+        constexpr int SLOT = decltype(slot_c)::value;
+        constexpr BStep st = bstep(decltype(p_c)::value);
+        constexpr int t = st.idx & 1;
+        if constexpr (!st.corr) {
+            constexpr int ks = st.idx >> 1;
             x = lds_frag<SLOT * RG::KS + t * 32 * 256>(kaddr[ks]);
             if constexpr (SPLIT && !F8) y = lds_frag<SLOT * RG::KS + t * 32 * 256 + RG::K_LO - RG::K_HI>(kaddr[ks]);
         } else {
-            constexpr int c = (j - 16) >> 1;
+            constexpr int c = st.idx >> 1;
             x = lds_frag<SLOT * RG::KS + t * 32 * 256>(k8a[c][0]);
             y = lds_frag<SLOT * RG::KS + t * 32 * 256>(k8a[c][1]);
         }
     };
-    // LDS reads of QK step j, and of the reads issued after step j's own (steps j+1, j+2)
-    auto rk = [](int j) constexpr { return F8 ? (j < 16 ? 1 : 2) : (SPLIT ? 2 : 1); };
-    // S(tile in K slot SLOT) into sn, interleaved with fin(j) (the softmax-finish slice of step j) and dma(j)
+    // LDS reads of QK position p
+    auto rk = [](int p) constexpr { return F8 ? (p % 3 == 2 ? 2 : 1) : (SPLIT ? 2 : 1); };
+    // S(tile in K slot SLOT) into sn, interleaved with fin(p) (a softmax-finish slice) and dma(p)
     auto qk_phase = [&](auto slot_c, f32x16 (&sn)[2], auto&& fin, auto&& dma) {
         frag kh[3], kl[3];
         k_read(slot_c, std::integral_constant<int, 0>{}, kh[0], kl[0]);
         k_read(slot_c, std::integral_constant<int, 1>{}, kh[1], kl[1]);
-        static_for<0, NB>([&](auto j_c) {
-            constexpr int j = decltype(j_c)::value;
-            constexpr int t = j & 1, ks = j >> 1;
-            if constexpr (j + 2 < NB) k_read(slot_c, std::integral_constant<int, j + 2>{}, kh[(j + 2) % 3], kl[(j + 2) % 3]);
-            constexpr int after = (j + 1 < NB ? rk(j + 1) : 0) + (j + 2 < NB ? rk(j + 2) : 0);
+        static_for<0, NB>([&](auto p_c) {
+            constexpr int p = decltype(p_c)::value;
+            constexpr BStep st = bstep(p);
+            constexpr int t = st.idx & 1;
+            if constexpr (p + 2 < NB) k_read(slot_c, std::integral_constant<int, p + 2>{}, kh[(p + 2) % 3], kl[(p + 2) % 3]);
+            constexpr int after = (p + 1 < NB ? rk(p + 1) : 0) + (p + 2 < NB ? rk(p + 2) : 0);
             asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(after) : "memory");
-            asm volatile("" : "+v"(kh[j % 3]));
-            if constexpr (rk(j) == 2) asm volatile("" : "+v"(kl[j % 3]));
-            if constexpr (j >= 16) {
+            asm volatile("" : "+v"(kh[p % 3]));
+            if constexpr (rk(p) == 2) asm volatile("" : "+v"(kl[p % 3]));
+            if constexpr (st.corr) {
                 // Kl.Qh (c = 0, 1: the 2^-11 on A) + Kh.Ql (c = 2, 3: on B), e4m3 x e4m3, K = 64 per MFMA
-                constexpr int c = (j - 16) >> 1;
-                sn[t] = mfma_f8(cat8(kh[j % 3], kl[j % 3]), q8[c], sn[t], c < 2 ? F8_SCALE_LO : F8_SCALE_1,
+                constexpr int c = st.idx >> 1;
+                sn[t] = mfma_f8(cat8(kh[p % 3], kl[p % 3]), q8[c], sn[t], c < 2 ? F8_SCALE_LO : F8_SCALE_1,
                                 c < 2 ? F8_SCALE_1 : F8_SCALE_LO);
-            } else if constexpr (ks == 0) {
-                sn[t] = mfma32(kh[j % 3], qf[0], f32x16{});
             } else {
-                sn[t] = mfma32(kh[j % 3], qf[ks], sn[t]);
+                constexpr int ks = st.idx >> 1;
+                if constexpr (ks == 0) {
+                    sn[t] = mfma32(kh[p % 3], qf[0], f32x16{});
+                } else {
+                    sn[t] = mfma32(kh[p % 3], qf[ks], sn[t]);
+                }
+                if constexpr (SPLIT && !F8) {
+                    sn[t] = mfma32(kh[p % 3], qfl[ks], sn[t]);
+                    sn[t] = mfma32(kl[p % 3], qf[ks], sn[t]);
+                }
             }
-            if constexpr (SPLIT && !F8 && j < 16) {
-                sn[t] = mfma32(kh[j % 3], qfl[ks], sn[t]);
-                sn[t] = mfma32(kl[j % 3], qf[ks], sn[t]);
-            }
-            dma(j_c);
-            fin(j_c);
+            dma(p_c);
+            fin(p_c);
             __builtin_amdgcn_sched_barrier(0);
         });
     };
@@ -901,10 +917,12 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
         float lsum = 0.f;
         frag pf[4], pfl[4];
         uint32_t ph8[8], pl8[8];  // F8: fp8 P (hi) and P - f16(P) (lo), byte c = 16 t + r of the lane's 32 keys
-        // softmax finish of tile i, pair j (elements 2j, 2j + 1 of the flattened [t][r] scores)
-        auto fin = [&](auto j_c) {
-            constexpr int j = decltype(j_c)::value;
-            if constexpr (j < 16) {
+        // softmax finish of tile i at QK position p: pair j (elements 2j, 2j + 1 of the flattened [t][r] scores) =
+        // the position's hi step
+        auto fin = [&](auto p_c) {
+            constexpr BStep st = bstep(decltype(p_c)::value);
+            constexpr int j = st.idx;
+            if constexpr (!st.corr) {
                 constexpr int t = j >> 3, r = 2 * (j & 7);
                 float p0, p1;
                 if constexpr (KBIAS) {
@@ -948,57 +966,96 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
                 }
             }
         };
-        auto dma = [&](auto j_c) {
-            constexpr int j = decltype(j_c)::value;
-            static_assert(NPK + NPV <= NB, "one DMA piece per QK step");
-            if constexpr (j < NPK) {
+        // next tiles' LDS-DMA: K(i+2) in phase B (F8: behind the 64-cycle correction MFMAs); V(i+1) in phase B too
+        // for the fp16 mode, in phase C for the hi/lo modes (VL: waited for before the next iteration's phase C)
+        auto dma = [&](auto p_c) {
+            constexpr int p = decltype(p_c)::value;
+            constexpr BStep st = bstep(p);
+            constexpr int kp = F8 ? (st.corr ? st.idx : -1) : p;  // K piece of this position
+            static_assert(VL || NPK + NPV <= NB, "one DMA piece per QK step");
+            if constexpr (kp >= 0 && kp < NPK) {
                 if (more2) {
-                    k_piece(SLOT, ktk, j);
-                    if constexpr (j == 0) bias_piece(SLOT, ktk);
+                    k_piece(SLOT, ktk, kp);
+                    if constexpr (kp == 0) bias_piece(SLOT, ktk);
                 }
-            } else if constexpr (j < NPK + NPV) {
-                if (more) v_piece(NXT, ktv, j - NPK);
+            } else if constexpr (!VL && p >= NPK && p < NPK + NPV) {
+                if (more) v_piece(NXT, ktv, p - NPK);
             }
         };
         qk_phase(std::integral_constant<int, NXT>{}, sn, [&](auto j_c) { fin(j_c); }, [&](auto j_c) { dma(j_c); });
         l_run += lsum;
 
-        // phase C: O^T += V^T(i) P^T(i) || softmax start of tile i+1.  Steps j < 16: d-tile dt = j / 4, 16-key group
-        // g = j % 4 (fp16 hi, + lo for PVS); F8 steps 16..23: d-tile (j - 16) / 2, correction i = j % 2 (Vl.Ph, Vh.Pl)
+        // phase C: O^T += V^T(i) P^T(i) || softmax start of tile i+1, NC steps.  Position q runs the hi step hs (d-tile
+        // hs / 4, 16-key group hs % 4: fp16 hi, + lo for PVS) or, for F8, a correction step (one K = 64 fp8 MFMA of
+        // d-tile dt: Vl.Ph at q = 2, 5, 8, 11 (dt 0..3), Vh.Pl at q = 20..23, after every hi step has formed P's lo
+        // part)
+        if constexpr (VL) {  // V(i), requested in the previous iteration's phase C, landed for every wave
+            if (more2) {
+                if (KBIAS && wid == 0)
+                    wait_vmcnt<NPK + 1>();
+                else
+                    wait_vmcnt<NPK>();
+            } else {
+                wait_vmcnt<0>();
+            }
+            __builtin_amdgcn_s_barrier();
+        }
         bias_tile(std::integral_constant<int, NXT>{}, sn);
         mask_tile(sn, i + 1);
         float mr = -INFINITY;
         {
             constexpr int NC = F8 ? 24 : 16;
+            struct CStep {
+                int kind;  // 0 hi, 1 Vl.Ph, 2 Vh.Pl
+                int idx;   // hs, or the d-tile
+            };
+            auto cstep = [](int q) constexpr -> CStep {
+                if (!F8) return CStep{0, q};
+                if (q >= 20) return CStep{2, q - 20};
+                if (q < 12) return q % 3 == 2 ? CStep{1, q / 3} : CStep{0, q - (q + 1) / 3};
+                return CStep{0, q - 4};
+            };
             frag vh[3], vl[3];
-            auto v_read = [&](auto j_c, frag& x, frag& y) {
-                constexpr int j = decltype(j_c)::value;
-                if constexpr (j < 16) {
-                    constexpr int dt = j >> 2, g = j & 3;
+            auto v_read = [&](auto q_c, frag& x, frag& y) {
+                constexpr CStep st = cstep(decltype(q_c)::value);
+                if constexpr (st.kind == 0) {
+                    constexpr int dt = st.idx >> 2, g = st.idx & 3;
                     x = lds_frag<SLOT * RG::VS + dt * 32 * 128>(vaddr[g]);
                     if constexpr (PVS && !F8) y = lds_frag<SLOT * RG::VS + dt * 32 * 128 + RG::V_LO>(vaddr[g]);
                 } else {
-                    constexpr int dt = (j - 16) >> 1, ii = j & 1;
+                    constexpr int dt = st.idx, ii = st.kind - 1;
                     x = lds_frag<SLOT * RG::VS + dt * 32 * 128>(v8a[ii][0]);
                     y = lds_frag<SLOT * RG::VS + dt * 32 * 128>(v8a[ii][1]);
                 }
             };
-            auto rv = [](int j) constexpr { return F8 ? (j < 16 ? 1 : 2) : (PVS ? 2 : 1); };
+            auto rv = [](int q) constexpr { return F8 ? ((q >= 20 || (q < 12 && q % 3 == 2)) ? 2 : 1) : (PVS ? 2 : 1); };
+            // V(i+1) pieces of the hi/lo modes: F8 behind its 8 correction MFMAs, else the first NPV positions
+            auto vdma = [&](auto q_c) {
+                if constexpr (VL) {
+                    constexpr int q = decltype(q_c)::value;
+                    constexpr CStep st = cstep(q);
+                    constexpr int vp = F8 ? (st.kind == 1 ? st.idx : st.kind == 2 ? 4 + st.idx : -1) : q;
+                    if constexpr (vp >= 0 && vp < NPV)
+                        if (more) v_piece(NXT, ktv, vp);
+                }
+            };
             v_read(std::integral_constant<int, 0>{}, vh[0], vl[0]);
             v_read(std::integral_constant<int, 1>{}, vh[1], vl[1]);
-            static_for<0, NC>([&](auto j_c) {
-                constexpr int j = decltype(j_c)::value;
-                if constexpr (j + 2 < NC) v_read(std::integral_constant<int, j + 2>{}, vh[(j + 2) % 3], vl[(j + 2) % 3]);
-                constexpr int after = (j + 1 < NC ? rv(j + 1) : 0) + (j + 2 < NC ? rv(j + 2) : 0);
+            static_for<0, NC>([&](auto q_c) {
+                constexpr int q = decltype(q_c)::value;
+                constexpr CStep st = cstep(q);
+                if constexpr (q + 2 < NC) v_read(std::integral_constant<int, q + 2>{}, vh[(q + 2) % 3], vl[(q + 2) % 3]);
+                constexpr int after = (q + 1 < NC ? rv(q + 1) : 0) + (q + 2 < NC ? rv(q + 2) : 0);
                 asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(after) : "memory");
-                asm volatile("" : "+v"(vh[j % 3]));
-                if constexpr (rv(j) == 2) asm volatile("" : "+v"(vl[j % 3]));
-                if constexpr (j < 16) {
+                asm volatile("" : "+v"(vh[q % 3]));
+                if constexpr (rv(q) == 2) asm volatile("" : "+v"(vl[q % 3]));
+                if constexpr (st.kind == 0) {
+                    constexpr int j = st.idx;
                     constexpr int dt = j >> 2, g = j & 3;
-                    o[dt] = mfma32(vh[j % 3], pf[g], o[dt]);
+                    o[dt] = mfma32(vh[q % 3], pf[g], o[dt]);
                     if constexpr (PVS && !F8) {
-                        o[dt] = mfma32(vh[j % 3], pfl[g], o[dt]);
-                        o[dt] = mfma32(vl[j % 3], pf[g], o[dt]);
+                        o[dt] = mfma32(vh[q % 3], pfl[g], o[dt]);
+                        o[dt] = mfma32(vl[q % 3], pf[g], o[dt]);
                     }
                     // running max of tile i+1: two scores per step
                     constexpr int t = j >> 3, r = 2 * (j & 7);
@@ -1015,10 +1072,12 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
                         pl8[j >> 1] = (uint32_t)w8;
                     }
                 } else {
-                    constexpr int dt = (j - 16) >> 1, ii = j & 1;
-                    const v8i pb = ii == 0 ? cat8(ph8) : cat8(pl8);
-                    o[dt] = mfma_f8(cat8(vh[j % 3], vl[j % 3]), pb, o[dt], ii == 0 ? F8_SCALE_LO : F8_SCALE_1, F8_SCALE_1);
+                    constexpr int dt = st.idx;
+                    const v8i pb = st.kind == 1 ? cat8(ph8) : cat8(pl8);
+                    o[dt] = mfma_f8(cat8(vh[q % 3], vl[q % 3]), pb, o[dt], st.kind == 1 ? F8_SCALE_LO : F8_SCALE_1,
+                                    F8_SCALE_1);
                 }
+                vdma(q_c);
                 __builtin_amdgcn_sched_barrier(0);
             });
         }
@@ -1026,7 +1085,11 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
         if (more) {
             update_max(mnx);
             apply_rescale();
-            wait_vmcnt<0>();
+            // K(i+2) landed (VL: V(i+1), issued after it, may stay in flight) and every wave is done with K slot NXT
+            if constexpr (VL)
+                wait_vmcnt<NPV>();
+            else
+                wait_vmcnt<0>();
             __builtin_amdgcn_s_barrier();
         }
     };
