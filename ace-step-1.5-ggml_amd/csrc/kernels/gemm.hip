@@ -562,100 +562,6 @@ void launch_cfg8(const GemmParams& p, hipStream_t s) {
     hipLaunchKernelGGL((gemm8_kernel<BM, F16, EPI>), dim3(nbm * (p.N / 256)), dim3(512), 0, s, p);
 }
 
-// ---------------------------------------------------------------------------------------------
-// Skinny GEMM (variant 30, forced only: measured 2x slower than the tiled kernels at 10 s, see pick_variant)
-// for very short sequences (M <= 128: 10 s of audio is M = 125): every output
-// column slice of 16 * TN columns is one workgroup over ALL M rows, its four waves split K four ways and the
-// partial tiles are summed in wave order through LDS (no global join) before the shared epilogue.  Operands
-// come straight from global memory into registers (A is L2-resident: 125 x 2048 bf16 = 0.5 MB; each W
-// element is read once, streamed D = 8 k-steps ahead), so the kernel is a weight stream: N / (16 TN)
-// workgroups instead of the (M / 64) x (N / 64) tiles whose per-k-tile LDS round trip waits on cold HBM.
-// Summation order per element: k-steps in order inside a wave's quarter, then quarters 0..3 -- deterministic,
-// not the other tiles' order (tests compare against the fp64 product).
-template <int TM, int TN, bool F16, int EPI>
-__global__ void __launch_bounds__(256) gemm_skinny_kernel(GemmParams p) {
-    constexpr int KW = 4, D = 8;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int n0 = blockIdx.x * (16 * TN);
-    const int steps = p.K / 32 / KW;  // k-steps of 32 per wave (a multiple of D: launch_skinny)
-    const int k0 = wid * steps * 32 + (lane >> 4) * 8;
-    const uint16_t* ap[TM];
-#pragma unroll
-    for (int i = 0; i < TM; ++i) ap[i] = p.A + (int64_t)min(i * 16 + (lane & 15), p.M - 1) * p.lda + k0;
-    const uint16_t* wp[TN];
-#pragma unroll
-    for (int j = 0; j < TN; ++j) wp[j] = p.W + (int64_t)(n0 + j * 16 + (lane & 15)) * p.ldw + k0;
-
-    f32x4 acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    uint4 a[D][TM], b[D][TN];
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i) a[d][i] = *(const uint4*)(ap[i] + d * 32);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) b[d][j] = *(const uint4*)(wp[j] + d * 32);
-    }
-    for (int ks = 0; ks < steps; ks += D) {
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<F16>(a[d][i], b[d][j], acc[i][j]);
-            const int nx = ks + D + d;
-            if (nx < steps) {  // wave-uniform
-#pragma unroll
-                for (int i = 0; i < TM; ++i) a[d][i] = *(const uint4*)(ap[i] + nx * 32);
-#pragma unroll
-                for (int j = 0; j < TN; ++j) b[d][j] = *(const uint4*)(wp[j] + nx * 32);
-            }
-        }
-    }
-    // partial tiles of the four K quarters -> LDS; wave w then owns m-tiles [w * TM / 4, (w + 1) * TM / 4)
-    __shared__ f32x4 red[KW * TM * TN * 64];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) red[((wid * TM + i) * TN + j) * 64 + lane] = acc[i][j];
-    __syncthreads();
-    constexpr int TW = TM / KW;
-    f32x4 fin[TW][TN];
-#pragma unroll
-    for (int i = 0; i < TW; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const int mi = wid * TW + i;
-            f32x4 v = red[((0 * TM + mi) * TN + j) * 64 + lane];
-#pragma unroll
-            for (int w = 1; w < KW; ++w) {
-                const f32x4 t = red[((w * TM + mi) * TN + j) * 64 + lane];
-                v = f32x4{v[0] + t[0], v[1] + t[1], v[2] + t[2], v[3] + t[3]};
-            }
-            fin[i][j] = v;
-        }
-    if (wid * TW * 16 < p.M) gemm_epilogue<TW, TN, F16, EPI, 1024>(p, fin, wid * TW * 16, n0, lane);
-}
-
-template <bool F16, int EPI>
-bool launch_skinny(const GemmParams& p, hipStream_t s) {
-    if constexpr (EPI == EPI_QKV_PREP) {
-        return false;
-    } else {
-        constexpr int TN = EPI == EPI_SWIGLU ? 2 : 1;
-        if (p.M > 128 || p.K % (32 * 4 * 8) != 0 || p.N % (16 * TN) != 0) return false;
-        const dim3 grid(p.N / (16 * TN));
-        if (p.M <= 64)
-            hipLaunchKernelGGL((gemm_skinny_kernel<4, TN, F16, EPI>), grid, dim3(256), 0, s, p);
-        else
-            hipLaunchKernelGGL((gemm_skinny_kernel<8, TN, F16, EPI>), grid, dim3(256), 0, s, p);
-        return true;
-    }
-}
-
 // variant: 0 = 128x128 PIPE0, 1 = 128x128 PIPE1, 2 = 256x256 PIPE1 (8 waves 2x4), 3 = 256x128 PIPE1,
 // 4 = 192x128 PIPE1, 5 = 192x256 PIPE1 (8 waves 2x4), 6 = 192x64 PIPE1 (dense only), 7 = 96x128 PIPE1,
 // 8 = 64x128 PIPE1, 9 = 64x64 PIPE1 (8, 9 dense only: short sequences), 10 = 256x256 / 11 = 192x256 8-wave
@@ -664,10 +570,6 @@ bool launch_skinny(const GemmParams& p, hipStream_t s) {
 template <bool F16, int EPI>
 void launch_variant(int variant, const GemmParams& p, hipStream_t s) {
     const int S = variant / 100;
-    if (variant == 30) {
-        if (launch_skinny<F16, EPI>(p, s)) return;
-        variant = 9;  // shape or epilogue outside the skinny kernel's reach
-    }
     if (S > 1 && (variant % 100 == 10 || variant % 100 == 11)) throw std::runtime_error("gemm: split-K is for the 4-wave tiles");
     switch (variant % 100) {
         case 0: launch_cfg<128, 128, 2, 2, F16, EPI, 0>(p, S, s); break;
@@ -688,7 +590,6 @@ void launch_variant(int variant, const GemmParams& p, hipStream_t s) {
         case 15: launch_cfg<128, 128, 2, 2, F16, EPI, 3>(p, S, s); break;
         // 8 waves (4 x 2) on a 192x128 tile: one tile per CU at M = 3000, N = 2048 (256 tiles), two waves per SIMD
         case 16: launch_cfg<192, 128, 4, 2, F16, EPI, 1>(p, S, s); break;
-        case 17: launch_cfg<192, 128, 4, 2, F16, EPI, 3>(p, S, s); break;
         default: throw std::runtime_error("gemm: bad variant");
     }
 }
@@ -758,7 +659,7 @@ int pick_variant(int M, int N, int K, bool quant, int fmt) {
         const int f = v % 100, S = v / 100;
         const bool wide = f == 2 || f == 5 || f == 10 || f == 11 || f == 21;  // (12-15: multi-stage rings)
         const bool qr = f >= 20 && f <= 24;
-        const bool dense_only = (f == 6 || (f >= 8 && f < 20) || f == 30 || S > 1) && !qr;
+        const bool dense_only = (f == 6 || (f >= 8 && f < 20) || S > 1) && !qr;
         const bool sk_ok = S <= 1 || (qr ? (f == 22 || f == 23) && S <= 4 && K / 64 >= 2 * S
                                          : ((f == 1 || f == 3 || f == 4 ? S <= 2
                                                                        : (((f >= 6 && f <= 9) || (f >= 12 && f <= 15)) && S <= 4)) &&
@@ -775,8 +676,8 @@ int pick_variant(int M, int N, int K, bool quant, int fmt) {
     const int64_t mb192 = (M + 191) / 192;
     const bool edge_ok = m_edge(M, 192) >= m_edge(M, 128) - 0.02;
     if (quant) return pick_variant_q(M, N, K, fmt);
-    // (variant 30, the skinny weight-stream kernel, is forced-only: at 10 s it ran the block linears 2x slower
-    // than the tiles below -- every 16-column workgroup re-reads all of A with 16-byte row-scattered loads)
+    // (a skinny weight-stream kernel for M <= 128 ran the 10 s block linears 2x slower than the tiles below --
+    // every 16-column workgroup re-read all of A with 16-byte row-scattered loads -- and was removed in round 4)
     // 8-wave ping-pong tiles for batched sequences (tools/gemm_msweep.py on MI355X, TFLOP/s): M = 12000 gate|up
     // 1011 (256x256) vs 941 (v2), qkv 933 vs 902, down 922 (192x256) vs 818, o 814 vs 786; M = 24000 gate|up
     // 1089 vs 1016, qkv 941 vs 897, down 955 vs 915, o 767 (v2) vs 724; M = 6000 down 921 (192x256) vs 853.
@@ -850,7 +751,7 @@ void launch_gemm(const uint16_t* A, int lda, const WeightView& W, int M, int N, 
                         (epi.prep.v_col < 0 || epi.prep.v_col == 128 * (nqc + nkc)),
                     "gemm: fused attention prep expects the [q | k | v] head order");
         if (v >= 100 && g_forced_variant < 0) v %= 100;  // (the narrow-output split-K pick is not for the prep)
-        v = v == 2 ? 3 : v == 5 ? 4 : v == 6 ? 1 : v == 9 ? 8 : v == 12 || v == 30 ? 13 : v;
+        v = v == 2 ? 3 : v == 5 ? 4 : v == 6 ? 1 : v == 9 ? 8 : v == 12 ? 13 : v;
     }
     switch (W.fmt) {
         case WF_BF16:

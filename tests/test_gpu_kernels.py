@@ -192,7 +192,7 @@ def test_attention_running_max_moves_mid_sequence(nk, mode):
     _check_attn(got, q, kv, hq, hkv, 0, None, scale, mode)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 204, 207, 208, 212, 307, 409, 413, 414])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 204, 207, 208, 212, 307, 409, 413, 414])
 @pytest.mark.parametrize("M,N,K", [(1, 256, 64), (300, 512, 128), (1000, 768, 2048), (513, 256, 6144)])
 def test_gemm_all_variants(variant, M, N, K):
     """Every GEMM kernel variant (128x128 / 256x256 / 256x128 / 192x128 / 192x256 / 64x64 / 64x128, the
@@ -223,39 +223,7 @@ def test_gemm_all_variants(variant, M, N, K):
     np.testing.assert_allclose(_vals(got_sw, 0), sw, rtol=2.0 ** -8, atol=1e-4)
 
 
-@pytest.mark.parametrize("epi", [0, 2, 3, 4])
-@pytest.mark.parametrize("M,N,K", [(1, 256, 1024), (37, 512, 2048), (64, 256, 6144), (65, 384, 1024),
-                                   (125, 2048, 2048), (128, 512, 3072)])
-def test_gemm_skinny(M, N, K, epi):
-    """The skinny weight-stream GEMM (variant 30, M <= 128: K split over the four waves, partial tiles summed in
-    wave order through LDS) with the f32-store, residual (gated / plain) and SwiGLU epilogues, M edges."""
-    capi = _capi()
-    rng = np.random.default_rng(M * 31 + K + epi)
-    a = _bits(rng.standard_normal((M, K)).astype(np.float32), 0)
-    w = _bits((rng.standard_normal((N, K)) * 0.05).astype(np.float32), 0)
-    x = rng.standard_normal((M, N)).astype(np.float32)
-    gate = rng.standard_normal(N).astype(np.float32) if epi == 2 else None
-    capi.gemm_variant(30)
-    try:
-        got = capi.kernel_gemm(a, w, act_type=0, epi=epi, bias=gate, x=x if epi in (2, 3) else None)
-    finally:
-        capi.gemm_variant(-1)
-    av, wv = _vals(a, 0).astype(np.float64), _vals(w, 0).astype(np.float64)
-    acc = av @ wv.T
-    scale = np.abs(av) @ np.abs(wv).T
-    if epi == 0:
-        assert np.all(np.abs(got - acc) <= 2e-6 * scale + 1e-6)
-    elif epi == 4:
-        g = acc.reshape(M, N // 32, 2, 16)[:, :, 0, :].reshape(M, N // 2)
-        u = acc.reshape(M, N // 32, 2, 16)[:, :, 1, :].reshape(M, N // 2)
-        np.testing.assert_allclose(_vals(got, 0), (g / (1 + np.exp(-g))) * u, rtol=2.0 ** -8, atol=1e-4)
-    else:
-        gg = gate.astype(np.float64) if epi == 2 else np.ones(N)
-        ref = x.astype(np.float64) + acc * gg
-        assert np.all(np.abs(got - ref) <= (2e-6 * scale + 1e-6) * np.abs(gg) + 2e-7 * np.abs(ref))
-
-
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 204, 207, 213, 215, 408])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 204, 207, 213, 215, 408])
 @pytest.mark.parametrize("epi", [2, 3])
 @pytest.mark.parametrize("M,N,K", [(300, 512, 128), (1000, 768, 2048), (9001, 512, 256)])
 def test_gemm_residual_epilogues(variant, epi, M, N, K):
