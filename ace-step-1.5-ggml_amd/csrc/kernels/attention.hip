@@ -100,6 +100,20 @@ __device__ __forceinline__ v8i cat8(const uint32_t (&w)[8]) {
 constexpr int F8_SCALE_1 = 127;
 constexpr int F8_SCALE_LO = 127 - 11;
 constexpr float PSCALE_F8_LOG2 = 5.0f;  // f8c: P <= 2^(5 + RESCALE_LOG2) = 256, inside e4m3 (max 448)
+// attn2_kernel: fragment reads are issued RA steps ahead of their MFMA (ring of RA + 1 fragment sets)
+#ifndef ACEMI_ATTN_RA
+#define ACEMI_ATTN_RA 2
+#endif
+constexpr int RA = ACEMI_ATTN_RA;
+static_assert(RA >= 1 && 2 * RA <= 15, "lgkmcnt counts at most 15 outstanding reads");
+// LDS reads issued after step p's own, i.e. those of steps p+1 .. p+RA (< n), for the counted lgkmcnt of step p
+template <class F>
+constexpr int reads_after(int p, int n, F reads) {
+    int c = 0;
+    for (int k = 1; k <= RA; ++k)
+        if (p + k < n) c += reads(p + k);
+    return c;
+}
 __device__ __forceinline__ f32x16 mfma_f8(const v8i& a, const v8i& b, f32x16 c, int sa, int sb) {
     return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 0, 0, 0, sa, 0, sb);
 }
@@ -744,8 +758,6 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
     constexpr float PSC = F8 ? PSCALE_F8_LOG2 : PSCALE_LOG2;
 
     const float c_log2 = a.scale * 1.4426950408889634f;
-    constexpr int RK = SPLIT ? 2 : 1;   // LDS reads per QK step
-    constexpr int RV = PVS ? 2 : 1;     // LDS reads per PV step
 
     // ---- phase B: QK of the next tile in NB steps.  Position p runs the hi step h (k-slice ks = h / 2 of half
     // t = h % 2: fp16 hi, + lo for SPLIT) or, for F8, every third position (p % 3 == 2) the correction step
@@ -777,33 +789,36 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
     auto rk = [](int p) constexpr { return F8 ? (p % 3 == 2 ? 2 : 1) : (SPLIT ? 2 : 1); };
     // S(tile in K slot SLOT) into sn, interleaved with fin(p) (a softmax-finish slice) and dma(p)
     auto qk_phase = [&](auto slot_c, f32x16 (&sn)[2], auto&& fin, auto&& dma) {
-        frag kh[3], kl[3];
-        k_read(slot_c, std::integral_constant<int, 0>{}, kh[0], kl[0]);
-        k_read(slot_c, std::integral_constant<int, 1>{}, kh[1], kl[1]);
+        frag kh[RA + 1], kl[RA + 1];
+        static_for<0, RA>([&](auto r_c) {
+            constexpr int r = decltype(r_c)::value;
+            if constexpr (r < NB) k_read(slot_c, r_c, kh[r], kl[r]);
+        });
         static_for<0, NB>([&](auto p_c) {
             constexpr int p = decltype(p_c)::value;
             constexpr BStep st = bstep(p);
             constexpr int t = st.idx & 1;
-            if constexpr (p + 2 < NB) k_read(slot_c, std::integral_constant<int, p + 2>{}, kh[(p + 2) % 3], kl[(p + 2) % 3]);
-            constexpr int after = (p + 1 < NB ? rk(p + 1) : 0) + (p + 2 < NB ? rk(p + 2) : 0);
+            if constexpr (p + RA < NB)
+                k_read(slot_c, std::integral_constant<int, p + RA>{}, kh[(p + RA) % (RA + 1)], kl[(p + RA) % (RA + 1)]);
+            constexpr int after = reads_after(p, NB, rk);
             asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(after) : "memory");
-            asm volatile("" : "+v"(kh[p % 3]));
-            if constexpr (rk(p) == 2) asm volatile("" : "+v"(kl[p % 3]));
+            asm volatile("" : "+v"(kh[p % (RA + 1)]));
+            if constexpr (rk(p) == 2) asm volatile("" : "+v"(kl[p % (RA + 1)]));
             if constexpr (st.corr) {
                 // Kl.Qh (c = 0, 1: the 2^-11 on A) + Kh.Ql (c = 2, 3: on B), e4m3 x e4m3, K = 64 per MFMA
                 constexpr int c = st.idx >> 1;
-                sn[t] = mfma_f8(cat8(kh[p % 3], kl[p % 3]), q8[c], sn[t], c < 2 ? F8_SCALE_LO : F8_SCALE_1,
+                sn[t] = mfma_f8(cat8(kh[p % (RA + 1)], kl[p % (RA + 1)]), q8[c], sn[t], c < 2 ? F8_SCALE_LO : F8_SCALE_1,
                                 c < 2 ? F8_SCALE_1 : F8_SCALE_LO);
             } else {
                 constexpr int ks = st.idx >> 1;
                 if constexpr (ks == 0) {
-                    sn[t] = mfma32(kh[p % 3], qf[0], f32x16{});
+                    sn[t] = mfma32(kh[p % (RA + 1)], qf[0], f32x16{});
                 } else {
-                    sn[t] = mfma32(kh[p % 3], qf[ks], sn[t]);
+                    sn[t] = mfma32(kh[p % (RA + 1)], qf[ks], sn[t]);
                 }
                 if constexpr (SPLIT && !F8) {
-                    sn[t] = mfma32(kh[p % 3], qfl[ks], sn[t]);
-                    sn[t] = mfma32(kl[p % 3], qf[ks], sn[t]);
+                    sn[t] = mfma32(kh[p % (RA + 1)], qfl[ks], sn[t]);
+                    sn[t] = mfma32(kl[p % (RA + 1)], qf[ks], sn[t]);
                 }
             }
             dma(p_c);
@@ -1015,7 +1030,7 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
                 if (q < 12) return q % 3 == 2 ? CStep{1, q / 3} : CStep{0, q - (q + 1) / 3};
                 return CStep{0, q - 4};
             };
-            frag vh[3], vl[3];
+            frag vh[RA + 1], vl[RA + 1];
             auto v_read = [&](auto q_c, frag& x, frag& y) {
                 constexpr CStep st = cstep(decltype(q_c)::value);
                 if constexpr (st.kind == 0) {
@@ -1039,23 +1054,26 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
                         if (more) v_piece(NXT, ktv, vp);
                 }
             };
-            v_read(std::integral_constant<int, 0>{}, vh[0], vl[0]);
-            v_read(std::integral_constant<int, 1>{}, vh[1], vl[1]);
+            static_for<0, RA>([&](auto r_c) {
+                constexpr int r = decltype(r_c)::value;
+                if constexpr (r < NC) v_read(r_c, vh[r], vl[r]);
+            });
             static_for<0, NC>([&](auto q_c) {
                 constexpr int q = decltype(q_c)::value;
                 constexpr CStep st = cstep(q);
-                if constexpr (q + 2 < NC) v_read(std::integral_constant<int, q + 2>{}, vh[(q + 2) % 3], vl[(q + 2) % 3]);
-                constexpr int after = (q + 1 < NC ? rv(q + 1) : 0) + (q + 2 < NC ? rv(q + 2) : 0);
+                if constexpr (q + RA < NC)
+                    v_read(std::integral_constant<int, q + RA>{}, vh[(q + RA) % (RA + 1)], vl[(q + RA) % (RA + 1)]);
+                constexpr int after = reads_after(q, NC, rv);
                 asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(after) : "memory");
-                asm volatile("" : "+v"(vh[q % 3]));
-                if constexpr (rv(q) == 2) asm volatile("" : "+v"(vl[q % 3]));
+                asm volatile("" : "+v"(vh[q % (RA + 1)]));
+                if constexpr (rv(q) == 2) asm volatile("" : "+v"(vl[q % (RA + 1)]));
                 if constexpr (st.kind == 0) {
                     constexpr int j = st.idx;
                     constexpr int dt = j >> 2, g = j & 3;
-                    o[dt] = mfma32(vh[q % 3], pf[g], o[dt]);
+                    o[dt] = mfma32(vh[q % (RA + 1)], pf[g], o[dt]);
                     if constexpr (PVS && !F8) {
-                        o[dt] = mfma32(vh[q % 3], pfl[g], o[dt]);
-                        o[dt] = mfma32(vl[q % 3], pf[g], o[dt]);
+                        o[dt] = mfma32(vh[q % (RA + 1)], pfl[g], o[dt]);
+                        o[dt] = mfma32(vl[q % (RA + 1)], pf[g], o[dt]);
                     }
                     // running max of tile i+1: two scores per step
                     constexpr int t = j >> 3, r = 2 * (j & 7);
@@ -1074,7 +1092,7 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
                 } else {
                     constexpr int dt = st.idx;
                     const v8i pb = st.kind == 1 ? cat8(ph8) : cat8(pl8);
-                    o[dt] = mfma_f8(cat8(vh[q % 3], vl[q % 3]), pb, o[dt], st.kind == 1 ? F8_SCALE_LO : F8_SCALE_1,
+                    o[dt] = mfma_f8(cat8(vh[q % (RA + 1)], vl[q % (RA + 1)]), pb, o[dt], st.kind == 1 ? F8_SCALE_LO : F8_SCALE_1,
                                     F8_SCALE_1);
                 }
                 vdma(q_c);
