@@ -9,16 +9,18 @@
 // (qwen_model.cpp:618-637).  Scores never touch HBM; the sliding layers visit
 // only the key tiles inside the window, causal blocks stop at their last query.
 //
-// Numerics: the reference runs attention in F32.  The DiT runs SPLIT=false (single fp16 operands,
-// f32 accumulation, two workgroups per CU): at full width its parity equals the f32-faithful modes,
-// also with peaked softmax rows (logits of tens), because the bf16 activation rounding of every mul_mat
-// dominates (tests/test_gpu_parity_strict.py).  SPLIT=true (ACE_MI_ATTN_PRECISION=split or
-// f32 for the DiT) keeps Q and K as fp16 pairs x = hi + lo (hi = fp16(x), lo = fp16(x - hi)) and forms
-// each score as hi*hi + hi*lo + lo*hi with three v_mfma_f32_32x32x16_f16 (f32
-// accumulate) -> ~22-bit operands.  P.V runs on single fp16 operands (P rounded to nearest, V hi)
-// unless PVS (AttnArgs::pv_split: ACE_MI_ATTN_PRECISION=f32, the condition / text encoders' default)
-// asks for the same three-product form there too.  P is formed as exp2(s - m + 12) (scaled by
-// 2^12 so its lo part stays a normal fp16; O and l carry the same factor).
+// Numerics: the reference runs attention in F32 (ggml_mul_mat_set_prec(kq, GGML_PREC_F32), acestep_dit_model.cpp:
+// 1238-1251).  Four operand modes (AttnArgs split / pv_split / f8; ACE_MI_ATTN_PRECISION):
+//   fp16   single fp16 operands, f32 accumulation (two workgroups per CU);
+//   split  Q and K as fp16 pairs x = hi + lo (hi = fp16(x), lo = fp16(x - hi)): each score is hi*hi + hi*lo + lo*hi
+//          (three v_mfma_f32_32x32x16_f16, ~22-bit operands); P.V single fp16 (P rounded to nearest, V hi);
+//   f32    the same three-product form for P.V too (P hi = fp16 toward zero, lo = fp16(P - hi));
+//   f8c    (the DiT default) hi x hi in fp16 as above, the correction products Kl.Qh + Kh.Ql and Vl.Ph + Vh.Pl as
+//          block-scaled e4m3 MFMAs (v_mfma_scale_f32_32x32x64_f8f6f4, K = 64; the lo parts stored as fp8(2^11 lo)
+//          and scaled back by the MFMA's E8M0 block scale): ~2^-15 relative per product instead of ~2^-22, at 2/3 of
+//          the f32 mode's matrix-core time; meets the literal 1e-3 one-layer parity bound (tests/test_gpu_parity_strict.py).
+// P is formed as exp2(s - m + PSCALE) (2^12 in the fp16 hi/lo modes so the lo part stays a normal fp16; 2^5 in f8c so P
+// stays inside e4m3's range; O and l carry the same factor).
 // Online softmax in f32 (exp2 domain) with a lazy running max: O and l are
 // rescaled only when a row's max grows by more than 2^RESCALE_LOG2 (P then
 // stays below 2^15, inside fp16), which after the first tiles is almost never.
@@ -931,7 +933,7 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
         const float nm = -m_use;
         float lsum = 0.f;
         frag pf[4], pfl[4];
-        uint32_t ph8[8], pl8[8];  // F8: fp8 P (hi) and P - f16(P) (lo), byte c = 16 t + r of the lane's 32 keys
+        uint32_t ph8[8] = {}, pl8[8] = {};  // F8: fp8 P (hi) and P - f16(P) (lo), byte c = 16 t + r of the lane's keys
         // softmax finish of tile i at QK position p: pair j (elements 2j, 2j + 1 of the flattened [t][r] scores) =
         // the position's hi step
         auto fin = [&](auto p_c) {
@@ -957,7 +959,7 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
                     typedef _Float16 h2t __attribute__((ext_vector_type(2)));
                     const h2t hv = __builtin_convertvector((f2){p0, p1}, h2t);
                     uint32_t w = __builtin_bit_cast(uint32_t, hv);
-                    int w8 = (j & 1) ? (int)ph8[j >> 1] : 0;
+                    int w8 = (int)ph8[j >> 1];  // (the even pair writes the low word; the high word is written next)
                     w8 = __builtin_amdgcn_cvt_pk_fp8_f32(p0, p1, w8, (j & 1) != 0);
                     asm volatile("" : "+v"(w), "+v"(w8), "+v"(lsum), "+v"(p0), "+v"(p1));
                     pf[fi][fj] = w;
@@ -1081,10 +1083,16 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
                     asm volatile("" : "+v"(mr));
                     if constexpr (F8) {  // fp8 lo part of P pair j: P - f16(P) (exact in f32)
                         constexpr int fi = 2 * t + (r >> 3), fj = (r & 7) >> 1;
-                        typedef _Float16 h2t __attribute__((ext_vector_type(2)));
-                        const h2t hv = __builtin_bit_cast(h2t, (uint32_t)pf[fi][fj]);
-                        int w8 = (j & 1) ? (int)pl8[j >> 1] : 0;
-                        w8 = __builtin_amdgcn_cvt_pk_fp8_f32(sc[t][r] - (float)hv[0], sc[t][r + 1] - (float)hv[1], w8,
+                        int w8 = (int)pl8[j >> 1];
+                        // P - f16(P) as one mixed-precision FMA per value (v_fma_mix_f32 reads the f16 half in-op;
+                        // hipcc otherwise emits a v_cvt_f32_f16 + v_sub pair)
+                        const uint32_t hw = (uint32_t)pf[fi][fj];
+                        float l0, l1;
+                        asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(l0) : "v"(hw), "v"(sc[t][r]));
+                        asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+                            : "=v"(l1)
+                            : "v"(hw), "v"(sc[t][r + 1]));
+                        w8 = __builtin_amdgcn_cvt_pk_fp8_f32(l0, l1, w8,
                                                              (j & 1) != 0);
                         asm volatile("" : "+v"(w8));
                         pl8[j >> 1] = (uint32_t)w8;

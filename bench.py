@@ -51,7 +51,7 @@ METRIC = "DiT denoising steps/sec (240s@5Hz latent, bs=1..8) + single-step ms; 1
 # DiT attention operand precision of the headline (the engine's default; ACE_MI_BENCH_ATTN overrides for A/B runs):
 # "fp16" single fp16 operands, "split" hi/lo fp16 Q.K, "f32" hi/lo Q.K and P.V (ggml's F32 kq / kqv,
 # acestep_dit_model.cpp:1238-1251)
-HEADLINE_ATTN = os.environ.get("ACE_MI_BENCH_ATTN", "fp16")
+HEADLINE_ATTN = os.environ.get("ACE_MI_BENCH_ATTN", "f8c")
 ATTN_DESC = {"fp16": "fp16-operand f32-accumulate attention",
              "split": "split attention (hi/lo fp16 Q.K, fp16 P.V, f32 accumulate)",
              "f32": "f32-faithful attention (hi/lo fp16 Q.K and P.V, f32 accumulate)",
