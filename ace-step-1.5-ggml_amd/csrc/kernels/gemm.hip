@@ -30,6 +30,24 @@
 namespace acemi {
 namespace gemm_detail {
 
+// Diagnostic ablations (A/B builds only, tools/build_ab.sh; results are wrong by design): bit 0 drops the main loop's
+// LDS-DMA staging (every k-tile reuses the prologue's tiles), bit 1 its LDS fragment reads (registers of the first
+// k-tile reused), bit 2 stages k-tile 0 again and again (the DMA issue kept, its bytes L2-hot) -- what the loop costs
+// without that traffic.
+#ifndef ACEMI_GEMM_ABLATE
+#define ACEMI_GEMM_ABLATE 0
+#endif
+constexpr int kAblate = ACEMI_GEMM_ABLATE;
+
+// f(std::integral_constant<int, I>) for I = B..E-1
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
+
 // PIPE 0: stage(t+1) ; compute(t) ; vmcnt(0) ; __syncthreads        (2 LDS buffers)
 // PIPE 1: compute first half of tile t from registers read up front, release the LDS buffer with
 //         a raw s_barrier, stage tile t+2 into it, compute the second half, then a COUNTED
@@ -118,8 +136,8 @@ __global__ void __launch_bounds__(WM * WN * 64, (GemmTwoPerCU<BM, BN, WM, WN, EP
 #pragma unroll
         for (int j = 0; j < G_PER_WAVE; ++j) {
             const int g = wid + NW * j;
-            __builtin_amdgcn_global_load_lds((const void*)(src[j] + kt * BK), (lds_void*)(base + g * 1024), 16, 0,
-                                             0);
+            __builtin_amdgcn_global_load_lds((const void*)(src[j] + ((kAblate & 4) ? 0 : kt) * BK),
+                                             (lds_void*)(base + g * 1024), 16, 0, 0);
         }
     };
 
@@ -224,11 +242,20 @@ __global__ void __launch_bounds__(WM * WN * 64, (GemmTwoPerCU<BM, BN, WM, WN, EP
         // HBM after the main loop.  The two peeled calls keep the prefetched registers out of any loop.
         float xo[TM][4][TN];  // (dead unless XPF)
         float g0[TN], g1[TN];
+        uint4 a_keep[TM][2], b_keep[TN][2];  // (ablation builds only)
         auto body = [&](int kt, auto pf_tag) {
             constexpr bool PF = decltype(pf_tag)::value;
             const int cur = kt % NS;
             uint4 a[TM][2], b[TN][2];
-            read_frags_asm(cur, a, b);
+            if constexpr (kAblate & 2) {
+                if (kt == 0) read_frags_asm(cur, a_keep, b_keep);
+#pragma unroll
+                for (int i = 0; i < TM; ++i) a[i][0] = a_keep[i][0], a[i][1] = a_keep[i][1];
+#pragma unroll
+                for (int j = 0; j < TN; ++j) b[j][0] = b_keep[j][0], b[j][1] = b_keep[j][1];
+            } else {
+                read_frags_asm(cur, a, b);
+            }
 #pragma unroll
             for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -236,7 +263,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (GemmTwoPerCU<BM, BN, WM, WN, EP
 #pragma unroll
                     for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<F16>(a[i][kk], b[j][kk], acc[i][j]);
             __builtin_amdgcn_s_barrier();  // every wave has its fragments of tile kt: buffer `cur` is free
-            const bool more = kt + NS < nk;
+            const bool more = kt + NS < nk && !(kAblate & 1);
             if (more) stage(cur, kt + NS);
             if constexpr (PF) resid_prefetch<TM, TN, EPI>(p, m0 + wm0, n0 + wn0, lane, BM / WM, xo, g0, g1);
 #pragma unroll
@@ -277,6 +304,141 @@ __global__ void __launch_bounds__(WM * WN * 64, (GemmTwoPerCU<BM, BN, WM, WN, EP
         gemm_epilogue<TM, TN, F16, EPI, (SK ? 32 : (NW > 4 ? NW : 1024))>(p, acc, m0 + wm0, n0 + wn0, lane);
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Warp-specialized GEMM (variant 18): BM x BN tile, 512 threads = 4 MFMA waves (2 x 2, one per SIMD) + 4
+// loader waves (one per SIMD) that issue every LDS-DMA piece.  Measured on the single-role tiles (tools/build_ab.sh
+// ablations, profiles/r04/gemm_ablation.md): dropping the main loop's LDS-DMA took the 192x128 tile from 930 to 1127
+// TFLOP/s at gate|up and the 96x128 one from 784 to 1051 at the N = 2048 projections, and re-staging L2-hot bytes
+// (the DMA issue kept) recovered only 5 % of that -- a wave that issues LDS-DMA pieces stalls its own MFMA stream
+// (≈60 cycles per 1 KiB piece, MI355X_MICROARCH.md), whatever the bytes cost.  Here the MFMA waves only read LDS
+// and issue MFMAs; the pieces come from waves that have nothing else to issue.
+//   ring: NS k-tile slots; the loaders keep tiles t+1 .. t+NS-1 in flight and publish tile t+1 at barrier B(t+1);
+//   MFMA waves, k-tile t: half 0 (k 0..31) from registers while the half-1 fragments are read, lgkmcnt(0), B(t+1)
+//   (slot t fully read -> the loaders refill it with tile t+NS), half 1 while tile t+1's half-0 fragments are read.
+// One barrier per k-tile; a loader waits (counted vmcnt) for tile t+1 just before B(t+1), so tile t+1 has had the
+// NS-2 iterations since its issue to land.  Same operands, swizzled LDS image, MFMA and per-element k order as
+// gemm_kernel: results are bit-identical to the other dense tiles.
+template <int BM, int BN, bool F16, int EPI, int NS>
+__global__ void __launch_bounds__(512, 1) gemm_ws_kernel(GemmParams p) {
+    constexpr int NC = 4, WN = 2;  // MFMA waves (2 x 2)
+    constexpr int WTM = BM / 2, WTN = BN / WN;
+    constexpr int TM = WTM / 16, TN = WTN / 16;
+    constexpr int BK = 64, ROWB = BK * 2;
+    constexpr int STAGE = (BM + BN) * ROWB;
+    constexpr int G = (BM + BN) / 8 / 4;  // 1 KiB pieces per loader wave per k-tile
+    static_assert((BM + BN) % 32 == 0 && NS >= 3, "ws tile");
+    static_assert(EPI != EPI_SWIGLU || (TN % 2 == 0), "swiglu needs column pairs");
+    __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    int m0, n0;
+    block_tile<BM, BN>(p, m0, n0);
+    const int nk = p.K / BK;
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+
+    if (wid >= NC) {  // ---- loader wave ----
+        const int lw = wid - NC;
+        const uint16_t* src[G];
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            const int row = (lw + 4 * j) * 8 + (lane >> 3);
+            const int c = (lane & 7) ^ swz(row);
+            src[j] = row < BM ? p.A + (int64_t)min(m0 + row, p.M - 1) * p.lda + c * 8
+                              : p.W + (int64_t)(n0 + row - BM) * p.ldw + c * 8;
+        }
+        auto stage = [&](int slot, int kt) {
+#pragma unroll
+            for (int j = 0; j < G; ++j)
+                __builtin_amdgcn_global_load_lds((const void*)(src[j] + kt * BK),
+                                                 (lds_void*)(smem + slot * STAGE + (lw + 4 * j) * 1024), 16, 0, 0);
+        };
+        // wait until at most n (0 .. NS-1) younger k-tiles of this wave are in flight
+        auto wait_tiles = [&](int n) {
+            if (NS >= 4 && n >= 3) wait_vmcnt<(NS >= 4 ? 3 : 0) * G>();
+            else if (n == 2) wait_vmcnt<2 * G>();
+            else if (n == 1) wait_vmcnt<G>();
+            else wait_vmcnt<0>();
+        };
+#pragma unroll
+        for (int t = 0; t < NS; ++t)
+            if (t < nk) stage(t, t);
+        wait_tiles(min(NS, nk) - 1);  // tile 0
+        __builtin_amdgcn_s_barrier();  // B(0)
+        for (int j = 1; j < nk; ++j) {
+            wait_tiles(min(nk - 1, j - 2 + NS) - j);  // tile j landed (tiles up to j-2+NS issued)
+            __builtin_amdgcn_s_barrier();              // B(j): slot (j-1) % NS read by every MFMA wave
+            if (j - 1 + NS < nk) stage((j - 1) % NS, j - 1 + NS);
+        }
+        wait_vmcnt<0>();
+        if constexpr (EPI == EPI_QKV_PREP)
+            qkv_prep_head<BM, 8, NS * STAGE>(p, m0, n0 >> 7, tid, smem, [](float*, int, int) {});
+        return;
+    }
+
+    // ---- MFMA wave ----
+    const int wm0 = (wid / WN) * WTM, wn0 = (wid % WN) * WTN;
+    const int lrow = lane & 15, lchunk = lane >> 4;
+    const int rsw = (lrow >> 1) & 7;
+    const uint32_t ch[2] = {(uint32_t)((lchunk ^ rsw) * 16), (uint32_t)(((4 + lchunk) ^ rsw) * 16)};
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    uint4 a[TM][2], b[TN][2];
+    // fragment r of half h of the k-tile in `slot`: r < TN -> B fragment r, else A fragment r - TN
+    auto rd = [&](auto r_c, int slot, auto h_c) {
+        constexpr int r = decltype(r_c)::value, h = decltype(h_c)::value;
+        const uint32_t sb = lds0 + slot * STAGE + ch[h];
+        if constexpr (r < TN)
+            b[r][h] = ds_read_b128_off<r * 16 * ROWB>(sb + (BM + wn0 + lrow) * ROWB);
+        else
+            a[r - TN][h] = ds_read_b128_off<(r - TN) * 16 * ROWB>(sb + (wm0 + lrow) * ROWB);
+    };
+    // the TM x TN MFMAs of half h, the fragment reads of half hr (k-tile in `slot`) one after each of the first
+    // TM + TN MFMAs
+    auto half = [&](auto h_c, int slot, auto hr_c, auto reads_c) {
+        constexpr int h = decltype(h_c)::value;
+        static_for<0, TM * TN>([&](auto s_c) {
+            constexpr int st = decltype(s_c)::value;
+            acc[st / TN][st % TN] = mfma16<F16>(a[st / TN][h], b[st % TN][h], acc[st / TN][st % TN]);
+            if constexpr (decltype(reads_c)::value && st < TM + TN) rd(s_c, slot, hr_c);
+            __builtin_amdgcn_sched_barrier(0);
+        });
+    };
+    using H0 = std::integral_constant<int, 0>;
+    using H1 = std::integral_constant<int, 1>;
+    __builtin_amdgcn_s_barrier();  // B(0): tile 0 landed
+    static_for<0, TM + TN>([&](auto r_c) { rd(r_c, 0, H0{}); });
+    lds_wait_all();
+    using RD = std::true_type;
+    for (int kt = 0; kt < nk - 1; ++kt) {
+        half(H0{}, kt % NS, H1{}, RD{});
+        lds_wait_all();
+        __builtin_amdgcn_s_barrier();  // B(kt+1): tile kt+1 landed; slot kt is read
+        half(H1{}, (kt + 1) % NS, H0{}, RD{});
+        lds_wait_all();
+    }
+    half(H0{}, (nk - 1) % NS, H1{}, RD{});  // the last k-tile (no B(nk))
+    lds_wait_all();
+    half(H1{}, 0, H0{}, std::false_type{});
+    if constexpr (EPI == EPI_QKV_PREP)
+        qkv_prep_head<BM, 8, NS * STAGE>(p, m0, n0 >> 7, tid, smem, [&](float* tile, int c0, int CH) {
+            const int ccol = lane & 15, crow = (lane >> 4) * 4;
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int rb = wm0 + i * 16 - c0;
+                if (rb < 0 || rb >= CH) continue;
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) tile[(rb + crow + r) * PREP_LD + wn0 + j * 16 + ccol] = acc[i][j][r];
+            }
+        });
+    else
+        gemm_epilogue<TM, TN, F16, EPI, 64>(p, acc, m0 + wm0, n0 + wn0, lane);
+}
 
 // ---------------------------------------------------------------------------------------------
 // 8-wave ping-pong GEMM: BM x 256 tile, 512 threads as 2 (M) x 4 (N) waves, two wave groups
@@ -410,31 +572,33 @@ __global__ void __launch_bounds__(512) gemm8_kernel(GemmParams p) {
     for (int kt = 0; kt < nk; ++kt) {
         const int buf = kt & 1;
         // ph1
-        read_a(buf, 0, a);
-        read_b(buf, 0, b0);
-        stage_b(1, kt + 1);
+        if (!(kAblate & 2) || kt == 0) {
+            read_a(buf, 0, a);
+            read_b(buf, 0, b0);
+        }
+        if (!(kAblate & 1)) stage_b(1, kt + 1);
         wait_stages();
         seg();
         lds_wait_all();
         mma(a, b0, acc[0][0]);
         seg();
         // ph2
-        read_b(buf, 1, b1);
-        stage_a(1, kt + 1);
+        if (!(kAblate & 2) || kt == 0) read_b(buf, 1, b1);
+        if (!(kAblate & 1)) stage_a(1, kt + 1);
         wait_stages();
         seg();
         lds_wait_all();
         mma(a, b1, acc[0][1]);
         seg();
         // ph3: ph4 reads nothing, so no stage has to retire here (a wait here measured neutral)
-        read_a(buf, 1, a);
-        stage_a(0, kt + 2);
+        if (!(kAblate & 2) || kt == 0) read_a(buf, 1, a);
+        if (!(kAblate & 1)) stage_a(0, kt + 2);
         seg();
         lds_wait_all();
         mma(a, b1, acc[1][1]);
         seg();
         // ph4
-        stage_b(0, kt + 2);
+        if (!(kAblate & 1)) stage_b(0, kt + 2);
         wait_stages();
         seg();
         __builtin_amdgcn_sched_barrier(0);
@@ -555,6 +719,17 @@ void launch_cfg(GemmParams p, int S, hipStream_t s) {
     }
 }
 
+template <int BM, int BN, bool F16, int EPI, int NS>
+void launch_ws(const GemmParams& p, hipStream_t s) {
+    if (p.N % BN != 0) throw std::runtime_error("gemm: the warp-specialized tile needs N % BN == 0");
+    if constexpr (EPI == EPI_QKV_PREP && BN != 128) {
+        throw std::runtime_error("gemm: the fused attention prep needs 128-wide column tiles");
+    } else {
+        const int nbm = (p.M + BM - 1) / BM;
+        hipLaunchKernelGGL((gemm_ws_kernel<BM, BN, F16, EPI, NS>), dim3(nbm * (p.N / BN)), dim3(512), 0, s, p);
+    }
+}
+
 template <int BM, bool F16, int EPI>
 void launch_cfg8(const GemmParams& p, hipStream_t s) {
     if (p.N % 256 != 0) throw std::runtime_error("gemm: the 8-wave tiles need N % 256 == 0");
@@ -570,7 +745,7 @@ void launch_cfg8(const GemmParams& p, hipStream_t s) {
 template <bool F16, int EPI>
 void launch_variant(int variant, const GemmParams& p, hipStream_t s) {
     const int S = variant / 100;
-    if (S > 1 && (variant % 100 == 10 || variant % 100 == 11)) throw std::runtime_error("gemm: split-K is for the 4-wave tiles");
+    if (S > 1 && (variant % 100 == 10 || variant % 100 == 11 || variant % 100 == 18)) throw std::runtime_error("gemm: split-K is for the 4-wave tiles");
     switch (variant % 100) {
         case 0: launch_cfg<128, 128, 2, 2, F16, EPI, 0>(p, S, s); break;
         case 1: launch_cfg<128, 128, 2, 2, F16, EPI, 1>(p, S, s); break;
@@ -590,6 +765,10 @@ void launch_variant(int variant, const GemmParams& p, hipStream_t s) {
         case 15: launch_cfg<128, 128, 2, 2, F16, EPI, 3>(p, S, s); break;
         // 8 waves (4 x 2) on a 192x128 tile: one tile per CU at M = 3000, N = 2048 (256 tiles), two waves per SIMD
         case 16: launch_cfg<192, 128, 4, 2, F16, EPI, 1>(p, S, s); break;
+        // warp-specialized (4 MFMA + 4 loader waves) 192x128, three k-tiles in the ring (forced only: +18 % isolated at
+        // the K = 6144 down projection, neutral in the sampling loop; a 3-stage single-role 192x128 tile (0.7x) and a
+        // 4-slot ring (equal or slower) measured in round 4 are not built)
+        case 18: launch_ws<192, 128, F16, EPI, 3>(p, s); break;
         default: throw std::runtime_error("gemm: bad variant");
     }
 }
@@ -633,12 +812,10 @@ double m_edge(int M, int bm) { return (double)M / (double)(((M + bm - 1) / bm) *
 // ds_write dequant kernel (gemm_q_kernel, 0-7) only when forced.  Long sequences: 192-row tiles (8 waves where
 // N % 256 == 0 leaves a full round of 256-column tiles); short ones: 128 / 64-row tiles, split over K until
 // the grid covers the 256 CUs.
-int pick_variant_q(int M, int N, int K, int fmt) {
+int pick_variant_q(int M, int N, int K) {
     const int64_t mb192 = (M + 191) / 192;
     if (M > 1024) {
-        // 21 (8 waves, 256 columns) fails the fp64 check for Q4_K (test_gemm_q_matches_dequantized_product,
-        // round 3, not understood): Q4_K takes the 4-wave 192-row tile
-        if (fmt != WF_Q4_K && N % 256 == 0 && mb192 * (N / 256) >= 256) return 21;
+        if (N % 256 == 0 && mb192 * (N / 256) >= 256) return 21;
         return 20;
     }
     // Short sequences: round 1's LDS-dequant kernel (96 x 128).  Whole forwards through the 64 / 128-row
@@ -664,8 +841,7 @@ int pick_variant(int M, int N, int K, bool quant, int fmt) {
                                          : ((f == 1 || f == 3 || f == 4 ? S <= 2
                                                                        : (((f >= 6 && f <= 9) || (f >= 12 && f <= 15)) && S <= 4)) &&
                                             K / 64 >= 2 * S));
-        return !(wide && N % 256 != 0) && !(quant && dense_only) && !(!quant && qr) && sk_ok &&
-               !(f == 21 && fmt == WF_Q4_K);
+        return !(wide && N % 256 != 0) && !(quant && dense_only) && !(!quant && qr) && sk_ok;
     };
     if (g_forced_variant >= 0x10000) return g_forced_variant & 0xffff;  // diagnostics (selftest): no support check
     if (g_forced_variant >= 0 && supports(g_forced_variant)) return g_forced_variant;  // tests / micro-benchmarks
@@ -675,7 +851,7 @@ int pick_variant(int M, int N, int K, bool quant, int fmt) {
     }
     const int64_t mb192 = (M + 191) / 192;
     const bool edge_ok = m_edge(M, 192) >= m_edge(M, 128) - 0.02;
-    if (quant) return pick_variant_q(M, N, K, fmt);
+    if (quant) return pick_variant_q(M, N, K);
     // (a skinny weight-stream kernel for M <= 128 ran the 10 s block linears 2x slower than the tiles below --
     // every 16-column workgroup re-read all of A with 16-byte row-scattered loads -- and was removed in round 4)
     // 8-wave ping-pong tiles for batched sequences (tools/gemm_msweep.py on MI355X, TFLOP/s): M = 12000 gate|up

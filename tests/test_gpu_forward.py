@@ -333,7 +333,7 @@ def _batched(br, h, c, e, t):
     return out.cpu().numpy()
 
 
-@pytest.mark.parametrize("variant", [-1, 10, 11, 16])
+@pytest.mark.parametrize("variant", [-1, 10, 11, 16, 18])
 @pytest.mark.parametrize("width", ["tiny", "full"])
 def test_fused_qkv_prep_is_bit_exact(tiny_ckpt, monkeypatch, width, variant):
     """The QKV / cross-q GEMMs with QK-norm, RoPE and the attention re-layout fused into their epilogue

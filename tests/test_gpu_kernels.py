@@ -193,7 +193,8 @@ def test_attention_running_max_moves_mid_sequence(nk, mode):
     _check_attn(got, q, kv, hq, hkv, 0, None, scale, mode)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 204, 207, 208, 212, 307, 409, 413, 414])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 18, 204, 207, 208, 212, 307,
+                                     409, 413, 414])
 @pytest.mark.parametrize("M,N,K", [(1, 256, 64), (300, 512, 128), (1000, 768, 2048), (513, 256, 6144)])
 def test_gemm_all_variants(variant, M, N, K):
     """Every GEMM kernel variant (128x128 / 256x256 / 256x128 / 192x128 / 192x256 / 64x64 / 64x128, the
@@ -224,7 +225,8 @@ def test_gemm_all_variants(variant, M, N, K):
     np.testing.assert_allclose(_vals(got_sw, 0), sw, rtol=2.0 ** -8, atol=1e-4)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 204, 207, 213, 215, 408])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 18, 204, 207, 213, 215,
+                                     408])
 @pytest.mark.parametrize("epi", [2, 3])
 @pytest.mark.parametrize("M,N,K", [(300, 512, 128), (1000, 768, 2048), (9001, 512, 256)])
 def test_gemm_residual_epilogues(variant, epi, M, N, K):
@@ -249,6 +251,28 @@ def test_gemm_residual_epilogues(variant, epi, M, N, K):
     g = gate.astype(np.float64) if epi == 2 else np.ones(N)
     ref = x.astype(np.float64) + acc * g
     assert np.all(np.abs(got - ref) <= (2e-6 * scale + 1e-6) * np.abs(g) + 2e-7 * np.abs(ref))
+
+
+@pytest.mark.parametrize("variant", [18])
+@pytest.mark.parametrize("M,N,K", [(3000, 2048, 2048), (777, 384, 192), (5, 128, 64)])
+def test_gemm_tiles_bit_identical(variant, M, N, K):
+    """The warp-specialized 192x128 tile (one barrier per k-tile, loader waves) accumulates every element in the
+    same k order as the double-buffered 192x128 tile (4): identical bits, store and residual."""
+    capi = _capi()
+    rng = np.random.default_rng(M + K)
+    a = _bits(rng.standard_normal((M, K)).astype(np.float32), 0)
+    w = _bits((rng.standard_normal((N, K)) * 0.05).astype(np.float32), 0)
+    x = rng.standard_normal((M, N)).astype(np.float32)
+    gate = rng.standard_normal(N).astype(np.float32)
+    outs = {}
+    for v in (4, variant):
+        capi.gemm_variant(v)
+        try:
+            outs[v] = (capi.kernel_gemm(a, w, act_type=0, epi=0), capi.kernel_gemm(a, w, act_type=0, epi=2, bias=gate, x=x))
+        finally:
+            capi.gemm_variant(-1)
+    np.testing.assert_array_equal(outs[variant][0], outs[4][0])
+    np.testing.assert_array_equal(outs[variant][1], outs[4][1])
 
 
 def test_attention_key_split_with_one_part_fully_masked():

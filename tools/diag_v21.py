@@ -29,7 +29,7 @@ def main():
                     cm = np.unique(cols % 256)
                     msg += (f" cols%256 {cm[:12].tolist()}{'...' if len(cm) > 12 else ''} (n={len(cm)})"
                             f" col-waves {np.unique((cols % 256) // 32).tolist()} rows%192 n={len(np.unique(rows % 192))}"
-                            f" lane16 {np.unique(cols % 16).tolist()} max rel {float(np.max(np.abs(got - ref)[bad]) / (scale + 1e-6)):.3g}")
+                            f" lane16 {np.unique(cols % 16).tolist()} max rel {float(np.max((np.abs(got - ref) / (np.broadcast_to(scale, got.shape) + 1e-6))[bad])):.3g}")
                 print(msg, flush=True)
 
 
