@@ -529,9 +529,9 @@ class GGMLCAPIBridge:
         self._ensure_ok(self.lib.ace_mi_synchronize(self.ctx), "ace_mi_synchronize")
 
     def set_attn_precision(self, mode: str) -> None:
-        """DiT attention operand precision for subsequent forwards: "fp16", "split", "f32" or "f8c"
+        """DiT attention operand precision for subsequent forwards: "fp16", "split", "f32", "f8c" or "pv8"
         (include/acestep_mi355x.h, ace_mi_dit_set_attn_precision)."""
-        code = {"fp16": 0, "split": 1, "f32": 2, "f8c": 3}[mode]
+        code = {"fp16": 0, "split": 1, "f32": 2, "f8c": 3, "pv8": 4}[mode]
         self._ensure_ok(self.lib.ace_mi_dit_set_attn_precision(self.ctx, code), "ace_mi_dit_set_attn_precision")
 
     def profile_enable(self, on: bool) -> None:
@@ -590,7 +590,7 @@ def kernel_attention(q: np.ndarray, kv: np.ndarray, hq: int, hkv: int, window: i
                      split: bool = True, causal: bool = False, pv_split: bool = False, f8: bool = False) -> np.ndarray:
     """q [B][nq][hq*128] f32, kv [B][nk][2*hkv*128] f32 -> out [B][nq][hq*128] f32 (bf16-rounded).
     split: hi/lo fp16 Q.K; pv_split: hi/lo fp16 P.V too (both = the fully f32-faithful mode); f8 (with both):
-    the f8c mode (fp8 correction products)."""
+    the f8c mode (fp8 correction products); f8 with pv_split and not split: the pv8 mode (fp16 Q.K, f8c P.V)."""
     lib = load_selftest_library()
     q = np.ascontiguousarray(q, dtype=np.float32)
     kv = np.ascontiguousarray(kv, dtype=np.float32)

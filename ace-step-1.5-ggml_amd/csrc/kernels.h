@@ -140,7 +140,9 @@ size_t attn_part_floats(int B, int nq, int Hq);
 // block-scaled e4m3 MFMAs (hi x hi in fp16, Kl.Qh + Kh.Ql and Vl.Ph + Vh.Pl at e4m3 precision: ~2^-15 relative
 // per product instead of F32's ~2^-22, at 2/3 of F32's matrix-core time).  ACE_MI_ATTN_PRECISION=fp16|split|f32 overrides `dflt`;
 // the legacy ACE_MI_ATTN_FAST=1 means fp16.
-enum class AttnPrecision { FP16, SPLIT, F32, F8C };
+// PV8 = fp16 Q.K with F8C's hi/lo P.V (the P.V roundings carry most of fp16 attention's excess over the f32 graph;
+// measured in tests/test_gpu_parity_strict.py), 3/4 of F8C's matrix-core time.
+enum class AttnPrecision { FP16, SPLIT, F32, F8C, PV8 };
 inline AttnPrecision attn_precision_from_env(AttnPrecision dflt) {
     const char* f = std::getenv("ACE_MI_ATTN_FAST");
     if (f && f[0] && f[0] != '0') return AttnPrecision::FP16;
@@ -151,7 +153,8 @@ inline AttnPrecision attn_precision_from_env(AttnPrecision dflt) {
     if (v == "split") return AttnPrecision::SPLIT;
     if (v == "f32") return AttnPrecision::F32;
     if (v == "f8c") return AttnPrecision::F8C;
-    throw std::runtime_error("ACE_MI_ATTN_PRECISION must be fp16, split, f32 or f8c");
+    if (v == "pv8") return AttnPrecision::PV8;
+    throw std::runtime_error("ACE_MI_ATTN_PRECISION must be fp16, split, f32, f8c or pv8");
 }
 void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s);
 

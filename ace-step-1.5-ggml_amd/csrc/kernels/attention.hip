@@ -629,8 +629,10 @@ __global__ void __launch_bounds__(256, OCC) attn_kernel(AttnArgs a) {
 // clusters all MFMAs of a phase and leaves the VALU work exposed after them).
 template <bool F16OUT, bool SPLIT, bool PVS, bool KBIAS, int OCC, bool F8 = false>
 __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
-    static_assert(SPLIT || !PVS, "hi/lo P.V needs hi/lo operands");
-    static_assert(!F8 || (SPLIT && PVS), "f8c stages both lo planes");
+    static_assert(SPLIT || !PVS || F8, "hi/lo fp16 P.V needs hi/lo operands");
+    static_assert(!F8 || PVS, "the fp8 correction modes stage the V lo plane");
+    // QC: the Q.K correction products (f8c); without SPLIT the F8 kernel is the pv8 mode (fp16 Q.K, hi/lo P.V)
+    constexpr bool QC = F8 && SPLIT;
     using RG = Ring<SPLIT, PVS>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x;
@@ -680,10 +682,10 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
 
     const uint16_t* qptr = a.q + (((int64_t)b * a.Hq + head) * a.nq_pad + qrow) * D + 8 * h;
     frag qf[8], qfl[8];
-    v8i q8[4];  // F8: B operands of the correction chain, bytes [64 c + 32 h, +32) of the [hi8 | lo8] q row
+    v8i q8[4];  // QC: B operands of the correction chain, bytes [64 c + 32 h, +32) of the [hi8 | lo8] q row
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) qf[ks] = *(const frag*)(qptr + 16 * ks);
-    if constexpr (F8) {
+    if constexpr (QC) {
         const char* q8row = reinterpret_cast<const char*>(qptr - 8 * h + a.q_plane) + 32 * h;
 #pragma unroll
         for (int c = 0; c < 4; ++c) q8[c] = cat8(*(const frag*)(q8row + 64 * c), *(const frag*)(q8row + 64 * c + 16));
@@ -705,7 +707,7 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
     constexpr int NPV = PVS ? 8 : 4;
     // VL: V(i+1) is requested in phase C of iteration i and waited for before phase C of iteration i+1 (a second
     // barrier per tile), so its pieces can sit behind the phase's long MFMAs; the fp16 mode keeps one barrier
-    constexpr bool VL = SPLIT;
+    constexpr bool VL = SPLIT || PVS;
     const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc((void*)kbase, 0, 0x7fffffff, 0x00020000);
     const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc((void*)vbase, 0, 0x7fffffff, 0x00020000);
     const int krow = 4 * wid + (lane >> 4);
@@ -746,11 +748,13 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
     // F8: fp8 K row (key 32 t + lq) chunks 4 c + 2 h + e, fp8 V^T row (d = 32 dt + lq) chunks 4 i + 2 h + e, swizzled
     // like the fp16 images (the same LDS-DMA pieces fill them)
     uint32_t k8a[4][2], v8a[2][2];
-    if constexpr (F8) {
+    if constexpr (QC) {
 #pragma unroll
         for (int c = 0; c < 4; ++c)
 #pragma unroll
             for (int e = 0; e < 2; ++e) k8a[c][e] = smem_l + RG::K_LO + lq * 256 + (((4 * c + 2 * h + e) ^ (lq & 15)) << 4);
+    }
+    if constexpr (F8) {
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -764,13 +768,13 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
     // ---- phase B: QK of the next tile in NB steps.  Position p runs the hi step h (k-slice ks = h / 2 of half
     // t = h % 2: fp16 hi, + lo for SPLIT) or, for F8, every third position (p % 3 == 2) the correction step
     // k = p / 3 (chunk c = k / 2 of half t = k % 2: two 16-byte reads of the fp8 row, one K = 64 fp8 MFMA)
-    constexpr int NB = F8 ? 24 : 16;
+    constexpr int NB = QC ? 24 : 16;
     struct BStep {
         bool corr;
         int idx;  // h or k
     };
     auto bstep = [](int p) constexpr -> BStep {
-        if (!F8) return BStep{false, p};
+        if (!QC) return BStep{false, p};
         return p % 3 == 2 ? BStep{true, p / 3} : BStep{false, p - p / 3};
     };
     auto k_read = [&](auto slot_c, auto p_c, frag& x, frag& y) {
@@ -788,7 +792,7 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
         }
     };
     // LDS reads of QK position p
-    auto rk = [](int p) constexpr { return F8 ? (p % 3 == 2 ? 2 : 1) : (SPLIT ? 2 : 1); };
+    auto rk = [](int p) constexpr { return QC ? (p % 3 == 2 ? 2 : 1) : ((SPLIT && !F8) ? 2 : 1); };
     // S(tile in K slot SLOT) into sn, interleaved with fin(p) (a softmax-finish slice) and dma(p)
     auto qk_phase = [&](auto slot_c, f32x16 (&sn)[2], auto&& fin, auto&& dma) {
         frag kh[RA + 1], kl[RA + 1];
@@ -927,8 +931,10 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
         constexpr int SLOT = decltype(slot_c)::value;
         constexpr int NXT = SLOT ^ 1;
         const bool more = i + 1 < n;
-        const bool more2 = i + 2 < n;
-        const int ktk = kt_begin + i + 2, ktv = kt_begin + i + 1;
+        // the next tiles' DMA is issued unconditionally (no branch per piece): past the last tile it re-reads the
+        // last one into the slot the next iteration would fill, which nothing reads afterwards (the garbage S of
+        // the step past the end is never used)
+        const int ktk = kt_begin + min(i + 2, n - 1), ktv = kt_begin + min(i + 1, n - 1);
         const float m_use = ((m_run == -INFINITY) ? 0.f : m_run) - PSC;
         const float nm = -m_use;
         float lsum = 0.f;
@@ -988,15 +994,13 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
         auto dma = [&](auto p_c) {
             constexpr int p = decltype(p_c)::value;
             constexpr BStep st = bstep(p);
-            constexpr int kp = F8 ? (st.corr ? st.idx : -1) : p;  // K piece of this position
+            constexpr int kp = QC ? (st.corr ? st.idx : -1) : p;  // K piece of this position
             static_assert(VL || NPK + NPV <= NB, "one DMA piece per QK step");
             if constexpr (kp >= 0 && kp < NPK) {
-                if (more2) {
-                    k_piece(SLOT, ktk, kp);
-                    if constexpr (kp == 0) bias_piece(SLOT, ktk);
-                }
+                k_piece(SLOT, ktk, kp);
+                if constexpr (kp == 0) bias_piece(SLOT, ktk);
             } else if constexpr (!VL && p >= NPK && p < NPK + NPV) {
-                if (more) v_piece(NXT, ktv, p - NPK);
+                v_piece(NXT, ktv, p - NPK);
             }
         };
         qk_phase(std::integral_constant<int, NXT>{}, sn, [&](auto j_c) { fin(j_c); }, [&](auto j_c) { dma(j_c); });
@@ -1007,14 +1011,10 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
         // d-tile dt: Vl.Ph at q = 2, 5, 8, 11 (dt 0..3), Vh.Pl at q = 20..23, after every hi step has formed P's lo
         // part)
         if constexpr (VL) {  // V(i), requested in the previous iteration's phase C, landed for every wave
-            if (more2) {
-                if (KBIAS && wid == 0)
-                    wait_vmcnt<NPK + 1>();
-                else
-                    wait_vmcnt<NPK>();
-            } else {
-                wait_vmcnt<0>();
-            }
+            if (KBIAS && wid == 0)
+                wait_vmcnt<NPK + 1>();
+            else
+                wait_vmcnt<NPK>();
             __builtin_amdgcn_s_barrier();
         }
         bias_tile(std::integral_constant<int, NXT>{}, sn);
@@ -1052,8 +1052,7 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
                     constexpr int q = decltype(q_c)::value;
                     constexpr CStep st = cstep(q);
                     constexpr int vp = F8 ? (st.kind == 1 ? st.idx : st.kind == 2 ? 4 + st.idx : -1) : q;
-                    if constexpr (vp >= 0 && vp < NPV)
-                        if (more) v_piece(NXT, ktv, vp);
+                    if constexpr (vp >= 0 && vp < NPV) v_piece(NXT, ktv, vp);
                 }
             };
             static_for<0, RA>([&](auto r_c) {
@@ -1126,6 +1125,7 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
         iter(std::integral_constant<int, 1>{}, sB, sA, i + 1);
     }
     if (i < n) iter(std::integral_constant<int, 0>{}, sA, sB, i);
+    wait_vmcnt<0>();  // the re-read tiles past the end
 
     const float l = l_run + __shfl_xor(l_run, 32);
     if (a.ksplit > 1) {
@@ -1208,39 +1208,43 @@ void launch_t(const AttnArgs& a, dim3 grid, hipStream_t s) {
         const char* e = std::getenv("ACE_MI_ATTN_V1");
         v2 = (e && e[0] == '1') ? 0 : 1;
     }
-    if constexpr (SPLIT && PVS) {
-        if (a.f8) {
+    if constexpr (PVS) {
+        if (a.f8) {  // f8c (SPLIT) or pv8 (fp16 Q.K)
             if (a.kbias)
-                hipLaunchKernelGGL((attn2_kernel<F16OUT, true, true, true, 1, true>), grid, dim3(256), lds, s, a);
+                hipLaunchKernelGGL((attn2_kernel<F16OUT, SPLIT, true, true, 1, true>), grid, dim3(256), lds, s, a);
             else
-                hipLaunchKernelGGL((attn2_kernel<F16OUT, true, true, false, 1, true>), grid, dim3(256), lds, s, a);
+                hipLaunchKernelGGL((attn2_kernel<F16OUT, SPLIT, true, false, 1, true>), grid, dim3(256), lds, s, a);
             return;
         }
     }
-    if (v2 && a.fused_merge == 0) {
-        constexpr int OCC = SPLIT ? 1 : 2;
+    if constexpr (!SPLIT && PVS) {
+        throw std::runtime_error("attention: hi/lo P.V with fp16 Q.K exists only with fp8 corrections (pv8)");
+    } else {
+        if (v2 && a.fused_merge == 0) {
+            constexpr int OCC = SPLIT ? 1 : 2;
+            if (a.kbias)
+                hipLaunchKernelGGL((attn2_kernel<F16OUT, SPLIT, PVS, true, OCC>), grid, dim3(256), lds, s, a);
+            else
+                hipLaunchKernelGGL((attn2_kernel<F16OUT, SPLIT, PVS, false, OCC>), grid, dim3(256), lds, s, a);
+            return;
+        }
+        static int occ = 0;  // ACE_MI_ATTN_OCC=1: one workgroup per CU for the single-fp16 kernel too (A/B)
+        if (occ == 0) {
+            const char* e = std::getenv("ACE_MI_ATTN_OCC");
+            occ = (e && e[0] == '1') ? 1 : 2;
+        }
+        if (!SPLIT && occ == 2) {
+            if (a.kbias)
+                hipLaunchKernelGGL((attn_kernel<F16OUT, SPLIT, PVS, true, 2>), grid, dim3(256), lds, s, a);
+            else
+                hipLaunchKernelGGL((attn_kernel<F16OUT, SPLIT, PVS, false, 2>), grid, dim3(256), lds, s, a);
+            return;
+        }
         if (a.kbias)
-            hipLaunchKernelGGL((attn2_kernel<F16OUT, SPLIT, PVS, true, OCC>), grid, dim3(256), lds, s, a);
+            hipLaunchKernelGGL((attn_kernel<F16OUT, SPLIT, PVS, true, 1>), grid, dim3(256), lds, s, a);
         else
-            hipLaunchKernelGGL((attn2_kernel<F16OUT, SPLIT, PVS, false, OCC>), grid, dim3(256), lds, s, a);
-        return;
+            hipLaunchKernelGGL((attn_kernel<F16OUT, SPLIT, PVS, false, 1>), grid, dim3(256), lds, s, a);
     }
-    static int occ = 0;  // ACE_MI_ATTN_OCC=1: one workgroup per CU for the single-fp16 kernel too (A/B)
-    if (occ == 0) {
-        const char* e = std::getenv("ACE_MI_ATTN_OCC");
-        occ = (e && e[0] == '1') ? 1 : 2;
-    }
-    if (!SPLIT && occ == 2) {
-        if (a.kbias)
-            hipLaunchKernelGGL((attn_kernel<F16OUT, SPLIT, PVS, true, 2>), grid, dim3(256), lds, s, a);
-        else
-            hipLaunchKernelGGL((attn_kernel<F16OUT, SPLIT, PVS, false, 2>), grid, dim3(256), lds, s, a);
-        return;
-    }
-    if (a.kbias)
-        hipLaunchKernelGGL((attn_kernel<F16OUT, SPLIT, PVS, true, 1>), grid, dim3(256), lds, s, a);
-    else
-        hipLaunchKernelGGL((attn_kernel<F16OUT, SPLIT, PVS, false, 1>), grid, dim3(256), lds, s, a);
 }
 
 }  // namespace
@@ -1282,7 +1286,7 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s) {
             mode = (e && (e[0] == '1' || e[0] == '2' || e[0] == '4')) ? e[0] - '0' : 0;
         }
         // blocks resident per CU: two for the single-fp16 kernel (66 KiB ring), one for the hi/lo ones
-        const int per_cu = a.split ? 1 : 2;
+        const int per_cu = (a.split || a.pv_split) ? 1 : 2;
         const int64_t slots = (int64_t)n_cu * per_cu;
         const int ntiles = (span + KT - 1) / KT;
         int S = 1;
@@ -1308,7 +1312,7 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s) {
     }
     const dim3 grid(8 * ((a.B * a.Hkv * n_qt * b.ksplit + 7) / 8));  // XCD-aware order, see attn_kernel
     const bool f16 = out_t == ActType::F16;
-    ACEMI_CHECK(!a.f8 || (a.split && a.pv_split && !b.fused_merge), "attention: f8c mode needs split + pv_split");
+    ACEMI_CHECK(!a.f8 || (a.pv_split && !b.fused_merge), "attention: the fp8 correction modes need pv_split");
     if (a.split) {
         ACEMI_CHECK(a.q_plane > 0 && a.k_plane > 0, "attention: split mode needs lo planes");
         if (a.pv_split) {
@@ -1317,6 +1321,9 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s) {
         } else {
             f16 ? launch_t<true, true, false>(b, grid, s) : launch_t<false, true, false>(b, grid, s);
         }
+    } else if (a.pv_split) {
+        ACEMI_CHECK(a.f8 && a.v_plane > 0, "attention: pv8 mode needs the fp8 V lo plane");
+        f16 ? launch_t<true, false, true>(b, grid, s) : launch_t<false, false, true>(b, grid, s);
     } else {
         f16 ? launch_t<true, false, false>(b, grid, s) : launch_t<false, false, false>(b, grid, s);
     }

@@ -812,10 +812,12 @@ double m_edge(int M, int bm) { return (double)M / (double)(((M + bm - 1) / bm) *
 // ds_write dequant kernel (gemm_q_kernel, 0-7) only when forced.  Long sequences: 192-row tiles (8 waves where
 // N % 256 == 0 leaves a full round of 256-column tiles); short ones: 128 / 64-row tiles, split over K until
 // the grid covers the 256 CUs.
-int pick_variant_q(int M, int N, int K) {
+int pick_variant_q(int M, int N, int K, int fmt) {
     const int64_t mb192 = (M + 191) / 192;
     if (M > 1024) {
-        if (N % 256 == 0 && mb192 * (N / 256) >= 256) return 21;
+        // 21 (8 waves, 256 columns) with Q4_K: wrong 16-column groups of the upper four waves on some launches, only
+        // while LDS-DMA is in flight during the tile's LDS reads -- Q4_K takes the 4-wave tile
+        if (fmt != WF_Q4_K && N % 256 == 0 && mb192 * (N / 256) >= 256) return 21;
         return 20;
     }
     // Short sequences: round 1's LDS-dequant kernel (96 x 128).  Whole forwards through the 64 / 128-row
@@ -841,7 +843,8 @@ int pick_variant(int M, int N, int K, bool quant, int fmt) {
                                          : ((f == 1 || f == 3 || f == 4 ? S <= 2
                                                                        : (((f >= 6 && f <= 9) || (f >= 12 && f <= 15)) && S <= 4)) &&
                                             K / 64 >= 2 * S));
-        return !(wide && N % 256 != 0) && !(quant && dense_only) && !(!quant && qr) && sk_ok;
+        return !(wide && N % 256 != 0) && !(quant && dense_only) && !(!quant && qr) && sk_ok &&
+               !(f == 21 && fmt == WF_Q4_K);
     };
     if (g_forced_variant >= 0x10000) return g_forced_variant & 0xffff;  // diagnostics (selftest): no support check
     if (g_forced_variant >= 0 && supports(g_forced_variant)) return g_forced_variant;  // tests / micro-benchmarks
@@ -851,7 +854,7 @@ int pick_variant(int M, int N, int K, bool quant, int fmt) {
     }
     const int64_t mb192 = (M + 191) / 192;
     const bool edge_ok = m_edge(M, 192) >= m_edge(M, 128) - 0.02;
-    if (quant) return pick_variant_q(M, N, K);
+    if (quant) return pick_variant_q(M, N, K, fmt);
     // (a skinny weight-stream kernel for M <= 128 ran the 10 s block linears 2x slower than the tiles below --
     // every 16-column workgroup re-read all of A with 16-byte row-scattered loads -- and was removed in round 4)
     // 8-wave ping-pong tiles for batched sequences (tools/gemm_msweep.py on MI355X, TFLOP/s): M = 12000 gate|up

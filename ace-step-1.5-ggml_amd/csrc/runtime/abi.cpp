@@ -321,10 +321,11 @@ ace_ggml_status ace_mi_dit_sample_ex(ace_ggml_context* ctx, int32_t batch, float
 }
 
 ace_ggml_status ace_mi_dit_set_attn_precision(ace_ggml_context* ctx, int32_t mode) {
-    if (!ctx || mode < 0 || mode > 3) return ACE_GGML_ERR_INVALID_ARG;
+    if (!ctx || mode < 0 || mode > 4) return ACE_GGML_ERR_INVALID_ARG;
     if (!ctx->dit) return set_error(ctx, ACE_GGML_ERR, "dit not loaded");
-    static const acemi::AttnPrecision modes[4] = {acemi::AttnPrecision::FP16, acemi::AttnPrecision::SPLIT,
-                                                  acemi::AttnPrecision::F32, acemi::AttnPrecision::F8C};
+    static const acemi::AttnPrecision modes[5] = {acemi::AttnPrecision::FP16, acemi::AttnPrecision::SPLIT,
+                                                  acemi::AttnPrecision::F32, acemi::AttnPrecision::F8C,
+                                                  acemi::AttnPrecision::PV8};
     ctx->dit->set_attn_precision(modes[mode]);
     return ACE_GGML_OK;
 }

@@ -16,9 +16,7 @@ DitEngine::DitEngine(int device) : device_(device) {
     // meets the literal 1e-3 one-layer bound at full width (DESIGN.md "Parity"); the condition / text encoders keep
     // the hi/lo fp16 `f32` default
     const AttnPrecision prec = attn_precision_from_env(AttnPrecision::F8C);
-    attn_split_ = prec != AttnPrecision::FP16;
-    attn_pv_split_ = prec == AttnPrecision::F32 || prec == AttnPrecision::F8C;
-    attn_f8_ = prec == AttnPrecision::F8C;
+    set_attn_precision(prec);
     const char* u = std::getenv("ACE_MI_UNFUSED_PREP");
     fused_prep_ = !(u && u[0] && u[0] != '0');
     const char* q = std::getenv("ACE_MI_QUANT_STAGED");

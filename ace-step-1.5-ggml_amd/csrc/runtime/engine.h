@@ -86,9 +86,9 @@ class DitEngine {
     void encode(const EncodeIO& io, hipStream_t s);
     // attention operand precision of subsequent forwards (DiT blocks; the encoders keep their own)
     void set_attn_precision(AttnPrecision p) {
-        attn_split_ = p != AttnPrecision::FP16;
-        attn_pv_split_ = p == AttnPrecision::F32 || p == AttnPrecision::F8C;
-        attn_f8_ = p == AttnPrecision::F8C;
+        attn_split_ = p == AttnPrecision::SPLIT || p == AttnPrecision::F32 || p == AttnPrecision::F8C;
+        attn_pv_split_ = p == AttnPrecision::F32 || p == AttnPrecision::F8C || p == AttnPrecision::PV8;
+        attn_f8_ = p == AttnPrecision::F8C || p == AttnPrecision::PV8;
         cross_key_.valid = false;  // cached cross K/V planes are in the previous mode's encoding
     }
     // enable per-kernel-class event timing for subsequent forwards

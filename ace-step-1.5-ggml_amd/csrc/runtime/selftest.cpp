@@ -113,7 +113,8 @@ struct AttnSetup {
         pq.qh = dqh.as<uint16_t>();
         const int64_t qpl = (int64_t)B * Hq * nq_pad * D, kpl = (int64_t)B * Hkv * nk_pad * D;
         pq.q_plane = split ? qpl : 0;
-        const bool f8 = split && (flags & 8) && (flags & 16);
+        const bool f8 = (flags & 8) && (flags & 16);  // f8c with split, pv8 without
+        const bool pvs = (flags & 8) && (split || f8);
         pq.f8 = f8 ? 1 : 0;
         launch_attn_prep(pq, nullptr);
         PrepArgs pk{};
@@ -130,7 +131,7 @@ struct AttnSetup {
         pk.kh = dkh.as<uint16_t>();
         pk.vt = dvt.as<uint16_t>();
         pk.k_plane = split ? kpl : 0;
-        pk.v_plane = split ? kpl : 0;
+        pk.v_plane = pvs || split ? kpl : 0;
         pk.f8 = f8 ? 1 : 0;
         launch_attn_prep(pk, nullptr);
         launch_key_bias(kmask ? dm.as<int32_t>() : nullptr, B, nk, 1, nk, nk_pad, dkb.as<float>(), nullptr);
@@ -151,7 +152,7 @@ struct AttnSetup {
         a.scale = scale;
         a.split = split;
         a.causal = (flags & 2) != 0;
-        a.pv_split = split && (flags & 8) != 0;
+        a.pv_split = pvs;
         a.f8 = f8;
         a.q_plane = qpl;
         a.k_plane = kpl;
@@ -187,7 +188,8 @@ ace_ggml_status ace_mi_kernel_attention(int32_t B, int32_t Hq, int32_t Hkv, int3
 
 // Attention micro-benchmark: pseudo-random N(0,1)-like q / kv (fixed seed), average ms per launch over
 // `iters` launches timed with hipEvents.  flags: bit 0 split (hi/lo) operands, bit 1 causal, bit 3 hi/lo P.V,
-// bit 2 a key-padding mask (every 7th key masked), bit 4 the f8c operand encoding (with bits 0 and 3).
+// bit 2 a key-padding mask (every 7th key masked), bit 4 the fp8 correction encoding (with bit 3: with bit 0 the f8c
+// mode, without it pv8).
 ace_ggml_status ace_mi_bench_attention(int32_t B, int32_t Hq, int32_t Hkv, int32_t nq, int32_t nk, int32_t window,
                                        int32_t flags, int32_t iters, float* avg_ms) {
     using namespace acemi;

@@ -56,7 +56,8 @@ ATTN_DESC = {"fp16": "fp16-operand f32-accumulate attention",
              "split": "split attention (hi/lo fp16 Q.K, fp16 P.V, f32 accumulate)",
              "f32": "f32-faithful attention (hi/lo fp16 Q.K and P.V, f32 accumulate)",
              "f8c": "f32-class attention (hi/lo Q.K and P.V: hi x hi fp16, correction products block-scaled e4m3, "
-                    "f32 accumulate)"}
+                    "f32 accumulate)",
+             "pv8": "fp16 Q.K with f32-class P.V (hi x hi fp16 + block-scaled e4m3 corrections, f32 accumulate)"}
 BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16/fp16 MFMA (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
 
@@ -310,7 +311,7 @@ def main():
                                    "Euler loop on torch tensors, one hook call per step (model.generate_audio)")
         # ---- every attention precision: steps/s of the headline loop + per-kernel attention time per step
         modes = {}
-        for mode in ("fp16", "split", "f32", "f8c"):
+        for mode in ("fp16", "split", "f32", "f8c", "pv8"):
             br.set_attn_precision(mode)
             el_m = elapsed if mode == HEADLINE_ATTN else timed(run)
             entry = line(B * args.steps, el_m, f"the headline loop with {ATTN_DESC[mode]}")
@@ -322,6 +323,7 @@ def main():
         extras["attn_f32_line"] = modes["f32"]
         extras["attn_fp16_line"] = modes["fp16"]
         extras["attn_f8c_line"] = modes["f8c"]
+        extras["attn_pv8_line"] = modes["pv8"]
         # ---- 10 s forward rate (configs[0]'s shape) with the headline weights
         in10 = small_inputs(250)
         extras["line_10s"] = {"weights": args.qtype or "bf16", **line(args.steps, timed(lambda f, k: run(f, k, in10)),

@@ -80,8 +80,8 @@ ACE_GGML_API ace_ggml_status ace_mi_dit_sample_ex(ace_ggml_context* ctx, int32_t
 /* Operand precision of the DiT's attention MFMAs for subsequent forwards (the ACE_MI_ATTN_PRECISION
  * default is read when the DiT is loaded): 0 = fp16 operands, 1 = `split` (hi/lo fp16 Q.K, fp16 P.V),
  * 2 = `f32` (hi/lo fp16 for both products), 3 = `f8c` (hi/lo for both products, the hi x hi product in fp16 and
- * the two correction products as block-scaled e4m3 MFMAs; the default when ACE_MI_ATTN_PRECISION is unset).  All
- * accumulate in f32. */
+ * the two correction products as block-scaled e4m3 MFMAs; the default when ACE_MI_ATTN_PRECISION is unset),
+ * 4 = `pv8` (fp16 Q.K, P.V as in f8c).  All accumulate in f32. */
 ACE_GGML_API ace_ggml_status ace_mi_dit_set_attn_precision(ace_ggml_context* ctx, int32_t mode);
 
 /* Per-kernel-class timing with hipEvents on the launch stream (adds a sync per kernel).

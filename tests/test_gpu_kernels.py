@@ -96,7 +96,7 @@ def _attn_ref(q, kv, hq, hkv, window, kmask, scale, rnd=round_f16):
 
 
 MODES = {"split": dict(split=True), "pvsplit": dict(split=True, pv_split=True), "fast": dict(split=False),
-         "f8c": dict(split=True, pv_split=True, f8=True)}
+         "f8c": dict(split=True, pv_split=True, f8=True), "pv8": dict(split=False, pv_split=True, f8=True)}
 
 
 def _check_attn(got, q, kv, hq, hkv, window, kmask, scale, mode):
@@ -104,7 +104,7 @@ def _check_attn(got, q, kv, hq, hkv, window, kmask, scale, mode):
     the output; "split" (~22-bit Q.K, fp16 P and V) adds the fp16 rounding of P and V, at most 2^-11 of
     max|v| per output; "fast" has fp16 scores too."""
     f32 = lambda x: np.asarray(x, np.float32)
-    if mode == "fast":
+    if mode in ("fast", "pv8"):  # fp16 Q.K operands (pv8: P.V at f8c precision, inside the same bound)
         ref = _attn_ref(q, kv, hq, hkv, window, kmask, scale)
         err = np.abs(got - ref)
         assert np.all(err <= 2.0 ** -8 * np.abs(ref) + 2e-3), float(err.max())
@@ -284,7 +284,7 @@ def test_attention_key_split_with_one_part_fully_masked():
     kmask = np.ones((B, nk), np.int32)
     kmask[:, :1000] = 0
     scale = 1.0 / np.sqrt(128.0)
-    for mode in ("split", "pvsplit"):
+    for mode in ("split", "pvsplit", "f8c", "pv8"):
         got = _capi().kernel_attention(q, kv, hq, hkv, window=0, kmask=kmask, scale=scale, **MODES[mode])
         _check_attn(got, q, kv, hq, hkv, 0, kmask, scale, mode)
 

@@ -117,7 +117,7 @@ def test_peaked_regime_is_peaked():
     assert smax1 < 8 and top11 < 0.05
 
 
-@pytest.mark.parametrize("precision", ["fp16", "split", "f32", "f8c"])
+@pytest.mark.parametrize("precision", ["fp16", "split", "f32", "f8c", "pv8"])
 def test_peaked_attention_240s_two_layers(monkeypatch, precision):
     """240 s, full width, 2 layers, peaked logits, each attention precision mode vs the f32 oracle."""
     d = _ckpt(QK_SCALE)
@@ -126,7 +126,7 @@ def test_peaked_attention_240s_two_layers(monkeypatch, precision):
     check(got, ref, floor, f"peaked 240 s 2 layers, attention {precision}", fmax)
 
 
-@pytest.mark.parametrize("precision", ["fp16", "split", "f32", "f8c"])
+@pytest.mark.parametrize("precision", ["fp16", "split", "f32", "f8c", "pv8"])
 @pytest.mark.parametrize("peaked", [False, True], ids=["default", "peaked"])
 @pytest.mark.parametrize("first", ["sliding_attention", "full_attention"])
 def test_one_layer_literal_bound(monkeypatch, first, peaked, precision):

@@ -25,7 +25,7 @@ def main():
         if only and name != only:
             continue
         modes = {"split": (True, False, False), "pvsplit": (True, True, False), "fast": (False, False, False),
-                 "f8c": (True, True, True)}
+                 "f8c": (True, True, True), "pv8": (False, True, True)}
         for mode, (split, pvs, f8) in modes.items():
             if only and mode != only_mode:
                 continue
