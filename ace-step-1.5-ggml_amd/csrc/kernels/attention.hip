@@ -107,6 +107,12 @@ constexpr float PSCALE_F8_LOG2 = 5.0f;  // f8c: P <= 2^(5 + RESCALE_LOG2) = 256,
 #define ACEMI_ATTN_RA 2
 #endif
 constexpr int RA = ACEMI_ATTN_RA;
+// Diagnostic ablation (A/B builds only, tools/build_ab.sh; results wrong by design): 1 = no next-tile LDS-DMA inside
+// the attn2 pipeline (every tile computes on the prologue's K / V), 2 = no exp2 / packing VALU of the softmax finish
+#ifndef ACEMI_ATTN_ABLATE
+#define ACEMI_ATTN_ABLATE 0
+#endif
+constexpr int kAttnAblate = ACEMI_ATTN_ABLATE;
 static_assert(RA >= 1 && 2 * RA <= 15, "lgkmcnt counts at most 15 outstanding reads");
 // LDS reads issued after step p's own, i.e. those of steps p+1 .. p+RA (< n), for the counted lgkmcnt of step p
 template <class F>
@@ -996,7 +1002,8 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
             constexpr BStep st = bstep(p);
             constexpr int kp = QC ? (st.corr ? st.idx : -1) : p;  // K piece of this position
             static_assert(VL || NPK + NPV <= NB, "one DMA piece per QK step");
-            if constexpr (kp >= 0 && kp < NPK) {
+            if constexpr (kAttnAblate & 1) {
+            } else if constexpr (kp >= 0 && kp < NPK) {
                 k_piece(SLOT, ktk, kp);
                 if constexpr (kp == 0) bias_piece(SLOT, ktk);
             } else if constexpr (!VL && p >= NPK && p < NPK + NPV) {
@@ -1052,7 +1059,7 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
                     constexpr int q = decltype(q_c)::value;
                     constexpr CStep st = cstep(q);
                     constexpr int vp = F8 ? (st.kind == 1 ? st.idx : st.kind == 2 ? 4 + st.idx : -1) : q;
-                    if constexpr (vp >= 0 && vp < NPV) v_piece(NXT, ktv, vp);
+                    if constexpr (vp >= 0 && vp < NPV && !(kAttnAblate & 1)) v_piece(NXT, ktv, vp);
                 }
             };
             static_for<0, RA>([&](auto r_c) {

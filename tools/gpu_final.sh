@@ -1,5 +1,5 @@
 #!/bin/bash
-# GPU box (round 4): the driver's bench command, then the rocprofv3 kernel-trace summary of a short run of the same
+# GPU box: the driver's bench command, then the rocprofv3 kernel-trace summary of a short run of the same
 # workload, then the HBM-traffic PMC passes (FETCH_SIZE, WRITE_SIZE; separate counter-only runs).
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/final; export TMPDIR=/tmp
 timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 > gpurun_out/final/bench.json 2> gpurun_out/final/bench.err || exit $?
