@@ -101,18 +101,6 @@ struct ReadRows<N, N, STRIDE> {
     __device__ __forceinline__ static void run(uint32_t, uint4 (&)[N][2], int) {}
 };
 
-// LDS-DMA of SIZE (16 or 4) bytes per lane as a buffer load: base + voff (per lane) + soff (uniform) -> LDS at `lds`
-// (+ 16 / 4 bytes per lane).  A __device__ helper on purpose: building the buffer descriptor in the kernel body itself
-// (gemm_qr_kernel) made hipcc's host-side compile drop the kernels' launch stubs (ROCm 7.2).
-template <int SIZE>
-__device__ __forceinline__ void buf_lds(const void* base, void* lds, int voff, int soff) {
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
-    if constexpr (SIZE == 16)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)lds, 16, voff, soff, 0, 0);
-    else
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)lds, 4, voff, soff, 0, 0);
-}
-
 // s_waitcnt vmcnt(N) with N a compile-time constant (lgkmcnt/expcnt untouched)
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {

@@ -4,10 +4,6 @@
 // dequant arithmetic is ggml's (dequantize_row_q8_0 / _q4_K / _q6_K: one f32 product, RNE to bf16).
 #include "gemm_common.h"
 
-#ifndef ACEMI_QR_DIAG
-#define ACEMI_QR_DIAG 0
-#endif
-
 namespace acemi {
 namespace gemm_detail {
 
@@ -368,14 +364,8 @@ __device__ __forceinline__ void qd_read(uint32_t wq, uint32_t ws, int row, int g
     for (int j = 0; j < 2; ++j) {
         const uint32_t qa = wq + (row + j * 16) * QB, sa = ws + (row + j * 16) * SB;
         if constexpr (WQ == WF_Q4_K) {
-#if ACEMI_QR_DIAG & 2  // (diagnostic A/B build: the q bytes by ds_read_b64, as Q8_0 / Q6_K read theirs)
-            const uint2 q0 = ds_read_b64_off<0>(qa + (g & 2) * 4), q1 = ds_read_b64_off<16>(qa + (g & 2) * 4);
-            r.q[j][0][0] = (g & 1) ? q0.y : q0.x;
-            r.q[j][1][0] = (g & 1) ? q1.y : q1.x;
-#else
             r.q[j][0][0] = ds_read_b32_off<0>(qa + g * 4);
             r.q[j][1][0] = ds_read_b32_off<16>(qa + g * 4);
-#endif
             r.sc[j] = ds_read_b128_off<0>(sa);
         } else {
             const uint2 q0 = ds_read_b64_off<0>(qa + g * 8), q1 = ds_read_b64_off<32>(qa + g * 8);
@@ -458,53 +448,46 @@ __global__ void __launch_bounds__(NW * 64, (!SK && (NW == 8 || 2 * 3 * (BM * 128
     const int kt_begin = sk_part * nk_all / S;
     const int nk = (sk_part + 1) * nk_all / S - kt_begin;
 
-    // LDS-DMA sources as buffer loads: a per-lane byte offset fixed for the whole k loop (one VGPR per piece, never
-    // rewritten) + the k-tile's byte offset in an SGPR.  (Round 3's per-piece 64-bit addresses were rebuilt in one
-    // VGPR pair right after each global_load_lds issue; with Q4_K's piece mix on the 8-wave tile the last scale piece
-    // had its address pair overwritten two instructions after issue and lanes 48-63 of that piece -- scale rows
-    // 16 w + 12..15 of the tile's upper 128 columns -- landed wrong: variant 21's "wrong columns")
-    // A pieces: the swizzled chunk as the dense kernel; W q pieces: QB / 16 lanes per row; scale pieces: one f32
-    // per lane, SB / 4 per row.
-    const int qrow_bytes = WQ == WF_Q4_K ? K / 2 : K;
-    const int srow_floats = WQ == WF_Q8_0 ? K / 32 : K / 16;
-    int voA[PA / NW], voQ[PQ / NW], voS[PS / NW];
+    // LDS-DMA sources, fixed over k (+ kt * k-tile stride): A pieces (swizzled chunk as the dense kernel), W q
+    // pieces (QB / 16 lanes per row), W scale pieces (one f32 per lane, SB / 4 per row)
+    const uint16_t* srcA[PA / NW];
 #pragma unroll
     for (int j = 0; j < PA / NW; ++j) {
         const int row = (wid + NW * j) * 8 + (lane >> 3);
         const int c = (lane & 7) ^ swz(row);
-        voA[j] = (int)(((int64_t)min(m0 + row, M - 1) * p.lda + (int64_t)kt_begin * BK + c * 8) * 2);
+        srcA[j] = p.A + (int64_t)min(m0 + row, M - 1) * p.lda + (int64_t)kt_begin * BK + c * 8;
     }
+    const int qrow_bytes = WQ == WF_Q4_K ? K / 2 : K;
+    const int srow_floats = WQ == WF_Q8_0 ? K / 32 : K / 16;
+    const char* srcQ[PQ / NW];
 #pragma unroll
     for (int j = 0; j < PQ / NW; ++j) {
-        constexpr int LPR = QB / 16;
+        constexpr int LPR = QB / 16;  // lanes per row
         const int e = (wid + NW * j) * 64 + lane;
-        voQ[j] = (int)((int64_t)(n0 + e / LPR) * qrow_bytes + (int64_t)kt_begin * QB + (e % LPR) * 16);
+        srcQ[j] = static_cast<const char*>(p.Wq) + (int64_t)(n0 + e / LPR) * qrow_bytes + (int64_t)kt_begin * QB +
+                  (e % LPR) * 16;
     }
+    const float* srcS[PS / NW];
 #pragma unroll
     for (int j = 0; j < PS / NW; ++j) {
-        constexpr int FPR = SB / 4;
+        constexpr int FPR = SB / 4;  // floats per row
         const int e = (wid + NW * j) * 64 + lane;
-        voS[j] = (int)(((int64_t)(n0 + e / FPR) * srow_floats + (int64_t)kt_begin * FPR + (e % FPR)) * 4);
+        srcS[j] = p.Ws + (int64_t)(n0 + e / FPR) * srow_floats + (int64_t)kt_begin * FPR + (e % FPR);
     }
     auto stage = [&](int kt, int slot) {  // k-tile kt (relative) into ring slot `slot`
         char* base = smem + slot * SLOT;
-#if ACEMI_QR_DIAG & 4  // (diagnostic A/B build: scale pieces first, A pieces last)
+#pragma unroll
+        for (int j = 0; j < PA / NW; ++j)
+            __builtin_amdgcn_global_load_lds((const void*)(srcA[j] + kt * BK), (lds_void*)(base + (wid + NW * j) * 1024),
+                                             16, 0, 0);
+#pragma unroll
+        for (int j = 0; j < PQ / NW; ++j)
+            __builtin_amdgcn_global_load_lds((const void*)(srcQ[j] + (int64_t)kt * QB),
+                                             (lds_void*)(base + A_BYTES + (wid + NW * j) * 1024), 16, 0, 0);
 #pragma unroll
         for (int j = 0; j < PS / NW; ++j)
-            buf_lds<4>(p.Ws, base + A_BYTES + WQ_BYTES + (wid + NW * j) * 256, voS[j], kt * SB);
-#pragma unroll
-        for (int j = 0; j < PQ / NW; ++j) buf_lds<16>(p.Wq, base + A_BYTES + (wid + NW * j) * 1024, voQ[j], kt * QB);
-#pragma unroll
-        for (int j = 0; j < PA / NW; ++j) buf_lds<16>(p.A, base + (wid + NW * j) * 1024, voA[j], kt * BK * 2);
-#else
-#pragma unroll
-        for (int j = 0; j < PA / NW; ++j) buf_lds<16>(p.A, base + (wid + NW * j) * 1024, voA[j], kt * BK * 2);
-#pragma unroll
-        for (int j = 0; j < PQ / NW; ++j) buf_lds<16>(p.Wq, base + A_BYTES + (wid + NW * j) * 1024, voQ[j], kt * QB);
-#pragma unroll
-        for (int j = 0; j < PS / NW; ++j)
-            buf_lds<4>(p.Ws, base + A_BYTES + WQ_BYTES + (wid + NW * j) * 256, voS[j], kt * SB);
-#endif
+            __builtin_amdgcn_global_load_lds((const void*)(srcS[j] + kt * (SB / 4)),
+                                             (lds_void*)(base + A_BYTES + WQ_BYTES + (wid + NW * j) * 256), 4, 0, 0);
     };
 
     f32x4 acc[TM][TN];
@@ -523,15 +506,9 @@ __global__ void __launch_bounds__(NW * 64, (!SK && (NW == 8 || 2 * 3 * (BM * 128
     stage(0, 0);
     stage(min(1, nk - 1), 1);
     for (int kt = 0; kt < nk; ++kt) {
-#if ACEMI_QR_DIAG & 1  // (diagnostic A/B build: no LDS-DMA in flight while any wave reads LDS)
-        wait_vmcnt<0>();
-#else
         wait_vmcnt<G>();
-#endif
         __builtin_amdgcn_s_barrier();  // every wave's pieces of tile kt landed; slot (kt+2)%3 = (kt-1)%3 is free
-#if !(ACEMI_QR_DIAG & 1)
         stage(min(kt + 2, nk - 1), (kt + 2) % 3);
-#endif
         // W bytes and the kk = 0 A fragments in one LDS wait; the kk = 1 A reads are issued before the kk = 0
         // MFMAs, and the kk = 1 dequant VALU sits between those MFMAs (no scheduling barrier in between), so the
         // dequant of the second k half overlaps matrix work
@@ -554,10 +531,6 @@ __global__ void __launch_bounds__(NW * 64, (!SK && (NW == 8 || 2 * 3 * (BM * 128
         for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<false>(a1[i][1], b[j][1], acc[i][j]);
-#if ACEMI_QR_DIAG & 1
-        __builtin_amdgcn_s_barrier();  // every wave's reads of tile kt done (lgkmcnt(0) above)
-        stage(min(kt + 2, nk - 1), (kt + 2) % 3);
-#endif
     }
     wait_vmcnt<0>();  // the dummy stages past the end land before the epilogue reuses the ring
     __syncthreads();  // LDS reads done before the epilogue reuses the ring
@@ -602,9 +575,6 @@ template <int BM, int NW, int EPI, int WQ>
 void launch_qr_cfg(GemmParams p, int S, hipStream_t s) {
     constexpr int BN = 32 * NW;
     if (p.N % BN != 0) throw std::runtime_error("gemm: quantized tile needs N % (32 * waves) == 0");
-    // the staging's buffer loads take 32-bit byte offsets inside a 2 GiB record range
-    if ((int64_t)p.M * p.lda * 2 >= (int64_t)1 << 31 || (int64_t)p.N * p.K * 2 >= (int64_t)1 << 31)
-        throw std::runtime_error("gemm: quantized GEMM operands beyond 2 GiB");
     const int nbm = (p.M + BM - 1) / BM;
     const int nbn = p.N / BN;
     if (S > 1) {
