@@ -108,7 +108,8 @@ constexpr float PSCALE_F8_LOG2 = 5.0f;  // f8c: P <= 2^(5 + RESCALE_LOG2) = 256,
 #endif
 constexpr int RA = ACEMI_ATTN_RA;
 // Diagnostic ablation (A/B builds only, tools/build_ab.sh; results wrong by design): 1 = no next-tile LDS-DMA inside
-// the attn2 pipeline (every tile computes on the prologue's K / V), 2 = no exp2 / packing VALU of the softmax finish
+// the attn2 pipeline (every tile computes on the prologue's K / V), 2 = no exp2 in the softmax finish (P = the raw
+// score), 4 = no P lo formation in phase C (f8c / pv8)
 #ifndef ACEMI_ATTN_ABLATE
 #define ACEMI_ATTN_ABLATE 0
 #endif
@@ -770,6 +771,7 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
     constexpr float PSC = F8 ? PSCALE_F8_LOG2 : PSCALE_LOG2;
 
     const float c_log2 = a.scale * 1.4426950408889634f;
+    const float one_rt = a.scale / a.scale;  // exactly 1 (scale > 0), opaque to the compiler: see plo
 
     // ---- phase B: QK of the next tile in NB steps.  Position p runs the hi step h (k-slice ks = h / 2 of half
     // t = h % 2: fp16 hi, + lo for SPLIT) or, for F8, every third position (p % 3 == 2) the correction step
@@ -948,13 +950,40 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
         uint32_t ph8[8] = {}, pl8[8] = {};  // F8: fp8 P (hi) and P - f16(P) (lo), byte c = 16 t + r of the lane's keys
         // softmax finish of tile i at QK position p: pair j (elements 2j, 2j + 1 of the flattened [t][r] scores) =
         // the position's hi step
+        // fp8 lo part of P pair j: P - f16(P) (exact in f32), as one mixed-precision FMA per value: fma(-f16, one, P)
+        // with a run-time 1.0 (hipcc folds a literal 1 into a v_cvt_f32_f16 + v_sub pair, and an inline-asm
+        // v_fma_mix_f32 costs an s_nop per use: the hazard recognizer cannot see into it)
+        auto plo = [&](auto j_c) {
+            constexpr int j = decltype(j_c)::value;
+            constexpr int t = j >> 3, r = 2 * (j & 7);
+            constexpr int fi = 2 * t + (r >> 3), fj = (r & 7) >> 1;
+            int w8 = (int)pl8[j >> 1];
+            typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+            const h2v hv = __builtin_bit_cast(h2v, (uint32_t)pf[fi][fj]);
+            const float l0 = __builtin_fmaf(-(float)hv[0], one_rt, sc[t][r]);
+            const float l1 = __builtin_fmaf(-(float)hv[1], one_rt, sc[t][r + 1]);
+            w8 = __builtin_amdgcn_cvt_pk_fp8_f32(l0, l1, w8, (j & 1) != 0);
+            asm volatile("" : "+v"(w8));
+            pl8[j >> 1] = (uint32_t)w8;
+        };
+        // PLO_B (f8c): P's lo parts are formed on phase B's correction steps (64-cycle MFMAs with spare issue slots),
+        // pairs 2k and 2k + 1 on correction step k, right after the two hi steps that formed their P; otherwise on
+        // phase C's hi steps (measured: the P-lo VALU on phase C's 32-cycle steps cost 12 % of the f8c kernel)
+        constexpr bool PLO_B = QC && !(kAttnAblate & 4);
         auto fin = [&](auto p_c) {
             constexpr BStep st = bstep(decltype(p_c)::value);
             constexpr int j = st.idx;
+            if constexpr (st.corr && PLO_B) {
+                plo(std::integral_constant<int, 2 * j>{});
+                plo(std::integral_constant<int, 2 * j + 1>{});
+            }
             if constexpr (!st.corr) {
                 constexpr int t = j >> 3, r = 2 * (j & 7);
                 float p0, p1;
-                if constexpr (KBIAS) {
+                if constexpr (kAttnAblate & 2) {
+                    p0 = sc[t][r];
+                    p1 = sc[t][r + 1];
+                } else if constexpr (KBIAS) {
                     p0 = __builtin_amdgcn_exp2f(sc[t][r] + nm);
                     p1 = __builtin_amdgcn_exp2f(sc[t][r + 1] + nm);
                 } else {
@@ -1087,22 +1116,7 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
                     constexpr int t = j >> 3, r = 2 * (j & 7);
                     mr = fmaxf(mr, fmaxf(sn[t][r], sn[t][r + 1]));
                     asm volatile("" : "+v"(mr));
-                    if constexpr (F8) {  // fp8 lo part of P pair j: P - f16(P) (exact in f32)
-                        constexpr int fi = 2 * t + (r >> 3), fj = (r & 7) >> 1;
-                        int w8 = (int)pl8[j >> 1];
-                        // P - f16(P) as one mixed-precision FMA per value (v_fma_mix_f32 reads the f16 half in-op;
-                        // hipcc otherwise emits a v_cvt_f32_f16 + v_sub pair)
-                        const uint32_t hw = (uint32_t)pf[fi][fj];
-                        float l0, l1;
-                        asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(l0) : "v"(hw), "v"(sc[t][r]));
-                        asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
-                            : "=v"(l1)
-                            : "v"(hw), "v"(sc[t][r + 1]));
-                        w8 = __builtin_amdgcn_cvt_pk_fp8_f32(l0, l1, w8,
-                                                             (j & 1) != 0);
-                        asm volatile("" : "+v"(w8));
-                        pl8[j >> 1] = (uint32_t)w8;
-                    }
+                    if constexpr (F8 && !PLO_B && !(kAttnAblate & 4)) plo(std::integral_constant<int, j>{});
                 } else {
                     constexpr int dt = st.idx;
                     const v8i pb = st.kind == 1 ? cat8(ph8) : cat8(pl8);

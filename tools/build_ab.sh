@@ -7,7 +7,7 @@ set -e
 name=$1; flags=$2; shift 2
 root=$(cd "$(dirname "$0")/.." && pwd)
 src=$root/ace-step-1.5-ggml_amd/csrc; bld=$root/ace-step-1.5-ggml_amd/build; out=$root/ace-step-1.5-ggml_amd/acestep_mi355x/lib/ab
-make -C "$src" -j8 >/dev/null
+make -C "$src" -j8 >/dev/null  # (run the A/B builds one at a time: concurrent runs race on the regular objects)
 mkdir -p "$bld/ab_$name" "$out"
 objs=()
 for k in gemm gemm_q attention ops vae; do
