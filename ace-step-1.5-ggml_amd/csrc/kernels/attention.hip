@@ -109,7 +109,8 @@ constexpr float PSCALE_F8_LOG2 = 5.0f;  // f8c: P <= 2^(5 + RESCALE_LOG2) = 256,
 constexpr int RA = ACEMI_ATTN_RA;
 // Diagnostic ablation (A/B builds only, tools/build_ab.sh; results wrong by design): 1 = no next-tile LDS-DMA inside
 // the attn2 pipeline (every tile computes on the prologue's K / V), 2 = no exp2 in the softmax finish (P = the raw
-// score), 4 = no P lo formation in phase C (f8c / pv8)
+// score), 4 = no P lo formation in phase C (f8c / pv8), 8 = no workgroup barrier inside the tile loop, 16 = no wait
+// for the fragment reads before each step's MFMAs (the MFMAs read whatever the registers hold)
 #ifndef ACEMI_ATTN_ABLATE
 #define ACEMI_ATTN_ABLATE 0
 #endif
@@ -815,7 +816,7 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
             if constexpr (p + RA < NB)
                 k_read(slot_c, std::integral_constant<int, p + RA>{}, kh[(p + RA) % (RA + 1)], kl[(p + RA) % (RA + 1)]);
             constexpr int after = reads_after(p, NB, rk);
-            asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(after) : "memory");
+            if constexpr (!(kAttnAblate & 16)) asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(after) : "memory");
             asm volatile("" : "+v"(kh[p % (RA + 1)]));
             if constexpr (rk(p) == 2) asm volatile("" : "+v"(kl[p % (RA + 1)]));
             if constexpr (st.corr) {
@@ -1051,7 +1052,7 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
                 wait_vmcnt<NPK + 1>();
             else
                 wait_vmcnt<NPK>();
-            __builtin_amdgcn_s_barrier();
+            if constexpr (!(kAttnAblate & 8)) __builtin_amdgcn_s_barrier();
         }
         bias_tile(std::integral_constant<int, NXT>{}, sn);
         mask_tile(sn, i + 1);
@@ -1101,7 +1102,7 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
                 if constexpr (q + RA < NC)
                     v_read(std::integral_constant<int, q + RA>{}, vh[(q + RA) % (RA + 1)], vl[(q + RA) % (RA + 1)]);
                 constexpr int after = reads_after(q, NC, rv);
-                asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(after) : "memory");
+                if constexpr (!(kAttnAblate & 16)) asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(after) : "memory");
                 asm volatile("" : "+v"(vh[q % (RA + 1)]));
                 if constexpr (rv(q) == 2) asm volatile("" : "+v"(vl[q % (RA + 1)]));
                 if constexpr (st.kind == 0) {
@@ -1136,7 +1137,7 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
                 wait_vmcnt<NPV>();
             else
                 wait_vmcnt<0>();
-            __builtin_amdgcn_s_barrier();
+            if constexpr (!(kAttnAblate & 8)) __builtin_amdgcn_s_barrier();
         }
     };
 
