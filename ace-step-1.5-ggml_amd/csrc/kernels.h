@@ -130,6 +130,8 @@ struct AttnArgs {
     int ksplit = 1;  // set by launch_attention
     int xcd_order = 1;  // set by launch_attention: XCD-aware block order
     int fused_merge = 0;  // set by launch_attention: the last part of a key-split group merges (no merge kernel)
+    int split_from = 0;  // set by launch_attention: > 0 = tail split (blocks [0, split_from) whole, the rest in two
+                         // key-range parts; ksplit = 2 gives the partials' layout)
     bool f8 = false;  // f8c mode (needs split + pv_split): the lo planes hold fp8 hi / lo operands (prep_math.h), the
                       // correction products Kl.Qh + Kh.Ql and Vl.Ph + Vh.Pl run as block-scaled fp8 MFMAs
 };

@@ -115,6 +115,39 @@ constexpr int RA = ACEMI_ATTN_RA;
 #define ACEMI_ATTN_ABLATE 0
 #endif
 constexpr int kAttnAblate = ACEMI_ATTN_ABLATE;
+
+// The workgroup's logical block (item, kv head, query tile) and key-range part.  Uniform layout: every block in
+// a.ksplit parts, XCD-aware order over all of them (the hardware deals launch index j to XCD j % 8; logical
+// index (j % 8) * per + j / 8 gives each XCD one contiguous run, i.e. the blocks of one (item, kv head), whose
+// K / V^T tiles they all stream, share one XCD's L2).  Tail split (a.split_from = F > 0, a multiple of 8): launch
+// indices [0, F) are whole blocks 0..F-1 (one full round), the rest the two key-range halves of blocks F..n-1
+// (the last, partial round split so it fills the chip), XCD-aware within each range.  Returns false for the up
+// to 7 empty trailing workgroups of a range.
+__device__ __forceinline__ bool attn_block(const AttnArgs& a, int n_blk, int& blk, int& part, int& parts) {
+    const int x = blockIdx.x;
+    auto xcd = [&](int i, int n) { return a.xcd_order ? (i & 7) * ((n + 7) >> 3) + (i >> 3) : i; };
+    if (a.split_from > 0) {
+        const int F = a.split_from;
+        if (x < F) {
+            blk = xcd(x, F);
+            part = 0;
+            parts = 1;
+            return blk < F;
+        }
+        const int n2 = 2 * (n_blk - F);
+        const int y = xcd(x - F, n2);
+        blk = F + (y >> 1);
+        part = y & 1;
+        parts = 2;
+        return y < n2;
+    }
+    const int n = n_blk * a.ksplit;
+    const int y = xcd(x, n);
+    blk = y / a.ksplit;
+    part = y % a.ksplit;
+    parts = a.ksplit;
+    return y < n;
+}
 static_assert(RA >= 1 && 2 * RA <= 15, "lgkmcnt counts at most 15 outstanding reads");
 // LDS reads issued after step p's own, i.e. those of steps p+1 .. p+RA (< n), for the counted lgkmcnt of step p
 template <class F>
@@ -199,12 +232,8 @@ __global__ void __launch_bounds__(256, OCC) attn_kernel(AttnArgs a) {
     // logical block L = (j % 8) * per + j / 8 gives each XCD one contiguous run of logical blocks, i.e.
     // the blocks of one (item, kv head) -- whose K / V^T tiles they all stream -- share one XCD's L2
     // (at B = 1 with 8 kv heads: one kv head per XCD).  Up to 7 trailing hardware blocks are empty.
-    const int n_blocks = a.B * a.Hkv * n_qt * a.ksplit;
-    const int per = (n_blocks + 7) >> 3;
-    int bid = a.xcd_order ? (blockIdx.x & 7) * per + (blockIdx.x >> 3) : blockIdx.x;
-    if (bid >= n_blocks) return;
-    const int split = bid % a.ksplit;  // key-range part of this block (AttnArgs::part)
-    bid /= a.ksplit;
+    int bid, split, ks;  // logical block, its key-range part (AttnArgs::part) and the block's number of parts
+    if (!attn_block(a, a.B * a.Hkv * n_qt, bid, split, ks)) return;
     const int qt = bid % n_qt;
     bid /= n_qt;
     const int kvh = bid % a.Hkv;
@@ -223,7 +252,7 @@ __global__ void __launch_bounds__(256, OCC) attn_kernel(AttnArgs a) {
     }
     if (a.causal) khi = min(khi, q0 + qpb);  // no key after the block's last query
     const int n_all = max(0, (khi + KT - 1) / KT - klo / KT);
-    const int chunk = (n_all + a.ksplit - 1) / a.ksplit;
+    const int chunk = (n_all + ks - 1) / ks;
     const int kt_begin = klo / KT + split * chunk;
     const int n = max(0, min(chunk, n_all - split * chunk));
 
@@ -502,7 +531,7 @@ __global__ void __launch_bounds__(256, OCC) attn_kernel(AttnArgs a) {
     if (i < n) iter(std::integral_constant<int, 0>{}, i);
 
     const float l = l_run + __shfl_xor(l_run, 32);
-    if (a.ksplit > 1 && a.fused_merge) {
+    if (ks > 1 && a.fused_merge) {
         // Key split, merged in place: every part stores its unnormalised O, running max and sum with
         // device-coherent (sc1) stores, completes them (vmcnt 0) and takes a ticket; the part that takes the
         // last ticket (whichever finishes last: no block ever waits) reads all S parts back in part order with
@@ -584,7 +613,7 @@ __global__ void __launch_bounds__(256, OCC) attn_kernel(AttnArgs a) {
         }
         return;
     }
-    if (a.ksplit > 1) {  // unnormalised partial O, running max and sum for attn_merge_kernel
+    if (ks > 1) {  // unnormalised partial O, running max and sum for attn_merge_kernel
         if (qrow < a.nq) {
             const int64_t row = ((int64_t)split * a.B + b) * a.nq + qrow;
             float* po = a.part + row * (a.Hq * D) + head * D;
@@ -652,12 +681,8 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
     const int rep = a.Hq / a.Hkv;
     const int qpb = 128 / rep;
     const int n_qt = (a.nq + qpb - 1) / qpb;
-    const int n_blocks = a.B * a.Hkv * n_qt * a.ksplit;
-    const int per = (n_blocks + 7) >> 3;
-    int bid = a.xcd_order ? (blockIdx.x & 7) * per + (blockIdx.x >> 3) : blockIdx.x;
-    if (bid >= n_blocks) return;
-    const int split = bid % a.ksplit;
-    bid /= a.ksplit;
+    int bid, split, ks;  // logical block, its key-range part (AttnArgs::part) and the block's number of parts
+    if (!attn_block(a, a.B * a.Hkv * n_qt, bid, split, ks)) return;
     const int qt = bid % n_qt;
     bid /= n_qt;
     const int kvh = bid % a.Hkv;
@@ -675,7 +700,7 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
     }
     if (a.causal) khi = min(khi, q0 + qpb);
     const int n_all = max(0, (khi + KT - 1) / KT - klo / KT);
-    const int chunk = (n_all + a.ksplit - 1) / a.ksplit;
+    const int chunk = (n_all + ks - 1) / ks;
     const int kt_begin = klo / KT + split * chunk;
     const int n = max(0, min(chunk, n_all - split * chunk));
 
@@ -1150,7 +1175,7 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
     wait_vmcnt<0>();  // the re-read tiles past the end
 
     const float l = l_run + __shfl_xor(l_run, 32);
-    if (a.ksplit > 1) {
+    if (ks > 1) {
         if (qrow < a.nq) {
             const int64_t row = ((int64_t)split * a.B + b) * a.nq + qrow;
             float* po = a.part + row * (a.Hq * D) + head * D;
@@ -1188,10 +1213,21 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
 // Combine the S key-range parts of one (item, query, head) row: M = max m_k, weights 2^(m_k - M) (0 for a
 // part whose keys were all masked), out = sum w_k O_k / sum w_k l_k; a row with no unmasked key at all stays
 // 0/0 = NaN as in ggml.  Half a wave per row, 16-byte partial reads, every load issued before the first use.
-template <bool F16OUT, int S>
+// TAIL (tail split, AttnArgs::split_from): only the rows of the split blocks F.., 128 (query, head) rows per block.
+template <bool F16OUT, int S, bool TAIL = false>
 __global__ void __launch_bounds__(256) attn_merge_kernel(AttnArgs a) {
     const int64_t rows = (int64_t)a.B * a.nq * a.Hq;
-    const int64_t r = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
+    int64_t r = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
+    if constexpr (TAIL) {
+        const int rep = a.Hq / a.Hkv, qpb = 128 / rep, n_qt = (a.nq + qpb - 1) / qpb;
+        const int64_t tb = r >> 7;
+        if (tb >= (int64_t)a.B * a.Hkv * n_qt - a.split_from) return;
+        const int blk = a.split_from + (int)tb, w = (int)(r & 127);
+        const int qt = blk % n_qt, kvh = (blk / n_qt) % a.Hkv, b = blk / n_qt / a.Hkv;
+        const int q = qt * qpb + w % qpb;
+        if (q >= a.nq) return;
+        r = ((int64_t)b * a.nq + q) * a.Hq + kvh * rep + w / qpb;
+    }
     if (r >= rows) return;
     const int d = (threadIdx.x & 31) * 4;
     const float* ml = a.part + S * rows * D;
@@ -1281,6 +1317,7 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s) {
     ACEMI_CHECK(a.nq_pad >= n_qt * qpb, "attention: nq_pad too small");
     AttnArgs b = a;
     b.ksplit = 1;
+    b.split_from = 0;
     {
         static int xcd = -1;  // ACE_MI_ATTN_XCD_ORDER=0: plain block order (A/B measurements)
         if (xcd < 0) {
@@ -1323,6 +1360,17 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s) {
         }
         if (a.part && mode == 2) b.ksplit = 2;
         else if (a.part && (mode == 0 || mode == 4)) b.ksplit = S;
+        // tail split (default; ACE_MI_ATTN_TAIL_SPLIT=0: every block split): when the whole blocks overfill one
+        // round by at most half a round, run one round of whole blocks and split only the rest -- the same
+        // 1 + 1/2 rounds of key tiles per CU as splitting every block, one block prologue fewer per CU, a third of
+        // the rows through the merge (240 s, B = 1: 256 whole blocks + 2 x 120 halves)
+        static int tail = -1;
+        if (tail < 0) {
+            const char* e = std::getenv("ACE_MI_ATTN_TAIL_SPLIT");
+            tail = (e && e[0] == '0') ? 0 : 1;
+        }
+        const int64_t F = slots & ~int64_t(7);
+        if (tail && mode == 0 && b.ksplit == 2 && F > 0 && blocks > F && 2 * (blocks - F) <= slots) b.split_from = (int)F;
         // ACE_MI_ATTN_FUSED_MERGE=1: the last part of a group merges in the attention kernel (sc1 partial
         // round trip, no merge launch) -- measured 2.6x slower attention at 60 s, so off by default
         static int fm = -1;
@@ -1332,7 +1380,11 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s) {
         }
         b.fused_merge = fm;
     }
-    const dim3 grid(8 * ((a.B * a.Hkv * n_qt * b.ksplit + 7) / 8));  // XCD-aware order, see attn_kernel
+    b.split_from = b.fused_merge ? 0 : b.split_from;
+    const int64_t n_blk = (int64_t)a.B * a.Hkv * n_qt;
+    // XCD-aware order (attn_block): whole multiples of 8 launch indices per range
+    const dim3 grid(b.split_from > 0 ? (unsigned)(b.split_from + 8 * ((2 * (n_blk - b.split_from) + 7) / 8))
+                                     : (unsigned)(8 * ((n_blk * b.ksplit + 7) / 8)));
     const bool f16 = out_t == ActType::F16;
     ACEMI_CHECK(!a.f8 || (a.pv_split && !b.fused_merge), "attention: the fp8 correction modes need pv_split");
     if (a.split) {
@@ -1354,7 +1406,13 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s) {
         const int64_t rows = (int64_t)a.B * a.nq * a.Hq;
         ACEMI_CHECK(b.ksplit == 2 || b.ksplit == 4, "attention: the merge handles 2 or 4 key-split parts");
         const dim3 mgrid((unsigned)((rows + 7) / 8));
-        if (b.ksplit == 2) {
+        if (b.split_from > 0) {
+            const dim3 tgrid((unsigned)((n_blk - b.split_from) * 16));  // 128 rows per split block, 8 per workgroup
+            if (out_t == ActType::F16)
+                hipLaunchKernelGGL((attn_merge_kernel<true, 2, true>), tgrid, dim3(256), 0, s, b);
+            else
+                hipLaunchKernelGGL((attn_merge_kernel<false, 2, true>), tgrid, dim3(256), 0, s, b);
+        } else if (b.ksplit == 2) {
             if (out_t == ActType::F16)
                 hipLaunchKernelGGL((attn_merge_kernel<true, 2>), mgrid, dim3(256), 0, s, b);
             else

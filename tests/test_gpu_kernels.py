@@ -131,6 +131,9 @@ def _check_attn(got, q, kv, hq, hkv, window, kmask, scale, mode):
     (1, 4, 1, 97, 500, 0, False),
     (1, 2, 1, 1100, 1100, 0, False),   # >= 16 key tiles on a small grid: two-way key split + merge
     (1, 2, 1, 150, 1500, 0, True),
+    # 376 blocks on 256 CUs (the 240 s grid at 18 key tiles): hi/lo modes run one round of whole blocks and split
+    # only the remaining 120 (tail split + tail merge); fp16 (two blocks per CU) splits every block
+    (1, 16, 8, 3000, 1100, 0, True),
 ])
 @pytest.mark.parametrize("mode", list(MODES))
 def test_attention_vs_fp64(B, hq, hkv, nq, nk, window, masked, mode):
