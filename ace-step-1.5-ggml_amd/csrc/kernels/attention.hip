@@ -1349,6 +1349,20 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s) {
         const int64_t slots = (int64_t)n_cu * per_cu;
         const int ntiles = (span + KT - 1) / KT;
         int S = 1;
+        // tail split (default; ACE_MI_ATTN_TAIL_SPLIT=0: every block split): when the whole blocks overfill one
+        // round by at most half a round, run one round of whole blocks and split only the rest -- the same
+        // 1 + 1/2 rounds of key tiles per CU as splitting every block, one block prologue fewer per CU, a third of
+        // the rows through the merge (240 s, B = 1: 256 whole blocks + 2 x 120 halves).  ACE_MI_ATTN_TAIL_MIN: the
+        // fewest key tiles per block for which it is used where every-block splitting is not (default 16 = never)
+        static int tail = -1, tail_min = 0;
+        if (tail < 0) {
+            const char* e = std::getenv("ACE_MI_ATTN_TAIL_SPLIT");
+            tail = (e && e[0] == '0') ? 0 : 1;
+            const char* m = std::getenv("ACE_MI_ATTN_TAIL_MIN");
+            tail_min = m ? std::max(2, std::atoi(m)) : 16;
+        }
+        const int64_t F = slots & ~int64_t(7);
+        const bool tail_fits = tail && mode == 0 && F > 0 && blocks > F && 2 * (blocks - F) <= slots;
         if (ntiles >= 16) {
             if (blocks * 10 < slots * 16) S = 2;
         } else if (mode == 4) {
@@ -1357,20 +1371,12 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s) {
             // (rocprof, profiles/r03_trace_60s_*.txt): attention 698 us + 48 merges 275 us per forward against
             // ~950 us unsplit -- the merge launches (~5 us each) eat the gain, so not the default
             while (S < 4 && blocks * 2 * S <= slots && ntiles >= 4 * S) S *= 2;
+        } else if (tail_fits && ntiles >= tail_min) {
+            S = 2;
         }
         if (a.part && mode == 2) b.ksplit = 2;
         else if (a.part && (mode == 0 || mode == 4)) b.ksplit = S;
-        // tail split (default; ACE_MI_ATTN_TAIL_SPLIT=0: every block split): when the whole blocks overfill one
-        // round by at most half a round, run one round of whole blocks and split only the rest -- the same
-        // 1 + 1/2 rounds of key tiles per CU as splitting every block, one block prologue fewer per CU, a third of
-        // the rows through the merge (240 s, B = 1: 256 whole blocks + 2 x 120 halves)
-        static int tail = -1;
-        if (tail < 0) {
-            const char* e = std::getenv("ACE_MI_ATTN_TAIL_SPLIT");
-            tail = (e && e[0] == '0') ? 0 : 1;
-        }
-        const int64_t F = slots & ~int64_t(7);
-        if (tail && mode == 0 && b.ksplit == 2 && F > 0 && blocks > F && 2 * (blocks - F) <= slots) b.split_from = (int)F;
+        if (tail_fits && b.ksplit == 2) b.split_from = (int)F;
         // ACE_MI_ATTN_FUSED_MERGE=1: the last part of a group merges in the attention kernel (sc1 partial
         // round trip, no merge launch) -- measured 2.6x slower attention at 60 s, so off by default
         static int fm = -1;
