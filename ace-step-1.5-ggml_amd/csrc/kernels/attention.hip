@@ -110,7 +110,8 @@ constexpr int RA = ACEMI_ATTN_RA;
 // Diagnostic ablation (A/B builds only, tools/build_ab.sh; results wrong by design): 1 = no next-tile LDS-DMA inside
 // the attn2 pipeline (every tile computes on the prologue's K / V), 2 = no exp2 in the softmax finish (P = the raw
 // score), 4 = no P lo formation in phase C (f8c / pv8), 8 = no workgroup barrier inside the tile loop, 16 = no wait
-// for the fragment reads before each step's MFMAs (the MFMAs read whatever the registers hold)
+// for the fragment reads before each step's MFMAs (the MFMAs read whatever the registers hold); precision probes
+// (results deliberately less exact, not slower): 32 = f8c without the Kh.Ql correction, 64 = without Kl.Qh
 #ifndef ACEMI_ATTN_ABLATE
 #define ACEMI_ATTN_ABLATE 0
 #endif
@@ -847,7 +848,8 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
             if constexpr (st.corr) {
                 // Kl.Qh (c = 0, 1: the 2^-11 on A) + Kh.Ql (c = 2, 3: on B), e4m3 x e4m3, K = 64 per MFMA
                 constexpr int c = st.idx >> 1;
-                sn[t] = mfma_f8(cat8(kh[p % (RA + 1)], kl[p % (RA + 1)]), q8[c], sn[t], c < 2 ? F8_SCALE_LO : F8_SCALE_1,
+                if constexpr (!((kAttnAblate & 32) && c >= 2) && !((kAttnAblate & 64) && c < 2))
+                    sn[t] = mfma_f8(cat8(kh[p % (RA + 1)], kl[p % (RA + 1)]), q8[c], sn[t], c < 2 ? F8_SCALE_LO : F8_SCALE_1,
                                 c < 2 ? F8_SCALE_1 : F8_SCALE_LO);
             } else {
                 constexpr int ks = st.idx >> 1;
