@@ -815,8 +815,9 @@ double m_edge(int M, int bm) { return (double)M / (double)(((M + bm - 1) / bm) *
 int pick_variant_q(int M, int N, int K, int fmt) {
     const int64_t mb192 = (M + 191) / 192;
     if (M > 1024) {
-        // 21 (8 waves, 256 columns) with Q4_K: wrong 16-column groups of the upper four waves on some launches, only
-        // while LDS-DMA is in flight during the tile's LDS reads -- Q4_K takes the 4-wave tile
+        // 21 with Q4_K: its kernel-level wrong 16-column groups are gone since round 5 (the MFMA operand
+        // write-after-read of gemm_q.hip:mfma_war_guard), but whole forwards through it are still not run-to-run
+        // identical (tools/diag_det_qr.py) -- Q4_K keeps the 4-wave tile
         if (fmt != WF_Q4_K && N % 256 == 0 && mb192 * (N / 256) >= 256) return 21;
         return 20;
     }
@@ -843,8 +844,8 @@ int pick_variant(int M, int N, int K, bool quant, int fmt) {
                                          : ((f == 1 || f == 3 || f == 4 ? S <= 2
                                                                        : (((f >= 6 && f <= 9) || (f >= 12 && f <= 15)) && S <= 4)) &&
                                             K / 64 >= 2 * S));
-        return !(wide && N % 256 != 0) && !(quant && dense_only) && !(!quant && qr) && sk_ok &&
-               !(f == 21 && fmt == WF_Q4_K);
+        (void)fmt;
+        return !(wide && N % 256 != 0) && !(quant && dense_only) && !(!quant && qr) && sk_ok;
     };
     if (g_forced_variant >= 0x10000) return g_forced_variant & 0xffff;  // diagnostics (selftest): no support check
     if (g_forced_variant >= 0 && supports(g_forced_variant)) return g_forced_variant;  // tests / micro-benchmarks

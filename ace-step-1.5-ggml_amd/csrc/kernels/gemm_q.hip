@@ -328,8 +328,17 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_q_kernel(GemmParams p) {
 // k-tile is a compile-time constant, so one counted vmcnt per k-tile retires exactly the tile being consumed
 // while the next stays in flight (a register-held weight prefetch made hipcc drain every load, vmcnt(0), at
 // each k-tile: 0.62 of the dense kernel's rate).
-// Pipeline per k-tile t: vmcnt(G) retires A/W(t) [A/W(t+1) in flight], barrier, stage A/W(t+2) into the slot
-// last read at t-1, B bytes -> registers -> bf16 fragments, then per kk: A fragments from LDS, TM x 2 MFMAs.
+// Pipeline (RS ring slots, RS = 4 where the LDS fits them, else 3): a tile is READ one barrier after the counted
+// vmcnt that retires it, never right behind that wait.  Per k-tile t: vmcnt retires tile t+1 [tiles up to t+RS-2 stay
+// in flight], barrier, stage tile t+RS-1 into the slot last read at t-1, then read tile t (retired by the previous
+// iteration's wait, so at least one barrier and a whole MFMA phase lie between its retiring wait and these reads):
+// B bytes -> registers -> bf16 fragments, then per kk: A fragments from LDS, TM x 2 MFMAs.
+// Why not read right behind the wait (rounds 2-4's schedule): on gfx950 a wave's counted vmcnt can be satisfied
+// before its own LDS-DMA bytes are visible to ds_read -- the wave that arrives last at the barrier and then reads a
+// piece it staged itself saw the slot's previous contents (variant 21 x Q4_K, whose q rows are the only ones a wave
+// both stages and reads: whole 16-column groups of waves 4-7 wrong on some launches; the 64-row tiles, whose MFMA
+// phase is the shortest, not run-to-run identical in whole forwards; DESIGN.md §10, the guide's "read a staged buffer
+// one phase AFTER the wait that retires it").
 template <int WQ>
 struct QTile {  // bytes of one weight row per 64-wide k-tile (q plane, scale plane)
     static constexpr int QB = WQ == WF_Q4_K ? 32 : 64;
@@ -405,10 +414,39 @@ __device__ __forceinline__ void qd_dequant(const QRaw& r, int g, int kk, uint4 (
     }
 }
 
+// MFMA operand write-after-read guard.  On gfx950 with two waves per SIMD, a VALU that writes an A / B source register of
+// an MFMA issued just before it can corrupt that product: the register-dequant tile with the kk = 1 dequant VALU
+// scheduled between the kk = 0 MFMAs (hipcc pads this pair for the C operand only) gave whole wrong 16-column groups
+// of waves 4-7 on some launches -- rounds 3-4's "variant 21 x Q4_K" and "64-row tile not run-to-run identical"
+// anomalies.  Measured (tools/diag_v21.py, profiles/r05/qr_war/): a scheduling fence between the MFMA block and the
+// VALU that follows it removes every failure; padding only the end of the tile does not.  The fence keeps hipcc from
+// interleaving the two, the s_nops keep 16 wait states between the last MFMA and the first overwrite.
+__device__ __forceinline__ void mfma_war_guard() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 7\n\ts_nop 7");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+#ifdef ACEMI_QR_DIAG
+// Diagnostic build only (tools/build_ab.sh ... -DACEMI_QR_DIAG): every lane's raw LDS reads of every k-tile (q words and
+// scales as first read, then the same LDS words re-read after the tile's MFMAs), to tell a late-landing DMA from a wrong one.
+__device__ uint32_t g_qr_dbg[1 << 22];
+#endif
+
+template <int BM, int NW, int WQ>
+struct QRing {
+    static constexpr int SLOT = BM * 128 + 32 * NW * (QTile<WQ>::QB + QTile<WQ>::SB);
+#ifdef ACEMI_QR_RING3  // A/B build: the 3-slot ring everywhere
+    static constexpr int RS = 3;
+#else
+    static constexpr int RS = 4 * SLOT <= 160 * 1024 ? 4 : 3;  // ring slots
+#endif
+    static constexpr int BYTES = RS * SLOT;
+};
+
 // two workgroups per CU where the ring allows it (not for split-K: its join needs the registers)
 template <int BM, int NW, int EPI, int WQ, bool SK = false>
-__global__ void __launch_bounds__(NW * 64, (!SK && (NW == 8 || 2 * 3 * (BM * 128 + 128 * (QTile<WQ>::QB + QTile<WQ>::SB)) <=
-                                                                     160 * 1024)) ? 2 : 1)
+__global__ void __launch_bounds__(NW * 64, (!SK && (NW == 8 || 2 * QRing<BM, NW, WQ>::BYTES <= 160 * 1024)) ? 2 : 1)
     gemm_qr_kernel(GemmParams p) {
     constexpr int BN = 32 * NW;
     constexpr int TM = BM / 16;
@@ -418,6 +456,8 @@ __global__ void __launch_bounds__(NW * 64, (!SK && (NW == 8 || 2 * 3 * (BM * 128
     constexpr int QB = QTile<WQ>::QB, SB = QTile<WQ>::SB;
     constexpr int A_BYTES = BM * ROWB, WQ_BYTES = BN * QB, WS_BYTES = BN * SB;
     constexpr int SLOT = A_BYTES + WQ_BYTES + WS_BYTES;
+    constexpr int RS = QRing<BM, NW, WQ>::RS;
+    static_assert(SLOT == QRing<BM, NW, WQ>::SLOT, "ring slot size");
     constexpr int PA = BM / 8;             // 1 KiB pieces (8 rows x 128 B)
     constexpr int PQ = WQ_BYTES / 1024;    // 1 KiB pieces (64 lanes x 16 B)
     constexpr int PS = WS_BYTES / 256;     // 256 B pieces (64 lanes x one f32)
@@ -425,7 +465,7 @@ __global__ void __launch_bounds__(NW * 64, (!SK && (NW == 8 || 2 * 3 * (BM * 128
     constexpr int G = (PA + PQ + PS) / NW;  // LDS-DMA instructions per wave per k-tile
     static_assert(EPI != EPI_SWIGLU || (TN % 2 == 0), "swiglu needs column pairs");
 
-    __shared__ __attribute__((aligned(16))) char smem[3 * SLOT];
+    __shared__ __attribute__((aligned(16))) char smem[RS * SLOT];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -500,19 +540,21 @@ __global__ void __launch_bounds__(NW * 64, (!SK && (NW == 8 || 2 * 3 * (BM * 128
     const int lrow = lane & 15, lchunk = lane >> 4;
     const int rsw = (lrow >> 1) & 7;
 
-    // prologue: k-tiles 0 and 1 in flight.  The body is branch-free: past the last k-tile it re-stages the final
-    // one into the slot nobody reads again, so every iteration issues the same G DMA instructions per wave and
-    // the counted vmcnt(G) at its top always retires exactly the tile it consumes.
-    stage(0, 0);
-    stage(min(1, nk - 1), 1);
+    // prologue: k-tiles 0 .. RS-2 requested, tile 0 retired + published.  The body is branch-free: past the last k-tile
+    // it re-stages the final one into the slot nobody reads again, so every iteration issues the same G DMA
+    // instructions per wave and the counted vmcnt at its top always retires exactly tile kt+1.
+#pragma unroll
+    for (int s = 0; s < RS - 1; ++s) stage(min(s, nk - 1), s);
+    wait_vmcnt<G*(RS - 2)>();
+    __builtin_amdgcn_s_barrier();
     for (int kt = 0; kt < nk; ++kt) {
-        wait_vmcnt<G>();
-        __builtin_amdgcn_s_barrier();  // every wave's pieces of tile kt landed; slot (kt+2)%3 = (kt-1)%3 is free
-        stage(min(kt + 2, nk - 1), (kt + 2) % 3);
+        wait_vmcnt<G*(RS - 3)>();      // this wave's pieces of tile kt+1 landed (read next iteration)
+        __builtin_amdgcn_s_barrier();  // every wave: tile kt+1 retired, reads of tile kt-1 done -> its slot is free
+        stage(min(kt + RS - 1, nk - 1), (kt + RS - 1) % RS);
         // W bytes and the kk = 0 A fragments in one LDS wait; the kk = 1 A reads are issued before the kk = 0
         // MFMAs, and the kk = 1 dequant VALU sits between those MFMAs (no scheduling barrier in between), so the
         // dequant of the second k half overlaps matrix work
-        const uint32_t sbase = lds0 + (kt % 3) * SLOT;
+        const uint32_t sbase = lds0 + (kt % RS) * SLOT;
         const uint32_t abase = sbase + lrow * ROWB;
         QRaw raw;
         qd_read<WQ>(sbase + A_BYTES, sbase + A_BYTES + WQ_BYTES, wn0 + lrow, lchunk, raw);
@@ -520,29 +562,55 @@ __global__ void __launch_bounds__(NW * 64, (!SK && (NW == 8 || 2 * 3 * (BM * 128
         ReadRows<0, TM, 16 * ROWB>::run(abase + (((0 * 4 + lchunk) ^ rsw) * 16), a0, 0);
         lds_wait_all();
         qd_dequant<WQ>(raw, lchunk, 0, b);
+#ifdef ACEMI_QR_GUARD_RAW
+        mfma_war_guard();
+#endif
         ReadRows<0, TM, 16 * ROWB>::run(abase + (((1 * 4 + lchunk) ^ rsw) * 16), a1, 1);
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<false>(a0[i][0], b[j][0], acc[i][j]);
+        mfma_war_guard();  // the kk = 1 dequant below overwrites A / B registers of the MFMAs just issued
         qd_dequant<WQ>(raw, lchunk, 1, b);
         lds_wait_all();
+#ifdef ACEMI_QR_GUARD_RAW
+        mfma_war_guard();
+#endif
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<false>(a1[i][1], b[j][1], acc[i][j]);
+        mfma_war_guard();  // the next k-tile's address VALU and LDS reads reuse this tile's operand registers
+#ifdef ACEMI_QR_DIAG
+        if constexpr (!SK) {
+            QRaw raw2;
+            qd_read<WQ>(sbase + A_BYTES, sbase + A_BYTES + WQ_BYTES, wn0 + lrow, lchunk, raw2);
+            lds_wait_all();
+            uint32_t* d = g_qr_dbg + ((size_t)(blockIdx.x * nk + kt) * (NW * 64) + tid) * 24;
+            if ((size_t)(blockIdx.x * nk + kt + 1) * (NW * 64) * 24 <= (1u << 22)) {
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    d[j * 12 + 0] = raw.q[j][0][0]; d[j * 12 + 1] = raw.q[j][0][1];
+                    d[j * 12 + 2] = raw.q[j][1][0]; d[j * 12 + 3] = raw.q[j][1][1];
+                    d[j * 12 + 4] = raw.sc[j].x; d[j * 12 + 5] = raw.sc[j].y; d[j * 12 + 6] = raw.sc[j].z; d[j * 12 + 7] = raw.sc[j].w;
+                    d[j * 12 + 8] = raw2.q[j][0][0]; d[j * 12 + 9] = raw2.q[j][1][0];
+                    d[j * 12 + 10] = raw2.sc[j].x; d[j * 12 + 11] = raw2.sc[j].z;
+                }
+            }
+        }
+#endif
     }
     wait_vmcnt<0>();  // the dummy stages past the end land before the epilogue reuses the ring
     __syncthreads();  // LDS reads done before the epilogue reuses the ring
 
     if constexpr (SK)
-        if (!splitk_join<TM, TN, NW, 4, 3 * SLOT>(p, acc, S, sk_tile, sk_part, tid, smem, ticket0)) return;
+        if (!splitk_join<TM, TN, NW, 4, RS * SLOT>(p, acc, S, sk_tile, sk_part, tid, smem, ticket0)) return;
     if constexpr (EPI == EPI_QKV_PREP) {
         // one head per 128 columns: waves [4 hb, 4 hb + 4) hold head (n0 >> 7) + hb
         const int ccol = lane & 15, crow = (lane >> 4) * 4;
 #pragma unroll
         for (int hb = 0; hb < BN / 128; ++hb)
-            qkv_prep_head<BM, NW, 3 * SLOT>(p, m0, (n0 >> 7) + hb, tid, smem, [&](float* tile, int c0, int CH) {
+            qkv_prep_head<BM, NW, RS * SLOT>(p, m0, (n0 >> 7) + hb, tid, smem, [&](float* tile, int c0, int CH) {
                 if ((wn0 >> 7) != hb) return;
 #pragma unroll
                 for (int i = 0; i < TM; ++i) {
@@ -641,6 +709,20 @@ void dispatch_quant(int fmt, int variant, const GemmParams& p, hipStream_t s) {
 }  // namespace gemm_detail
 
 using namespace gemm_detail;
+
+#ifdef ACEMI_QR_DIAG
+extern "C" __attribute__((visibility("default"))) int ace_mi_qr_diag_read(uint32_t* out, size_t n_words, int clear) {
+    if (n_words > (1u << 22)) return 2;
+    if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(gemm_detail::g_qr_dbg), n_words * 4, 0, hipMemcpyDeviceToHost) != hipSuccess)
+        return 1;
+    if (clear) {
+        void* p = nullptr;
+        if (hipGetSymbolAddress(&p, HIP_SYMBOL(gemm_detail::g_qr_dbg)) != hipSuccess || hipMemset(p, 0xff, (1u << 22) * 4) != hipSuccess)
+            return 1;
+    }
+    return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
+}
+#endif
 
 void launch_dequant_bf16_batch(const DequantJob* jobs, int n, hipStream_t s) {
     ACEMI_CHECK(n >= 1 && n <= 8, "dequant: 1..8 matrices per launch");

@@ -55,8 +55,6 @@ def test_gemm_q_matches_dequantized_product(qtype, variant, M, N, K):
     capi = _capi()
     if variant in (2, 5, 21) and N % 256:
         pytest.skip("256-wide tiles need N % 256 == 0")
-    if variant == 21 and qtype == "q4_k":
-        pytest.skip("8-wave tile x Q4_K: timing race under in-flight LDS-DMA (DESIGN.md §10); not used for Q4_K")
     if variant >= 100 and K // 64 < 2 * (variant // 100):
         pytest.skip("split-K needs two k-tiles per part")
     rng = np.random.default_rng(M + K + variant)
@@ -80,8 +78,6 @@ def test_gemm_q_residual_epilogues(qtype, variant, epi):
     M, N, K = 300, 512, 512
     if variant in (21,) and N % 256:
         pytest.skip("256-wide tiles need N % 256 == 0")
-    if variant == 21 and qtype == "q4_k":
-        pytest.skip("8-wave tile x Q4_K: timing race under in-flight LDS-DMA (DESIGN.md §10); not used for Q4_K")
     rng = np.random.default_rng(7 * epi + variant + 100)
     a = f32_to_bf16_bits(rng.standard_normal((M, K)).astype(np.float32))
     w = (rng.standard_normal((N, K)) * 0.02).astype(np.float32)

@@ -28,12 +28,12 @@ def fwd(d, T, L, H):
 os.environ["ACE_GGML_DIT_MAX_LAYERS"] = "3"
 full = cached_checkpoint(make_config(num_hidden_layers=3), seed=0, backend="torch")
 lib = capi.load_library()
-for qt in ("q4_k", "q8_0"):
+for qt in os.environ.get("QTYPES", "q4_k,q8_0").split(","):
     os.environ["ACE_GGML_DIT_WEIGHT_QTYPE"] = qt
     os.environ["ACE_MI_QUANT_STAGED"] = "1"
     ref = fwd(full, 400, 64, 2048)[0]
     os.environ["ACE_MI_QUANT_STAGED"] = "0"
-    for v in (22, 23, 222, 223, 423, 20, 21):
+    for v in [int(x) for x in os.environ.get("VARIANTS", "22,23,222,223,423,20,21").split(",")]:
         capi.gemm_variant(v)
         try:
             o = fwd(full, 400, 64, 2048)

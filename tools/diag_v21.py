@@ -19,9 +19,9 @@ def main():
             a = f32_to_bf16_bits(rng.standard_normal((M, K)).astype(np.float32))
             w = (rng.standard_normal((N, K)) * 0.02).astype(np.float32)
             blocks = capi.quantize(w, qtype)
-            for v in (20, 21):
+            ref, scale = _q_ref(a, blocks, qtype)
+            for v in [v for v in (20, 21, 22, 23) for _ in range(int(os.environ.get("REPS", "1")))]:
                 got = capi.kernel_gemm_q(a, blocks, qtype, epi=0, variant=v | 0x10000)
-                ref, scale = _q_ref(a, blocks, qtype)
                 bad = np.abs(got - ref) > 2e-6 * scale + 1e-6
                 rows, cols = np.nonzero(bad)
                 msg = f"{qtype} v{v} M={M} N={N} K={K}: bad {int(bad.sum())}/{bad.size}"
