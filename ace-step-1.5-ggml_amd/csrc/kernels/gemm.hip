@@ -39,14 +39,6 @@ namespace gemm_detail {
 #endif
 constexpr int kAblate = ACEMI_GEMM_ABLATE;
 
-// f(std::integral_constant<int, I>) for I = B..E-1
-template <int B, int E, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-    if constexpr (B < E) {
-        f(std::integral_constant<int, B>{});
-        static_for<B + 1, E>(f);
-    }
-}
 
 // PIPE 0: stage(t+1) ; compute(t) ; vmcnt(0) ; __syncthreads        (2 LDS buffers)
 // PIPE 1: compute first half of tile t from registers read up front, release the LDS buffer with
@@ -814,12 +806,13 @@ double m_edge(int M, int bm) { return (double)M / (double)(((M + bm - 1) / bm) *
 // the grid covers the 256 CUs.
 int pick_variant_q(int M, int N, int K, int fmt) {
     const int64_t mb192 = (M + 191) / 192;
+    (void)fmt;
     if (M > 1024) {
-        // 21 with Q4_K: its kernel-level wrong 16-column groups are gone since round 5 (the MFMA operand
-        // write-after-read of gemm_q.hip:mfma_war_guard), but whole forwards through it are still not run-to-run
-        // identical (tools/diag_det_qr.py) -- Q4_K keeps the 4-wave tile
-        if (fmt != WF_Q4_K && N % 256 == 0 && mb192 * (N / 256) >= 256) return 21;
-        return 20;
+        // M = 3000 (tools/wsq_bench.py, profiles/r05/wsq/): gate|up / qkv on the 8-wave register-dequant tile (21),
+        // the N = 2048 projections on the warp-specialized tile (25: the expansion on loader waves; down 662 vs 539,
+        // o 560 vs 451 TFLOP/s for the 4-wave register-dequant tile)
+        if (N > 2048 && N % 256 == 0 && mb192 * (N / 256) >= 256) return 21;
+        return 25;
     }
     // Short sequences: round 1's LDS-dequant kernel (96 x 128).  Whole forwards through the 64 / 128-row
     // register-dequant tiles (22, 23, split or not) were not run-to-run identical (tools/diag_det.py, round 3;
@@ -838,7 +831,7 @@ int pick_variant(int M, int N, int K, bool quant, int fmt) {
     auto supports = [&](int v) {  // the tile / split-K factor handles this shape (and weight format)
         const int f = v % 100, S = v / 100;
         const bool wide = f == 2 || f == 5 || f == 10 || f == 11 || f == 21;  // (12-15: multi-stage rings)
-        const bool qr = f >= 20 && f <= 24;
+        const bool qr = f >= 20 && f <= 25;
         const bool dense_only = (f == 6 || (f >= 8 && f < 20) || S > 1) && !qr;
         const bool sk_ok = S <= 1 || (qr ? (f == 22 || f == 23) && S <= 4 && K / 64 >= 2 * S
                                          : ((f == 1 || f == 3 || f == 4 ? S <= 2

@@ -101,6 +101,15 @@ struct ReadRows<N, N, STRIDE> {
     __device__ __forceinline__ static void run(uint32_t, uint4 (&)[N][2], int) {}
 };
 
+// f(std::integral_constant<int, I>) for I = B..E-1
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
+
 // s_waitcnt vmcnt(N) with N a compile-time constant (lgkmcnt/expcnt untouched)
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {

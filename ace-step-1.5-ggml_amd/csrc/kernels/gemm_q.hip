@@ -420,7 +420,9 @@ __device__ __forceinline__ void qd_dequant(const QRaw& r, int g, int kk, uint4 (
 // of waves 4-7 on some launches -- rounds 3-4's "variant 21 x Q4_K" and "64-row tile not run-to-run identical"
 // anomalies.  Measured (tools/diag_v21.py, profiles/r05/qr_war/): a scheduling fence between the MFMA block and the
 // VALU that follows it removes every failure; padding only the end of the tile does not.  The fence keeps hipcc from
-// interleaving the two, the s_nops keep 16 wait states between the last MFMA and the first overwrite.
+// interleaving the two, the s_nops keep 16 wait states between the last MFMA and the first overwrite.  The same
+// fence between the dequant VALU and the MFMAs that read its B fragments (read-after-write) made the split-K forms
+// (223 / 423) and the residual epilogue of 21 x Q4_K exact as well (profiles/r05/qr_war/).
 __device__ __forceinline__ void mfma_war_guard() {
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_nop 7\n\ts_nop 7");
@@ -562,9 +564,7 @@ __global__ void __launch_bounds__(NW * 64, (!SK && (NW == 8 || 2 * QRing<BM, NW,
         ReadRows<0, TM, 16 * ROWB>::run(abase + (((0 * 4 + lchunk) ^ rsw) * 16), a0, 0);
         lds_wait_all();
         qd_dequant<WQ>(raw, lchunk, 0, b);
-#ifdef ACEMI_QR_GUARD_RAW
-        mfma_war_guard();
-#endif
+        mfma_war_guard();  // (read side: the kk = 0 MFMAs read B fragments just written by this VALU)
         ReadRows<0, TM, 16 * ROWB>::run(abase + (((1 * 4 + lchunk) ^ rsw) * 16), a1, 1);
 #pragma unroll
         for (int i = 0; i < TM; ++i)
@@ -573,9 +573,7 @@ __global__ void __launch_bounds__(NW * 64, (!SK && (NW == 8 || 2 * QRing<BM, NW,
         mfma_war_guard();  // the kk = 1 dequant below overwrites A / B registers of the MFMAs just issued
         qd_dequant<WQ>(raw, lchunk, 1, b);
         lds_wait_all();
-#ifdef ACEMI_QR_GUARD_RAW
         mfma_war_guard();
-#endif
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -628,6 +626,243 @@ __global__ void __launch_bounds__(NW * 64, (!SK && (NW == 8 || 2 * QRing<BM, NW,
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Warp-specialized dequant-fused GEMM (variant 25): the dense warp-specialized tile (gemm.hip gemm_ws_kernel,
+// variant 18) with the dequantization moved onto its loader waves.  512 threads: 4 MFMA waves (2 x 2, 96 x 64 each,
+// one per SIMD) that only read bf16 fragments from LDS and issue MFMAs -- the same instruction stream as the dense
+// tile -- and 4 loader waves that, per k-tile t, (1) stage A(t) (bf16 activations) and the raw ggml-format W(t)
+// bytes + f32 scale planes by LDS-DMA into ring slot t % NS, (2) once those landed, expand W(t) with the staged
+// dequant's arithmetic (dequant_block: one f32 product, RNE to bf16) into the slot's swizzled bf16 B image, and
+// (3) publish the slot at barrier B(t).  So each weight is expanded once per block by a wave that issues no MFMA
+// (the VALU work runs beside the MFMA wave of its SIMD instead of in its stream), the MFMA operands and the k order
+// are those of staged dequant + the dense kernel (bit-identical results), and no bf16 image exists in HBM.
+// Ring: NS slots of (A image | B image) plus NS raw-W buffers; the loaders keep tiles t+1 .. t+NS-1 in flight.  The
+// loaders' LDS reads / writes are inline asm (a compiler-visible LDS access beside an in-flight LDS-DMA draws a
+// vmcnt(0) from hipcc); each group of B writes is retired (lgkmcnt(0)) inside its own statement, so no later VALU can
+// overwrite their data registers before the LDS unit has read them.
+template <int WQ>
+__device__ __forceinline__ void wsq_read_raw(uint32_t q_addr, uint32_t s_addr, WRaw& r) {
+    if constexpr (WQ == WF_Q4_K) {
+        u32x4 q;
+        uint2 sc;
+        asm volatile("ds_read_b128 %0, %2\n\tds_read_b64 %1, %3\n\ts_waitcnt lgkmcnt(0)"
+                     : "=&v"(q), "=&v"(sc) : "v"(q_addr), "v"(s_addr) : "memory");
+        r.q0 = q;
+        r.s0 = __uint_as_float(sc.x);
+        r.s1 = __uint_as_float(sc.y);
+    } else {
+        u32x4 q0, q1;
+        if constexpr (WQ == WF_Q8_0) {
+            uint32_t sc;
+            asm volatile("ds_read_b128 %0, %3\n\tds_read_b128 %1, %3 offset:16\n\tds_read_b32 %2, %4\n\ts_waitcnt lgkmcnt(0)"
+                         : "=&v"(q0), "=&v"(q1), "=&v"(sc) : "v"(q_addr), "v"(s_addr) : "memory");
+            r.s0 = __uint_as_float(sc);
+            r.s1 = r.s0;
+        } else {
+            uint2 sc;
+            asm volatile("ds_read_b128 %0, %3\n\tds_read_b128 %1, %3 offset:16\n\tds_read_b64 %2, %4\n\ts_waitcnt lgkmcnt(0)"
+                         : "=&v"(q0), "=&v"(q1), "=&v"(sc) : "v"(q_addr), "v"(s_addr) : "memory");
+            r.s0 = __uint_as_float(sc.x);
+            r.s1 = __uint_as_float(sc.y);
+        }
+        r.q0 = q0;
+        r.q1 = q1;
+    }
+}
+
+template <int BM, int BN, int EPI, int WQ, int NS>
+__global__ void __launch_bounds__(512, 1) gemm_wsq_kernel(GemmParams p) {
+    constexpr int NC = 4, WN = 2;  // MFMA waves (2 x 2)
+    constexpr int WTM = BM / 2, WTN = BN / WN;
+    constexpr int TM = WTM / 16, TN = WTN / 16;
+    constexpr int BK = 64, ROWB = BK * 2;
+    constexpr int STAGE = (BM + BN) * ROWB;
+    constexpr int QB = QTile<WQ>::QB, SB = QTile<WQ>::SB;
+    constexpr int RAW = BN * (QB + SB);
+    constexpr int GA = BM / 8 / 4;            // A pieces (1 KiB) per loader wave per k-tile
+    constexpr int GQ = BN * QB / 1024 / 4;    // q pieces (1 KiB) per loader wave
+    constexpr int GS = BN * SB / 256 / 4;     // scale pieces (256 B: one f32 per lane) per loader wave
+    constexpr int G = GA + GQ + GS;
+    static_assert(BM % 32 == 0 && (BN * QB) % 4096 == 0 && (BN * SB) % 1024 == 0 && BN * 2 == 256, "wsq tile");
+    static_assert(NS >= 3 && NS * (STAGE + RAW) <= 160 * 1024, "wsq ring");
+    static_assert(EPI != EPI_SWIGLU || (TN % 2 == 0), "swiglu needs column pairs");
+    __shared__ __attribute__((aligned(16))) char smem[NS * (STAGE + RAW)];
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    int m0, n0;
+    block_tile<BM, BN>(p, m0, n0);
+    const int nk = p.K / BK;
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+
+    if (wid >= NC) {  // ---- loader wave ----
+        const int lw = wid - NC, ltid = tid - NC * 64;
+        const uint16_t* srcA[GA];
+#pragma unroll
+        for (int j = 0; j < GA; ++j) {
+            const int row = (lw + 4 * j) * 8 + (lane >> 3);
+            const int c = (lane & 7) ^ swz(row);
+            srcA[j] = p.A + (int64_t)min(m0 + row, p.M - 1) * p.lda + c * 8;
+        }
+        const int qrow_bytes = WQ == WF_Q4_K ? p.K / 2 : p.K;
+        const int srow_floats = WQ == WF_Q8_0 ? p.K / 32 : p.K / 16;
+        // raw W pieces: loader wave lw stages exactly the rows its own lanes expand (rows 32 lw .. 32 lw + 31), so its
+        // own counted vmcnt orders its LDS reads of them (no workgroup barrier between staging and dequant)
+        const char* srcQ[GQ];
+#pragma unroll
+        for (int j = 0; j < GQ; ++j) {
+            constexpr int LPR = QB / 16;  // lanes per row
+            const int e = (lw * GQ + j) * 64 + lane;
+            srcQ[j] = static_cast<const char*>(p.Wq) + (int64_t)(n0 + e / LPR) * qrow_bytes + (e % LPR) * 16;
+        }
+        const float* srcS[GS];
+#pragma unroll
+        for (int j = 0; j < GS; ++j) {
+            constexpr int FPR = SB / 4;  // floats per row
+            const int e = (lw * GS + j) * 64 + lane;
+            srcS[j] = p.Ws + (int64_t)(n0 + e / FPR) * srow_floats + (e % FPR);
+        }
+        auto stage = [&](int t) {  // raw W(t) pieces first, then A(t): a counted vmcnt can retire W(t+1) with A(t+1) in flight
+            const int slot = t % NS;
+            char* base = smem + slot * STAGE;
+            char* raw = smem + NS * STAGE + slot * RAW;
+#pragma unroll
+            for (int j = 0; j < GQ; ++j)
+                __builtin_amdgcn_global_load_lds((const void*)(srcQ[j] + (int64_t)t * QB),
+                                                 (lds_void*)(raw + (lw * GQ + j) * 1024), 16, 0, 0);
+#pragma unroll
+            for (int j = 0; j < GS; ++j)
+                __builtin_amdgcn_global_load_lds((const void*)(srcS[j] + t * (SB / 4)),
+                                                 (lds_void*)(raw + BN * QB + (lw * GS + j) * 256), 4, 0, 0);
+#pragma unroll
+            for (int j = 0; j < GA; ++j)
+                __builtin_amdgcn_global_load_lds((const void*)(srcA[j] + t * BK), (lds_void*)(base + (lw + 4 * j) * 1024), 16,
+                                                 0, 0);
+        };
+        // this lane's 32-value block of W(t): row wr of the tile, k half wh
+        const int wr = ltid >> 1, wh = ltid & 1;
+        const int wsw = swz(wr);
+        constexpr int QOFF = WQ == WF_Q4_K ? 16 : 32;  // q bytes of one 32-value block
+        constexpr int SOFF = WQ == WF_Q8_0 ? 4 : 8;    // scale bytes of one 32-value block
+        auto dequant = [&](int t, auto&& between) {  // (between: work the compiler may interleave with the VALU)
+            const int slot = t % NS;
+            const uint32_t raw = lds0 + NS * STAGE + slot * RAW;
+            WRaw r;
+            wsq_read_raw<WQ>(raw + wr * QB + wh * QOFF, raw + BN * QB + wr * SB + wh * SOFF, r);
+            between();  // (LDS-DMA issue the compiler may interleave with the dequant VALU below)
+            uint32_t o[16];
+            dequant_block<WQ>(r, o);
+            const uint32_t row = lds0 + slot * STAGE + (BM + wr) * ROWB;
+            const uint32_t c0 = row + (((wh * 4 + 0) ^ wsw) * 16), c1 = row + (((wh * 4 + 1) ^ wsw) * 16);
+            const uint32_t c2 = row + (((wh * 4 + 2) ^ wsw) * 16), c3 = row + (((wh * 4 + 3) ^ wsw) * 16);
+            const u32x4 d0{o[0], o[1], o[2], o[3]}, d1{o[4], o[5], o[6], o[7]};
+            const u32x4 d2{o[8], o[9], o[10], o[11]}, d3{o[12], o[13], o[14], o[15]};
+            asm volatile(
+                "ds_write_b128 %0, %4\n\tds_write_b128 %1, %5\n\tds_write_b128 %2, %6\n\tds_write_b128 %3, %7\n\t"
+                "s_waitcnt lgkmcnt(0)"
+                :
+                : "v"(c0), "v"(c1), "v"(c2), "v"(c3), "v"(d0), "v"(d1), "v"(d2), "v"(d3)
+                : "memory");
+        };
+        // Raw W(t) is read one barrier after the counted wait that retires it (the guide's rule for LDS-DMA data: a
+        // read right behind its own wait gave run-to-run differences in whole Q4_K / Q6_K forwards): the wait before
+        // B(j) retires A(j) and W(j+1) (A(j+1) stays in flight), the dequant of W(j+1) runs after B(j).
+        static_assert(NS == 3, "the counted waits below assume three ring slots");
+#pragma unroll
+        for (int t = 0; t < NS; ++t)
+            if (t < nk) stage(t);
+        if (nk > 1) wait_vmcnt<GA + G>();  // W(0) A(0) W(1) retired; A(1) W(2) A(2) in flight
+        else wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();  // P: (a barrier between W(0)'s retiring wait and its reads)
+        auto none = [] {};
+        dequant(0, none);
+        __builtin_amdgcn_s_barrier();  // B(0): A(0) landed, B image of tile 0 written
+        for (int j = 1; j < nk; ++j) {
+            dequant(j, none);  // W(j) retired before B(j-1)
+            if (j + 1 < nk) wait_vmcnt<GA>();  // A(j), W(j+1) retired; A(j+1) in flight
+            else wait_vmcnt<0>();
+            __builtin_amdgcn_s_barrier();  // B(j): slot (j-1) % NS read by every MFMA wave
+            if (j - 1 + NS < nk) stage(j - 1 + NS);
+        }
+        wait_vmcnt<0>();
+        if constexpr (EPI == EPI_QKV_PREP)
+            qkv_prep_head<BM, 8, NS * STAGE>(p, m0, n0 >> 7, tid, smem, [](float*, int, int) {});
+        return;
+    }
+
+    // ---- MFMA wave (gemm_ws_kernel's) ----
+    const int wm0 = (wid / WN) * WTM, wn0 = (wid % WN) * WTN;
+    const int lrow = lane & 15, lchunk = lane >> 4;
+    const int rsw = (lrow >> 1) & 7;
+    const uint32_t ch[2] = {(uint32_t)((lchunk ^ rsw) * 16), (uint32_t)(((4 + lchunk) ^ rsw) * 16)};
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    uint4 a[TM][2], b[TN][2];
+    auto rd = [&](auto r_c, int slot, auto h_c) {
+        constexpr int r = decltype(r_c)::value, h = decltype(h_c)::value;
+        const uint32_t sb = lds0 + slot * STAGE + ch[h];
+        if constexpr (r < TN)
+            b[r][h] = ds_read_b128_off<r * 16 * ROWB>(sb + (BM + wn0 + lrow) * ROWB);
+        else
+            a[r - TN][h] = ds_read_b128_off<(r - TN) * 16 * ROWB>(sb + (wm0 + lrow) * ROWB);
+    };
+    auto half = [&](auto h_c, int slot, auto hr_c, auto reads_c) {
+        constexpr int h = decltype(h_c)::value;
+        static_for<0, TM * TN>([&](auto s_c) {
+            constexpr int st = decltype(s_c)::value;
+            acc[st / TN][st % TN] = mfma16<false>(a[st / TN][h], b[st % TN][h], acc[st / TN][st % TN]);
+            if constexpr (decltype(reads_c)::value && st < TM + TN) rd(s_c, slot, hr_c);
+            __builtin_amdgcn_sched_barrier(0);
+        });
+    };
+    using H0 = std::integral_constant<int, 0>;
+    using H1 = std::integral_constant<int, 1>;
+    __builtin_amdgcn_s_barrier();  // P
+    __builtin_amdgcn_s_barrier();  // B(0): tile 0 published
+    static_for<0, TM + TN>([&](auto r_c) { rd(r_c, 0, H0{}); });
+    lds_wait_all();
+    using RD = std::true_type;
+    for (int kt = 0; kt < nk - 1; ++kt) {
+        half(H0{}, kt % NS, H1{}, RD{});
+        lds_wait_all();
+        __builtin_amdgcn_s_barrier();  // B(kt+1): tile kt+1 published; slot kt is read
+        half(H1{}, (kt + 1) % NS, H0{}, RD{});
+        lds_wait_all();
+    }
+    half(H0{}, (nk - 1) % NS, H1{}, RD{});  // the last k-tile (no B(nk))
+    lds_wait_all();
+    half(H1{}, 0, H0{}, std::false_type{});
+    mfma_war_guard();
+    if constexpr (EPI == EPI_QKV_PREP)
+        qkv_prep_head<BM, 8, NS * STAGE>(p, m0, n0 >> 7, tid, smem, [&](float* tile, int c0, int CH) {
+            const int ccol = lane & 15, crow = (lane >> 4) * 4;
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int rb = wm0 + i * 16 - c0;
+                if (rb < 0 || rb >= CH) continue;
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) tile[(rb + crow + r) * PREP_LD + wn0 + j * 16 + ccol] = acc[i][j][r];
+            }
+        });
+    else
+        gemm_epilogue<TM, TN, false, EPI, 64>(p, acc, m0 + wm0, n0 + wn0, lane);
+}
+
+template <int BM, int BN, int EPI, int WQ, int NS>
+void launch_wsq_cfg(const GemmParams& p, hipStream_t s) {
+    if (p.N % BN != 0) throw std::runtime_error("gemm: the warp-specialized quantized tile needs N % 128 == 0");
+    if constexpr (EPI == EPI_QKV_PREP && BN != 128) {
+        throw std::runtime_error("gemm: the fused attention prep needs 128-wide column tiles");
+    } else {
+        const int nbm = (p.M + BM - 1) / BM;
+        hipLaunchKernelGGL((gemm_wsq_kernel<BM, BN, EPI, WQ, NS>), dim3(nbm * (p.N / BN)), dim3(512), 0, s, p);
+    }
+}
+
 template <int BM, int BN, int WM, int WN, int EPI, int WQ>
 void launch_q_cfg(const GemmParams& p, hipStream_t s) {
     const int nbm = (p.M + BM - 1) / BM;
@@ -667,6 +902,10 @@ void launch_q_variant(int variant, const GemmParams& p, hipStream_t s) {
         case 22: launch_qr_cfg<128, 4, EPI, WQ>(p, S, s); return;
         case 23: launch_qr_cfg<64, 4, EPI, WQ>(p, S, s); return;
         case 24: launch_qr_cfg<256, 4, EPI, WQ>(p, S, s); return;
+        case 25:
+            if (S > 1) throw std::runtime_error("gemm: no split-K for the warp-specialized quantized tile");
+            launch_wsq_cfg<192, 128, EPI, WQ, 3>(p, s);
+            return;
         default: break;
     }
     if (S > 1) throw std::runtime_error("gemm: split-K is for the register-dequant tiles");

@@ -351,7 +351,7 @@ ace_ggml_status ace_mi_kernel_gemm_q(int32_t qtype, int32_t epi, int32_t variant
         return ACE_GGML_ERR_INVALID_ARG;
     if (epi == EPI_RESID_GATED && !bias) return ACE_GGML_ERR_INVALID_ARG;
     const int vb = variant >= 0 ? (variant & 0xffff) : variant;  // (0x10000: forced past the picker's support check)
-    if (variant < -1 || variant > 0x1ffff || vb % 100 > 24 || vb > 424) return ACE_GGML_ERR_INVALID_ARG;
+    if (variant < -1 || variant > 0x1ffff || vb % 100 > 25 || vb > 424) return ACE_GGML_ERR_INVALID_ARG;
     try {
         std::vector<uint8_t> qp(quant::q_plane_bytes(t, N, K));
         std::vector<float> sp(quant::s_plane_floats(t, N, K));

@@ -9,7 +9,7 @@ extern "C" {
 
 // Force a GEMM kernel variant for subsequent launches (-1 = automatic).
 ace_ggml_status ace_mi_gemm_variant(int32_t variant) {
-    if (variant < -1 || variant % 100 > 24 || variant > 424) return ACE_GGML_ERR_INVALID_ARG;
+    if (variant < -1 || variant % 100 > 25 || variant > 424) return ACE_GGML_ERR_INVALID_ARG;
     acemi::gemm_force_variant(variant);
     return ACE_GGML_OK;
 }

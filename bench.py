@@ -34,6 +34,8 @@ Extra lines beside the headline (one GPU only; each the same 27-step schedule, t
   line_10s         10 s (T = 250, configs[0]'s shape) forward rate with the headline weights and with bf16
   lowmem_line      quantized weights with ACE_MI_QUANT_STAGE_SCOPE=layer (planes + one 117 MB bf16 slot,
                    expanded before every layer of every step) and its device-memory footprint
+  fused_line       quantized weights with ACE_MI_QUANT_STAGED=0: every quantized block linear through the
+                   dequant-fused GEMMs (no bf16 weight image), its memory and per-GEMM launch times
 `memory` reports the device bytes taken by the weights (after load_dit) and by the workspace (after the timed
 run; with the default `model` scope it holds the bf16 images of the quantized block weights).
 """
@@ -344,6 +346,33 @@ def main():
                                         "shared bf16 slot expanded before every layer of every step"),
                                  "weights_bytes": mw, "workspace_bytes": dev_used() - m0 - mw}
         os.environ.pop("ACE_MI_QUANT_STAGE_SCOPE", None)
+    # ---- dequant-fused quantized GEMMs (ACE_MI_QUANT_STAGED=0): no bf16 image of any block weight; the
+    #      quantized bytes are expanded inside the GEMM (register-dequant / warp-specialized tiles, gemm_q.hip)
+    if args.qtype and single and not args.no_extra_lines and os.environ.get("ACE_MI_QUANT_STAGED", "1") != "0":
+        br.close()
+        os.environ["ACE_MI_QUANT_STAGED"] = "0"
+        m0 = dev_used()
+        br = GGMLCAPIBridge(device=local, lib_path=lib_path) if lib_path else GGMLCAPIBridge(device=local)
+        br.load_dit(ckpt)
+        mw = dev_used() - m0
+        el_fu = timed(run)
+        extras["fused_line"] = {**line(B * args.steps, el_fu,
+                                       "the headline loop with ACE_MI_QUANT_STAGED=0: dequant-fused GEMMs for every "
+                                       "quantized block linear (no bf16 weight images)"),
+                                "weights_bytes": mw, "workspace_bytes": dev_used() - m0 - mw}
+        if not args.no_profile:
+            br.profile_enable(True)
+            br.profile_reset()
+            run(0, args.steps)
+            sync()
+            prof_f = br.profile_get()
+            br.profile_enable(False)
+            frac = block_linear_frac(prof_f, args.steps, T, b_loc, info)
+            if frac is not None:
+                extras["fused_line"]["dit_block_linears_frac_of_bf16_peak"] = frac
+            extras["fused_line"]["gemm_us_per_launch"] = {n: round(1000.0 * ms / max(c, 1), 2) for n, ms, c in prof_f
+                                                           if n.startswith("gemm_")}
+        os.environ.pop("ACE_MI_QUANT_STAGED", None)
     # ---- the same workload with bf16 weights, reported beside a quantized line (single GPU only)
     bf16_line = None
     if args.qtype and single and not args.no_bf16_line:

@@ -47,7 +47,7 @@ def test_staged_dequant_kernel_is_exact(qtype, N, K):
 
 
 @pytest.mark.parametrize("qtype", ["q8_0", "q4_k", "q6_k"])
-@pytest.mark.parametrize("variant", [-1, 1, 2, 3, 4, 5, 7, 20, 21, 22, 23, 24, 222, 223, 423])
+@pytest.mark.parametrize("variant", [-1, 1, 2, 3, 4, 5, 7, 20, 21, 22, 23, 24, 25, 222, 223, 423])
 @pytest.mark.parametrize("M,N,K", [(1, 256, 256), (300, 512, 512), (1000, 256, 2048), (129, 768, 6144)])
 def test_gemm_q_matches_dequantized_product(qtype, variant, M, N, K):
     """Both dequant-fused kernels (round 1's LDS-dequant tiles 1-7; the register-dequant tiles 20-24, + 100 S for
@@ -69,7 +69,7 @@ def test_gemm_q_matches_dequantized_product(qtype, variant, M, N, K):
 
 
 @pytest.mark.parametrize("qtype", ["q8_0", "q4_k", "q6_k"])
-@pytest.mark.parametrize("variant", [-1, 20, 21, 22, 23, 24, 222, 423])
+@pytest.mark.parametrize("variant", [-1, 20, 21, 22, 23, 24, 25, 222, 423])
 @pytest.mark.parametrize("epi", [2, 3])
 def test_gemm_q_residual_epilogues(qtype, variant, epi):
     """x += A.bf16(dequant(W))^T (* gate[n]) in place (the o / cross-o / down projections) through the

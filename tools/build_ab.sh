@@ -12,8 +12,9 @@ mkdir -p "$bld/ab_$name" "$out"
 objs=()
 for k in gemm gemm_q attention ops vae; do
     if [[ " $* " == *" $k "* ]]; then
+        kf=""; [ "$k" = gemm_q ] || [ "$k" = gemm ] || [ "$k" = ops ] && kf="-fno-slp-vectorize"  # (as the Makefile's KFLAGS_gemm*)
         (cd "$bld/ab_$name" && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -save-temps=obj -std=c++17 -fPIC -fvisibility=hidden \
-            -Wall -Wno-unused-result -ffp-contract=fast-honor-pragmas -munsafe-fp-atomics $flags -c "$src/kernels/$k.hip" \
+            -Wall -Wno-unused-result -ffp-contract=fast-honor-pragmas -munsafe-fp-atomics $kf $flags -c "$src/kernels/$k.hip" \
             -o "$bld/ab_$name/k_$k.o")
         objs+=("$bld/ab_$name/k_$k.o")
     else

@@ -20,7 +20,7 @@ def main():
             w = (rng.standard_normal((N, K)) * 0.02).astype(np.float32)
             blocks = capi.quantize(w, qtype)
             ref, scale = _q_ref(a, blocks, qtype)
-            for v in [v for v in (20, 21, 22, 23) for _ in range(int(os.environ.get("REPS", "1")))]:
+            for v in [v for v in [int(x) for x in os.environ.get("VARIANTS", "20,21,22,23").split(",")] for _ in range(int(os.environ.get("REPS", "1")))]:
                 got = capi.kernel_gemm_q(a, blocks, qtype, epi=0, variant=v | 0x10000)
                 bad = np.abs(got - ref) > 2e-6 * scale + 1e-6
                 rows, cols = np.nonzero(bad)
