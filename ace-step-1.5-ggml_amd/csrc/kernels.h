@@ -207,6 +207,7 @@ void launch_fault_tile(float* x, int ld, int rows, int row0, int col0, float amp
 // Test-only hooks (runtime/test_hooks.cpp): read from the environment in the self-test library only; the product
 // library's versions return "off"
 bool test_fault_from_env(int& layer, int& row, int& col, float& amp);
+bool test_vae_fault_from_env(int& block, int& row, int& col, float& amp);
 int gemm_override_from_env(int N, int K);
 // xt -= v * dt
 void launch_euler(float* xt, const float* v, int64_t n, float dt, hipStream_t s);

@@ -2,6 +2,8 @@
 // -DACEMI_TEST_HOOKS, Makefile SELFTEST): the product library is compiled without it and never reads them.
 //   ACE_MI_TEST_FAULT="layer,row,col,amp"  adds amp to one 16 x 128 tile of the residual after that layer's
 //                                          o-projection (the parity negative control, tests/test_gpu_parity_strict.py)
+//   ACE_MI_TEST_VAE_FAULT="block,row,col,amp"  adds amp to one 16 x 128 tile of the VAE decoder's residual stream
+//                                          after that block's first residual unit (tests/test_gpu_vae.py)
 //   ACE_MI_GEMM_OVERRIDE="N:K:variant,..." dense-weight GEMM tile picks per shape (in-loop A/B runs,
 //                                          tools/gpu_pick_inloop.sh)
 #include <array>
@@ -20,6 +22,14 @@ bool test_fault_from_env(int& layer, int& row, int& col, float& amp) {
     if (!f || !f[0]) return false;
     if (std::sscanf(f, "%d,%d,%d,%f", &layer, &row, &col, &amp) != 4)
         throw std::runtime_error("ACE_MI_TEST_FAULT must be layer,row,col,amp");
+    return true;
+}
+
+bool test_vae_fault_from_env(int& block, int& row, int& col, float& amp) {
+    const char* f = std::getenv("ACE_MI_TEST_VAE_FAULT");
+    if (!f || !f[0]) return false;
+    if (std::sscanf(f, "%d,%d,%d,%f", &block, &row, &col, &amp) != 4)
+        throw std::runtime_error("ACE_MI_TEST_VAE_FAULT must be block,row,col,amp");
     return true;
 }
 
@@ -42,6 +52,7 @@ int gemm_override_from_env(int N, int K) {
 }
 #else
 bool test_fault_from_env(int&, int&, int&, float&) { return false; }
+bool test_vae_fault_from_env(int&, int&, int&, float&) { return false; }
 int gemm_override_from_env(int, int) { return -1; }
 #endif
 

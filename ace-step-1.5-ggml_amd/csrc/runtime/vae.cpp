@@ -430,6 +430,10 @@ void VaeEngine::decode(const float* d_latents, int n_frames, float* d_out, hipSt
         for (int j = 0; j < 3; ++j) {
             const VaeSnake* next = j < 2 ? &b.res[j + 1].s1 : (i + 1 < m.blocks.size() ? &m.blocks[i + 1].s1 : &m.snake1);
             cur = run_res(b.res[j], (int)L, X, cur, cur == Sb ? Sc : Sb, j < 2 ? nullptr : Sa, next, s);
+            // test-only negative control: one 16 x 128 tile of the residual stream after the block's first unit (the
+            // next unit's input Snake was already formed from the clean X, so the fault enters through the residual)
+            if (j == 0 && fault_.block == (int)i)
+                launch_fault_tile(X, b.ct.cout, (int)(L * items), fault_.row, fault_.col, fault_.amp, s);
         }
     }
     // decoder.snake1 (applied into Sa) -> decoder.conv2

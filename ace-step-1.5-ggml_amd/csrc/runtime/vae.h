@@ -81,6 +81,8 @@ public:
     explicit VaeEngine(int device) : device_(device) {
         const char* e = std::getenv("ACE_MI_VAE_FUSE_RES");
         fuse_res_ = !(e && e[0] == '0');
+        // TEST ONLY (self-test library builds): ACE_MI_TEST_VAE_FAULT, runtime/test_hooks.cpp
+        if (!test_vae_fault_from_env(fault_.block, fault_.row, fault_.col, fault_.amp)) fault_.block = -1;
     }
     ~VaeEngine();
     VaeModel& model() { return model_; }
@@ -109,6 +111,10 @@ private:
     int items_ = 1;  // sequences per conv launch during decode (ConvGemmArgs::items)
     // 128-channel residual units as one launch (ConvGemmArgs::W2); ACE_MI_VAE_FUSE_RES=0: two launches
     bool fuse_res_ = true;
+    struct {
+        int block = -1, row = 0, col = 0;
+        float amp = 0.f;
+    } fault_;  // test-only negative control (ACE_MI_TEST_VAE_FAULT)
     const VaeRes* fused2_ = nullptr;  // set while run_conv launches the fused k7 + k1 of this unit
     void run_conv(const VaeConv& c, const uint16_t* S, int T_in, int T_out, float* X, bool resid, bool store,
                   uint16_t* S_out, const VaeSnake* next, hipStream_t s);

@@ -30,15 +30,23 @@ from .dit_oracle import read_safetensors
 from .ggml_numerics import round_f16
 
 
-# Test-only knob (as ggml_numerics.MULMAT_PERTURB): relative perturbation of every conv result, used
-# to measure the decoder's own sensitivity to f32 summation order (fp16 re-rounding of every conv
-# input amplifies it) -- the floor two correct implementations agree to.
+# Test-only knob (as ggml_numerics.MULMAT_PERTURB): relative perturbation of every conv result, used to measure the
+# decoder's own sensitivity to f32 summation order (fp16 re-rounding of every conv input amplifies it) -- the floor
+# two correct implementations agree to.  Independent per-element noise y * (1 + p * N(0, 1)) (PERTURB_RNG, re-seeded by
+# the floor helpers), like the DiT oracle's: a different summation order changes each dot product by ~1e-7 with no
+# correlation between elements.  (Rounds 1-4 scaled every conv output coherently by (1 + p), which the next Snake and
+# fp16 rounding see as a smooth change: a looser floor for the L2 statistic and none for the element-wise one.)
 CONV_PERTURB = 0.0
+PERTURB_RNG = np.random.default_rng(0)
+# the restatement of the VAE's test-only ACE_MI_TEST_VAE_FAULT hook (runtime/vae.cpp): (block, row, col, amp) adds amp
+# to rows [row, row + 16) x channels [col, col + 128) of the residual stream after the block's first residual unit
+FAULT = None
 
 
 def _perturb(y):
     if CONV_PERTURB:
-        return (y.astype(np.float64) * (1.0 + CONV_PERTURB)).astype(np.float32)
+        noise = PERTURB_RNG.standard_normal(y.shape)
+        return (y.astype(np.float64) * (1.0 + CONV_PERTURB * noise)).astype(np.float32)
     return y
 
 
@@ -171,24 +179,32 @@ class VaeWeights:
             self.enc = enc
 
 
-def residual_unit(ru, x):
-    """residual_forward (:724-733)."""
+def residual_unit(ru, x, skip=None):
+    """residual_forward (:724-733): skip + conv2(snake2(conv1(snake1(x)))), skip = x (the test-only FAULT restatement
+    passes a different skip: the faulted residual stream beside the clean unit input)."""
     y = conv1d(snake(x, **ru["snake1"]), ru["conv1"]["w"], ru["conv1"]["b"], ru["dil"], 3 * ru["dil"])
     y = conv1d(snake(y, **ru["snake2"]), ru["conv2"]["w"], ru["conv2"]["b"], 1, 0)
-    n = min(len(x), len(y))
-    cx, cy = (len(x) - n) // 2, (len(y) - n) // 2
-    return (x[cx:cx + n] + y[cy:cy + n]).astype(np.float32)
+    skip = x if skip is None else skip
+    n = min(len(skip), len(y))
+    cx, cy = (len(skip) - n) // 2, (len(y) - n) // 2
+    return (skip[cx:cx + n] + y[cy:cy + n]).astype(np.float32)
 
 
 def decode(W: VaeWeights, latents: np.ndarray) -> np.ndarray:
     """forward_decode (:957-1002): latents [T][C_lat] -> audio [T*hop][audio_channels]."""
     x = conv1d(np.asarray(latents, np.float32), W.conv1["w"], W.conv1["b"], 1, 3)
-    for blk in W.blocks:
+    for bi, blk in enumerate(W.blocks):
         s = blk["stride"]
         x = snake(x, **blk["snake1"])
         x = conv_transpose1d(x, blk["conv_t1"]["w"], blk["conv_t1"]["b"], s, (s + 1) // 2)
-        for ru in blk["res"]:
-            x = residual_unit(ru, x)
+        skip = None
+        for ri, ru in enumerate(blk["res"]):
+            x = residual_unit(ru, x, skip)
+            skip = None
+            if FAULT is not None and FAULT[0] == bi and ri == 0:  # ACE_MI_TEST_VAE_FAULT, restated: the engine adds
+                _, r0, c0, amp = FAULT                             # the tile to the f32 residual stream after the unit;
+                skip = x.copy()                                    # the next unit's input Snake was already formed
+                skip[r0:r0 + 16, c0:c0 + 128] = (skip[r0:r0 + 16, c0:c0 + 128] + np.float32(amp)).astype(np.float32)
     x = snake(x, **W.snake1)
     return conv1d(x, W.conv2["w"], None, 1, 3)
 
@@ -209,16 +225,31 @@ def encode(W: VaeWeights, audio: np.ndarray) -> np.ndarray:
     return x[:, :W.cfg.decoder_input_channels].copy()
 
 
-def decode_with_floor(W: VaeWeights, latents, perturb: float = 1e-6):
-    """(audio, floor): decode() and its relative L2 change under a `perturb` relative change of
-    every conv result (see CONV_PERTURB)."""
-    global CONV_PERTURB
-    out = decode(W, latents)
+def decode_with_floor(W: VaeWeights, latents, perturb: float = 1e-7):
+    """(audio, floor): decode() and its relative L2 change under an independent `perturb` relative
+    perturbation of every conv result element (see CONV_PERTURB)."""
+    out, floor, _ = decode_with_floor_stats(W, latents, perturb=perturb)
+    return out, floor
+
+
+def floor_stats(fn, perturb: float = 1e-7):
+    """(out, floor_l2, floor_maxabs) of a decode-like callable: its output, and the relative L2 and the element-wise
+    max|pert - out| / rms(out) of its change when every conv result element is perturbed (the DiT oracle's
+    forward_with_floor_stats, restated for the decoder)."""
+    global CONV_PERTURB, PERTURB_RNG
+    out = fn()
     old = CONV_PERTURB
     CONV_PERTURB = perturb
+    PERTURB_RNG = np.random.default_rng(12345)
     try:
-        pert = decode(W, latents)
+        pert = fn()
     finally:
         CONV_PERTURB = old
-    floor = float(np.linalg.norm(pert.astype(np.float64) - out) / np.linalg.norm(out.astype(np.float64)))
-    return out, floor
+    o64, p64 = out.astype(np.float64), pert.astype(np.float64)
+    floor = float(np.linalg.norm(p64 - o64) / np.linalg.norm(o64))
+    maxabs = float(np.max(np.abs(p64 - o64)) / np.sqrt(np.mean(o64 * o64)))
+    return out, floor, maxabs
+
+
+def decode_with_floor_stats(W: VaeWeights, latents, perturb: float = 1e-7):
+    return floor_stats(lambda: decode(W, latents), perturb=perturb)

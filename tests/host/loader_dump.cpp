@@ -41,6 +41,8 @@ void launch_conv_gemm(const ConvGemmArgs&, hipStream_t) {}
 void launch_to_f16(const float*, int64_t, uint16_t*, hipStream_t) {}
 void launch_pack_f16(const float*, int64_t, int, int, uint16_t*, hipStream_t) {}
 void launch_conv_out(const uint16_t*, int, int, const uint16_t*, int, float*, hipStream_t, int) {}
+void launch_fault_tile(float*, int, int, int, int, float, hipStream_t) {}
+bool test_vae_fault_from_env(int&, int&, int&, float&) { return false; }
 }  // namespace acemi
 
 namespace {

@@ -3,8 +3,11 @@ oracle restatement of ace_vae::forward_decode (oracle/vae_oracle.py).
 
 Tolerance: every conv re-rounds its input to fp16 (ggml im2col), so any f32 difference (summation
 order, a 1-ulp sinf) can flip an fp16 rounding and propagate; the bound is
-max(1e-3, FLOOR_K * floor), floor = the oracle's own rel-L2 change when every conv result is
-perturbed by 1e-6 (vae_oracle.decode_with_floor)."""
+max(1e-3, FLOOR_K * floor), floor = the oracle's own rel-L2 change when every conv result element is
+perturbed by independent 1e-7 relative noise (vae_oracle.floor_stats, as the DiT oracle's floor); the
+full-size decodes also assert the element-wise max|gpu - ref| / rms(ref) <= MAXABS_K x the oracle's own
+spread of that statistic (test_gpu_forward.check), which a wrong conv output tile fails even where the L2
+absorbs it (test_vae_fault_injection_is_caught)."""
 import tempfile
 
 import numpy as np
@@ -34,14 +37,18 @@ def tiny_vae():
     br.close()
 
 
-def _check(got, ref, floor, tag):
+def _check(got, ref, floor, tag, floor_max=None):
     got = np.asarray(got, np.float64)
     ref = np.asarray(ref, np.float64)
     assert got.shape == ref.shape, (got.shape, ref.shape)
+    if floor_max is not None:  # rel-L2 and the element-wise bound (test_gpu_forward.check)
+        from test_gpu_forward import check
+        return check(got, ref, floor, tag, floor_max)
     l2 = float(np.linalg.norm(got - ref) / np.linalg.norm(ref))
     bound = max(REL_L2, FLOOR_K * floor)
     print(f"{tag}: rel_l2={l2:.3e} floor={floor:.3e} bound={bound:.3e} max_abs={np.abs(got - ref).max():.3e}")
     assert np.isfinite(l2) and l2 <= bound, (tag, l2, floor)
+    return l2
 
 
 @pytest.mark.parametrize("T", [1, 20, 37])
@@ -138,18 +145,57 @@ def test_halo_staged_residual_convs_equal_generic(tiny_vae, T, monkeypatch):
 @pytest.mark.parametrize("T", [6, 5])
 def test_full_size_vae_decode(T):
     """The real ACE-Step 1.5 decoder shape (128 x [1,2,4,8,16] channels, strides 10,6,4,4,2,
-    hop 1920) on 6 / 5 latent frames (11520 / 9600 samples; 5: ragged 128-row tiles in the 128-channel blocks)."""
+    hop 1920) on 6 / 5 latent frames (11520 / 9600 samples; 5: ragged 128-row tiles in the 128-channel blocks),
+    rel-L2 and element-wise against the oracle's noise floor."""
     from acestep_mi355x.capi import GGMLCAPIBridge
     from acestep_mi355x.synthetic import VAE_FULL_CONFIG
-    from oracle.vae_oracle import VaeWeights, decode_with_floor
+    from oracle.vae_oracle import VaeWeights, decode_with_floor_stats
     d = _ckpt(VAE_FULL_CONFIG)
     br = GGMLCAPIBridge()
     br.load_vae(d)
     lat = np.random.default_rng(11).standard_normal((T, 64)).astype(np.float32)
     got = br.vae_decode_tfirst(lat)
     br.close()
-    ref, floor = decode_with_floor(VaeWeights(d), lat)
-    _check(got, ref, floor, f"full VAE T={T}")
+    ref, floor, fmax = decode_with_floor_stats(VaeWeights(d), lat)
+    _check(got, ref, floor, f"full VAE T={T}", fmax)
+
+
+# one corrupted tile: 16 samples x 128 channels of the residual stream after block 3's first residual unit
+# (the 128 x 2-channel block, 4800 rows at T = 5 frames), restated in the oracle as vae_oracle.FAULT
+VAE_FAULT = (3, 2000, 0, 0.02)
+
+
+def test_vae_fault_injection_is_caught(monkeypatch):
+    """Negative control: a wrong conv output tile inside the decoder passes the rel-L2 bound but fails the element-wise
+    bound; the faulted GPU output equals the oracle with the same fault restated (so the failure is the fault's)."""
+    from acestep_mi355x.capi import GGMLCAPIBridge, selftest_library_path
+    from acestep_mi355x.synthetic import VAE_FULL_CONFIG
+    from oracle import vae_oracle as V
+    from test_gpu_forward import FLOOR_K as FK, MAXABS_K, check, maxabs_rms, rel_errors
+    d = _ckpt(VAE_FULL_CONFIG)
+    lat = np.random.default_rng(11).standard_normal((5, 64)).astype(np.float32)
+    W = V.VaeWeights(d)
+    ref, floor, fmax = V.decode_with_floor_stats(W, lat)
+    monkeypatch.setenv("ACE_MI_TEST_VAE_FAULT", ",".join(str(v) for v in VAE_FAULT))
+    br = GGMLCAPIBridge(lib_path=selftest_library_path())  # the fault hook is read by the self-test library only
+    try:
+        br.load_vae(d)
+        bad = br.vae_decode_tfirst(lat)
+    finally:
+        br.close()
+    l2, _ = rel_errors(bad, ref)
+    ma = maxabs_rms(bad, ref)
+    print(f"VAE faulted: rel_l2={l2:.3e} (bound {max(REL_L2, FK * floor):.3e}) maxabs/rms={ma:.3e} "
+          f"(bound {MAXABS_K * fmax:.3e}, ratio {ma / fmax:.2f})")
+    assert l2 <= max(REL_L2, FK * floor), "the L2 bound alone would have caught it: raise the control's subtlety"
+    with pytest.raises(AssertionError):
+        check(bad, ref, floor, "VAE negative control: faulted run", fmax)
+    V.FAULT = VAE_FAULT
+    try:
+        fref = V.decode(W, lat)
+    finally:
+        V.FAULT = None
+    check(bad, fref, floor, "VAE faulted GPU vs faulted oracle", fmax)
 
 
 @pytest.mark.parametrize("n", [120, 126, 600])
@@ -162,12 +208,7 @@ def test_tiny_vae_encode(tiny_vae, n):
     audio = np.random.default_rng(n).standard_normal((n, 2)).astype(np.float32)
     W = VaeWeights(d)
     ref = encode(W, audio)
-    V.CONV_PERTURB = 1e-6
-    try:
-        pert = encode(W, audio)
-    finally:
-        V.CONV_PERTURB = 0.0
-    floor = float(np.linalg.norm(pert - ref) / np.linalg.norm(ref))
+    _, floor, _ = V.floor_stats(lambda: encode(W, audio))
     assert br.vae_enc_out_len(n) == ref.shape[0]
     got = br.vae_encode_tfirst(audio)
     _check(got[:ref.shape[0]], ref, floor, f"tiny VAE encode n={n}")
