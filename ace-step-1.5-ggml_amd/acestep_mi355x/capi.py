@@ -46,7 +46,7 @@ EXPORTED_SYMBOLS = (
 # Every symbol declared in include/acestep_mi355x_selftest.h: the TEST library (libacestep_mi355x_selftest.so = the
 # product objects + the kernel self-test / micro-benchmark entries); the product library does not export them.
 SELFTEST_SYMBOLS = ("ace_mi_kernel_gemm", "ace_mi_kernel_attention", "ace_mi_bench_attention", "ace_mi_bench_gemm",
-                    "ace_mi_kernel_gemm_q", "ace_mi_kernel_dequant", "ace_mi_bench_gemm_q")
+                    "ace_mi_kernel_gemm_q", "ace_mi_kernel_dequant", "ace_mi_bench_gemm_q", "ace_mi_kernel_gemm_a8")
 
 # qtype codes of ace_mi_quantize & co. (names as parse_quant_type, acestep_dit_model.cpp:27-37)
 QTYPES = {"q8_0": 1, "q4_k": 2, "q6_k": 3}
@@ -225,6 +225,9 @@ def load_selftest_library() -> ctypes.CDLL:
     lib.ace_mi_kernel_dequant.restype = ctypes.c_int
     lib.ace_mi_bench_gemm_q.argtypes = [i32, i32, i32, i32, i32, i32, i32, fp]
     lib.ace_mi_bench_gemm_q.restype = ctypes.c_int
+    i8p = ctypes.POINTER(ctypes.c_int8)
+    lib.ace_mi_kernel_gemm_a8.argtypes = [i32, i32, i32, i32, i32, fp, u8p, fp, fp, i8p, fp, fp]
+    lib.ace_mi_kernel_gemm_a8.restype = ctypes.c_int
     _SELFTEST = lib
     return lib
 
@@ -698,6 +701,30 @@ def kernel_gemm_q(a_bits: np.ndarray, w_blocks: np.ndarray, qtype: str, epi: int
     if st != ACE_GGML_OK:
         raise RuntimeError(f"ace_mi_kernel_gemm_q failed (status={st})")
     return out
+
+
+def kernel_gemm_a8(x: np.ndarray, w_blocks: np.ndarray, qtype: str, epi: int = 0, bias: Optional[np.ndarray] = None,
+                   x0: Optional[np.ndarray] = None):
+    """ggml-faithful quantized-activation GEMM (ACE_MI_QUANT_ACT=q8): x f32 [M][K] quantized on the device, then the
+    integer-dot GEMM against ggml block rows w_blocks [N][nb][bb].  epi 0: acc (+ bias); 3: x0 + (acc + bias);
+    7: silu(g) * u.  Returns (out, q int8 [M][K], s f32 [K/32][M], bsum f32 [K/32][M])."""
+    lib = load_selftest_library()
+    xa = np.ascontiguousarray(x, dtype=np.float32)
+    w = np.ascontiguousarray(w_blocks, dtype=np.uint8)
+    M, K = xa.shape
+    N = w.shape[0]
+    ncol = N // 2 if epi == 7 else N
+    out = np.ascontiguousarray(x0, dtype=np.float32).copy() if epi == 3 else np.empty((M, ncol), np.float32)
+    q = np.empty((M, K), np.int8)
+    s = np.empty((K // 32, M), np.float32)
+    bs = np.empty((K // 32, M), np.float32)
+    b = None if bias is None else np.ascontiguousarray(bias, dtype=np.float32)
+    st = lib.ace_mi_kernel_gemm_a8(QTYPES[qtype], epi, M, N, K, _fptr(xa), w.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
+                                   _fptr(b), _fptr(out), q.ctypes.data_as(ctypes.POINTER(ctypes.c_int8)), _fptr(s),
+                                   _fptr(bs))
+    if st != ACE_GGML_OK:
+        raise RuntimeError(f"ace_mi_kernel_gemm_a8 failed (status={st})")
+    return out, q, s, bs
 
 
 def bench_gemm_q(M: int, N: int, K: int, qtype: str, variant: int = -1, epi: int = 0, iters: int = 20) -> float:

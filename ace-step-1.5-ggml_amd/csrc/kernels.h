@@ -48,6 +48,7 @@ enum GemmEpiKind : int {
                             // (sections present per prep.q_col / k_col / v_col >= 0), written straight into
                             // the attention layouts of `prep` (QK-RMSNorm, RoPE, fp16 hi/lo, V^T); 128-wide
                             // column tiles only, no bias
+    EPI_SWIGLU_F32 = 7,     // EPI_SWIGLU with an f32 output c_f32 (the quantized-activation GEMM only)
 };
 
 struct GemmEpilogue {
@@ -104,6 +105,38 @@ struct DequantJob {
 };
 void launch_dequant_bf16_batch(const DequantJob* jobs, int n, hipStream_t s);
 
+// ------------------------------------------------- ggml-faithful quantized activations (kernels/gemm_a8.hip)
+// ggml's mul_mat against a quantized weight first converts the f32 activation rows to the weight's vec_dot_type
+// (Q8_0 blocks for Q8_0 weights, Q8_K for K-quants) and takes integer dot products per block
+// (ggml-metal-embed.metal:222-227, 3110-3128; ggml-cpu quantize_row_q8_0 / quantize_row_q8_K_ref / vec_dot_*).
+// ACE_MI_QUANT_ACT=q8 runs the DiT that way (DitEngine::forward_qact).
+// Activation blocks on the device: q int8 [M][K]; s f32 [K/32][ld_s] per 32-value block (Q8_0: fp16(d);
+// Q8_K: the 256-block's d in each of its eight 32-blocks); bsum f32 [K/32][ld_s] = sum of the block's q (Q8_K
+// only: the Q4_K min term).  ld_s >= M rounded up to 128 (the GEMM reads whole 128-row tiles of s / bsum).
+enum QActKind : int { QACT_Q8_0 = 0, QACT_Q8_K = 1 };
+struct QAct {
+    int kind = QACT_Q8_0;
+    const int8_t* q = nullptr;
+    const float* s = nullptr;
+    const float* bsum = nullptr;
+    int64_t ld_s = 0;
+};
+inline int qact_kind_for(int weight_fmt) { return weight_fmt == WF_Q8_0 ? QACT_Q8_0 : QACT_Q8_K; }
+// x f32 [M][ldx] (silu first when silu_in) -> the blocks of `kind` in q / s / bsum (layout above)
+void launch_quantize_act(int kind, const float* x, int64_t ldx, int M, int K, bool silu_in, int8_t* q, float* s,
+                         float* bsum, int64_t ld_s, hipStream_t st);
+// C = dequant(A blocks) . dequant(W)^T with ggml's per-block integer dot products (v_mfma_i32_16x16x32_i8) and an
+// f32 sum of d_w * d_a * isum over the blocks; W quantized (WF_Q8_0 with QACT_Q8_0, WF_Q4_K / WF_Q6_K with
+// QACT_Q8_K); the epilogues of launch_gemm plus EPI_SWIGLU_F32 (a bias on EPI_RESID adds to the product first).
+// N % 128 == 0, K % 32 (Q8_0) / % 256 (K-quants) == 0.
+void launch_gemm_a8(const QAct& a, const WeightView& W, int M, int N, int K, const GemmEpilogue& epi, hipStream_t s);
+// launch_rmsnorm_mod's operator with an f32 output [M][H]
+void launch_rmsnorm_mod_f32(const float* x, int M, int H, const float* w, const float* scale, const float* shift,
+                            int64_t mod_stride, int rows_per_item, float eps, float* out, hipStream_t s);
+// launch_pack_input's packing with f32 output [B*Np][P*Cin]
+void launch_pack_input_f32(const float* hidden, const float* context, int B, int T, int Np, int P, int audio_dim,
+                           int ctx_dim, float* out, hipStream_t s);
+
 // ------------------------------------------------------------ attention
 // Flash-style fp16 attention, f32 softmax/accumulate.  D = 128.
 // Qh [B][Hq][nq_pad][128] f16, Kh [B][Hkv][nk_pad][128] f16,
@@ -132,6 +165,9 @@ struct AttnArgs {
     int fused_merge = 0;  // set by launch_attention: the last part of a key-split group merges (no merge kernel)
     int split_from = 0;  // set by launch_attention: > 0 = tail split (blocks [0, split_from) whole, the rest in two
                          // key-range parts; ksplit = 2 gives the partials' layout)
+    // f32 output [B*nq][Hq*128] instead of `out` (the ggml-faithful quantized-activation mode, whose next linear
+    // quantizes the f32 rows): every block runs as two key-range parts (needs `part`), merged into f32
+    float* out_f32 = nullptr;
     bool f8 = false;  // f8c mode (needs split + pv_split): the lo planes hold fp8 hi / lo operands (prep_math.h), the
                       // correction products Kl.Qh + Kh.Ql and Vl.Ph + Vh.Pl run as block-scaled fp8 MFMAs
 };

@@ -1216,7 +1216,7 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
 // part whose keys were all masked), out = sum w_k O_k / sum w_k l_k; a row with no unmasked key at all stays
 // 0/0 = NaN as in ggml.  Half a wave per row, 16-byte partial reads, every load issued before the first use.
 // TAIL (tail split, AttnArgs::split_from): only the rows of the split blocks F.., 128 (query, head) rows per block.
-template <bool F16OUT, int S, bool TAIL = false>
+template <bool F16OUT, int S, bool TAIL = false, bool OUTF32 = false>
 __global__ void __launch_bounds__(256) attn_merge_kernel(AttnArgs a) {
     const int64_t rows = (int64_t)a.B * a.nq * a.Hq;
     int64_t r = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
@@ -1255,6 +1255,10 @@ __global__ void __launch_bounds__(256) attn_merge_kernel(AttnArgs a) {
     }
     const float inv = 1.0f / den;
     // row r = (b * nq + q) * Hq + head: out[b][q][head*128 + d] is contiguous in r * 128 + d
+    if constexpr (OUTF32) {
+        *(float4*)(a.out_f32 + r * D + d) = make_float4(v[0] * inv, v[1] * inv, v[2] * inv, v[3] * inv);
+        return;
+    }
     *(uint2*)(a.out + r * D + d) =
         make_uint2((uint32_t)to_act<F16OUT>(v[0] * inv) | ((uint32_t)to_act<F16OUT>(v[1] * inv) << 16),
                    (uint32_t)to_act<F16OUT>(v[2] * inv) | ((uint32_t)to_act<F16OUT>(v[3] * inv) << 16));
@@ -1389,6 +1393,12 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s) {
         b.fused_merge = fm;
     }
     b.split_from = b.fused_merge ? 0 : b.split_from;
+    if (a.out_f32) {  // f32 output: every block in two key-range parts, merged into f32 rows
+        ACEMI_CHECK(a.part != nullptr, "attention: f32 output needs the partials workspace");
+        b.ksplit = 2;
+        b.split_from = 0;
+        b.fused_merge = 0;
+    }
     const int64_t n_blk = (int64_t)a.B * a.Hkv * n_qt;
     // XCD-aware order (attn_block): whole multiples of 8 launch indices per range
     const dim3 grid(b.split_from > 0 ? (unsigned)(b.split_from + 8 * ((2 * (n_blk - b.split_from) + 7) / 8))
@@ -1414,7 +1424,9 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s) {
         const int64_t rows = (int64_t)a.B * a.nq * a.Hq;
         ACEMI_CHECK(b.ksplit == 2 || b.ksplit == 4, "attention: the merge handles 2 or 4 key-split parts");
         const dim3 mgrid((unsigned)((rows + 7) / 8));
-        if (b.split_from > 0) {
+        if (a.out_f32) {
+            hipLaunchKernelGGL((attn_merge_kernel<false, 2, false, true>), mgrid, dim3(256), 0, s, b);
+        } else if (b.split_from > 0) {
             const dim3 tgrid((unsigned)((n_blk - b.split_from) * 16));  // 128 rows per split block, 8 per workgroup
             if (out_t == ActType::F16)
                 hipLaunchKernelGGL((attn_merge_kernel<true, 2, true>), tgrid, dim3(256), 0, s, b);

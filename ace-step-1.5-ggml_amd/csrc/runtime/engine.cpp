@@ -25,6 +25,7 @@ DitEngine::DitEngine(int device) : device_(device) {
     stage_per_call_ = !(h && std::strcmp(h, "layer") == 0);
     stage_model_ = !(h && (std::strcmp(h, "call") == 0 || std::strcmp(h, "layer") == 0));  // default: model
     if (const char* pf = std::getenv("ACE_MI_WEIGHT_PREFETCH")) prefetch_blocks_ = std::max(0, std::atoi(pf));
+    qact_ = quant_act_from_env();
     // TEST ONLY (self-test library builds): ACE_MI_TEST_FAULT, runtime/test_hooks.cpp
     if (!test_fault_from_env(fault_.layer, fault_.row, fault_.col, fault_.amp)) fault_.layer = -1;
 }
@@ -32,7 +33,8 @@ DitEngine::DitEngine(int device) : device_(device) {
 DitEngine::~DitEngine() {
     for (Buf* b : {&a0_, &x_, &act_, &attn_, &act2_, &qkv_, &qh_, &kh_, &vt_, &kbias_, &enc_act_, &encp_, &ckv_, &kc_,
                    &vc_, &kbias_c_, &attn_part_, &freq_, &freq_act_, &th_, &th_act_, &temb_t_, &temb_r_, &temb_act_, &proj_,
-                   &mods_, &outmod_, &cos_, &sin_, &ein_, &knorm_tab_, &ts_proj_, &ts_temb_t_, &ts_temb_r_}) {
+                   &mods_, &outmod_, &cos_, &sin_, &ein_, &knorm_tab_, &ts_proj_, &ts_temb_t_, &ts_temb_r_, &qf_, &qa_,
+                   &qs_, &qb_, &encf_}) {
         if (b->p) (void)hipFree(b->p);
     }
     if (pf_stream_) {
@@ -285,6 +287,10 @@ void DitEngine::rope_for(int Np, hipStream_t s) {
 }
 
 void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
+    if (qact_) {
+        forward_qact(io, s);
+        return;
+    }
     const DitModel& m = model_;
     const DitConfig& c = m.cfg;
     const ActType at = m.act;
@@ -657,6 +663,10 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
 
 void DitEngine::timestep_embed(const float* t, const float* r, int rows, float* proj, float* temb_t, float* temb_r,
                                hipStream_t s) {
+    if (qact_) {
+        timestep_embed_qact(t, r, rows, proj, temb_t, temb_r, s);
+        return;
+    }
     const DitModel& m = model_;
     const int H = m.cfg.hidden;
     const float log_max = std::log(10000.0f);

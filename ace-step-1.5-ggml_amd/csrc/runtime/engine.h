@@ -142,6 +142,18 @@ class DitEngine {
     bool fused_prep_ = true;      // EPI_QKV_PREP (ACE_MI_UNFUSED_PREP=1: f32 store + attn_prep)
     void qkv_gemm(const uint16_t* act, const WeightView& w, int M, int N, PrepArgs pa, float* scratch,
                   const char* name, hipStream_t s);
+    // ggml-faithful quantized-activation mode (ACE_MI_QUANT_ACT=q8, runtime/engine_qact.cpp): every linear with a
+    // block-format weight quantizes its f32 input rows to Q8_0 / Q8_K blocks and runs the integer-dot GEMM
+    // (launch_gemm_a8), the activations between the linears stay f32 (RMSNorm, attention output, SwiGLU), and
+    // attention runs at the f32 precision -- the arithmetic of the reference's ggml graph.  A parity mode: the
+    // product path keeps bf16 activations.
+    bool qact_ = false;
+    Buf qf_, qa_, qs_, qb_, encf_;  // f32 activation rows, their int8 blocks, block scales / sums, f32 condition
+    void forward_qact(const ForwardIO& io, hipStream_t s);
+    void qlinear(const float* x, int64_t ldx, int M, const WeightView& w, int N, int K, const GemmEpilogue& e,
+                 const char* name, hipStream_t s, bool silu_in = false);
+    void timestep_embed_qact(const float* t, const float* r, int rows, float* proj, float* temb_t, float* temb_r,
+                             hipStream_t s);
     // Staged dequant of quantized block weights (ACE_MI_QUANT_STAGED, default on; 0 = the dequant-fused GEMMs):
     // right before each layer its Q8_0 / Q4_K / Q6_K matrices are expanded to their bf16 image
     // (launch_dequant_bf16, bit-identical to the dequant-fused GEMM's LDS tiles) in one workspace slot, and

@@ -19,6 +19,13 @@ DitModel::~DitModel() {
     for (void* p : allocs) (void)hipFree(p);
 }
 
+bool quant_act_from_env() {
+    const char* e = std::getenv("ACE_MI_QUANT_ACT");
+    if (!e || !e[0] || std::strcmp(e, "bf16") == 0) return false;
+    if (std::strcmp(e, "q8") == 0) return true;
+    throw std::runtime_error("ACE_MI_QUANT_ACT must be bf16 or q8");
+}
+
 void load_config(const std::string& path, DitConfig& c) {
     // acestep_dit_config.cpp:19-93 (required keys + optional ones)
     std::string text;
@@ -174,6 +181,11 @@ void load_dit_model(const std::string& dir, DitModel& m, int& status_hint) {
             m.te[e].bp = L.vec_f32(p2 + "time_proj.bias", 6LL * H);
             if (a1 != a2 || a2 != a3) throw Unsupported("mixed timestep weight types");
             m.te[e].act = a1;
+            if (quant_act_from_env()) {
+                m.te[e].q1 = L.finish(L.mat(p2 + "linear_1.weight", H, fin));
+                m.te[e].q2 = L.finish(L.mat(p2 + "linear_2.weight", H, H));
+                m.te[e].qp = L.finish(L.mat(p2 + "time_proj.weight", 6LL * H, H));
+            }
         }
         std::vector<float> tables((size_t)c.layers * 6 * H);
         std::vector<Mat> ckv(c.layers);  // cross k|v rows per layer, uploaded as one matrix below

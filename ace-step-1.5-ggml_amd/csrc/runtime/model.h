@@ -96,6 +96,9 @@ struct DevTimestep {
     float* b1 = nullptr;
     float* b2 = nullptr;
     float* bp = nullptr;
+    // the same three weights in their ggml block format, kept only for the quantized-activation mode
+    // (ACE_MI_QUANT_ACT=q8 at load: ggml multiplies Q8 activation blocks with the quantized weights themselves)
+    DevWeight q1, q2, qp;
 };
 
 struct DitModel {
@@ -123,6 +126,10 @@ struct DitModel {
 
     ~DitModel();
 };
+
+// ACE_MI_QUANT_ACT=q8: the ggml-faithful quantized-activation mode (DitEngine::forward_qact); anything else (the
+// default, "bf16") = the product arithmetic, bf16 activations x bf16(dequant(W))
+bool quant_act_from_env();
 
 // Throws std::runtime_error with a reference-style message on failure.
 // `status_hint` receives 3 (IO) or 4 (UNSUPPORTED) for the ABI status code.

@@ -398,6 +398,72 @@ ace_ggml_status ace_mi_kernel_gemm_q(int32_t qtype, int32_t epi, int32_t variant
     return ACE_GGML_OK;
 }
 
+// ggml-faithful quantized-activation GEMM (kernels/gemm_a8.hip): x f32 [M][K] -> Q8_0 / Q8_K blocks on the device
+// (returned in q_out [M][K], s_out [K/32][M], bsum_out [K/32][M] when non-null), then the integer-dot GEMM against
+// ggml block rows W [N][K] with epilogue epi: 0 f32 store (+ bias), 3 residual (out_f32 holds x on entry; + bias),
+// 7 SwiGLU f32 (out [M][N/2], gate|up interleaved in 16-column groups).
+ace_ggml_status ace_mi_kernel_gemm_a8(int32_t qtype, int32_t epi, int32_t M, int32_t N, int32_t K, const float* x,
+                                      const uint8_t* W_blocks, const float* bias, float* out_f32, int8_t* q_out,
+                                      float* s_out, float* bsum_out) {
+    using namespace acemi;
+    const auto t = static_cast<quant::QType>(qtype);
+    if (!x || !W_blocks || !out_f32 || M <= 0 || N % 128 != 0) return ACE_GGML_ERR_INVALID_ARG;
+    if (t != quant::Q8_0 && t != quant::Q4_K && t != quant::Q6_K) return ACE_GGML_ERR_INVALID_ARG;
+    if (!quant::applies(t, K)) return ACE_GGML_ERR_INVALID_ARG;
+    if (epi != EPI_STORE_F32 && epi != EPI_RESID && epi != EPI_SWIGLU_F32) return ACE_GGML_ERR_UNSUPPORTED;
+    try {
+        const int64_t ld_s = (M + 127) / 128 * 128;
+        const int nb = K / 32;
+        const int ncol = epi == EPI_SWIGLU_F32 ? N / 2 : N;
+        std::vector<uint8_t> qp(quant::q_plane_bytes(t, N, K));
+        std::vector<float> sp(quant::s_plane_floats(t, N, K));
+        quant::to_planes(t, W_blocks, N, K, qp.data(), sp.data());
+        DevMem dX((size_t)M * K * 4), dQ(qp.size()), dS(sp.size() * 4), dB((size_t)N * 4), dC((size_t)M * ncol * 4),
+            dAq((size_t)M * K), dAs((size_t)nb * ld_s * 4), dAb((size_t)nb * ld_s * 4);
+        ACEMI_HIP(hipMemcpy(dX.p, x, (size_t)M * K * 4, hipMemcpyHostToDevice));
+        ACEMI_HIP(hipMemcpy(dQ.p, qp.data(), qp.size(), hipMemcpyHostToDevice));
+        ACEMI_HIP(hipMemcpy(dS.p, sp.data(), sp.size() * 4, hipMemcpyHostToDevice));
+        ACEMI_HIP(hipMemset(dAs.p, 0, (size_t)nb * ld_s * 4));
+        ACEMI_HIP(hipMemset(dAb.p, 0, (size_t)nb * ld_s * 4));
+        if (bias) ACEMI_HIP(hipMemcpy(dB.p, bias, (size_t)N * 4, hipMemcpyHostToDevice));
+        if (epi == EPI_RESID) ACEMI_HIP(hipMemcpy(dC.p, out_f32, (size_t)M * N * 4, hipMemcpyHostToDevice));
+        ACEMI_HIP(hipDeviceSynchronize());
+        QAct a;
+        a.kind = t == quant::Q8_0 ? QACT_Q8_0 : QACT_Q8_K;
+        a.q = dAq.as<int8_t>();
+        a.s = dAs.as<float>();
+        a.bsum = dAb.as<float>();
+        a.ld_s = ld_s;
+        launch_quantize_act(a.kind, dX.as<float>(), K, M, K, false, dAq.as<int8_t>(), dAs.as<float>(), dAb.as<float>(),
+                            ld_s, nullptr);
+        GemmEpilogue e;
+        e.kind = epi;
+        e.bias = bias ? dB.as<float>() : nullptr;
+        e.c_f32 = dC.as<float>();
+        e.ldc = ncol;
+        WeightView w;
+        w.fmt = t == quant::Q8_0 ? WF_Q8_0 : (t == quant::Q4_K ? WF_Q4_K : WF_Q6_K);
+        w.q = dQ.p;
+        w.s = dS.as<float>();
+        launch_gemm_a8(a, w, M, N, K, e, nullptr);
+        ACEMI_HIP(hipDeviceSynchronize());
+        ACEMI_HIP(hipMemcpy(out_f32, dC.p, (size_t)M * ncol * 4, hipMemcpyDeviceToHost));
+        if (q_out) ACEMI_HIP(hipMemcpy(q_out, dAq.p, (size_t)M * K, hipMemcpyDeviceToHost));
+        for (int b = 0; b < nb; ++b) {
+            if (s_out)
+                ACEMI_HIP(hipMemcpy(s_out + (size_t)b * M, dAs.as<float>() + (size_t)b * ld_s, (size_t)M * 4,
+                                    hipMemcpyDeviceToHost));
+            if (bsum_out)
+                ACEMI_HIP(hipMemcpy(bsum_out + (size_t)b * M, dAb.as<float>() + (size_t)b * ld_s, (size_t)M * 4,
+                                    hipMemcpyDeviceToHost));
+        }
+    } catch (const std::exception& ex) {
+        std::fprintf(stderr, "ace_mi_kernel_gemm_a8: %s\n", ex.what());
+        return ACE_GGML_ERR;
+    }
+    return ACE_GGML_OK;
+}
+
 // Dequant-fused GEMM micro-benchmark (random N(0, 0.02) weights quantized with the loader's encoder).
 ace_ggml_status ace_mi_bench_gemm_q(int32_t qtype, int32_t epi, int32_t variant, int32_t M, int32_t N, int32_t K,
                                     int32_t iters, float* avg_ms) {

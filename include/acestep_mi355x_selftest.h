@@ -49,6 +49,14 @@ ACE_GGML_API ace_ggml_status ace_mi_kernel_gemm_q(int32_t qtype, int32_t epi, in
  * bf16(dequant(W)) [N][K] for ggml block rows W [N][K]. */
 ACE_GGML_API ace_ggml_status ace_mi_kernel_dequant(int32_t qtype, int32_t N, int32_t K, const uint8_t* W_blocks,
                                                    uint16_t* out);
+/* ggml-faithful quantized-activation GEMM (ACE_MI_QUANT_ACT=q8): x f32 [M][K] quantized on the device to Q8_0
+ * (Q8_0 weights) or Q8_K (K-quants) blocks -- returned as q_out int8 [M][K], s_out f32 [K/32][M] (block scale d),
+ * bsum_out f32 [K/32][M] (sum of q per 32, Q8_K) when non-null -- then ggml's per-block integer dot products against
+ * the ggml block rows W [N][K].  epi 0: out [M][N] = acc (+ bias); 3: out += acc (+ bias); 7: out [M][N/2] =
+ * silu(g) * u (gate|up interleaved in 16-column groups). */
+ACE_GGML_API ace_ggml_status ace_mi_kernel_gemm_a8(int32_t qtype, int32_t epi, int32_t M, int32_t N, int32_t K,
+                                                   const float* x, const uint8_t* W_blocks, const float* bias,
+                                                   float* out_f32, int8_t* q_out, float* s_out, float* bsum_out);
 /* Dequant-fused GEMM micro-benchmark: average ms per launch (HIP events). */
 ACE_GGML_API ace_ggml_status ace_mi_bench_gemm_q(int32_t qtype, int32_t epi, int32_t variant, int32_t M, int32_t N,
                                                  int32_t K, int32_t iters, float* avg_ms);

@@ -251,9 +251,10 @@ def dequantize_q4_k(raw: np.ndarray) -> np.ndarray:
     return y.reshape(rows, nb * 256).astype(np.float32)
 
 
-def q8_k_activation_roundtrip(x: np.ndarray) -> np.ndarray:
+def quantize_q8_k_activations(x: np.ndarray):
     """quantize_row_q8_K_ref: per 256-block iscale = -127/max (max = signed value of
-    largest magnitude), q = min(127, nearest_int(iscale*x)), d = 1/iscale (f32)."""
+    largest magnitude, the first one on ties), q = min(127, nearest_int(iscale*x)),
+    d = 1/iscale (f32); an all-zero block is d = 0, q = 0.  Returns (d f32 [rows, nb], q int8 [rows, nb, 256])."""
     x = np.asarray(x, dtype=np.float32)
     rows, k = x.shape
     blk = x.reshape(rows, k // QK_K, QK_K)
@@ -261,9 +262,15 @@ def q8_k_activation_roundtrip(x: np.ndarray) -> np.ndarray:
     mxv = np.take_along_axis(blk, idx[:, :, None], axis=2)[:, :, 0]
     zero = mxv == 0
     iscale = np.where(zero, np.float32(0.0), np.float32(-127.0) / np.where(zero, 1, mxv)).astype(np.float32)
-    q = np.minimum(_nearest_int(iscale[:, :, None] * blk), 127).astype(np.float32)
+    q = np.minimum(_nearest_int(iscale[:, :, None] * blk), 127).astype(np.int8)
     d = np.where(zero, np.float32(0.0), np.float32(1.0) / np.where(zero, 1, iscale)).astype(np.float32)
-    return (q * d[:, :, None]).reshape(rows, k).astype(np.float32)
+    return d, q
+
+
+def q8_k_activation_roundtrip(x: np.ndarray) -> np.ndarray:
+    d, q = quantize_q8_k_activations(x)
+    rows = d.shape[0]
+    return (q.astype(np.float32) * d[:, :, None]).reshape(rows, -1).astype(np.float32)
 
 
 # --------------------------------------------------------------------------

@@ -240,7 +240,10 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t) {
         touch(a.k, a.split ? a.k_plane + nk : nk);
         touch(a.vt, a.pv_split ? a.v_plane + nk : nk);
         if (a.kbias) touch(a.kbias, (int64_t)a.B * a.nk_pad);
-        touch(a.out, (int64_t)a.B * a.nq * a.Hq * D);
+        if (a.out_f32)
+            touch(a.out_f32, (int64_t)a.B * a.nq * a.Hq * D);
+        else
+            touch(a.out, (int64_t)a.B * a.nq * a.Hq * D);
     }
     std::vector<double> s((size_t)a.nk_pad), o((size_t)D);
     auto val = [&](const uint16_t* base, int64_t idx, int64_t plane) {
@@ -279,10 +282,163 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t) {
                         o[d] += p * val(a.vt, (((int64_t)b * a.Hkv + hk) * D + d) * a.nk_pad + pk,
                                         a.pv_split ? a.v_plane : 0);
                 }
+                if (a.out_f32) {  // f32 output (quantized-activation mode)
+                    float* of = a.out_f32 + ((int64_t)b * a.nq + q) * a.Hq * D + h * D;
+                    for (int d = 0; d < D; ++d) of[d] = (float)(o[d] / sum);
+                    continue;
+                }
                 uint16_t* out = a.out + ((int64_t)b * a.nq + q) * a.Hq * D + h * D;
                 for (int d = 0; d < D; ++d) out[d] = to_act(out_t == ActType::F16, (float)(o[d] / sum));  // 0/0 -> NaN
             }
         }
+}
+
+// ---- quantized-activation mode (kernels/gemm_a8.hip), restated
+void launch_quantize_act(int kind, const float* x, int64_t ldx, int M, int K, bool sl, int8_t* q, float* s, float* bs,
+                         int64_t ld_s, hipStream_t) {
+    ACEMI_CHECK(M >= 1 && ld_s >= M && ldx >= K, "quantize_act: bad shape");
+    const int QK = kind == QACT_Q8_0 ? 32 : 256;
+    ACEMI_CHECK(K % QK == 0, "quantize_act: K");
+    for (int m = 0; m < M; ++m)
+        for (int b0 = 0; b0 < K; b0 += QK) {
+            float v[256];
+            float amax = 0.f, mx = 0.f;
+            for (int i = 0; i < QK; ++i) {
+                v[i] = sl ? silu(x[(int64_t)m * ldx + b0 + i]) : x[(int64_t)m * ldx + b0 + i];
+                if (std::fabs(v[i]) > amax) {
+                    amax = std::fabs(v[i]);
+                    mx = v[i];
+                }
+            }
+            int8_t* qr = q + (int64_t)m * K + b0;
+            if (kind == QACT_Q8_0) {
+                const float d = amax / 127.0f, id = amax != 0.f ? 127.0f / amax : 0.f;
+                for (int i = 0; i < 32; ++i) qr[i] = (int8_t)std::nearbyint(v[i] * id);
+                s[(int64_t)(b0 / 32) * ld_s + m] = f16f(to_f16(d));
+                continue;
+            }
+            const float iscale = amax != 0.f ? -127.0f / mx : 0.f;
+            for (int j = 0; j < 8; ++j) {
+                int sum = 0;
+                for (int i = 32 * j; i < 32 * j + 32; ++i) {
+                    qr[i] = amax != 0.f ? (int8_t)std::min(127, (int)std::nearbyint(iscale * v[i])) : 0;
+                    sum += qr[i];
+                }
+                s[(int64_t)(b0 / 32 + j) * ld_s + m] = amax != 0.f ? 1.0f / iscale : 0.f;
+                bs[(int64_t)(b0 / 32 + j) * ld_s + m] = (float)sum;
+            }
+        }
+}
+
+void launch_gemm_a8(const QAct& a, const WeightView& W, int M, int N, int K, const GemmEpilogue& e, hipStream_t st) {
+    ACEMI_CHECK(weight_quantized(W.fmt) && a.kind == qact_kind_for(W.fmt), "gemm_a8: format mismatch");
+    ACEMI_CHECK(M >= 1 && N % 128 == 0 && a.ld_s >= (M + 127) / 128 * 128, "gemm_a8: bad shape");
+    touch(a.s, (int64_t)(K / 32 - 1) * a.ld_s + (M + 127) / 128 * 128);
+    std::vector<float> acc((size_t)M * N);
+    const int nb = K / 32;
+    for (int m = 0; m < M; ++m)
+        for (int n = 0; n < N; ++n) {
+            double sum = 0;
+            for (int b = 0; b < nb; ++b) {
+                const float da = a.s[(int64_t)b * a.ld_s + m];
+                for (int k = 32 * b; k < 32 * b + 32; ++k) {
+                    float w;  // the dequantized weight element in f32 (not rounded to bf16)
+                    if (W.fmt == WF_Q8_0) {
+                        w = (float)((const int8_t*)W.q)[(int64_t)n * K + k] * W.s[(int64_t)n * nb + b];
+                    } else if (W.fmt == WF_Q6_K) {
+                        w = (float)((const int8_t*)W.q)[(int64_t)n * K + k] * W.s[(int64_t)n * (K / 16) + k / 16];
+                    } else {
+                        const int i = k % 32, dw = i / 8, r = i % 8;
+                        const uint8_t byte = ((const uint8_t*)W.q)[(int64_t)n * (K / 2) + b * 16 + dw * 4 + (r & 3)];
+                        const int qv = r < 4 ? (byte & 0xF) : (byte >> 4);
+                        const float* sm = W.s + ((int64_t)n * nb + b) * 2;
+                        w = (float)qv * sm[0] - sm[1];
+                    }
+                    sum += (double)a.q[(int64_t)m * K + k] * da * w;
+                }
+            }
+            acc[(size_t)m * N + n] = (float)sum;
+        }
+    if (e.kind == EPI_QKV_PREP) {
+        PrepArgs pa = e.prep;
+        pa.src = acc.data();
+        pa.ld = N;
+        launch_attn_prep(pa, st);
+        return;
+    }
+    for (int m = 0; m < M; ++m) {
+        if (e.kind == EPI_SWIGLU_F32 || e.kind == EPI_SWIGLU) {
+            for (int n = 0; n < N; n += 32)
+                for (int j = 0; j < 16; ++j) {
+                    const float g = acc[(size_t)m * N + n + j], u = acc[(size_t)m * N + n + 16 + j];
+                    if (e.kind == EPI_SWIGLU_F32)
+                        e.c_f32[(int64_t)m * e.ldc + (n >> 1) + j] = silu(g) * u;
+                    else
+                        e.c_act[(int64_t)m * e.ldc + (n >> 1) + j] = to_bf16(silu(g) * u);
+                }
+            continue;
+        }
+        for (int n = 0; n < N; ++n) {
+            float v = acc[(size_t)m * N + n];
+            switch (e.kind) {
+                case EPI_STORE_F32:
+                    e.c_f32[(int64_t)m * e.ldc + n] = e.bias ? v + e.bias[n] : v;
+                    break;
+                case EPI_RESID_GATED: {
+                    if (e.bias) v += e.bias[n];
+                    float* xp = e.c_f32 + (int64_t)m * e.ldc + n;
+                    *xp = *xp + v * e.gate[(int64_t)(m / e.rows_per_item) * e.gate_stride + n];
+                    break;
+                }
+                case EPI_RESID:
+                    e.c_f32[(int64_t)m * e.ldc + n] += e.bias ? v + e.bias[n] : v;
+                    break;
+                case EPI_PROJ_OUT: {
+                    const int item = m / e.rows_per_item, pp = m - item * e.rows_per_item;
+                    const int kpos = n / e.out_ch, c = n - kpos * e.out_ch, t = pp * e.patch + kpos;
+                    if (t < e.out_T) e.c_f32[((int64_t)item * e.out_T + t) * e.out_ch + c] = v + e.bias[c];
+                    break;
+                }
+                default: throw std::runtime_error("emul gemm_a8: bad epilogue");
+            }
+        }
+    }
+}
+
+void launch_rmsnorm_mod_f32(const float* x, int M, int H, const float* w, const float* scale, const float* shift,
+                            int64_t mod_stride, int rows_per_item, float eps, float* out, hipStream_t) {
+    for (int m = 0; m < M; ++m) {
+        const float* xr = x + (int64_t)m * H;
+        double ss = 0;
+        for (int i = 0; i < H; ++i) ss += (double)xr[i] * xr[i];
+        const float sc = 1.0f / sqrtf((float)(ss / H) + eps);
+        const int item = m / rows_per_item;
+        for (int i = 0; i < H; ++i) {
+            float y = xr[i] * sc * w[i];
+            if (scale) y = y * (scale[(int64_t)item * mod_stride + i] + 1.0f) + shift[(int64_t)item * mod_stride + i];
+            out[(int64_t)m * H + i] = y;
+        }
+    }
+}
+
+void launch_pack_input_f32(const float* hidden, const float* context, int B, int T, int Np, int P, int audio, int cdim,
+                           float* out, hipStream_t) {
+    const int cin = audio + cdim;
+    for (int b = 0; b < B; ++b)
+        for (int p = 0; p < Np; ++p)
+            for (int k = 0; k < P; ++k)
+                for (int c = 0; c < cin; ++c) {
+                    const int tt = p * P + k;
+                    float v = 0.f;
+                    if (tt < T) {
+                        if (c < cdim) {
+                            if (context) v = context[((int64_t)b * T + tt) * cdim + c];
+                        } else if (hidden) {
+                            v = hidden[((int64_t)b * T + tt) * audio + (c - cdim)];
+                        }
+                    }
+                    out[((int64_t)b * Np + p) * P * cin + (int64_t)k * cin + c] = v;
+                }
 }
 
 void launch_pack_input(ActType t, const float* hidden, const float* context, int B, int T, int Np, int P, int audio,

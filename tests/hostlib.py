@@ -8,7 +8,7 @@ import tempfile
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "ace-step-1.5-ggml_amd", "csrc")
 CLANG = "/opt/rocm/llvm/bin/clang++"
-RUNTIME = ("json.cpp", "gguf.cpp", "quant.cpp", "model.cpp", "blocks.cpp", "engine.cpp", "text_encoder.cpp", "vae.cpp",
+RUNTIME = ("json.cpp", "gguf.cpp", "quant.cpp", "model.cpp", "blocks.cpp", "engine.cpp", "engine_qact.cpp", "text_encoder.cpp", "vae.cpp",
            "abi.cpp", "cond.cpp", "text.cpp", "generate.cpp", "util_abi.cpp", "selftest.cpp", "test_hooks.cpp")
 
 

@@ -19,7 +19,7 @@ import numpy as np
 import pytest
 
 from test_gpu_forward import check
-from test_gpu_quant import QUANT_FLOOR_K, engine_view
+from test_gpu_quant import engine_view
 
 pytestmark = [pytest.mark.gpu, pytest.mark.slow]
 
@@ -123,31 +123,38 @@ def test_config2_q8_0_sampling_loop_240s(monkeypatch):
 
 @pytest.mark.parametrize("qtype,T,seed", [("q8_0", 6000, 2), ("q4_k", 15000, 4)])
 def test_quantized_configs_full_width(monkeypatch, qtype, T, seed):
-    """configs[2] (Q8_0, 240 s) and configs[4] (Q4_K, 600 s) at full width: vs the oracle on the same
-    quantized bytes with the engine's arithmetic (bf16 activations x bf16(dequant W)), floor-relative,
-    and vs ggml's own Q8_0 / Q8_K activation quantization within QUANT_FLOOR_K x that path's floor."""
+    """configs[2] (Q8_0, 240 s) and configs[4] (Q4_K, 600 s) at full width, 2 layers:
+      * the product path (bf16 activations x bf16(dequant W)) vs the oracle on the same quantized bytes with that
+        arithmetic, floor-relative, element-wise too;
+      * the ggml-faithful mode (ACE_MI_QUANT_ACT=q8: Q8_0 / Q8_K activation blocks, integer block dots, f32
+        activations between the linears) vs the oracle with ggml's own activation quantization, within 1.5x that
+        path's floor, element-wise too.  The product path's distance to ggml's semantics is printed (reported)."""
     from acestep_mi355x import capi
     from acestep_mi355x.capi import GGMLCAPIBridge
     from acestep_mi355x.synthetic import cached_checkpoint, make_config
     from oracle import ggml_numerics
-    from oracle.dit_oracle import DitWeights, forward_with_floor, forward_with_floor_stats
+    from oracle.dit_oracle import DitWeights, forward_with_floor_stats
     d = cached_checkpoint(make_config(num_hidden_layers=2), seed=0, backend="torch")
     monkeypatch.setenv("ACE_GGML_DIT_MAX_LAYERS", "2")
     monkeypatch.setenv("ACE_GGML_DIT_WEIGHT_QTYPE", qtype)
     L = 512
     h, c, e = _inputs(T, L, seed)
-    br = GGMLCAPIBridge()
-    br.load_dit(d)
-    got = br.dit_forward_tfirst(h, c, e, None, None, 0.75, 0.75)
-    br.close()
+    got = {}
+    for mode in ("bf16", "q8"):
+        monkeypatch.setenv("ACE_MI_QUANT_ACT", mode)
+        br = GGMLCAPIBridge()
+        br.load_dit(d)
+        got[mode] = br.dit_forward_tfirst(h, c, e, None, None, 0.75, 0.75)
+        br.close()
     monkeypatch.setattr(ggml_numerics, "QUANTIZER", capi.quantize)  # byte-identical C++ encoder (K-quants)
     W = DitWeights(d, qtype=qtype)
     ref, floor, fmax = forward_with_floor_stats(engine_view(W), h, c, e, None, None, T, L, 0.75, 0.75, max_layers=2)
-    check(got, ref, floor, f"{qtype} T={T} (dequant semantics)", fmax)
-    gref, gfloor = forward_with_floor(W, h, c, e, None, None, T, L, 0.75, 0.75, max_layers=2)
-    l2 = float(np.linalg.norm(got.astype(np.float64) - gref) / np.linalg.norm(gref.astype(np.float64)))
-    print(f"{qtype} T={T} vs ggml Q8 activation semantics: rel_l2={l2:.3e} floor={gfloor:.3e} ratio={l2 / gfloor:.2f}")
-    assert l2 <= QUANT_FLOOR_K * gfloor, (l2, gfloor)
+    check(got["bf16"], ref, floor, f"{qtype} T={T} product path (dequant semantics)", fmax)
+    gref, gfloor, gfmax = forward_with_floor_stats(W, h, c, e, None, None, T, L, 0.75, 0.75, max_layers=2)
+    l2 = float(np.linalg.norm(got["bf16"].astype(np.float64) - gref) / np.linalg.norm(gref.astype(np.float64)))
+    print(f"{qtype} T={T} product path vs ggml Q8 activation semantics (reported): rel_l2={l2:.3e} "
+          f"floor={gfloor:.3e} ratio={l2 / gfloor:.2f}")
+    check(got["q8"], gref, gfloor, f"{qtype} T={T} ACE_MI_QUANT_ACT=q8 (ggml semantics)", gfmax)
 
 
 def test_config3_batch8_240s_every_item():

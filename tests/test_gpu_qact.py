@@ -1,0 +1,93 @@
+"""GPU parity of the ggml-faithful quantized-activation mode (ACE_MI_QUANT_ACT=q8, kernels/gemm_a8.hip).
+
+ggml's mul_mat against a quantized weight converts the f32 activations to Q8_0 / Q8_K blocks and takes integer
+dot products per block (oracle/ggml_numerics.py convert_activation + mul_mat; ggml-metal-embed.metal:3110-3128).
+Checked here:
+  * the activation quantizers bit for bit against the oracle's restatement (q, d and the Q8_K block sums);
+  * the integer-dot GEMM against an fp64 product of the same dequantized blocks (its f32 sum of exact per-block
+    integer dots differs from fp64 by f32 rounding only), with each epilogue the mode uses;
+Whole DiT forwards in this mode against the oracle WITH ggml's activation quantization (within 1.5x the oracle's own
+floor) are test_gpu_quant.py::test_quantized_full_width_vs_ggml_semantics and
+test_gpu_configs.py::test_quantized_configs_full_width."""
+import numpy as np
+import pytest
+
+
+pytestmark = pytest.mark.gpu
+
+
+def _capi():
+    from acestep_mi355x import capi
+    return capi
+
+
+def _deq(w_blocks, qtype):
+    from oracle import ggml_numerics as g
+    return {"q8_0": lambda r: g.dequantize_q8_0(*g.unpack_q8_0(r)), "q4_k": g.dequantize_q4_k,
+            "q6_k": g.dequantize_q6_k}[qtype](w_blocks).astype(np.float64)
+
+
+def _act_blocks(x, qtype):
+    """oracle activation blocks: (q int8 [M][K], d per 32-value block [K/32][M], block sums [K/32][M] or None)"""
+    from oracle import ggml_numerics as g
+    M, K = x.shape
+    if qtype == "q8_0":
+        d, q = g.quantize_q8_0_activations(x)
+        return q.reshape(M, K), d.astype(np.float32).T, None
+    d, q = g.quantize_q8_k_activations(x)
+    q = q.reshape(M, K)
+    d32 = np.repeat(d, 8, axis=1).T
+    bs = q.reshape(M, K // 32, 32).astype(np.int64).sum(axis=2).astype(np.float32).T
+    return q, d32, bs
+
+
+@pytest.mark.parametrize("qtype", ["q8_0", "q4_k", "q6_k"])
+@pytest.mark.parametrize("M,N,K", [(1, 128, 256), (77, 256, 512), (300, 384, 2048), (129, 128, 6144)])
+def test_gemm_a8_matches_block_integer_dot(qtype, M, N, K):
+    capi = _capi()
+    rng = np.random.default_rng(M * 7 + K + len(qtype))
+    x = rng.standard_normal((M, K)).astype(np.float32)
+    x[:, :32] *= 40.0  # a block of large values, all-zero blocks, exact ties of the largest |x| (the first wins)
+    if K >= 512:
+        x[:, 256:288] = 0.0
+        x[0, 300], x[0, 301] = 100.0, -100.0
+    if K >= 1024 and M > 1:
+        x[1, 512:768] = 0.0
+    x[0, 40], x[0, 41] = 3.0, -3.0
+    w = (rng.standard_normal((N, K)) * 0.02).astype(np.float32)
+    blocks = capi.quantize(w, qtype)
+    out, q, s, bs = capi.kernel_gemm_a8(x, blocks, qtype)
+    qr, dr, bsr = _act_blocks(x, qtype)
+    np.testing.assert_array_equal(q, qr)
+    np.testing.assert_array_equal(s, dr)
+    if bsr is not None:
+        np.testing.assert_array_equal(bs, bsr)
+    xa = (qr.reshape(M, K // 32, 32).astype(np.float64) * dr.T[:, :, None]).reshape(M, K)
+    ref = xa @ _deq(blocks, qtype).T
+    mag = np.abs(xa) @ np.abs(_deq(blocks, qtype)).T
+    err = np.abs(out - ref)
+    assert np.all(err <= 5e-6 * mag + 1e-30), float(np.max(err / (mag + 1e-30)))
+
+
+@pytest.mark.parametrize("qtype", ["q8_0", "q4_k"])
+def test_gemm_a8_epilogues(qtype):
+    """bias store, residual with bias (x + (acc + b): ggml adds the bias to the mul_mat result), SwiGLU in f32"""
+    capi = _capi()
+    rng = np.random.default_rng(5)
+    M, N, K = 200, 256, 512
+    x = rng.standard_normal((M, K)).astype(np.float32)
+    w = (rng.standard_normal((N, K)) * 0.05).astype(np.float32)
+    b = rng.standard_normal(N).astype(np.float32)
+    blocks = capi.quantize(w, qtype)
+    qr, dr, _ = _act_blocks(x, qtype)
+    xa = (qr.reshape(M, K // 32, 32).astype(np.float64) * dr.T[:, :, None]).reshape(M, K)
+    ref = xa @ _deq(blocks, qtype).T
+    got, *_ = capi.kernel_gemm_a8(x, blocks, qtype, epi=0, bias=b)
+    np.testing.assert_allclose(got, ref + b, rtol=1e-5, atol=1e-5)
+    x0 = rng.standard_normal((M, N)).astype(np.float32)
+    got, *_ = capi.kernel_gemm_a8(x, blocks, qtype, epi=3, bias=b, x0=x0)
+    np.testing.assert_allclose(got, x0 + (ref + b), rtol=1e-5, atol=1e-5)
+    got, *_ = capi.kernel_gemm_a8(x, blocks, qtype, epi=7)
+    gcols = np.concatenate([np.arange(grp * 32, grp * 32 + 16) for grp in range(N // 32)])
+    g, u = ref[:, gcols], ref[:, gcols + 16]
+    np.testing.assert_allclose(got, g / (1.0 + np.exp(-g)) * u, rtol=1e-5, atol=1e-5)

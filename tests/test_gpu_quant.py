@@ -157,43 +157,41 @@ def test_quantized_tiny_matches_dequant_semantics(tiny_ckpt, monkeypatch, qtype)
     print(f"tiny {qtype}: vs ggml Q8-activation semantics rel_l2={l2:.3e} (ggml floor {ggml_ref[1]:.3e})")
 
 
-QUANT_FLOOR_K = 2.5
-
-
 @pytest.mark.slow
 @pytest.mark.parametrize("qtype", ["q8_0", "q4_k"])
 def test_quantized_full_width_vs_ggml_semantics(monkeypatch, qtype):
-    """Full width, 2 layers, vs the oracle WITH ggml's activation quantization (Q8_0 blocks for Q8_0
-    weights, Q8_K for K-quants).  8-bit activation rounding amplifies any f32 difference much
-    harder than bf16 does: the oracle's own 1e-7-perturbation spread is ~7e-3 here (1.1e-2 at 8
-    layers), so the bound is QUANT_FLOOR_K x that floor (measured ratio ~1.8 on the CPU model of
-    the engine's arithmetic; DESIGN.md "Parity")."""
+    """Full width, 2 layers, T = 400, against the oracle WITH ggml's activation quantization (Q8_0 blocks for Q8_0
+    weights, Q8_K for K-quants): the ggml-faithful mode (ACE_MI_QUANT_ACT=q8, kernels/gemm_a8.hip) within 1.5x the
+    oracle's own floor, element-wise too.  The product path (bf16 activations) is checked against its own arithmetic
+    and its distance to ggml's semantics printed: 8-bit activation rounding amplifies any f32 difference much harder
+    than bf16 does, so that distance sits at 1.3-1.6x the ggml path's floor (DESIGN.md "Parity")."""
     from acestep_mi355x.capi import GGMLCAPIBridge
     from acestep_mi355x.synthetic import cached_checkpoint, make_config
-    from oracle.dit_oracle import DitWeights, forward_with_floor
+    from oracle.dit_oracle import DitWeights, forward_with_floor, forward_with_floor_stats
     cfg = make_config(num_hidden_layers=2)
     d = cached_checkpoint(cfg, seed=0, backend="torch")
     monkeypatch.setenv("ACE_GGML_DIT_MAX_LAYERS", "2")
     monkeypatch.setenv("ACE_GGML_DIT_WEIGHT_QTYPE", qtype)
-    br = GGMLCAPIBridge()
-    br.load_dit(d)
     rng = np.random.default_rng(77)
     T, L = 400, 64
     h = rng.standard_normal((T, 64)).astype(np.float32)
     c = np.concatenate([rng.standard_normal((T, 64)), np.ones((T, 64))], axis=1).astype(np.float32)
     e = rng.standard_normal((L, 2048)).astype(np.float32)
-    got = br.dit_forward_tfirst(h, c, e, None, None, 0.8, 0.8)
-    br.close()
+    got = {}
+    for mode in ("bf16", "q8"):
+        monkeypatch.setenv("ACE_MI_QUANT_ACT", mode)
+        br = GGMLCAPIBridge()
+        br.load_dit(d)
+        got[mode] = br.dit_forward_tfirst(h, c, e, None, None, 0.8, 0.8)
+        br.close()
     W = DitWeights(d, qtype=qtype)
-    ref, floor = forward_with_floor(W, h, c, e, None, None, T, L, 0.8, 0.8, max_layers=2)
-    l2, mx = rel_errors(got, ref)
-    cos = float(np.dot(got.ravel().astype(np.float64), ref.ravel()) /
-                (np.linalg.norm(got.astype(np.float64)) * np.linalg.norm(ref.astype(np.float64))))
-    print(f"full-width {qtype} vs ggml semantics: rel_l2={l2:.3e} floor={floor:.3e} ratio={l2 / floor:.2f} "
-          f"cos={cos:.6f}")
-    assert l2 <= QUANT_FLOOR_K * floor and cos >= 0.999, (l2, floor, cos)
+    ref, floor, fmax = forward_with_floor_stats(W, h, c, e, None, None, T, L, 0.8, 0.8, max_layers=2)
+    l2, _ = rel_errors(got["bf16"], ref)
+    print(f"full-width {qtype} product path vs ggml semantics (reported): rel_l2={l2:.3e} floor={floor:.3e} "
+          f"ratio={l2 / floor:.2f}")
+    check(got["q8"], ref, floor, f"full-width {qtype} ACE_MI_QUANT_ACT=q8 (ggml semantics)", fmax)
     eng = forward_with_floor(engine_view(W), h, c, e, None, None, T, L, 0.8, 0.8, max_layers=2)
-    check(got, eng[0], eng[1], f"full-width {qtype} (dequant semantics)")
+    check(got["bf16"], eng[0], eng[1], f"full-width {qtype} product path (dequant semantics)")
 
 
 # ---------------------------------------------------------------- GGUF weights (a14 / SURVEY §8f)

@@ -79,6 +79,26 @@ def test_dit_forward_online_quantized(host_lib, tiny_ckpt, monkeypatch, qtype):
     br.close()
 
 
+@pytest.mark.parametrize("qtype", ["q8_0", "q4_k", "q6_k"])
+def test_dit_forward_quant_act_ggml_semantics(host_lib, tiny_ckpt, monkeypatch, qtype):
+    """ACE_MI_QUANT_ACT=q8 (DitEngine::forward_qact): f32 activations quantized to Q8_0 / Q8_K blocks before every
+    quantized linear, against the oracle's ggml semantics (no engine_view) -- the orchestration of the mode, with
+    the host restatement of its kernels; the sampler entry's precomputed timestep rows take the same path."""
+    from oracle.dit_oracle import DitWeights, forward_with_floor
+    monkeypatch.setenv("ACE_GGML_DIT_WEIGHT_QTYPE", qtype)
+    monkeypatch.setenv("ACE_MI_QUANT_ACT", "q8")
+    br = bridge(host_lib)
+    br.load_dit(tiny_ckpt)
+    h, c, e = inputs(9, 70, 11)
+    got = br.dit_forward_tfirst(h, c, e, None, None, 0.7, 0.4)
+    ref, floor = forward_with_floor(DitWeights(tiny_ckpt, qtype=qtype), h, c, e, None, None, 70, 11, 0.7, 0.4)
+    assert rel(got, ref) <= max(1e-3, 1.5 * floor), (rel(got, ref), floor)
+    dq, dq_floor = forward_with_floor(engine_view(DitWeights(tiny_ckpt, qtype=qtype)), h, c, e, None, None, 70, 11,
+                                      0.7, 0.4)
+    assert rel(got, dq) > rel(got, ref), "the mode should sit closer to ggml's arithmetic than to bf16 activations"
+    br.close()
+
+
 @pytest.mark.parametrize("quant", ["Q8", "Q4", "F16"])
 def test_dit_forward_gguf(host_lib, tiny_ckpt, quant):
     from acestep_mi355x.synthetic import write_gguf
