@@ -271,6 +271,7 @@ def main():
     # ---- per-kernel timing (HIP events on the launch stream, one event pair per launch)
     breakdown = {}
     roofline = None
+    roofline_attn = None
     if not args.no_profile:
         br.profile_enable(True)
         br.profile_reset()
@@ -303,6 +304,7 @@ def main():
         frac = block_linear_frac(prof, nprof, T, b_loc, info)
         if frac is not None:
             breakdown["_dit_block_linears"] = {"tflops": round(frac * BF16_PEAK_TFLOPS, 1), "frac_of_bf16_peak": frac}
+        roofline_attn = attention_roofline(prof, nprof, T, L, b_loc, info)
 
     extras = {}
     single = world == 1 and not args.emulate
@@ -486,6 +488,7 @@ def main():
             "ranks": {"elapsed_s": [round(v, 5) for v in rank_elapsed], "broadcast_bytes_per_rank": bcast_bytes,
                       "items_per_rank": [len(shard_indices(B, world, r)) for r in range(world)]},
             "roofline": roofline,
+            "roofline_attention": roofline_attn,
             "bf16_line": bf16_line,
             **extras,
             "cpu_baseline": cpu,
@@ -623,6 +626,35 @@ def block_linear_frac(prof, nprof, T, b_loc, info):
     if lin_ms <= 0:
         return None
     return round(per_layer * info.num_layers / (lin_ms / 1000.0) / 1e12 / BF16_PEAK_TFLOPS, 4)
+
+
+def attention_roofline(prof, nprof, T, L, b_loc, info):
+    """The attention operator (the headline precision's kernel + its key-split merge, one HIP-event pair per layer)
+    against the dense fp16/bf16 MFMA peak: algorithmic FLOP per launch = 4 * (query, key) pairs inside the mask *
+    head_dim * q heads (Q.K^T and P.V; SURVEY §8(d) F_attn), per class -- full layers (every key), sliding layers
+    (|q - k| <= window) and cross attention (L encoder keys) -- and over the whole step."""
+    N = (T + 1) // 2
+    w = max(int(info.sliding_window), 0)
+    pairs_sliding = sum(min(N - 1, q + w) - max(0, q - w) + 1 for q in range(N)) if w > 0 else N * N
+    per_pair = 4.0 * info.head_dim * info.num_heads * b_loc
+    classes = {"attn_self_full": per_pair * N * N, "attn_self_sliding": per_pair * pairs_sliding,
+               "attn_cross": per_pair * N * L}
+    out, tot_flops, tot_ms = {}, 0.0, 0.0
+    for name, ms, cnt in prof:
+        if name not in classes or cnt <= 0:
+            continue
+        avg_s = ms / cnt / 1000.0
+        ach = classes[name] / avg_s / 1e12
+        out[name] = {"flops_per_launch": classes[name], "avg_launch_us": round(avg_s * 1e6, 2), "launches": cnt,
+                     "achieved": round(ach, 1), "frac": round(ach / BF16_PEAK_TFLOPS, 4)}
+        tot_flops += classes[name] * cnt
+        tot_ms += ms
+    if not out:
+        return None
+    ach = tot_flops / (tot_ms / 1000.0) / 1e12
+    return {"kernel": f"attention ({ATTN_DESC[HEADLINE_ATTN]}; operator time incl. its key-split merge)", "bound": "mfma",
+            "achieved": round(ach, 1), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / BF16_PEAK_TFLOPS, 4),
+            "ms_per_step": round(tot_ms / nprof, 4), "classes": out}
 
 
 def pmc_traffic(T, L, b_loc, weights):
