@@ -875,6 +875,12 @@ int pick_variant(int M, int N, int K, bool quant, int fmt) {
         if (M >= 20000) return K >= 4096 ? 10 : 2;
         return 11;
     }
+    // two 240 s items (M = 6000): the ping-pong tiles, measured as whole bs = 2 lines through ACE_MI_GEMM_OVERRIDE
+    // (profiles/r05/pick_inloop_bs2/, item-steps/s): gate|up on 256x256 (1152 tiles, 4.5 rounds) 76.1 against 72.2-72.5
+    // for the 192x128 4-wave pick (192x256 75.3, 256x256 4-wave-family 73.8); then, with that pick, o / cross q / cross o
+    // (N = K = 2048, 256 tiles: one round) on 192x256 78.8 against 76.0-76.5 (256x256 76.9, 256x128 72.1) and qkv on
+    // 192x256 77.5 (256x256 75.9); the K = 6144 down projection stays on 192x256 (256x256 71.8, 8-wave 192x128 72.3)
+    if (N % 256 == 0 && M >= 5000 && M < 6800) return N >= 8192 ? 10 : 11;
     if (N % 256 == 0 && M >= 4500 && N <= 2048 && K >= 4096) return 11;
     if (edge_ok && mb192 * (N / 128) >= 384) return 4;
     // short sequences (60 s: M = 750): too few 96-row tiles to cover the CUs -> 64-row tiles, and

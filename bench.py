@@ -24,6 +24,7 @@ Extra lines beside the headline (one GPU only; each the same 27-step schedule, t
   hook_line        the reference pipeline's drop-in path: a Python Euler loop over torch ROCm tensors calling
                    the installed `decoder.forward` (acestep_mi355x.hook, scripts/run_non_ggml_real_case.py:
                    460-533) once per step, as model.generate_audio does
+  qact_line        the headline loop in the ggml-faithful quantized-activation mode (ACE_MI_QUANT_ACT=q8)
   attn_{fp16,split,f32}_line  the headline loop in each attention precision (fp16 operands; hi/lo Q.K; hi/lo Q.K and
                    P.V = ggml's F32 kq / kqv), each with its per-kernel attention time per step
   line_bs          the metric's bs = 2, 4, 8 per GPU at 240 s (item-steps/s, block-linear fraction of peak)
@@ -375,6 +376,29 @@ def main():
             extras["fused_line"]["gemm_us_per_launch"] = {n: round(1000.0 * ms / max(c, 1), 2) for n, ms, c in prof_f
                                                            if n.startswith("gemm_")}
         os.environ.pop("ACE_MI_QUANT_STAGED", None)
+    # ---- ggml's own quantized arithmetic (ACE_MI_QUANT_ACT=q8, the parity mode): Q8 activation blocks, integer
+    #      block dots, f32 activations between the linears, f32-precision attention
+    if args.qtype and single and not args.no_extra_lines and os.environ.get("ACE_MI_QUANT_ACT", "bf16") == "bf16":
+        br.close()
+        os.environ["ACE_MI_QUANT_ACT"] = "q8"
+        br = GGMLCAPIBridge(device=local, lib_path=lib_path) if lib_path else GGMLCAPIBridge(device=local)
+        br.load_dit(ckpt)
+        el_qa = timed(run)
+        extras["qact_line"] = line(B * args.steps, el_qa,
+                                   "the headline loop with ACE_MI_QUANT_ACT=q8: ggml's quantized arithmetic (Q8_0 "
+                                   "activation blocks, i8-MFMA block dots, f32 activations, f32-precision attention)")
+        if not args.no_profile:
+            br.profile_enable(True)
+            br.profile_reset()
+            run(0, args.steps)
+            sync()
+            prof_q = br.profile_get()
+            br.profile_enable(False)
+            frac = block_linear_frac(prof_q, args.steps, T, b_loc, info)
+            if frac is not None:
+                extras["qact_line"]["dit_block_linears_frac_of_bf16_peak"] = frac
+            extras["qact_line"]["us_per_launch"] = {n: round(1000.0 * ms / max(c, 1), 2) for n, ms, c in prof_q}
+        os.environ.pop("ACE_MI_QUANT_ACT", None)
     # ---- the same workload with bf16 weights, reported beside a quantized line (single GPU only)
     bf16_line = None
     if args.qtype and single and not args.no_bf16_line:
