@@ -872,7 +872,9 @@ int pick_variant(int M, int N, int K, bool quant, int fmt) {
     }
     if (N % 256 == 0 && M >= 8192) {
         if (N >= 4096) return 10;
-        if (M >= 20000) return K >= 4096 ? 10 : 2;
+        // (M = 24000, eight 240 s items: o / cross q / cross o on the ping-pong 256x256 tile 83.7 item-steps/s against
+        //  80.9-81.0 for the 4-wave-family 256x256 and 82.9 for 192x256, profiles/r05/pick_inloop_bs8/)
+        if (M >= 20000) return 10;
         return 11;
     }
     // two 240 s items (M = 6000): the ping-pong tiles, measured as whole bs = 2 lines through ACE_MI_GEMM_OVERRIDE
