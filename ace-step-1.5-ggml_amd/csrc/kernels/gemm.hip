@@ -867,6 +867,9 @@ int pick_variant(int M, int N, int K, bool quant, int fmt) {
     // slower at M = 12000 (profiles/r03_bs_ab/), so the picks below 6800 and from 8192 stay as they were.
     if (M >= 6800 && M < 8192) {
         if (N <= 2048 && N % 256 == 0) return 10;
+        // qkv (N = 4096) on the 192x256 ping-pong tile with the fused prep: 26.94 steps/s at 600 s against 26.43-26.59
+        // for the 8-wave 192x128 tile (profiles/r05/pick_inloop_600s/); o / down / gate|up stay (192x256: 25.2 / 25.3 / 26.2)
+        if (N == 4096 && N % 256 == 0) return 11;
         if (N <= 4096) return 16;
         if (N % 256 == 0) return 10;
     }
