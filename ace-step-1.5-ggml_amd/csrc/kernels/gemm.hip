@@ -894,7 +894,9 @@ int pick_variant(int M, int N, int K, bool quant, int fmt) {
     // split-K (tools/gemm_msweep.py, MI355X): only the K = 6144 down projection between the short and the
     // full-length tiles gains (M = 1500: 96x128 over 2 parts 722 vs 637 TFLOP/s for 64x128); elsewhere the
     // join's device-coherent partial round trip (~3-4 us after the main loop) costs more than the fuller grid
-    if (N <= 2048 && K >= 4096 && M >= 1000 && M < 2000) return 207;
+    // (and at 60 s, M = 750: 163.4 steps/s against 158.5-159.4 for the 64x128 3-stage split-K pick,
+    //  profiles/r05/pick_inloop_60s/)
+    if (N <= 2048 && K >= 4096 && M >= 600 && M < 2000) return 207;
     const int64_t mb96 = (M + 95) / 96, mb64 = (M + 63) / 64;
     // Short sequences read every weight cold (each layer's weights were last touched one step earlier), so the
     // picks below follow the cold-weight sweep (ACE_MI_BENCH_COLD=24, profiles/r03_msweep_cold_ns.jsonl), where
