@@ -449,7 +449,12 @@ __global__ void __launch_bounds__(512, 1) gemm_ws_kernel(GemmParams p) {
 // lgkmcnt(0), MFMAs, barrier.  A half-tile is re-staged >= 2 phases after its last read (WAR across
 // the staggered groups) and read >= 1 phase after the wait that retires it (RAW); stages past the
 // last K-tile go to a scratch LDS region so the per-phase vmcnt counts stay uniform.
-template <int BM, bool F16, int EPI>
+// SK: split-K instance (variants 210 / 211: p.ksplit = 2 blocks per tile over the two halves of K, splitk_join).  Built
+// for the N = 2048 projections at M = 3000 (16 x 8 tiles of 192 x 256 = one round of 256 blocks with two K parts) and
+// measured slower there (tools/sk8_bench.py, profiles/r05/sk8/: o 577 against 834 TFLOP/s for the 96x128 pick, down 838
+// against 947): with one block per CU and 16 k-tiles per part the prologue, the join and the epilogue are exposed.
+// Forced-only.
+template <int BM, bool F16, int EPI, bool SK = false>
 __global__ void __launch_bounds__(512) gemm8_kernel(GemmParams p) {
     constexpr int BN = 256, BK = 64, ROWB = BK * 2;
     constexpr int HA = BM / 2;         // rows per A half-tile
@@ -467,10 +472,21 @@ __global__ void __launch_bounds__(512) gemm8_kernel(GemmParams p) {
     const int lane = tid & 63;
     const int wid = tid >> 6;
     const int wr = wid >> 2, wc = wid & 3;
-    int m0, n0;
-    block_tile<BM, BN>(p, m0, n0);
+    int m0, n0, sk_tile = 0, sk_part = 0;
+    unsigned ticket0 = 0;  // thread 0's split-K ticket
+    const int S = SK ? p.ksplit : 1;
+    if constexpr (SK) {
+        int ntiles;
+        splitk_block(S, sk_tile, sk_part, ntiles);
+        block_tile<BM, BN>(p, m0, n0, sk_tile, ntiles);
+        if (tid == 0) ticket0 = __hip_atomic_fetch_add(p.sk_cnt + sk_tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        block_tile<BM, BN>(p, m0, n0);
+    }
     const int M = p.M;
-    const int nk = p.K / BK;
+    const int nk_all = p.K / BK;
+    const int kt_begin = sk_part * nk_all / S;  // this block's K-tiles [kt_begin, kt_end)
+    const int nk = (sk_part + 1) * nk_all / S - kt_begin;
 
     // LDS-DMA sources: this wave stages pieces wid and wid + 8 of every half-tile (A halves of BM = 192
     // have 12 pieces: waves 4..7 stage one).  Piece rows are wid*8 + (lane >> 3) (+ 64, + half offset),
@@ -486,8 +502,8 @@ __global__ void __launch_bounds__(512) gemm8_kernel(GemmParams p) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int ra = min(m0 + h * HA + j * 64 + prow, M - 1);
-            srcA[h][j] = p.A + (int64_t)ra * p.lda + pch * 8;
-            srcB[h][j] = p.W + (int64_t)(n0 + h * 128 + j * 64 + prow) * p.ldw + pch * 8;
+            srcA[h][j] = p.A + (int64_t)ra * p.lda + pch * 8 + kt_begin * BK;
+            srcB[h][j] = p.W + (int64_t)(n0 + h * 128 + j * 64 + prow) * p.ldw + pch * 8 + kt_begin * BK;
         }
     auto stage_a = [&](int h, int t) {
         char* dst = t < nk ? smem + (t & 1) * STAGE + h * HA * ROWB : smem + SCRATCH;
@@ -599,6 +615,13 @@ __global__ void __launch_bounds__(512) gemm8_kernel(GemmParams p) {
     }
     if (wr == 0) __builtin_amdgcn_s_barrier();  // both groups now at the same barrier count
     wait_vmcnt<0>();                            // the scratch-region stages of the last tiles
+    if constexpr (SK) {
+        // acc[2][2][QM][QN] is the 4 QM x QN accumulator grid the join moves in the MFMA register layout
+        auto& acc2 = reinterpret_cast<f32x4 (&)[4 * QM][QN]>(acc);
+        if (!splitk_join<4 * QM, QN, 8, SplitKMax<BM, BN>::value, 2 * STAGE + 16 * 1024>(p, acc2, S, sk_tile, sk_part, tid,
+                                                                                        smem, ticket0))
+            return;
+    }
 
     if constexpr (EPI == EPI_QKV_PREP) {
         const int ccol = lane & 15, crow = (lane >> 4) * 4;
@@ -723,9 +746,16 @@ void launch_ws(const GemmParams& p, hipStream_t s) {
 }
 
 template <int BM, bool F16, int EPI>
-void launch_cfg8(const GemmParams& p, hipStream_t s) {
+void launch_cfg8(GemmParams p, int S, hipStream_t s) {
     if (p.N % 256 != 0) throw std::runtime_error("gemm: the 8-wave tiles need N % 256 == 0");
     const int nbm = (p.M + BM - 1) / BM;
+    if (S > 1) {
+        if (S != 2) throw std::runtime_error("gemm: the ping-pong tiles split K over two parts only");
+        if (p.K / 64 < 2 * S) throw std::runtime_error("gemm: split-K needs at least two K-tiles per part");
+        splitk_setup(p, nbm * (p.N / 256), S, (size_t)BM * 256 * 4, s);
+        hipLaunchKernelGGL((gemm8_kernel<BM, F16, EPI, true>), dim3(nbm * (p.N / 256) * S), dim3(512), 0, s, p);
+        return;
+    }
     hipLaunchKernelGGL((gemm8_kernel<BM, F16, EPI>), dim3(nbm * (p.N / 256)), dim3(512), 0, s, p);
 }
 
@@ -737,7 +767,7 @@ void launch_cfg8(const GemmParams& p, hipStream_t s) {
 template <bool F16, int EPI>
 void launch_variant(int variant, const GemmParams& p, hipStream_t s) {
     const int S = variant / 100;
-    if (S > 1 && (variant % 100 == 10 || variant % 100 == 11 || variant % 100 == 18)) throw std::runtime_error("gemm: split-K is for the 4-wave tiles");
+    if (S > 1 && variant % 100 == 18) throw std::runtime_error("gemm: split-K is not built for the warp-specialized tile");
     switch (variant % 100) {
         case 0: launch_cfg<128, 128, 2, 2, F16, EPI, 0>(p, S, s); break;
         case 1: launch_cfg<128, 128, 2, 2, F16, EPI, 1>(p, S, s); break;
@@ -749,8 +779,8 @@ void launch_variant(int variant, const GemmParams& p, hipStream_t s) {
         case 7: launch_cfg<96, 128, 2, 2, F16, EPI, 1>(p, S, s); break;
         case 8: launch_cfg<64, 128, 2, 2, F16, EPI, 1>(p, S, s); break;
         case 9: launch_cfg<64, 64, 2, 2, F16, EPI, 1>(p, S, s); break;
-        case 10: launch_cfg8<256, F16, EPI>(p, s); break;
-        case 11: launch_cfg8<192, F16, EPI>(p, s); break;
+        case 10: launch_cfg8<256, F16, EPI>(p, S, s); break;
+        case 11: launch_cfg8<192, F16, EPI>(p, S, s); break;
         case 12: launch_cfg<64, 64, 2, 2, F16, EPI, 4>(p, S, s); break;
         case 13: launch_cfg<64, 128, 2, 2, F16, EPI, 3>(p, S, s); break;
         case 14: launch_cfg<96, 128, 2, 2, F16, EPI, 3>(p, S, s); break;
@@ -834,8 +864,9 @@ int pick_variant(int M, int N, int K, bool quant, int fmt) {
         const bool qr = f >= 20 && f <= 25;
         const bool dense_only = (f == 6 || (f >= 8 && f < 20) || S > 1) && !qr;
         const bool sk_ok = S <= 1 || (qr ? (f == 22 || f == 23) && S <= 4 && K / 64 >= 2 * S
-                                         : ((f == 1 || f == 3 || f == 4 ? S <= 2
-                                                                       : (((f >= 6 && f <= 9) || (f >= 12 && f <= 15)) && S <= 4)) &&
+                                         : ((f == 1 || f == 3 || f == 4 || f == 10 || f == 11
+                                                 ? S <= 2
+                                                 : (((f >= 6 && f <= 9) || (f >= 12 && f <= 15)) && S <= 4)) &&
                                             K / 64 >= 2 * S));
         (void)fmt;
         return !(wide && N % 256 != 0) && !(quant && dense_only) && !(!quant && qr) && sk_ok;
