@@ -257,37 +257,53 @@ __global__ void __launch_bounds__(256) gemm_a8_kernel(A8Params p) {
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     const i32x4 zero = {0, 0, 0, 0};
 
-    for (int b = 0; b < nb; ++b) {
-        long av[4], wv[4], wv2[4] = {0, 0, 0, 0};
-        float s0[4], s1[4] = {0.f, 0.f, 0.f, 0.f};
-        float4 sa[4], sb[4] = {};
+    // one 32-value block's operands, loaded raw (the Q4_K unpack and the Q6_K half masks run at compute time, so the
+    // next block's loads are in flight while this one's MFMAs and scaling run: a two-block software pipeline)
+    struct Ops {
+        long av[4], wv[4];
+        float s0[4], s1[4];
+        float4 sa[4], sb[4];
+    };
+    auto load = [&](int b, Ops& o) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            av[i] = *(const long*)(arow[i] + b * 32);
-            sa[i] = *(const float4*)(asb + (int64_t)b * p.ld_s + i * 16);
-            if constexpr (WQ == WF_Q4_K) sb[i] = *(const float4*)(abb + (int64_t)b * p.ld_s + i * 16);
+            o.av[i] = *(const long*)(arow[i] + b * 32);
+            o.sa[i] = *(const float4*)(asb + (int64_t)b * p.ld_s + i * 16);
+            if constexpr (WQ == WF_Q4_K) o.sb[i] = *(const float4*)(abb + (int64_t)b * p.ld_s + i * 16);
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             if constexpr (WQ == WF_Q4_K) {
                 // 16 bytes per block; byte i: low nibble k = 8 (i / 4) + i % 4, high nibble k + 4 (runtime/quant.h)
-                const uint32_t u = *(const uint32_t*)(static_cast<const uint8_t*>(p.wq) + wrow[j] * (K / 2) + b * 16 + 4 * g);
-                const uint64_t lo = u & 0x0f0f0f0fu, hi = (u >> 4) & 0x0f0f0f0fu;
-                wv[j] = (long)(lo | (hi << 32));
+                o.wv[j] = (long)*(const uint32_t*)(static_cast<const uint8_t*>(p.wq) + wrow[j] * (K / 2) + b * 16 + 4 * g);
                 const float2 sc = *(const float2*)(p.ws + (wrow[j] * nb + b) * 2);  // (d*sc, dmin*m)
-                s0[j] = sc.x;
-                s1[j] = sc.y;
+                o.s0[j] = sc.x;
+                o.s1[j] = sc.y;
             } else {
-                wv[j] = *(const long*)(static_cast<const int8_t*>(p.wq) + wrow[j] * K + b * 32 + 8 * g);
+                o.wv[j] = *(const long*)(static_cast<const int8_t*>(p.wq) + wrow[j] * K + b * 32 + 8 * g);
                 if constexpr (WQ == WF_Q6_K) {
                     const float2 sc = *(const float2*)(p.ws + (wrow[j] * nb + b) * 2);  // d*sc of the two 16-halves
-                    s0[j] = sc.x;
-                    s1[j] = sc.y;
-                    wv2[j] = g < 2 ? 0 : wv[j];  // second half: k 16..31 (lanes 32..63)
-                    wv[j] = g < 2 ? wv[j] : 0;
+                    o.s0[j] = sc.x;
+                    o.s1[j] = sc.y;
                 } else {
-                    s0[j] = p.ws[wrow[j] * nb + b];
+                    o.s0[j] = p.ws[wrow[j] * nb + b];
                 }
+            }
+        }
+    };
+    auto compute = [&](Ops& o) {
+        long wv[4], wv2[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if constexpr (WQ == WF_Q4_K) {
+                const uint32_t u = (uint32_t)o.wv[j];
+                const uint64_t lo = u & 0x0f0f0f0fu, hi = (u >> 4) & 0x0f0f0f0fu;
+                wv[j] = (long)(lo | (hi << 32));
+            } else if constexpr (WQ == WF_Q6_K) {
+                wv2[j] = g < 2 ? 0 : o.wv[j];  // second half: k 16..31 (lanes 32..63)
+                wv[j] = g < 2 ? o.wv[j] : 0;
+            } else {
+                wv[j] = o.wv[j];
             }
         }
         mfma_war_guard();  // the operands' VALU writes are done before the MFMAs read them
@@ -296,28 +312,44 @@ __global__ void __launch_bounds__(256) gemm_a8_kernel(A8Params p) {
         for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                is[i][j] = __builtin_amdgcn_mfma_i32_16x16x32_i8(av[i], wv[j], zero, 0, 0, 0);
-                if constexpr (WQ == WF_Q6_K) is2[i][j] = __builtin_amdgcn_mfma_i32_16x16x32_i8(av[i], wv2[j], zero, 0, 0, 0);
+                is[i][j] = __builtin_amdgcn_mfma_i32_16x16x32_i8(o.av[i], wv[j], zero, 0, 0, 0);
+                if constexpr (WQ == WF_Q6_K) is2[i][j] = __builtin_amdgcn_mfma_i32_16x16x32_i8(o.av[i], wv2[j], zero, 0, 0, 0);
             }
         mfma_war_guard();  // no operand register is rewritten while an MFMA may still read it
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const float a4[4] = {sa[i].x, sa[i].y, sa[i].z, sa[i].w};
-            const float b4[4] = {sb[i].x, sb[i].y, sb[i].z, sb[i].w};
+            const float a4[4] = {o.sa[i].x, o.sa[i].y, o.sa[i].z, o.sa[i].w};
+            const float b4[4] = {o.sb[i].x, o.sb[i].y, o.sb[i].z, o.sb[i].w};
 #pragma unroll
             for (int j = 0; j < 4; ++j)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    float v;
                     if constexpr (WQ == WF_Q8_0) {
-                        v = rn_mul((float)is[i][j][r], rn_mul(s0[j], a4[r]));  // sumi * (d_w * d_a)
+                        // acc += sumi * (d_w * d_a) as one FMA: ggml's AVX2 vec_dot_q8_0_q8_0 (_mm256_fmadd_ps)
+                        acc[i][j][r] = __builtin_fmaf((float)is[i][j][r], rn_mul(o.s0[j], a4[r]), acc[i][j][r]);
                     } else if constexpr (WQ == WF_Q4_K) {
-                        v = rn_mul(a4[r], rn_sub(rn_mul(s0[j], (float)is[i][j][r]), rn_mul(s1[j], b4[r])));
+                        const float v = rn_mul(a4[r], rn_sub(rn_mul(o.s0[j], (float)is[i][j][r]), rn_mul(o.s1[j], b4[r])));
+                        acc[i][j][r] = rn_add(acc[i][j][r], v);
                     } else {
-                        v = rn_mul(a4[r], rn_add(rn_mul(s0[j], (float)is[i][j][r]), rn_mul(s1[j], (float)is2[i][j][r])));
+                        const float v =
+                            rn_mul(a4[r], rn_add(rn_mul(o.s0[j], (float)is[i][j][r]), rn_mul(o.s1[j], (float)is2[i][j][r])));
+                        acc[i][j][r] = rn_add(acc[i][j][r], v);
                     }
-                    acc[i][j][r] = rn_add(acc[i][j][r], v);
                 }
+        }
+    };
+    Ops o0, o1;
+    o0.sb[0] = o0.sb[1] = o0.sb[2] = o0.sb[3] = make_float4(0.f, 0.f, 0.f, 0.f);
+    o1.sb[0] = o1.sb[1] = o1.sb[2] = o1.sb[3] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o0.s1[j] = o1.s1[j] = 0.f;
+    load(0, o0);
+    for (int b = 0; b < nb; b += 2) {
+        if (b + 1 < nb) load(b + 1, o1);
+        compute(o0);
+        if (b + 1 < nb) {
+            if (b + 2 < nb) load(b + 2, o0);
+            compute(o1);
         }
     }
 
