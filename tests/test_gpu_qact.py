@@ -91,3 +91,69 @@ def test_gemm_a8_epilogues(qtype):
     gcols = np.concatenate([np.arange(grp * 32, grp * 32 + 16) for grp in range(N // 32)])
     g, u = ref[:, gcols], ref[:, gcols + 16]
     np.testing.assert_allclose(got, g / (1.0 + np.exp(-g)) * u, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("qtype", ["q8_0", "q4_k", "q6_k"])
+def test_qact_tiny_with_masks_vs_ggml_semantics(tiny_ckpt, monkeypatch, qtype):
+    """The tiny model in ACE_MI_QUANT_ACT=q8 with a key-padding mask, an encoder mask, odd T and r != t: against the
+    oracle with ggml's Q8_0 / Q8_K activation quantization -- every block format, the masked attention's f32-output
+    path and the t - r timestep branch.  rel-L2 bound only (max(1e-3, 1.5 x floor)): at this size the 1e-7
+    perturbation floor is a count of a few discrete q flips (Q8_K: often none, floor 7e-7), so its element-wise
+    statistic is no scale for an implementation whose f32 order differs at 1e-6; the element-wise bound is held at
+    full width (test_gpu_quant.py / test_gpu_configs.py)."""
+    from acestep_mi355x.capi import GGMLCAPIBridge
+    from oracle.dit_oracle import DitWeights, forward_with_floor_stats
+    from test_gpu_forward import check
+    monkeypatch.setenv("ACE_GGML_DIT_WEIGHT_QTYPE", qtype)
+    monkeypatch.setenv("ACE_MI_QUANT_ACT", "q8")
+    rng = np.random.default_rng(41)
+    T, L = 301, 20
+    h = rng.standard_normal((T, 64)).astype(np.float32)
+    c = rng.standard_normal((T, 128)).astype(np.float32)
+    e = rng.standard_normal((L, 256)).astype(np.float32)
+    mask = np.ones(T, np.int32)
+    mask[280:] = 0
+    emask = np.ones(L, np.int32)
+    emask[15:] = 0
+    br = GGMLCAPIBridge()
+    br.load_dit(tiny_ckpt)
+    got = br.dit_forward_tfirst(h, c, e, mask, emask, 0.7, 0.4)
+    br.close()
+    ref, floor, _ = forward_with_floor_stats(DitWeights(tiny_ckpt, qtype=qtype), h, c, e, mask, emask, T, L, 0.7, 0.4)
+    check(got, ref, floor, f"tiny {qtype} ACE_MI_QUANT_ACT=q8 with masks (ggml semantics)")
+
+
+def test_qact_sampling_loop_equals_per_step_forwards(tiny_ckpt, monkeypatch):
+    """ace_mi_dit_sample_ex in ACE_MI_QUANT_ACT=q8 (timestep rows of every step precomputed in one pass, cross K/V
+    recomputed) equals per-step batched forwards + the same f32 Euler updates, bit for bit, at B = 2."""
+    import torch
+    from acestep_mi355x.capi import GGMLCAPIBridge
+    monkeypatch.setenv("ACE_GGML_DIT_WEIGHT_QTYPE", "q8_0")
+    monkeypatch.setenv("ACE_MI_QUANT_ACT", "q8")
+    rng = np.random.default_rng(43)
+    B, T, L = 2, 90, 12
+    sched = np.array([1.0, 0.8, 0.45], np.float32)
+    dev = torch.device("cuda:0")
+    x0 = torch.from_numpy(rng.standard_normal((B, T, 64)).astype(np.float32)).to(dev)
+    dc = torch.from_numpy(rng.standard_normal((B, T, 128)).astype(np.float32)).to(dev)
+    de = torch.from_numpy(rng.standard_normal((B, L, 256)).astype(np.float32)).to(dev)
+    br = GGMLCAPIBridge()
+    br.load_dit(tiny_ckpt)
+    xt = x0.clone()
+    torch.cuda.synchronize()
+    br.dit_sample_ex_device(B, T, L, xt.data_ptr(), dc.data_ptr(), de.data_ptr(), 0, 0, list(sched), cache_cross=False)
+    br.synchronize()
+    loop = xt.cpu().numpy()
+    x = x0.clone()
+    v = torch.empty_like(x)
+    for i, t in enumerate(sched):
+        tt = torch.full((B,), float(t), dtype=torch.float32, device=dev)
+        torch.cuda.synchronize()
+        br.dit_forward_batched_device(B, T, L, x.data_ptr(), dc.data_ptr(), de.data_ptr(), 0, 0, tt.data_ptr(),
+                                      tt.data_ptr(), v.data_ptr(), 0)
+        br.synchronize()
+        dt = np.float32(t) if i + 1 == len(sched) else np.float32(np.float32(t) - np.float32(sched[i + 1]))
+        x = x - v * float(dt)
+    torch.cuda.synchronize()
+    br.close()
+    np.testing.assert_array_equal(loop, x.cpu().numpy())
