@@ -1177,6 +1177,91 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
     wait_vmcnt<0>();  // the re-read tiles past the end
 
     const float l = l_run + __shfl_xor(l_run, 32);
+    if (ks > 1 && a.fused_merge) {
+        // Key split merged in place (attn_kernel's protocol): every part stores its unnormalised O, running max and
+        // sum with device-coherent stores, completes them and takes a ticket; the part that takes the last ticket
+        // (whichever finishes last: no block ever waits) reads all parts back in part order and writes the
+        // normalised rows -- attn_merge_kernel's arithmetic and order, without its launch
+        const int S = a.ksplit;
+        const int64_t rows = (int64_t)a.B * a.nq * a.Hq;
+        const int64_t r = ((int64_t)b * a.nq + qrow) * a.Hq + head;
+        const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void*)a.part, 0, 0x7fffffff, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rm =
+            __builtin_amdgcn_make_buffer_rsrc((void*)(a.part + S * rows * D), 0, 0x7fffffff, 0x00020000);
+        if (qrow < a.nq) {
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int g4 = 0; g4 < 4; ++g4) {
+                    const u32x4_t v = {__float_as_uint(o[dt][4 * g4 + 0]), __float_as_uint(o[dt][4 * g4 + 1]),
+                                       __float_as_uint(o[dt][4 * g4 + 2]), __float_as_uint(o[dt][4 * g4 + 3])};
+                    __builtin_amdgcn_raw_buffer_store_b128(
+                        v, ro, (int)((((int64_t)split * rows + r) * D + 32 * dt + 8 * g4 + 4 * h) * 4), 0, 16);
+                }
+            if (h == 0) {
+                const u32x2_t v = {__float_as_uint(m_run), __float_as_uint(l)};
+                __builtin_amdgcn_raw_buffer_store_b64(v, rm, (int)(((int64_t)split * rows + r) * 2 * 4), 0, 16);
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();  // every lane's stores are complete; the ring is free
+        unsigned* cnt = reinterpret_cast<unsigned*>(a.part + 4 * rows * (D + 2));
+        const int group = (b * a.Hkv + kvh) * n_qt + qt;
+        volatile unsigned* flag = reinterpret_cast<volatile unsigned*>(smem);
+        if (tid == 0) *flag = __hip_atomic_fetch_add(cnt + group, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        if (*flag != (unsigned)(S - 1)) return;
+        if (tid == 0) __hip_atomic_store(cnt + group, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (qrow >= a.nq) return;
+        float mk[4], lk[4];
+        float Mx = -INFINITY;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (k < S) {
+                const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(rm, (int)(((int64_t)k * rows + r) * 2 * 4), 0, 16);
+                mk[k] = __uint_as_float(v[0]);
+                lk[k] = __uint_as_float(v[1]);
+                Mx = fmaxf(Mx, mk[k]);
+            }
+        }
+        float wk[4], den = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (k < S) {
+                wk[k] = mk[k] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(mk[k] - Mx);
+                den += wk[k] * lk[k];
+            }
+        }
+        const float inv = 1.0f / den;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+                const int d = 32 * dt + 8 * g4 + 4 * h;
+                float v[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    if (k < S) {
+                        const u32x4_t t =
+                            __builtin_amdgcn_raw_buffer_load_b128(ro, (int)((((int64_t)k * rows + r) * D + d) * 4), 0, 16);
+                        v[0] += wk[k] * __uint_as_float(t[0]);
+                        v[1] += wk[k] * __uint_as_float(t[1]);
+                        v[2] += wk[k] * __uint_as_float(t[2]);
+                        v[3] += wk[k] * __uint_as_float(t[3]);
+                    }
+                }
+                if (a.out_f32) {
+                    *(float4*)(a.out_f32 + r * D + d) = make_float4(v[0] * inv, v[1] * inv, v[2] * inv, v[3] * inv);
+                } else {
+                    uint2 w;
+                    w.x = (uint32_t)to_act<F16OUT>(v[0] * inv) | ((uint32_t)to_act<F16OUT>(v[1] * inv) << 16);
+                    w.y = (uint32_t)to_act<F16OUT>(v[2] * inv) | ((uint32_t)to_act<F16OUT>(v[3] * inv) << 16);
+                    *(uint2*)(a.out + r * D + d) = w;
+                }
+            }
+        }
+        return;
+    }
     if (ks > 1) {
         if (qrow < a.nq) {
             const int64_t row = ((int64_t)split * a.B + b) * a.nq + qrow;
@@ -1284,7 +1369,7 @@ void launch_t(const AttnArgs& a, dim3 grid, hipStream_t s) {
     if constexpr (!SPLIT && PVS) {
         throw std::runtime_error("attention: hi/lo P.V with fp16 Q.K exists only with fp8 corrections (pv8)");
     } else {
-        if (v2 && a.fused_merge == 0) {
+        if (v2) {
             constexpr int OCC = SPLIT ? 1 : 2;
             if (a.kbias)
                 hipLaunchKernelGGL((attn2_kernel<F16OUT, SPLIT, PVS, true, OCC>), grid, dim3(256), lds, s, a);
@@ -1384,7 +1469,9 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s) {
         else if (a.part && (mode == 0 || mode == 4)) b.ksplit = S;
         if (tail_fits && b.ksplit == 2) b.split_from = (int)F;
         // ACE_MI_ATTN_FUSED_MERGE=1: the last part of a group merges in the attention kernel (sc1 partial
-        // round trip, no merge launch) -- measured 2.6x slower attention at 60 s, so off by default
+        // round trip, no merge launch) -- measured 2.6x slower attention at 60 s in the first kernel; in attn2
+        // (profiles/r05/attn_fused_merge.txt) neutral at 60 s, 4 % slower lines at 240 s (it replaces the tail
+        // split by splitting every block) and 5 % slower at 60 s with ACE_MI_ATTN_KSPLIT=4, so off by default
         static int fm = -1;
         if (fm < 0) {
             const char* e = std::getenv("ACE_MI_ATTN_FUSED_MERGE");
@@ -1404,7 +1491,7 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s) {
     const dim3 grid(b.split_from > 0 ? (unsigned)(b.split_from + 8 * ((2 * (n_blk - b.split_from) + 7) / 8))
                                      : (unsigned)(8 * ((n_blk * b.ksplit + 7) / 8)));
     const bool f16 = out_t == ActType::F16;
-    ACEMI_CHECK(!a.f8 || (a.pv_split && !b.fused_merge), "attention: the fp8 correction modes need pv_split");
+    ACEMI_CHECK(!a.f8 || a.pv_split, "attention: the fp8 correction modes need pv_split");
     if (a.split) {
         ACEMI_CHECK(a.q_plane > 0 && a.k_plane > 0, "attention: split mode needs lo planes");
         if (a.pv_split) {
