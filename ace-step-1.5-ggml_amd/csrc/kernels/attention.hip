@@ -1430,10 +1430,12 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s) {
         const int span = a.window > 0 ? std::min(a.nk, qpb + 2 * a.window) : a.nk;
         // (measured: full 240 s 317 -> 262 us incl. the merge; at 8 key tiles or fewer -- cross attention,
         // sliding windows -- the extra prologue and merge cost more than the round saves)
-        static int mode = -1;  // ACE_MI_ATTN_KSPLIT=1 never / 2 always (where a workspace exists) / 4 see below / auto
+        // ACE_MI_ATTN_KSPLIT=1 never / 2 always (where a workspace exists) / 3 auto without the short-range split /
+        // 4 see below / auto
+        static int mode = -1;
         if (mode < 0) {
             const char* e = std::getenv("ACE_MI_ATTN_KSPLIT");
-            mode = (e && (e[0] == '1' || e[0] == '2' || e[0] == '4')) ? e[0] - '0' : 0;
+            mode = (e && (e[0] == '1' || e[0] == '2' || e[0] == '3' || e[0] == '4')) ? e[0] - '0' : 0;
         }
         // blocks resident per CU: two for the single-fp16 kernel (66 KiB ring), one for the hi/lo ones
         const int per_cu = (a.split || a.pv_split) ? 1 : 2;
@@ -1453,20 +1455,21 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s) {
             tail_min = m ? std::max(2, std::atoi(m)) : 16;
         }
         const int64_t F = slots & ~int64_t(7);
-        const bool tail_fits = tail && mode == 0 && F > 0 && blocks > F && 2 * (blocks - F) <= slots;
+        const bool tail_fits = tail && (mode == 0 || mode == 3) && F > 0 && blocks > F && 2 * (blocks - F) <= slots;
         if (ntiles >= 16) {
             if (blocks * 10 < slots * 16) S = 2;
-        } else if (mode == 4) {
-            // ACE_MI_ATTN_KSPLIT=4: short key ranges (cross attention, sliding windows, short sequences) split too,
-            // while the grid stays within one round and every part keeps >= 2 key tiles.  Measured at 60 s
-            // (rocprof, profiles/r03_trace_60s_*.txt): attention 698 us + 48 merges 275 us per forward against
-            // ~950 us unsplit -- the merge launches (~5 us each) eat the gain, so not the default
+        } else if (mode == 4 || (mode == 0 && blocks * 2 <= slots)) {
+            // short key ranges (cross attention, sliding windows, short sequences) split too when the grid fills at
+            // most half a round (ACE_MI_ATTN_KSPLIT=4: whatever the grid), while it stays within one round and every
+            // part keeps >= 2 key tiles.  Round 3 (the first kernel, profiles/r03_trace_60s_*.txt) lost: 698 us +
+            // 48 merges 275 us per forward against ~950 us unsplit.  With attn2 it pays: 60 s (96 blocks on 256 CUs)
+            // 165.1 against 163.1-163.4 steps/s (profiles/r05/attn_ksplit_short.txt)
             while (S < 4 && blocks * 2 * S <= slots && ntiles >= 4 * S) S *= 2;
         } else if (tail_fits && ntiles >= tail_min) {
             S = 2;
         }
         if (a.part && mode == 2) b.ksplit = 2;
-        else if (a.part && (mode == 0 || mode == 4)) b.ksplit = S;
+        else if (a.part && (mode == 0 || mode == 3 || mode == 4)) b.ksplit = S;
         if (tail_fits && b.ksplit == 2) b.split_from = (int)F;
         // ACE_MI_ATTN_FUSED_MERGE=1: the last part of a group merges in the attention kernel (sc1 partial
         // round trip, no merge launch) -- measured 2.6x slower attention at 60 s in the first kernel; in attn2
