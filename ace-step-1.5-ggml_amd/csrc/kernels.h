@@ -190,13 +190,11 @@ struct AttnArgs {
     bool split = true;                 // hi/lo fp16 Q.K operands (see attention.hip)
     bool pv_split = false;             // hi/lo fp16 P.V operands too (needs split)
     int64_t q_plane = 0, k_plane = 0, v_plane = 0;  // element offset of the lo planes
-    // Optional f32 workspace of attn_part_floats() (zeroed before first use: its tail holds the key-split
-    // tickets, which every launch leaves at zero): with it, a grid too small to fill the chip in whole rounds
-    // splits every block's key range in two or four; the last part of each group merges them.
+    // Optional f32 workspace of attn_part_floats(): with it, a grid too small to fill the chip in whole rounds
+    // splits block key ranges in two or four parts, merged by attn_merge_kernel.
     float* part = nullptr;
     int ksplit = 1;  // set by launch_attention
     int xcd_order = 1;  // set by launch_attention: XCD-aware block order
-    int fused_merge = 0;  // set by launch_attention: the last part of a key-split group merges (no merge kernel)
     int split_from = 0;  // set by launch_attention: > 0 = tail split (blocks [0, split_from) whole, the rest in two
                          // key-range parts; ksplit = 2 gives the partials' layout)
     // f32 output [B*nq][Hq*128] instead of `out` (the ggml-faithful quantized-activation mode, whose next linear

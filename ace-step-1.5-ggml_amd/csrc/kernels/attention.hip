@@ -213,445 +213,8 @@ __device__ __forceinline__ void static_for(F&& f) {
 // the 32x32 C/D map puts rows (= keys of S^T) at 8*(r/4) + 4*h + r%4
 __device__ __forceinline__ constexpr int key_of(int t, int r) { return 32 * t + (r & 3) + 8 * (r >> 2); }
 
-// OCC = workgroups per CU the register allocation targets (2: <= 256 registers per lane; the
-// single-fp16 ring of 66 KiB lets two workgroups share a CU's LDS)
-template <bool F16OUT, bool SPLIT, bool PVS, bool KBIAS, int OCC>
-__global__ void __launch_bounds__(256, OCC) attn_kernel(AttnArgs a) {
-    static_assert(SPLIT || !PVS, "hi/lo P.V needs hi/lo operands");
-    using RG = Ring<SPLIT, PVS>;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int h = lane >> 5;     // lane half
-    const int lq = lane & 31;
-
-    const int rep = a.Hq / a.Hkv;
-    const int qpb = 128 / rep;   // query rows per head in this block
-    const int n_qt = (a.nq + qpb - 1) / qpb;
-    // XCD-aware order: the hardware deals blocks round-robin over the 8 XCDs (block j -> XCD j % 8), so
-    // logical block L = (j % 8) * per + j / 8 gives each XCD one contiguous run of logical blocks, i.e.
-    // the blocks of one (item, kv head) -- whose K / V^T tiles they all stream -- share one XCD's L2
-    // (at B = 1 with 8 kv heads: one kv head per XCD).  Up to 7 trailing hardware blocks are empty.
-    int bid, split, ks;  // logical block, its key-range part (AttnArgs::part) and the block's number of parts
-    if (!attn_block(a, a.B * a.Hkv * n_qt, bid, split, ks)) return;
-    const int qt = bid % n_qt;
-    bid /= n_qt;
-    const int kvh = bid % a.Hkv;
-    const int b = bid / a.Hkv;
-    const int waves_per_head = 4 / rep;
-    const int head = kvh * rep + wid / waves_per_head;
-    const int q0 = qt * qpb;
-    const int qw0 = q0 + (wid % waves_per_head) * 32;  // this wave's first row
-    const int qrow = qw0 + lq;
-
-    // ---- key tile range of the block
-    int klo = 0, khi = a.nk;
-    if (a.window > 0) {
-        klo = max(0, q0 - a.window);
-        khi = min(a.nk, q0 + qpb - 1 + a.window + 1);
-    }
-    if (a.causal) khi = min(khi, q0 + qpb);  // no key after the block's last query
-    const int n_all = max(0, (khi + KT - 1) / KT - klo / KT);
-    const int chunk = (n_all + ks - 1) / ks;
-    const int kt_begin = klo / KT + split * chunk;
-    const int n = max(0, min(chunk, n_all - split * chunk));
-
-    // ---- this lane's valid absolute key range [lo_abs, hi_abs): padding, window, causal
-    int lo_abs = 0, hi_abs = a.nk;
-    if (a.window > 0) {
-        lo_abs = max(lo_abs, qrow - a.window);
-        hi_abs = min(hi_abs, qrow + a.window + 1);
-    }
-    if (a.causal) hi_abs = min(hi_abs, qrow + 1);
-    lo_abs -= 4 * h;  // compared against the lane-independent part of the key index
-    hi_abs -= 4 * h;
-
-    // ---- Q fragments (B operand of S^T = K Q^T): Q[q][16ks + 8h + j]
-    const uint16_t* qptr = a.q + (((int64_t)b * a.Hq + head) * a.nq_pad + qrow) * D + 8 * h;
-    frag qf[8], qfl[8];
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) qf[ks] = *(const frag*)(qptr + 16 * ks);
-    if constexpr (SPLIT) {
-#pragma unroll
-        for (int ks = 0; ks < 8; ++ks) qfl[ks] = *(const frag*)(qptr + a.q_plane + 16 * ks);
-    }
-
-    const uint16_t* kbase = a.k + ((int64_t)b * a.Hkv + kvh) * a.nk_pad * D;
-    const uint16_t* vbase = a.vt + ((int64_t)b * a.Hkv + kvh) * D * a.nk_pad;
-    const float* kb = KBIAS ? a.kbias + (int64_t)b * a.nk_pad : nullptr;
-
-    auto stage_k = [&](int slot, int kt) {
-        char* base = smem + slot * RG::KS;
-        const int k0 = kt * KT;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {  // K: 16 instr of 4 rows
-            const int g = wid + 4 * j;
-            const int row = 4 * g + (lane >> 4);
-            const int ch = (lane & 15) ^ (row & 15);
-            const uint16_t* src = kbase + (int64_t)(k0 + row) * D + ch * 8;
-            __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(base + RG::K_HI + g * 1024), 16, 0, 0);
-            if constexpr (SPLIT)
-                __builtin_amdgcn_global_load_lds((const void*)(src + a.k_plane), (lds_void*)(base + RG::K_LO + g * 1024),
-                                                 16, 0, 0);
-        }
-        if constexpr (KBIAS) {
-            if (wid == 0)
-                __builtin_amdgcn_global_load_lds((const void*)(kb + k0 + lane), (lds_void*)(base + RG::KB), 4, 0, 0);
-        }
-    };
-    auto stage_v = [&](int slot, int kt) {
-        char* base = smem + RG::V0 + slot * RG::VS;
-        const int k0 = kt * KT;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {  // V^T: 16 instr of 8 d-rows
-            const int g = wid + 4 * j;
-            const int d = 8 * g + (lane >> 3);
-            const int ch = (lane & 7) ^ ((d >> 1) & 7);
-            const uint16_t* src = vbase + (int64_t)d * a.nk_pad + k0 + ch * 8;
-            __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(base + g * 1024), 16, 0, 0);
-            if constexpr (PVS)
-                __builtin_amdgcn_global_load_lds((const void*)(src + a.v_plane), (lds_void*)(base + RG::V_LO + g * 1024),
-                                                 16, 0, 0);
-        }
-    };
-
-    // Per-lane LDS read addresses.  K rows are 256 B with 16-B chunk c stored at c ^ (key & 15); the
-    // fragment chunk of k-step ks is 2*ks + h, so its physical chunk is (2*ks) ^ cK (cK lane constant).
-    // V^T rows are 128 B with chunk c at c ^ ((d >> 1) & 7): chunk of key-step g is (2*g) ^ cV.
-    const int cK = h ^ (lq & 15);
-    const int cV = h ^ ((lq >> 1) & 7);
-    const uint32_t smem_l = lds_addr(smem);
-    uint32_t kaddr[8], vaddr[4];
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) kaddr[ks] = smem_l + RG::K_HI + lq * 256 + (((2 * ks) ^ cK) << 4);
-#pragma unroll
-    for (int g = 0; g < 4; ++g) vaddr[g] = smem_l + RG::V0 + lq * 128 + (((2 * g) ^ cV) << 4);
-    const uint32_t kbaddr = smem_l + RG::KB + 16 * h;
-
-    // S^T(tile in K slot SLOT) -> s (two 32-key halves); SPLIT: Kh.Qh + Kh.Ql + Kl.Qh
-    auto s_tile = [&](auto slot_c, f32x16 (&s)[2]) {
-        constexpr int SLOT = decltype(slot_c)::value;
-        static_for<0, 2>([&](auto t_c) {
-            constexpr int t = decltype(t_c)::value;
-            frag kf[SPLIT ? 16 : 8];  // hi frags, then lo frags
-#pragma unroll
-            for (int ks = 0; ks < 8; ++ks) kf[ks] = lds_frag<SLOT * RG::KS + t * 32 * 256>(kaddr[ks]);
-            if constexpr (SPLIT) {
-#pragma unroll
-                for (int ks = 0; ks < 8; ++ks)
-                    kf[8 + ks] = lds_frag<SLOT * RG::KS + t * 32 * 256 + RG::K_LO - RG::K_HI>(kaddr[ks]);
-            }
-            lds_wait_tie(kf);
-#pragma unroll
-            for (int r = 0; r < 16; ++r) s[t][r] = 0.f;
-#pragma unroll
-            for (int ks = 0; ks < 8; ++ks) {
-                s[t] = mfma32(kf[ks], qf[ks], s[t]);
-                if constexpr (SPLIT) {
-                    s[t] = mfma32(kf[ks], qfl[ks], s[t]);
-                    s[t] = mfma32(kf[8 + ks], qf[ks], s[t]);
-                }
-            }
-        });
-    };
-
-    const float c_log2 = a.scale * 1.4426950408889634f;
-    // scale + mask S of the tile at relative index i (its key bias in K slot SLOT) in place; returns
-    // the lane's max over its 32 keys (combined across the two lane halves by the caller)
-    auto prep = [&](auto slot_c, f32x16 (&s)[2], int i) -> float {
-        constexpr int SLOT = decltype(slot_c)::value;
-        const int k0 = (kt_begin + i) * KT;
-        const int lo = lo_abs - k0, hi = hi_abs - k0;
-        frag kbv[8];  // key bias of element r of half t: kbv[4t + r/4][r%4]
-        if constexpr (KBIAS) {
-            static_for<0, 8>([&](auto j_c) {
-                constexpr int j = decltype(j_c)::value;  // (t, g4) = (j / 4, j % 4): keys 32t + 8g4 + 4h + 0..3
-                kbv[j] = lds_frag<SLOT * RG::KS + (32 * (j / 4) + 8 * (j % 4)) * 4>(kbaddr);
-            });
-            lds_wait_tie(kbv);
-        }
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                float x = s[t][r] * c_log2;
-                if constexpr (KBIAS) x += __uint_as_float(kbv[4 * t + (r >> 2)][r & 3]);
-                s[t][r] = x;
-            }
-        }
-        // padding / window / causal bounds: only tiles that cross a bound for some lane of the wave
-        // (key_of spans 0..59 before the lane-half offset, already folded into lo / hi)
-        if (__builtin_amdgcn_ballot_w64(lo > 0 || hi < 60) != 0) {
-#pragma unroll
-            for (int t = 0; t < 2; ++t)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int kr = key_of(t, r);
-                    s[t][r] = (kr >= lo && kr < hi) ? s[t][r] : -INFINITY;
-                }
-        }
-        float mloc = -INFINITY;
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) mloc = fmaxf(mloc, s[t][r]);
-        return fmaxf(mloc, __shfl_xor(mloc, 32));
-    };
-
-    float m_run = -INFINITY;   // running reference max (exp2 domain) of this lane's query
-    float l_run = 0.f;
-    float alpha = 1.f;         // rescale of O and l for the latest max move
-    bool rescale = false;      // wave-uniform
-    f32x16 o[4];
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
-
-    // new tile max -> lazy update of the running max; sets (alpha, rescale) for the caller
-    auto update_max = [&](float mloc) {
-        const bool move = mloc > m_run + RESCALE_LOG2;
-        alpha = move ? __builtin_amdgcn_exp2f(m_run - mloc) : 1.f;
-        m_run = move ? mloc : m_run;
-        rescale = __builtin_amdgcn_ballot_w64(move) != 0;
-    };
-
-    // rescale O and l to a moved running max (rare: a max grew by more than 2^RESCALE_LOG2); done right
-    // after the P.V that precedes the move, so the accumulators are touched only on that branch
-    auto apply_rescale = [&]() {
-        if (rescale) {
-#pragma unroll
-            for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
-            l_run *= alpha;
-        }
-    };
-
-    f32x16 s_cur[2], s_nxt[2];
-    if (n > 0) {
-        stage_k(0, kt_begin);
-        stage_v(0, kt_begin);
-        if (n > 1) stage_k(1, kt_begin + 1);
-        wait_vmcnt<0>();
-        __builtin_amdgcn_s_barrier();
-        s_tile(std::integral_constant<int, 0>{}, s_cur);
-        update_max(prep(std::integral_constant<int, 0>{}, s_cur, 0));
-        apply_rescale();
-        __builtin_amdgcn_s_barrier();  // every wave has read K slot 0: iteration 0 restages it
-    }
-
-    // one pipeline iteration for relative tile i (its K slot and V slot are SLOT = i & 1)
-    auto iter = [&](auto slot_c, int i) {
-        constexpr int SLOT = decltype(slot_c)::value;
-        constexpr int NXT = SLOT ^ 1;
-        const bool more = i + 1 < n;
-        if (i + 2 < n) stage_k(SLOT, kt_begin + i + 2);
-        if (more) stage_v(NXT, kt_begin + i + 1);
-
-        // S(i+1) from K slot NXT (on the last tile: a discarded product of the slot's stale but
-        // finite contents, which keeps this block branch-free) || P(i) = exp2(S(i) - m + 12)
-        s_tile(std::integral_constant<int, NXT>{}, s_nxt);
-        const float m_use = ((m_run == -INFINITY) ? 0.f : m_run) - PSCALE_LOG2;
-        float lsum = 0.f;
-        frag pf[4], pfl[4];
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float pr = __builtin_amdgcn_exp2f(s_cur[t][r] - m_use);
-                s_cur[t][r] = pr;
-                lsum += pr;
-            }
-#pragma unroll
-            for (int ss = 0; ss < 2; ++ss) {
-                frag f, fl;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const float p0 = s_cur[t][8 * ss + 2 * j], p1 = s_cur[t][8 * ss + 2 * j + 1];
-                    if constexpr (PVS) {
-                        // hi = fp16 toward zero (one v_cvt_pkrtz per pair); p - hi is exact in f32 and
-                        // its fp16 lo keeps the pair at ~22 bits, as with round-to-nearest
-                        const auto h2 = __builtin_amdgcn_cvt_pkrtz(p0, p1);
-                        f[j] = __builtin_bit_cast(uint32_t, h2);
-                        fl[j] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(p0 - (float)h2[0], p1 - (float)h2[1]));
-                    } else {
-                        f[j] = pack_f16x2(p0, p1);  // v_cvt_pk_f16_f32, round to nearest
-                    }
-                }
-                pf[2 * t + ss] = f;
-                if constexpr (PVS) pfl[2 * t + ss] = fl;
-            }
-        }
-        l_run += lsum;
-
-        // O^T += V^T(i) . P^T(i) ; PVS: Vh.Ph + Vh.Pl + Vl.Ph  ||  scale / mask / max of S(i+1)
-        static_for<0, 2>([&](auto dp_c) {  // two 32-row d-tiles per LDS round trip
-            constexpr int dp = 2 * decltype(dp_c)::value;
-            frag vf[PVS ? 16 : 8];  // [u][g] hi, then lo
-            static_for<0, 2>([&](auto u_c) {
-                constexpr int u = decltype(u_c)::value;
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    vf[4 * u + g] = lds_frag<SLOT * RG::VS + (dp + u) * 32 * 128>(vaddr[g]);
-                    if constexpr (PVS)
-                        vf[8 + 4 * u + g] = lds_frag<SLOT * RG::VS + (dp + u) * 32 * 128 + RG::V_LO>(vaddr[g]);
-                }
-            });
-            lds_wait_tie(vf);
-#pragma unroll
-            for (int u = 0; u < 2; ++u)
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    o[dp + u] = mfma32(vf[4 * u + g], pf[g], o[dp + u]);
-                    if constexpr (PVS) {
-                        o[dp + u] = mfma32(vf[4 * u + g], pfl[g], o[dp + u]);
-                        o[dp + u] = mfma32(vf[8 + 4 * u + g], pf[g], o[dp + u]);
-                    }
-                }
-        });
-        const float mnx = prep(std::integral_constant<int, NXT>{}, s_nxt, i + 1);
-        if (more) {
-            update_max(mnx);
-            apply_rescale();
-        }
-#pragma unroll
-        for (int t = 0; t < 2; ++t) s_cur[t] = s_nxt[t];
-        if (more) {
-            wait_vmcnt<0>();                   // K(i+2), V(i+1) landed (requested at the top)
-            __builtin_amdgcn_s_barrier();      // ... for every wave; K slot NXT / V slot SLOT released
-        }
-    };
-
-    int i = 0;
-    for (; i + 1 < n; i += 2) {
-        iter(std::integral_constant<int, 0>{}, i);
-        iter(std::integral_constant<int, 1>{}, i + 1);
-    }
-    if (i < n) iter(std::integral_constant<int, 0>{}, i);
-
-    const float l = l_run + __shfl_xor(l_run, 32);
-    if (ks > 1 && a.fused_merge) {
-        // Key split, merged in place: every part stores its unnormalised O, running max and sum with
-        // device-coherent (sc1) stores, completes them (vmcnt 0) and takes a ticket; the part that takes the
-        // last ticket (whichever finishes last: no block ever waits) reads all S parts back in part order with
-        // sc1 loads and writes the normalised output -- the same arithmetic and order as attn_merge_kernel.
-        const int S = a.ksplit;
-        const int64_t rows = (int64_t)a.B * a.nq * a.Hq;
-        const int64_t r = ((int64_t)b * a.nq + qrow) * a.Hq + head;
-        const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void*)a.part, 0, 0x7fffffff, 0x00020000);
-        const __amdgpu_buffer_rsrc_t rm =
-            __builtin_amdgcn_make_buffer_rsrc((void*)(a.part + S * rows * D), 0, 0x7fffffff, 0x00020000);
-        if (qrow < a.nq) {
-#pragma unroll
-            for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-                for (int g4 = 0; g4 < 4; ++g4) {
-                    const u32x4_t v = {__float_as_uint(o[dt][4 * g4 + 0]), __float_as_uint(o[dt][4 * g4 + 1]),
-                                       __float_as_uint(o[dt][4 * g4 + 2]), __float_as_uint(o[dt][4 * g4 + 3])};
-                    __builtin_amdgcn_raw_buffer_store_b128(
-                        v, ro, (int)((((int64_t)split * rows + r) * D + 32 * dt + 8 * g4 + 4 * h) * 4), 0, 16);
-                }
-            if (h == 0) {
-                const u32x2_t v = {__float_as_uint(m_run), __float_as_uint(l)};
-                __builtin_amdgcn_raw_buffer_store_b64(v, rm, (int)(((int64_t)split * rows + r) * 2 * 4), 0, 16);
-            }
-        }
-        __builtin_amdgcn_s_waitcnt(0);
-        __syncthreads();  // every lane's stores are complete; the ring is free
-        unsigned* cnt = reinterpret_cast<unsigned*>(a.part + 4 * rows * (D + 2));
-        const int group = (b * a.Hkv + kvh) * n_qt + qt;
-        volatile unsigned* flag = reinterpret_cast<volatile unsigned*>(smem);
-        if (tid == 0) *flag = __hip_atomic_fetch_add(cnt + group, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();
-        if (*flag != (unsigned)(S - 1)) return;
-        if (tid == 0) __hip_atomic_store(cnt + group, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (qrow >= a.nq) return;
-        float mk[4], lk[4];
-        float M = -INFINITY;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (k < S) {
-                const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(rm, (int)(((int64_t)k * rows + r) * 2 * 4), 0, 16);
-                mk[k] = __uint_as_float(v[0]);
-                lk[k] = __uint_as_float(v[1]);
-                M = fmaxf(M, mk[k]);
-            }
-        }
-        float wk[4], den = 0.f;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (k < S) {
-                wk[k] = mk[k] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(mk[k] - M);
-                den += wk[k] * lk[k];
-            }
-        }
-        const float inv = 1.0f / den;
-        uint16_t* op = a.out + ((int64_t)b * a.nq + qrow) * (a.Hq * D) + head * D;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-#pragma unroll
-            for (int g4 = 0; g4 < 4; ++g4) {
-                const int d = 32 * dt + 8 * g4 + 4 * h;
-                float v[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    if (k < S) {
-                        const u32x4_t t = __builtin_amdgcn_raw_buffer_load_b128(
-                            ro, (int)((((int64_t)k * rows + r) * D + d) * 4), 0, 16);
-                        v[0] += wk[k] * __uint_as_float(t[0]);
-                        v[1] += wk[k] * __uint_as_float(t[1]);
-                        v[2] += wk[k] * __uint_as_float(t[2]);
-                        v[3] += wk[k] * __uint_as_float(t[3]);
-                    }
-                }
-                uint2 w;
-                w.x = (uint32_t)to_act<F16OUT>(v[0] * inv) | ((uint32_t)to_act<F16OUT>(v[1] * inv) << 16);
-                w.y = (uint32_t)to_act<F16OUT>(v[2] * inv) | ((uint32_t)to_act<F16OUT>(v[3] * inv) << 16);
-                *(uint2*)(op + d) = w;
-            }
-        }
-        return;
-    }
-    if (ks > 1) {  // unnormalised partial O, running max and sum for attn_merge_kernel
-        if (qrow < a.nq) {
-            const int64_t row = ((int64_t)split * a.B + b) * a.nq + qrow;
-            float* po = a.part + row * (a.Hq * D) + head * D;
-#pragma unroll
-            for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-                for (int g4 = 0; g4 < 4; ++g4)
-                    *(float4*)(po + 32 * dt + 8 * g4 + 4 * h) =
-                        make_float4(o[dt][4 * g4 + 0], o[dt][4 * g4 + 1], o[dt][4 * g4 + 2], o[dt][4 * g4 + 3]);
-            if (h == 0)
-                *(float2*)(a.part + (int64_t)a.ksplit * a.B * a.nq * a.Hq * D + (row * a.Hq + head) * 2) =
-                    make_float2(m_run, l);
-        }
-        return;
-    }
-    // ---- normalise and store O[q][head*128 + d]
-    const float inv = 1.0f / l;
-    if (qrow < a.nq) {
-        uint16_t* op = a.out + ((int64_t)b * a.nq + qrow) * (a.Hq * D) + head * D;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-#pragma unroll
-            for (int g4 = 0; g4 < 4; ++g4) {
-                const int d = 32 * dt + 8 * g4 + 4 * h;
-                uint2 w;
-                w.x = (uint32_t)to_act<F16OUT>(o[dt][4 * g4 + 0] * inv) |
-                      ((uint32_t)to_act<F16OUT>(o[dt][4 * g4 + 1] * inv) << 16);
-                w.y = (uint32_t)to_act<F16OUT>(o[dt][4 * g4 + 2] * inv) |
-                      ((uint32_t)to_act<F16OUT>(o[dt][4 * g4 + 3] * inv) << 16);
-                *(uint2*)(op + d) = w;
-            }
-        }
-    }
-}
-
 // ---------------------------------------------------------------------------------------------------------------
-// attn2_kernel (round 4): the same operands, layouts, block decomposition and online softmax as attn_kernel, with
+// attn2_kernel (round 4): the operands, layouts, block decomposition and online softmax of round 3's kernel, with
 // the per-tile instruction stream laid out by hand for one wave per SIMD (the hi/lo modes run one workgroup per CU):
 //   phase B  S(i+1) = K(i+1) Q^T  (16 k-steps of (k-slice, 32-key half), 1 or 3 MFMAs each)  interleaved step by
 //            step with the softmax finish of tile i: p = exp2(s * c - m'), the row sum and the fp16 packing of
@@ -1177,91 +740,6 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
     wait_vmcnt<0>();  // the re-read tiles past the end
 
     const float l = l_run + __shfl_xor(l_run, 32);
-    if (ks > 1 && a.fused_merge) {
-        // Key split merged in place (attn_kernel's protocol): every part stores its unnormalised O, running max and
-        // sum with device-coherent stores, completes them and takes a ticket; the part that takes the last ticket
-        // (whichever finishes last: no block ever waits) reads all parts back in part order and writes the
-        // normalised rows -- attn_merge_kernel's arithmetic and order, without its launch
-        const int S = a.ksplit;
-        const int64_t rows = (int64_t)a.B * a.nq * a.Hq;
-        const int64_t r = ((int64_t)b * a.nq + qrow) * a.Hq + head;
-        const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void*)a.part, 0, 0x7fffffff, 0x00020000);
-        const __amdgpu_buffer_rsrc_t rm =
-            __builtin_amdgcn_make_buffer_rsrc((void*)(a.part + S * rows * D), 0, 0x7fffffff, 0x00020000);
-        if (qrow < a.nq) {
-#pragma unroll
-            for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-                for (int g4 = 0; g4 < 4; ++g4) {
-                    const u32x4_t v = {__float_as_uint(o[dt][4 * g4 + 0]), __float_as_uint(o[dt][4 * g4 + 1]),
-                                       __float_as_uint(o[dt][4 * g4 + 2]), __float_as_uint(o[dt][4 * g4 + 3])};
-                    __builtin_amdgcn_raw_buffer_store_b128(
-                        v, ro, (int)((((int64_t)split * rows + r) * D + 32 * dt + 8 * g4 + 4 * h) * 4), 0, 16);
-                }
-            if (h == 0) {
-                const u32x2_t v = {__float_as_uint(m_run), __float_as_uint(l)};
-                __builtin_amdgcn_raw_buffer_store_b64(v, rm, (int)(((int64_t)split * rows + r) * 2 * 4), 0, 16);
-            }
-        }
-        __builtin_amdgcn_s_waitcnt(0);
-        __syncthreads();  // every lane's stores are complete; the ring is free
-        unsigned* cnt = reinterpret_cast<unsigned*>(a.part + 4 * rows * (D + 2));
-        const int group = (b * a.Hkv + kvh) * n_qt + qt;
-        volatile unsigned* flag = reinterpret_cast<volatile unsigned*>(smem);
-        if (tid == 0) *flag = __hip_atomic_fetch_add(cnt + group, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();
-        if (*flag != (unsigned)(S - 1)) return;
-        if (tid == 0) __hip_atomic_store(cnt + group, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (qrow >= a.nq) return;
-        float mk[4], lk[4];
-        float Mx = -INFINITY;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (k < S) {
-                const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(rm, (int)(((int64_t)k * rows + r) * 2 * 4), 0, 16);
-                mk[k] = __uint_as_float(v[0]);
-                lk[k] = __uint_as_float(v[1]);
-                Mx = fmaxf(Mx, mk[k]);
-            }
-        }
-        float wk[4], den = 0.f;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (k < S) {
-                wk[k] = mk[k] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(mk[k] - Mx);
-                den += wk[k] * lk[k];
-            }
-        }
-        const float inv = 1.0f / den;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-#pragma unroll
-            for (int g4 = 0; g4 < 4; ++g4) {
-                const int d = 32 * dt + 8 * g4 + 4 * h;
-                float v[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    if (k < S) {
-                        const u32x4_t t =
-                            __builtin_amdgcn_raw_buffer_load_b128(ro, (int)((((int64_t)k * rows + r) * D + d) * 4), 0, 16);
-                        v[0] += wk[k] * __uint_as_float(t[0]);
-                        v[1] += wk[k] * __uint_as_float(t[1]);
-                        v[2] += wk[k] * __uint_as_float(t[2]);
-                        v[3] += wk[k] * __uint_as_float(t[3]);
-                    }
-                }
-                if (a.out_f32) {
-                    *(float4*)(a.out_f32 + r * D + d) = make_float4(v[0] * inv, v[1] * inv, v[2] * inv, v[3] * inv);
-                } else {
-                    uint2 w;
-                    w.x = (uint32_t)to_act<F16OUT>(v[0] * inv) | ((uint32_t)to_act<F16OUT>(v[1] * inv) << 16);
-                    w.y = (uint32_t)to_act<F16OUT>(v[2] * inv) | ((uint32_t)to_act<F16OUT>(v[3] * inv) << 16);
-                    *(uint2*)(a.out + r * D + d) = w;
-                }
-            }
-        }
-        return;
-    }
     if (ks > 1) {
         if (qrow < a.nq) {
             const int64_t row = ((int64_t)split * a.B + b) * a.nq + qrow;
@@ -1352,11 +830,10 @@ __global__ void __launch_bounds__(256) attn_merge_kernel(AttnArgs a) {
 template <bool F16OUT, bool SPLIT, bool PVS>
 void launch_t(const AttnArgs& a, dim3 grid, hipStream_t s) {
     const size_t lds = Ring<SPLIT, PVS>::BYTES;
-    static int v2 = -1;  // ACE_MI_ATTN_V1=1: round 3's kernel (A/B)
-    if (v2 < 0) {
-        const char* e = std::getenv("ACE_MI_ATTN_V1");
-        v2 = (e && e[0] == '1') ? 0 : 1;
-    }
+    // One workgroup per CU in every mode (round 6): each instance then runs one wave per SIMD, the only occupancy at
+    // which attn2's hand-laid stream may reuse an MFMA's A / B register right after issuing it (tools/audit_mfma_war.py
+    // classifies those pairs as single-wave).  Round 3's kernel (attn_kernel, ACE_MI_ATTN_V1) and the
+    // two-per-CU fp16 instance are gone: the fp16 mode is a diagnostic precision, not a product one.
     if constexpr (PVS) {
         if (a.f8) {  // f8c (SPLIT) or pv8 (fp16 Q.K)
             if (a.kbias)
@@ -1369,30 +846,10 @@ void launch_t(const AttnArgs& a, dim3 grid, hipStream_t s) {
     if constexpr (!SPLIT && PVS) {
         throw std::runtime_error("attention: hi/lo P.V with fp16 Q.K exists only with fp8 corrections (pv8)");
     } else {
-        if (v2) {
-            constexpr int OCC = SPLIT ? 1 : 2;
-            if (a.kbias)
-                hipLaunchKernelGGL((attn2_kernel<F16OUT, SPLIT, PVS, true, OCC>), grid, dim3(256), lds, s, a);
-            else
-                hipLaunchKernelGGL((attn2_kernel<F16OUT, SPLIT, PVS, false, OCC>), grid, dim3(256), lds, s, a);
-            return;
-        }
-        static int occ = 0;  // ACE_MI_ATTN_OCC=1: one workgroup per CU for the single-fp16 kernel too (A/B)
-        if (occ == 0) {
-            const char* e = std::getenv("ACE_MI_ATTN_OCC");
-            occ = (e && e[0] == '1') ? 1 : 2;
-        }
-        if (!SPLIT && occ == 2) {
-            if (a.kbias)
-                hipLaunchKernelGGL((attn_kernel<F16OUT, SPLIT, PVS, true, 2>), grid, dim3(256), lds, s, a);
-            else
-                hipLaunchKernelGGL((attn_kernel<F16OUT, SPLIT, PVS, false, 2>), grid, dim3(256), lds, s, a);
-            return;
-        }
         if (a.kbias)
-            hipLaunchKernelGGL((attn_kernel<F16OUT, SPLIT, PVS, true, 1>), grid, dim3(256), lds, s, a);
+            hipLaunchKernelGGL((attn2_kernel<F16OUT, SPLIT, PVS, true, 1>), grid, dim3(256), lds, s, a);
         else
-            hipLaunchKernelGGL((attn_kernel<F16OUT, SPLIT, PVS, false, 1>), grid, dim3(256), lds, s, a);
+            hipLaunchKernelGGL((attn2_kernel<F16OUT, SPLIT, PVS, false, 1>), grid, dim3(256), lds, s, a);
     }
 }
 
@@ -1437,8 +894,8 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s) {
             const char* e = std::getenv("ACE_MI_ATTN_KSPLIT");
             mode = (e && (e[0] == '1' || e[0] == '2' || e[0] == '3' || e[0] == '4')) ? e[0] - '0' : 0;
         }
-        // blocks resident per CU: two for the single-fp16 kernel (66 KiB ring), one for the hi/lo ones
-        const int per_cu = (a.split || a.pv_split) ? 1 : 2;
+        // blocks resident per CU: one in every mode (launch_t)
+        const int per_cu = 1;
         const int64_t slots = (int64_t)n_cu * per_cu;
         const int ntiles = (span + KT - 1) / KT;
         int S = 1;
@@ -1471,23 +928,14 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s) {
         if (a.part && mode == 2) b.ksplit = 2;
         else if (a.part && (mode == 0 || mode == 3 || mode == 4)) b.ksplit = S;
         if (tail_fits && b.ksplit == 2) b.split_from = (int)F;
-        // ACE_MI_ATTN_FUSED_MERGE=1: the last part of a group merges in the attention kernel (sc1 partial
-        // round trip, no merge launch) -- measured 2.6x slower attention at 60 s in the first kernel; in attn2
-        // (profiles/r05/attn_fused_merge.txt) neutral at 60 s, 4 % slower lines at 240 s (it replaces the tail
-        // split by splitting every block) and 5 % slower at 60 s with ACE_MI_ATTN_KSPLIT=4, so off by default
-        static int fm = -1;
-        if (fm < 0) {
-            const char* e = std::getenv("ACE_MI_ATTN_FUSED_MERGE");
-            fm = (e && e[0] == '1') ? 1 : 0;
-        }
-        b.fused_merge = fm;
+        // (round 5 also built an in-kernel merge -- the last part of a group merging through an sc1 partial round
+        // trip and a ticket, no merge launch: neutral at 60 s, 4 % slower lines at 240 s, profiles/r05/attn_fused_merge.txt;
+        // removed from the product library in round 6)
     }
-    b.split_from = b.fused_merge ? 0 : b.split_from;
     if (a.out_f32) {  // f32 output: every block in two key-range parts, merged into f32 rows
         ACEMI_CHECK(a.part != nullptr, "attention: f32 output needs the partials workspace");
         b.ksplit = 2;
         b.split_from = 0;
-        b.fused_merge = 0;
     }
     const int64_t n_blk = (int64_t)a.B * a.Hkv * n_qt;
     // XCD-aware order (attn_block): whole multiples of 8 launch indices per range
@@ -1510,7 +958,7 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s) {
         f16 ? launch_t<true, false, false>(b, grid, s) : launch_t<false, false, false>(b, grid, s);
     }
     ACEMI_HIP(hipGetLastError());
-    if (b.ksplit > 1 && !b.fused_merge) {
+    if (b.ksplit > 1) {
         const int64_t rows = (int64_t)a.B * a.nq * a.Hq;
         ACEMI_CHECK(b.ksplit == 2 || b.ksplit == 4, "attention: the merge handles 2 or 4 key-split parts");
         const dim3 mgrid((unsigned)((rows + 7) / 8));
@@ -1539,8 +987,8 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s) {
 
 size_t attn_part_floats(int B, int nq, int Hq) {
     const size_t rows = (size_t)B * nq * Hq;
-    // up to four key-split parts + one ticket word per (item, kv head, query tile) group (qpb >= 32)
-    return 4 * rows * (D + 2) + (size_t)B * Hq * ((nq + 31) / 32 + 1);
+    // up to four key-split parts: unnormalised O rows + (running max, sum) per row
+    return 4 * rows * (D + 2);
 }
 
 }  // namespace acemi

@@ -205,6 +205,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (GemmTwoPerCU<BM, BN, WM, WN, EP
                 for (int i = 0; i < TM; ++i)
 #pragma unroll
                     for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<F16>(a[i][kk], b[j][kk], acc[i][j]);
+            mfma_war_retire(a, b);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
         }
@@ -255,6 +256,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (GemmTwoPerCU<BM, BN, WM, WN, EP
                 for (int i = 0; i < I_EARLY; ++i)
 #pragma unroll
                     for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<F16>(a[i][kk], b[j][kk], acc[i][j]);
+            if constexpr (I_EARLY > 0) mfma_war_retire(a, b);
             __builtin_amdgcn_s_barrier();  // every wave has its fragments of tile kt: buffer `cur` is free
             const bool more = kt + NS < nk && !(kAblate & 1);
             if (more) stage(cur, kt + NS);
@@ -265,6 +267,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (GemmTwoPerCU<BM, BN, WM, WN, EP
                 for (int i = I_EARLY; i < TM; ++i)
 #pragma unroll
                     for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<F16>(a[i][kk], b[j][kk], acc[i][j]);
+            mfma_war_retire(a, b);
             if (kt + 1 < nk) {
                 if constexpr (PF)
                     wait_vmcnt<XW>();  // tile kt+1 (the last) landed, the residual prefetch still in flight
@@ -566,6 +569,7 @@ __global__ void __launch_bounds__(512) gemm8_kernel(GemmParams p) {
             for (int i = 0; i < QM; ++i)
 #pragma unroll
                 for (int j = 0; j < QN; ++j) c[i][j] = mfma16<F16>(a[i][kk], b[j][kk], c[i][j]);
+        mfma_war_retire(a, b);
         __builtin_amdgcn_s_setprio(0);
     };
     // segment boundary: the barrier that hands over to the other group

@@ -11,6 +11,7 @@
 #include "../kernels.h"
 #include "norm_math.h"
 #include "prep_math.h"
+#include "mfma_guard.h"
 
 namespace acemi {
 namespace gemm_detail {
@@ -109,21 +110,6 @@ __device__ __forceinline__ void static_for(F&& f) {
         f(std::integral_constant<int, B>{});
         static_for<B + 1, E>(f);
     }
-}
-
-// MFMA operand write-after-read guard.  On gfx950 with two waves per SIMD, a VALU that writes an A / B source register of
-// an MFMA issued just before it can corrupt that product: the register-dequant tile with the kk = 1 dequant VALU
-// scheduled between the kk = 0 MFMAs (hipcc pads this pair for the C operand only) gave whole wrong 16-column groups
-// of waves 4-7 on some launches -- rounds 3-4's "variant 21 x Q4_K" and "64-row tile not run-to-run identical"
-// anomalies.  Measured (tools/diag_v21.py, profiles/r05/qr_war/): a scheduling fence between the MFMA block and the
-// VALU that follows it removes every failure; padding only the end of the tile does not.  The fence keeps hipcc from
-// interleaving the two, the s_nops keep 16 wait states between the last MFMA and the first overwrite.  The same
-// fence between the dequant VALU and the MFMAs that read its B fragments (read-after-write) made the split-K forms
-// (223 / 423) and the residual epilogue of 21 x Q4_K exact as well (profiles/r05/qr_war/).
-__device__ __forceinline__ void mfma_war_guard() {
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_nop 7\n\ts_nop 7");
-    __builtin_amdgcn_sched_barrier(0);
 }
 
 // s_waitcnt vmcnt(N) with N a compile-time constant (lgkmcnt/expcnt untouched)

@@ -274,6 +274,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_q_kernel(GemmParams p) {
             for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<false>(a[i][kk], b[j][kk], acc[i][j]);
+        mfma_war_retire(a, b);
     };
 
     // One branch-free body for every tile: past the end, the tile indices clamp to nk-1, so the last
@@ -755,7 +756,8 @@ __global__ void __launch_bounds__(512, 1) gemm_wsq_kernel(GemmParams p) {
 #pragma unroll
         for (int t = 0; t < NS; ++t)
             if (t < nk) stage(t);
-        if (nk > 1) wait_vmcnt<GA + G>();  // W(0) A(0) W(1) retired; A(1) W(2) A(2) in flight
+        if (nk > 2) wait_vmcnt<GA + G>();       // W(0) A(0) W(1) retired; A(1) W(2) A(2) in flight
+        else if (nk == 2) wait_vmcnt<GA>();    // (K = 128: only tiles 0, 1 staged) W(0) A(0) W(1) retired; A(1) in flight
         else wait_vmcnt<0>();
         __builtin_amdgcn_s_barrier();  // P: (a barrier between W(0)'s retiring wait and its reads)
         auto none = [] {};

@@ -22,6 +22,7 @@
 #include "../kernels.h"
 #include "lds_asm.h"
 #include "prep_math.h"
+#include "mfma_guard.h"
 
 namespace acemi {
 namespace {
@@ -231,6 +232,7 @@ __global__ void __launch_bounds__(256, 2) conv_gemm_kernel(ConvGemmArgs p) {
         if (more) stage(cur, kt + 2);
         mma(a, b, 0);
         mma(a, b, TM / 2);
+        mfma_war_retire(a, b);
         if (kt + 1 < nk) {
             if (more)
                 wait_vmcnt<G_PER_WAVE>();
@@ -292,6 +294,7 @@ __global__ void __launch_bounds__(256, 2) conv_gemm_kernel(ConvGemmArgs p) {
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a2[i]),
                                                                        __builtin_bit_cast(f16x8, b2f[j][ks]),
                                                                        acc[i][j], 0, 0, 0);
+            mfma_war_retire(a2, b2f);
         }
         (void)y0;
     }

@@ -54,6 +54,25 @@ def check(got, ref, floor, tag, floor_max=None):
     return l2
 
 
+# The shipped quantized path (bf16 activations x bf16(dequant(W))) against ggml's OWN quantized arithmetic (Q8_0 / Q8_K
+# activation blocks): its arithmetic differs from ggml's by the activation rounding, so it is held to a looser, asserted
+# multiple of the ggml-semantics floor (measured 1.28-1.64x in round 5): rel-L2 <= GGML_PRODUCT_K x floor and
+# max|d| / rms <= GGML_PRODUCT_K x MAXABS_K x that statistic's floor.  A regression that moves the product path away
+# from ggml fails here even while it still matches its own arithmetic (check() against engine_view).
+GGML_PRODUCT_K = 1.75
+
+
+def check_product_vs_ggml(got, ref, floor, floor_max, tag):
+    l2, _ = rel_errors(got, ref)
+    ma = maxabs_rms(got, ref)
+    print(f"{tag}: product path vs ggml semantics rel_l2={l2:.3e} floor={floor:.3e} ratio={l2 / floor:.2f} "
+          f"maxabs/rms={ma:.3e} floor_maxabs={floor_max:.3e} maxabs_ratio={ma / floor_max:.2f} "
+          f"(bounds {GGML_PRODUCT_K} / {GGML_PRODUCT_K * MAXABS_K})")
+    assert np.isfinite(l2) and l2 <= GGML_PRODUCT_K * floor, (tag, l2, floor)
+    assert ma <= GGML_PRODUCT_K * MAXABS_K * floor_max, (tag, ma, floor_max)
+    return l2
+
+
 def maxabs_rms(got, ref):
     from oracle.dit_oracle import maxabs_rms as f
     return f(got, ref)

@@ -292,6 +292,24 @@ def test_attention_key_split_with_one_part_fully_masked():
         _check_attn(got, q, kv, hq, hkv, 0, kmask, scale, mode)
 
 
+@pytest.mark.parametrize("nk", [566, 600])
+@pytest.mark.parametrize("mode", list(MODES))
+def test_attention_short_range_four_way_split(nk, mode):
+    """Short key ranges on a grid of at most a quarter round are split in four parts by default (launch_attention,
+    mode 0): 9 / 10 key tiles give parts of 3, 3, 3, 0 / 3, 3, 3, 1 tiles -- an EMPTY last part (n = 0) -- and the
+    key mask below leaves the first part with no visible key (m = -inf, l = 0).  Against the fp64 reference."""
+    rng = np.random.default_rng(nk)
+    B, hq, hkv, nq = 1, 2, 1, 100  # 2 blocks of 64 queries
+    q = rng.standard_normal((B, nq, hq * 128)).astype(np.float32) * 2.0
+    kv = rng.standard_normal((B, nk, 2 * hkv * 128)).astype(np.float32) * 0.3
+    kmask = (rng.random((B, nk)) > 0.3).astype(np.int32)
+    kmask[:, :3 * 64] = 0  # part 0 fully masked
+    kmask[:, 3 * 64] = 1
+    scale = 1.0 / np.sqrt(128.0)
+    got = _capi().kernel_attention(q, kv, hq, hkv, window=0, kmask=kmask, scale=scale, **MODES[mode])
+    _check_attn(got, q, kv, hq, hkv, 0, kmask, scale, mode)
+
+
 @pytest.mark.parametrize("variant", [204, 207, 211, 212, 307, 408])
 def test_gemm_splitk_deterministic(variant):
     """Split-K: the last block of a tile adds the parts in K order, so repeated launches (with the per-tile
@@ -315,3 +333,36 @@ def test_gemm_splitk_deterministic(variant):
         av, wv = _vals(a, 0).astype(np.float64), _vals(w, 0).astype(np.float64)
         assert np.all(np.abs(outs[-1] - av @ wv.T) <= 2e-6 * (np.abs(av) @ np.abs(wv).T) + 1e-6)
     np.testing.assert_array_equal(outs[0], outs[4])
+
+
+# ---------------------------------------------------------------- run-to-run identity of the product kernels
+# The round-5 MFMA operand hazard showed as launch-dependent wrong column groups; the static audit
+# (tests/test_mfma_war_audit.py) finds no unguarded pair in a two-wave kernel.  These tests are its dynamic side: the
+# product picks at the 240 s shapes (M = 3000) launched repeatedly must give identical bits every time.
+@pytest.mark.parametrize("name,N,K,epi", [("o / cross-o (gated residual)", 2048, 2048, 2),
+                                          ("down (gated residual)", 2048, 6144, 2),
+                                          ("gate|up (SwiGLU)", 12288, 2048, 4), ("qkv-shaped store", 4096, 2048, 0)])
+def test_product_gemm_picks_run_to_run_identical(name, N, K, epi):
+    capi = _capi()
+    M = 3000
+    rng = np.random.default_rng(N + K)
+    a = _bits(rng.standard_normal((M, K)).astype(np.float32), 0)
+    w = _bits((rng.standard_normal((N, K)) * 0.02).astype(np.float32), 0)
+    x = rng.standard_normal((M, N)).astype(np.float32) if epi == 2 else None
+    gate = rng.standard_normal(N).astype(np.float32) if epi == 2 else None
+    outs = [capi.kernel_gemm(a, w, act_type=0, epi=epi, bias=gate, x=x) for _ in range(6)]
+    for i, o in enumerate(outs[1:], 1):
+        assert np.array_equal(o.view(np.uint32) if o.dtype == np.float32 else o,
+                              outs[0].view(np.uint32) if outs[0].dtype == np.float32 else outs[0]), (name, i)
+
+
+@pytest.mark.parametrize("window", [0, 128])
+def test_product_attention_run_to_run_identical(window):
+    """f8c (the DiT default) at the 240 s self-attention shape: full layers (tail split + merge) and sliding ones."""
+    rng = np.random.default_rng(5 + window)
+    q = rng.standard_normal((1, 3000, 16 * 128)).astype(np.float32)
+    kv = rng.standard_normal((1, 3000, 2 * 8 * 128)).astype(np.float32) * 0.5
+    outs = [_capi().kernel_attention(q, kv, 16, 8, window=window, scale=1 / np.sqrt(128.0), **MODES["f8c"])
+            for _ in range(5)]
+    for i, o in enumerate(outs[1:], 1):
+        assert np.array_equal(o.view(np.uint32), outs[0].view(np.uint32)), (window, i)
