@@ -48,8 +48,7 @@ def test_staged_dequant_kernel_is_exact(qtype, N, K):
 
 @pytest.mark.parametrize("qtype", ["q8_0", "q4_k", "q6_k"])
 @pytest.mark.parametrize("variant", [-1, 1, 2, 3, 4, 5, 7, 20, 21, 22, 23, 24, 25, 222, 223, 423])
-@pytest.mark.parametrize("M,N,K", [(1, 256, 256), (300, 512, 512), (1000, 256, 2048), (129, 768, 6144), (1100, 256, 128),
-                                   (1100, 256, 64)])
+@pytest.mark.parametrize("M,N,K", [(1, 256, 256), (300, 512, 512), (1000, 256, 2048), (129, 768, 6144)])
 def test_gemm_q_matches_dequantized_product(qtype, variant, M, N, K):
     """Both dequant-fused kernels (round 1's LDS-dequant tiles 1-7; the register-dequant tiles 20-24, + 100 S for
     split-K over S blocks) against an fp64 product of the same bf16 operands."""
@@ -58,10 +57,6 @@ def test_gemm_q_matches_dequantized_product(qtype, variant, M, N, K):
         pytest.skip("256-wide tiles need N % 256 == 0")
     if variant >= 100 and K // 64 < 2 * (variant // 100):
         pytest.skip("split-K needs two k-tiles per part")
-    if qtype != "q8_0" and K % 256:
-        pytest.skip("K-quant super-blocks are 256 wide")
-    # (K = 128 / 64 at M > 1024: the warp-specialised tile (25) with only two / one k-tile in its 3-slot ring -- the
-    # prologue's counted wait; pick_variant_q picks 25 there whatever K is)
     rng = np.random.default_rng(M + K + variant)
     a = f32_to_bf16_bits(rng.standard_normal((M, K)).astype(np.float32))
     w = (rng.standard_normal((N, K)) * 0.02).astype(np.float32)
@@ -69,6 +64,25 @@ def test_gemm_q_matches_dequantized_product(qtype, variant, M, N, K):
     bias = rng.standard_normal(N).astype(np.float32)
     got = capi.kernel_gemm_q(a, blocks, qtype, epi=0, variant=variant, bias=bias)
     ref, scale = _q_ref(a, blocks, qtype)
+    ref = ref + bias
+    assert np.all(np.abs(got - ref) <= 2e-6 * scale + 1e-6), np.max(np.abs(got - ref) / (scale + 1e-6))
+
+
+@pytest.mark.parametrize("variant", [-1, 1, 3, 4, 20, 22, 23, 24, 25])
+@pytest.mark.parametrize("M,K", [(1100, 128), (1100, 64), (300, 128)])
+def test_gemm_q_short_k_q8_0(variant, M, K):
+    """Q8_0 rows of K = 128 / 64 (four / two blocks): the warp-specialised tile (25, what pick_variant_q takes at
+    M > 1024 with N <= 2048 whatever K is) with only two / one k-tile in its 3-slot ring -- its prologue's counted wait
+    (round 6 fix) -- and the other fused tiles' short pipelines."""
+    capi = _capi()
+    N = 256
+    rng = np.random.default_rng(M + K + variant)
+    a = f32_to_bf16_bits(rng.standard_normal((M, K)).astype(np.float32))
+    w = (rng.standard_normal((N, K)) * 0.02).astype(np.float32)
+    blocks = capi.quantize(w, "q8_0")
+    bias = rng.standard_normal(N).astype(np.float32)
+    got = capi.kernel_gemm_q(a, blocks, "q8_0", epi=0, variant=variant, bias=bias)
+    ref, scale = _q_ref(a, blocks, "q8_0")
     ref = ref + bias
     assert np.all(np.abs(got - ref) <= 2e-6 * scale + 1e-6), np.max(np.abs(got - ref) / (scale + 1e-6))
 
