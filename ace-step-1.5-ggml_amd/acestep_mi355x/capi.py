@@ -33,7 +33,7 @@ EXPORTED_SYMBOLS = (
     "ace_mi_dit_sample_ex",
     "ace_mi_profile_enable", "ace_mi_dit_set_attn_precision", "ace_mi_profile_reset", "ace_mi_profile_get", "ace_mi_probe_gemm",
     "ace_mi_synchronize",
-    "ace_mi_gemm_variant", "ace_mi_norm_fuse", "ace_ggml_load_vae", "ace_ggml_vae_get_info", "ace_ggml_vae_decode",
+    "ace_mi_gemm_variant", "ace_ggml_load_vae", "ace_ggml_vae_get_info", "ace_ggml_vae_decode",
     "ace_mi_vae_out_len", "ace_mi_vae_decode_device", "ace_ggml_vae_encode", "ace_mi_vae_enc_out_len",
     "ace_mi_vae_encode_device", "ace_mi_quantize", "ace_mi_dequantize",
     "ace_mi_cond_get_info", "ace_mi_text_project", "ace_mi_lyric_encode", "ace_mi_timbre_encode",
@@ -130,8 +130,6 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.ace_mi_synchronize.restype = ctypes.c_int
     lib.ace_mi_gemm_variant.argtypes = [i32]
     lib.ace_mi_gemm_variant.restype = ctypes.c_int
-    lib.ace_mi_norm_fuse.argtypes = [i32]
-    lib.ace_mi_norm_fuse.restype = ctypes.c_int
     i64, u8p = ctypes.c_int64, ctypes.POINTER(ctypes.c_uint8)
     lib.ace_ggml_load_vae.argtypes = [vp, ctypes.c_char_p]
     lib.ace_ggml_load_vae.restype = ctypes.c_int
@@ -751,10 +749,3 @@ def gemm_variant(variant: int) -> None:
     if lib.ace_mi_gemm_variant(int(variant)) != ACE_GGML_OK:
         raise ValueError(variant)
 
-
-def norm_fuse(mode: int) -> None:
-    """Fused row norm of the residual GEMMs: -1 environment, 0 off, 1 on, 2 on without waiting (hand-over path),
-    3 off with the standalone norm in the fused epilogue's summation order."""
-    lib = load_library()
-    if lib.ace_mi_norm_fuse(int(mode)) != ACE_GGML_OK:
-        raise ValueError(mode)

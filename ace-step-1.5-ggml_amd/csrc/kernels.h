@@ -51,26 +51,6 @@ enum GemmEpiKind : int {
     EPI_SWIGLU_F32 = 7,     // EPI_SWIGLU with an f32 output c_f32 (the quantized-activation GEMM only)
 };
 
-// The row RMSNorm + AdaLN modulation that follows a residual GEMM (x += ...; act = norm(x) * w * (1 + scale) +
-// shift), fused into that GEMM's epilogue by launch_gemm_resid_norm: the column tiles of a row block publish
-// their partial sums of squares, and each normalises its own tile once the row block is complete
-// (gemm_common.h norm_fuse; summation order of kernels/norm_math.h, the standalone kernel's).
-struct NormFuse {
-    const float* w = nullptr;  // [N] norm weight (nullptr: no fused norm)
-    const float* scale = nullptr;
-    const float* shift = nullptr;  // per item, [item * mod_stride + n]; both or neither
-    int64_t mod_stride = 0;
-    int rows_per_item = 1;
-    float eps = 1e-6f;
-    uint16_t* out = nullptr;  // act [M][N], the GEMM's act type
-    // set by the launch: partial sums [M][N / BN], per-row-block arrival counts [nbm] (stride 32) and per-tile claims
-    // [nbm][N / BN] (zero between launches), how long a tile waits for its row block (s_memrealtime ticks)
-    float* part = nullptr;
-    unsigned* cnt = nullptr;
-    unsigned* claim = nullptr;
-    long long spin_ticks = 0;
-};
-
 struct GemmEpilogue {
     int kind = EPI_STORE_F32;
     const float* bias = nullptr;
@@ -84,7 +64,6 @@ struct GemmEpilogue {
     int out_ch = 0;       // EPI_PROJ_OUT: channels (64)
     int patch = 2;        // EPI_PROJ_OUT
     PrepArgs prep{};      // EPI_QKV_PREP (src / ld unused)
-    NormFuse norm{};      // launch_gemm_resid_norm only
 };
 
 // Weight operand.  Dense: 16-bit [N][ld] in the activation type.  Quantized (ggml block formats
@@ -105,25 +84,12 @@ inline bool weight_quantized(int fmt) { return fmt >= WF_Q8_0; }
 
 void launch_gemm(const uint16_t* A, int lda, const WeightView& W, int M, int N, int K, const GemmEpilogue& epi,
                  hipStream_t s);
-// A residual GEMM (EPI_RESID / EPI_RESID_GATED) followed by the row norm epi.norm: fused into the GEMM when the
-// picked tile supports it (dense weights, the 4-wave residual-prefetch tiles, N / BN <= 32) and it is on
-// (ACE_MI_NORM_FUSE=1 or gemm_norm_fuse_mode) -- returns true; otherwise runs the plain GEMM and returns false, and
-// the caller launches the norm.
-bool launch_gemm_resid_norm(const uint16_t* A, int lda, const WeightView& W, int M, int N, int K,
-                            const GemmEpilogue& epi, hipStream_t s);
 // dense shorthand: W 16-bit of type t
 void launch_gemm(ActType t, const uint16_t* A, int lda, const uint16_t* W, int ldw, int M, int N, int K,
                  const GemmEpilogue& epi, hipStream_t s);
 // -1 = automatic tile choice; 0..11 force a kernel variant, + 100 * S (S = 2..4) split-K over S blocks per
 // tile for the 4-wave tiles (micro-benchmarks / tests)
 void gemm_force_variant(int v);
-// fused row norm mode of launch_gemm_resid_norm: -1 = environment, 0 = off, 1 = on, 2 = on with no wait (the
-// hand-over path), 3 = off with the standalone kernel in the canonical order (the tests' reference)
-void gemm_norm_fuse_mode(int mode);
-// whether launch_gemm_resid_norm currently fuses (mode / ACE_MI_NORM_FUSE)
-bool gemm_norm_fuse_on();
-// whether launch_rmsnorm_mod sums in the canonical order of kernels/norm_math.h (fusion on, or mode 3)
-bool gemm_norm_canonical();
 // Throws (once) if a split-K GEMM join on the current device timed out since the last check: reads a per-device
 // host-pinned error word, no stream is synchronised (called at the library's synchronisation points and on entry).
 void gemm_splitk_check();

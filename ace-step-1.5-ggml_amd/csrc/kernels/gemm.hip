@@ -54,8 +54,7 @@ struct GemmTwoPerCU {
         (TBM + TBN) * 256 * (TPIPE >= 3 ? TPIPE : 2) <= 160 * 1024;
 };
 
-// NF: the row-norm-fused instance (launch_gemm_resid_norm; residual-prefetch tiles only)
-template <int BM, int BN, int WM, int WN, bool F16, int EPI, int PIPE, bool SK = false, bool NF = false>
+template <int BM, int BN, int WM, int WN, bool F16, int EPI, int PIPE, bool SK = false>
 __global__ void __launch_bounds__(WM * WN * 64, (GemmTwoPerCU<BM, BN, WM, WN, EPI, PIPE, SK>::value ? 2 : 1))
     gemm_kernel(GemmParams p) {
     constexpr int NW = WM * WN;
@@ -281,12 +280,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (GemmTwoPerCU<BM, BN, WM, WN, EP
             for (int kt = 0; kt < kp; ++kt) body(kt, std::false_type{});
             body(kp, std::true_type{});
             if (kp + 1 < nk) body(kp + 1, std::false_type{});
-            if constexpr (NF) {  // the row norm that follows, fused (launch_gemm_resid_norm)
-                resid_apply<TM, TN, EPI, true>(p, acc, m0 + wm0, n0 + wn0, lane, BM / WM, xo, g0, g1);
-                norm_fuse<BM, BN, WM, WN, TM, TN, F16, NS * STAGE>(p, acc, m0, n0, wm0, wn0, tid, smem);
-            } else {
-                resid_apply<TM, TN, EPI>(p, acc, m0 + wm0, n0 + wn0, lane, BM / WM, xo, g0, g1);
-            }
+            resid_apply<TM, TN, EPI>(p, acc, m0 + wm0, n0 + wn0, lane, BM / WM, xo, g0, g1);
             return;
         } else {
             for (int kt = 0; kt < nk; ++kt) body(kt, std::false_type{});
@@ -724,13 +718,6 @@ template <int BM, int BN, int WM, int WN, bool F16, int EPI, int PIPE>
 void launch_cfg(GemmParams p, int S, hipStream_t s) {
     const int nbm = (p.M + BM - 1) / BM;
     const int nbn = p.N / BN;
-    {
-        // the fused row norm runs on the residual-prefetch path of gemm_kernel only (norm_fuse_bn lists those tiles)
-        constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
-        constexpr bool xpf = (EPI == EPI_RESID || EPI == EPI_RESID_GATED) && PIPE >= 1 && WM * WN == 4 &&
-                             TM * 4 * TN + (EPI == EPI_RESID_GATED ? 2 * TN : 0) <= 63;
-        if (p.e.norm.w != nullptr && (!xpf || S > 1)) throw std::runtime_error("gemm: no fused norm for this tile");
-    }
     if (S > 1) {
         if (p.K / 64 < 2 * S) throw std::runtime_error("gemm: split-K needs at least two K-tiles per part");
         if (S > SplitKMax<BM, BN>::value) throw std::runtime_error("gemm: split-K factor too large for this tile");
@@ -741,12 +728,8 @@ void launch_cfg(GemmParams p, int S, hipStream_t s) {
     if constexpr (EPI == EPI_QKV_PREP && BN != 128) {
         throw std::runtime_error("gemm: the fused attention prep needs 128-wide column tiles");
     } else if constexpr (WM * WN == 4 && PIPE >= 1) {  // split-K instances: the 4-wave pipelined tiles
-        constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
-        constexpr bool xpf = (EPI == EPI_RESID || EPI == EPI_RESID_GATED) && TM * 4 * TN + (EPI == EPI_RESID_GATED ? 2 * TN : 0) <= 63;
         if (S > 1)
             hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, F16, EPI, PIPE, true>), grid, block, 0, s, p);
-        else if (xpf && p.e.norm.w != nullptr)
-            hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, F16, EPI, PIPE, false, xpf>), grid, block, 0, s, p);
         else
             hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, F16, EPI, PIPE>), grid, block, 0, s, p);
     } else {
@@ -757,7 +740,6 @@ void launch_cfg(GemmParams p, int S, hipStream_t s) {
 
 template <int BM, int BN, bool F16, int EPI, int NS>
 void launch_ws(const GemmParams& p, hipStream_t s) {
-    if (p.e.norm.w != nullptr) throw std::runtime_error("gemm: no fused norm for this tile");
     if (p.N % BN != 0) throw std::runtime_error("gemm: the warp-specialized tile needs N % BN == 0");
     if constexpr (EPI == EPI_QKV_PREP && BN != 128) {
         throw std::runtime_error("gemm: the fused attention prep needs 128-wide column tiles");
@@ -769,7 +751,6 @@ void launch_ws(const GemmParams& p, hipStream_t s) {
 
 template <int BM, bool F16, int EPI>
 void launch_cfg8(GemmParams p, int S, hipStream_t s) {
-    if (p.e.norm.w != nullptr) throw std::runtime_error("gemm: no fused norm for this tile");
     if (p.N % 256 != 0) throw std::runtime_error("gemm: the 8-wave tiles need N % 256 == 0");
     const int nbm = (p.M + BM - 1) / BM;
     if (S > 1) {
@@ -979,7 +960,6 @@ void launch_gemm(const uint16_t* A, int lda, const WeightView& W, int M, int N, 
     ACEMI_CHECK(lda % 8 == 0, "gemm: leading dims must be multiples of 8");
     ACEMI_CHECK(W.q != nullptr, "gemm: null weight");
     GemmParams p{A, (const uint16_t*)W.q, W.q, W.s, lda, W.ld, M, N, K, epi};
-    p.e.norm = NormFuse{};  // (fused only through launch_gemm_resid_norm, which sets up its workspace)
     int v = pick_variant(M, N, K, weight_quantized(W.fmt), W.fmt);
     if (epi.kind == EPI_QKV_PREP) {  // 128-wide column tiles: one head per tile
         ACEMI_CHECK(epi.bias == nullptr && epi.prep.n_tok > 0 && M % epi.prep.n_tok == 0,
@@ -1020,101 +1000,6 @@ void launch_gemm(const uint16_t* A, int lda, const WeightView& W, int M, int N, 
     ACEMI_HIP(hipGetLastError());
 }
 
-namespace {
-// fused-norm workspace of one (device, stream), like the split-K one: partial sums [M][N / BN] (grows), arrival
-// counts + claims (zeroed once; every launch leaves them zero)
-struct NormWs {
-    float* part = nullptr;
-    size_t part_n = 0;
-    unsigned* cnt = nullptr;
-    size_t cnt_n = 0;
-};
-std::map<std::pair<int, hipStream_t>, NormWs> g_norm;
-int g_norm_mode = -1;
-
-// column-tile width of the variants whose instance takes the residual-prefetch path (gemm_kernel XPF: 4 waves,
-// pipelined, TM * 4 * TN (+ 2 TN gated) <= 63 prefetched values), 0 for the others
-int norm_fuse_bn(int v) {
-    switch (v) {
-        case 6: case 9: case 12: return 64;     // 192x64, 64x64, 64x64 4-stage
-        case 7: case 8: case 13: case 14: return 128;  // 96x128, 64x128, 64x128 3-stage, 96x128 3-stage
-        default: return 0;
-    }
-}
-}  // namespace
-
-bool launch_gemm_resid_norm(const uint16_t* A, int lda, const WeightView& W, int M, int N, int K,
-                            const GemmEpilogue& epi, hipStream_t s) {
-    ACEMI_CHECK(epi.kind == EPI_RESID || epi.kind == EPI_RESID_GATED, "gemm: the fused norm follows a residual GEMM");
-    ACEMI_CHECK(epi.norm.w != nullptr && epi.norm.out != nullptr && epi.norm.rows_per_item >= 1 &&
-                    (epi.norm.scale == nullptr) == (epi.norm.shift == nullptr),
-                "gemm: fused norm arguments");
-    // how long a tile waits for the rest of its row block before leaving its normalisation to the row block's last
-    // tile (ACE_MI_NORM_SPIN_US, default 50 us; 0: never waits -- the tests' path for the hand-over)
-    static const long long spin = [] {
-        const char* e = std::getenv("ACE_MI_NORM_SPIN_US");
-        const long long us = e ? std::atoll(e) : 50;
-        return (us < 0 ? 0 : us) * 100;  // s_memrealtime: 100 MHz
-    }();
-    const bool on = gemm_norm_fuse_on();
-    const long long spin_ticks = g_norm_mode == 2 ? 0 : spin;
-    const bool quant = weight_quantized(W.fmt);
-    const int v = quant ? -1 : pick_variant(M, N, K, false, W.fmt);
-    const int bn = v >= 0 && v < 100 ? norm_fuse_bn(v) : 0;
-    GemmEpilogue e = epi;
-    // (N % 256: the standalone kernel's canonical form, rmsnorm_mod_canon_kernel, which the fused rows must equal)
-    if (!on || bn == 0 || N % 256 != 0 || N / bn > 32 || epi.ldc < N || (int64_t)M * epi.ldc * 4 >= (1LL << 31)) {
-        e.norm = NormFuse{};
-        launch_gemm(A, lda, W, M, N, K, e, s);
-        return false;
-    }
-    ACEMI_CHECK(W.fmt == WF_BF16 || W.fmt == WF_F16, "gemm: fused norm needs dense weights");
-    const int bm = v == 6 ? 192 : (v == 7 || v == 14) ? 96 : 64;
-    const int nbm = (M + bm - 1) / bm, nbn = N / bn;
-    int dev = 0;
-    ACEMI_HIP(hipGetDevice(&dev));
-    {
-        std::lock_guard<std::mutex> lk(g_sk_mu);
-        NormWs& w = g_norm[std::make_pair(dev, s)];
-        // (arrival counts 128 bytes apart: every tile of a row block polls its count)
-        const size_t need_part = (size_t)M * nbn, need_cnt = (size_t)nbm * (nbn + 32);
-        if (w.part_n < need_part || w.cnt_n < need_cnt) ACEMI_HIP(hipStreamSynchronize(s));
-        if (w.part_n < need_part) {
-            if (w.part) ACEMI_HIP(hipFree(w.part));
-            w.part = nullptr;
-            w.part_n = 0;
-            ACEMI_HIP(hipMalloc(&w.part, need_part * sizeof(float)));
-            w.part_n = need_part;
-        }
-        if (w.cnt_n < need_cnt) {
-            if (w.cnt) ACEMI_HIP(hipFree(w.cnt));
-            w.cnt = nullptr;
-            w.cnt_n = 0;
-            const size_t n = std::max<size_t>(need_cnt, 1 << 16);
-            ACEMI_HIP(hipMalloc(&w.cnt, n * sizeof(unsigned)));
-            ACEMI_HIP(hipMemsetAsync(w.cnt, 0, n * sizeof(unsigned), s));
-            w.cnt_n = n;
-        }
-        e.norm.part = w.part;
-        e.norm.cnt = w.cnt;
-        e.norm.claim = w.cnt + (size_t)nbm * 32;
-        e.norm.spin_ticks = spin_ticks;
-    }
-    GemmParams p{A, (const uint16_t*)W.q, W.q, W.s, lda, W.ld, M, N, K, e};
-    {
-        std::lock_guard<std::mutex> lk(g_sk_mu);
-        unsigned* err = splitk_err_word(dev);
-        ACEMI_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&p.sk_err), err, 0));
-    }
-    ACEMI_CHECK(W.ld % 8 == 0 && lda % 8 == 0 && K % 64 == 0, "gemm: leading dims must be multiples of 8");
-    if (W.fmt == WF_F16)
-        dispatch_epi<true>(v, p, s);
-    else
-        dispatch_epi<false>(v, p, s);
-    ACEMI_HIP(hipGetLastError());
-    return true;
-}
-
 void launch_gemm(ActType t, const uint16_t* A, int lda, const uint16_t* W, int ldw, int M, int N, int K,
                  const GemmEpilogue& epi, hipStream_t s) {
     WeightView w;
@@ -1125,19 +1010,6 @@ void launch_gemm(ActType t, const uint16_t* A, int lda, const uint16_t* W, int l
 }
 
 void gemm_force_variant(int v) { g_forced_variant = v; }
-
-void gemm_norm_fuse_mode(int mode) { g_norm_mode = mode; }
-
-bool gemm_norm_fuse_on() {
-    // ACE_MI_NORM_FUSE=1: on (slower than the standalone kernel on MI355X: off by default)
-    static const int enabled = [] {
-        const char* e = std::getenv("ACE_MI_NORM_FUSE");
-        return (e && e[0] == '1') ? 1 : 0;
-    }();
-    return g_norm_mode >= 0 ? (g_norm_mode == 1 || g_norm_mode == 2) : enabled != 0;
-}
-
-bool gemm_norm_canonical() { return g_norm_mode == 3 || gemm_norm_fuse_on(); }
 
 void gemm_splitk_check() {
     std::lock_guard<std::mutex> lk(g_sk_mu);
@@ -1158,19 +1030,13 @@ void gemm_splitk_release(hipStream_t s) {
     ACEMI_HIP(hipGetDevice(&cur));
     auto it = g_sk.find(std::make_pair(cur, s));
     if (it == g_sk.end()) {
-        g_sk[std::make_pair(cur, s)] = SplitKWs{};  // (an empty entry: the norm workspace below is freed too)
+        g_sk[std::make_pair(cur, s)] = SplitKWs{};
         it = g_sk.find(std::make_pair(cur, s));
     }
     (void)hipStreamSynchronize(s);  // the stream is still alive here: its last joins are done with the buffers
     if (it->second.ws) (void)hipFree(it->second.ws);
     if (it->second.cnt) (void)hipFree(it->second.cnt);
     g_sk.erase(it);
-    auto nt = g_norm.find(std::make_pair(cur, s));  // the fused-norm workspace of the same stream
-    if (nt != g_norm.end()) {
-        if (nt->second.part) (void)hipFree(nt->second.part);
-        if (nt->second.cnt) (void)hipFree(nt->second.cnt);
-        g_norm.erase(nt);
-    }
 }
 
 }  // namespace acemi

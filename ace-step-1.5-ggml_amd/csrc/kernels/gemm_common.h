@@ -9,7 +9,6 @@
 #include <cstdlib>
 
 #include "../kernels.h"
-#include "norm_math.h"
 #include "prep_math.h"
 #include "mfma_guard.h"
 
@@ -275,8 +274,7 @@ __device__ __forceinline__ void resid_prefetch(const GemmParams& p, int mw, int 
     }
 }
 
-// KEEP: the new x values stay in acc (norm_fuse stores them) instead of being stored
-template <int TM, int TN, int EPI, bool KEEP = false>
+template <int TM, int TN, int EPI>
 __device__ __forceinline__ void resid_apply(const GemmParams& p, f32x4 (&acc)[TM][TN], int mw, int nw, int lane,
                                             int wrows, const float (&xo)[TM][4][TN], const float (&g0)[TN],
                                             const float (&g1)[TN]) {
@@ -299,10 +297,7 @@ __device__ __forceinline__ void resid_apply(const GemmParams& p, f32x4 (&acc)[TM
                 for (int j = 0; j < TN; ++j) {
                     float v = acc[i][j][r];
                     if constexpr (EPI == EPI_RESID_GATED) v = rn_mul(v, first ? g0[j] : g1[j]);
-                    if constexpr (KEEP)
-                        acc[i][j][r] = rn_add(xo[i][r][j], v);
-                    else
-                        e.c_f32[(int64_t)m * e.ldc + nw + j * 16 + ccol] = rn_add(xo[i][r][j], v);
+                    e.c_f32[(int64_t)m * e.ldc + nw + j * 16 + ccol] = rn_add(xo[i][r][j], v);
                 }
             }
     } else {
@@ -317,10 +312,7 @@ __device__ __forceinline__ void resid_apply(const GemmParams& p, f32x4 (&acc)[TM
                 for (int j = 0; j < TN; ++j) {
                     const int n = nw + j * 16 + ccol;
                     const float v = rn_mul(acc[i][j][r], e.gate[(int64_t)item * e.gate_stride + n]);
-                    if constexpr (KEEP)
-                        acc[i][j][r] = rn_add(xo[i][r][j], v);
-                    else
-                        e.c_f32[(int64_t)m * e.ldc + n] = rn_add(xo[i][r][j], v);
+                    e.c_f32[(int64_t)m * e.ldc + n] = rn_add(xo[i][r][j], v);
                 }
             }
     }
@@ -575,225 +567,6 @@ __device__ __forceinline__ bool splitk_join(const GemmParams& p, f32x4 (&acc)[TM
             splitk_gather<TM, TN, NW, 4, SMEM>(acc, slot0, PER_TILE, part, smem, wid, lane);
     }
     return true;
-}
-
-// Row norm fused into the residual epilogue (NormFuse, launch_gemm_resid_norm), after resid_apply<KEEP> left the new
-// x values of the block's BM x BN tile in acc.  The N / BN column tiles of a row block (BM rows) meet through
-// device-coherent memory, with the split-K join's discipline (sc1 stores completed before a relaxed counter, no
-// device-scope fence):
-//   1. x goes out (plain stores) and into LDS (so acc dies here: the main loop keeps its registers); the tile's
-//      per-row partial sum of squares (norm_math.h: chunk butterflies, an in-lane tree over the wave's chunks, a
-//      tree over the WN waves through LDS) goes to part[m][c];
-//   2. the block adds itself to cnt[R].  The last of the row block (ticket N / BN - 1) knows every partial is in.
-//      The others wait for cnt[R] to become complete, at most spin_ticks: then claim[R][c] = 1 and they normalise
-//      their own tile; on a timeout claim = 2 and they exit -- a block never waits for one that may not be resident;
-//   3. the last block waits for every other tile's claim (those blocks are running: bounded), resets cnt / claims
-//      for the next launch on this stream, normalises its own tile and the handed-over ones (their x from memory,
-//      released by a fence before the claim).
-// Every block reads the row block's partials back (sc1 loads) and finishes the same tree over them, so the
-// normalised rows equal the standalone kernel's (rmsnorm_mod_canon_kernel) bit for bit.
-template <int BM, int BN, int WM, int WN, int TM, int TN, bool F16, int SMEM>
-__device__ __forceinline__ void norm_fuse(const GemmParams& p, f32x4 (&acc)[TM][TN], int m0, int n0, int wm0,
-                                          int wn0, int tid, char* smem) {
-    constexpr int NT = WM * WN * 64;
-    constexpr int MAXT = 32;     // column tiles per row block (launch_gemm_resid_norm checks N / BN <= 32)
-    constexpr int XLD = BN + 4;  // LDS row stride of the x tile (floats)
-    static_assert((BM * XLD + (WN + 1) * BM + 4) * 4 <= SMEM, "fused norm: LDS");
-    const NormFuse& f = p.e.norm;
-    const int M = p.M, N = p.N, ldc = p.e.ldc;
-    // opaque copies: every index below is computed here, after the main loop (hipcc otherwise kept the x-store
-    // offsets, shared with the residual prefetch's, live across the last k-tiles and spilled the prefetched x)
-    asm volatile("" : "+v"(tid), "+v"(wm0), "+v"(wn0));
-    const int lane = tid & 63, ccol = lane & 15, crow = (lane >> 4) * 4;
-    const int wn = wn0 / (BN / WN);
-    const int nbn = N / BN, c = n0 / BN, R = m0 / BM;
-    const int mw = m0 + wm0, nw = n0 + wn0;
-    float* xt = reinterpret_cast<float*>(smem);  // [BM][XLD] x tile
-    float* red = xt + BM * XLD;                  // [WN][BM] wave partials
-    float* rsd = red + WN * BM;                  // [BM] row scales
-    unsigned* word = reinterpret_cast<unsigned*>(rsd + BM);  // [0] state, [1..2] abandoned-tile mask
-    // x rows >= M lie past the buffer's end: the hardware drops those stores
-    const __amdgpu_buffer_rsrc_t rx =
-        __builtin_amdgcn_make_buffer_rsrc((void*)p.e.c_f32, 0, (int)((int64_t)M * ldc * 4), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rp =
-        __builtin_amdgcn_make_buffer_rsrc((void*)f.part, 0, (int)((int64_t)M * nbn * 4), 0x00020000);
-    // (plain stores, merged into whole lines in L2 like the unfused epilogue's; a block that hands its tile over
-    // writes them back with a release fence first -- rare, see below)
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[i][j][r]), rx,
-                                                      ((mw + i * 16 + crow + r) * ldc + nw + j * 16 + ccol) * 4, 0, 0);
-    float rs[TM][4];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            float cj[TN];
-#pragma unroll
-            for (int j = 0; j < TN; ++j) cj[j] = normc::chunk16(rn_mul(acc[i][j][r], acc[i][j][r]));
-            rs[i][r] = normc::tree(cj);
-        }
-    __syncthreads();  // every wave is past the main loop's LDS reads
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) xt[(wm0 + i * 16 + crow + r) * XLD + wn0 + j * 16 + ccol] = acc[i][j][r];
-    if (ccol == 0) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) red[wn * BM + wm0 + i * 16 + crow + r] = rs[i][r];
-    }
-    __syncthreads();
-    // the normalisation sweep's columns and vectors, requested now so that they land under the protocol below
-    constexpr int CPR = BN / 4, RSTEP = NT / CPR, NIT = BM / RSTEP;
-    static_assert(NT % CPR == 0 && BM % RSTEP == 0, "fused norm: sweep shape");
-    const int cc = (tid % CPR) * 4, r0 = tid / CPR;
-    const bool mod = f.scale != nullptr;
-    const int rpi = f.rows_per_item;
-    const int64_t ms = f.mod_stride;
-    const int ia = min(m0, M - 1) / rpi, ib = min(m0 + BM - 1, M - 1) / rpi;
-    const bool two = ib - ia <= 1;
-    const float4 w4 = *reinterpret_cast<const float4*>(f.w + n0 + cc);
-    float4 sa = make_float4(0.f, 0.f, 0.f, 0.f), ha = sa, sb = sa, hb = sa;
-    if (mod) {
-        const float4 a = *reinterpret_cast<const float4*>(f.scale + ia * ms + n0 + cc);
-        const float4 b = *reinterpret_cast<const float4*>(f.scale + ib * ms + n0 + cc);
-        ha = *reinterpret_cast<const float4*>(f.shift + ia * ms + n0 + cc);
-        hb = *reinterpret_cast<const float4*>(f.shift + ib * ms + n0 + cc);
-        sa = make_float4(rn_add(a.x, 1.0f), rn_add(a.y, 1.0f), rn_add(a.z, 1.0f), rn_add(a.w, 1.0f));
-        sb = make_float4(rn_add(b.x, 1.0f), rn_add(b.y, 1.0f), rn_add(b.z, 1.0f), rn_add(b.w, 1.0f));
-    }
-    if (tid < BM) {
-        float wv[WN];
-#pragma unroll
-        for (int w = 0; w < WN; ++w) wv[w] = red[w * BM + tid];
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(normc::tree(wv)), rp, ((m0 + tid) * nbn + c) * 4, 0,
-                                              CPOL_SC1);
-    }
-    __builtin_amdgcn_s_waitcnt(0);  // this lane's x and partial stores are complete
-    __syncthreads();
-    if (tid == 0) {
-        const unsigned t = __hip_atomic_fetch_add(f.cnt + R * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        unsigned state = 1;  // 1: last of the row block, 0: normalises its own tile, 2: left it to the last
-        if (t != (unsigned)(nbn - 1)) {
-            const long long t0 = wall_clock64();
-            bool all = false;
-            for (;;) {
-                all = __hip_atomic_load(f.cnt + R * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)nbn;
-                if (all || wall_clock64() - t0 > f.spin_ticks) break;
-                __builtin_amdgcn_s_sleep(8);
-            }
-            state = all ? 0u : 2u;
-            // handing over: the last block reads this tile's x from memory -- make every wave's x stores (complete
-            // in this CU's L2, s_waitcnt + barrier above) device-visible first
-            if (!all) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            __hip_atomic_store(f.claim + R * nbn + c, all ? 1u : 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        word[0] = state;
-    }
-    __syncthreads();
-    const unsigned state = word[0];
-    if (state == 2) return;
-    if (state == 1 && tid < 64) {
-        // the last of the row block: every other tile has arrived (it is running) -- wave 0 waits for their claims,
-        // one lane per tile, all at once (bounded, ~0.2 s; a real wait is one poll interval of theirs, so that a
-        // protocol bug never hangs the GPU: on a timeout the error word is raised (gemm_splitk_check) and the
-        // counters are left as they are), then resets the claims and the count for the next launch on this stream
-        unsigned v = 1;
-        if (tid < nbn && tid != c) {
-            v = 0;
-            for (int it = 0; it < (1 << 22) && v == 0; ++it) {
-                v = __hip_atomic_load(f.claim + R * nbn + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (v == 0) __builtin_amdgcn_s_sleep(2);
-            }
-        }
-        const unsigned long long handed = __ballot(v == 2);
-        const bool ok = __all(v != 0);
-        if (ok && tid < nbn) __hip_atomic_store(f.claim + R * nbn + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (tid == 0) {
-            if (ok)
-                __hip_atomic_store(f.cnt + R * 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            else
-                __hip_atomic_store(p.sk_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            word[1] = (unsigned)handed;
-            word[2] = (unsigned)(handed >> 32);
-        }
-    }
-    // row scales of the block's rows from the row block's partials, in tile order
-    if (tid < BM && m0 + tid < M) {
-        // four partials per load, their subtree right away
-        float q4[MAXT / 4];
-#pragma unroll
-        for (int k4 = 0; k4 < MAXT / 4; ++k4) {
-            float t[4] = {0.f, 0.f, 0.f, 0.f};
-            if (4 * k4 < nbn) {
-                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rp, ((m0 + tid) * nbn + 4 * k4) * 4, 0, CPOL_SC1);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) t[e] = 4 * k4 + e < nbn ? __uint_as_float(v[e]) : 0.f;
-            }
-            q4[k4] = normc::tree(t);
-        }
-        rsd[tid] = normc::rms_scale(normc::tree(q4), N, f.eps);
-    }
-    __syncthreads();
-    // act(norm(x)) of the block's own tile from LDS: four consecutive columns per thread (8-byte stores), the same
-    // columns in every row of the sweep (w and the modulation vectors loaded above, under the protocol)
-    if (state != 2) {
-#pragma unroll
-        for (int k = 0; k < NIT; ++k) {
-            const int row = r0 + k * RSTEP, m = m0 + row;
-            const float4 v = *reinterpret_cast<const float4*>(xt + row * XLD + cc);
-            const float sc = rsd[row];
-            float4 s1 = sa, sh = ha;
-            if (mod && !two) {  // (a tile spanning more than two items: per-row vectors)
-                const int64_t it = min(m, M - 1) / rpi;
-                const float4 a = *reinterpret_cast<const float4*>(f.scale + it * ms + n0 + cc);
-                s1 = make_float4(rn_add(a.x, 1.0f), rn_add(a.y, 1.0f), rn_add(a.z, 1.0f), rn_add(a.w, 1.0f));
-                sh = *reinterpret_cast<const float4*>(f.shift + it * ms + n0 + cc);
-            } else if (m >= (ia + 1) * rpi) {
-                s1 = sb;
-                sh = hb;
-            }
-            const uint16_t o0 = to_act<F16>(normc::modulate(v.x, sc, w4.x, mod, s1.x, sh.x));
-            const uint16_t o1 = to_act<F16>(normc::modulate(v.y, sc, w4.y, mod, s1.y, sh.y));
-            const uint16_t o2 = to_act<F16>(normc::modulate(v.z, sc, w4.z, mod, s1.z, sh.z));
-            const uint16_t o3 = to_act<F16>(normc::modulate(v.w, sc, w4.w, mod, s1.w, sh.w));
-            if (m < M)
-                *reinterpret_cast<uint2*>(f.out + (int64_t)m * N + n0 + cc) =
-                    make_uint2((uint32_t)o0 | ((uint32_t)o1 << 16), (uint32_t)o2 | ((uint32_t)o3 << 16));
-        }
-    }
-    if (state != 1) return;
-    // the last block of the row block: the handed-over tiles, their x from memory (released by a fence before
-    // their claim)
-    const unsigned long long mask = (unsigned long long)word[1] | ((unsigned long long)word[2] << 32);
-    for (int c2 = 0; c2 < nbn; ++c2) {
-        if (!((mask >> c2) & 1ull)) continue;
-        for (int idx = tid; idx < BM * CPR; idx += NT) {
-            const int row = idx / CPR, n = c2 * BN + (idx % CPR) * 4;
-            const int m = m0 + row;
-            if (m >= M) continue;
-            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rx, (m * ldc + n) * 4, 0, CPOL_SC1);
-            const float sc = rsd[row];
-            const int64_t it = m / rpi;
-            uint16_t o[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const float s1 = mod ? rn_add(f.scale[it * ms + n + e], 1.0f) : 0.f;
-                const float sh = mod ? f.shift[it * ms + n + e] : 0.f;
-                o[e] = to_act<F16>(normc::modulate(__uint_as_float(v[e]), sc, f.w[n + e], mod, s1, sh));
-            }
-            *reinterpret_cast<uint2*>(f.out + (int64_t)m * N + n) =
-                make_uint2((uint32_t)o[0] | ((uint32_t)o[1] << 16), (uint32_t)o[2] | ((uint32_t)o[3] << 16));
-        }
-    }
 }
 
 // split-K workspace for `ntiles` tiles of `tile_bytes` each, S parts, on stream s (gemm.hip)

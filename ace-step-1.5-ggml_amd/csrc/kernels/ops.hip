@@ -1,7 +1,6 @@
 // Memory-bound kernels around the DiT GEMMs and attention (gfx950).
 // Each kernel cites the ggml graph nodes of ace_dit::forward_dit it fuses.
 #include "../kernels.h"
-#include "norm_math.h"
 #include "prep_math.h"
 
 namespace acemi {
@@ -292,78 +291,6 @@ __global__ void __launch_bounds__(256) rmsnorm_mod_persist_kernel(const float* _
         m = nxt;
 #pragma unroll
         for (int k = 0; k < 2 * NC; ++k) v[k] = vn[k];
-    }
-}
-
-// Same operator in the canonical summation order of norm_math.h (the default; the fused residual-GEMM epilogue,
-// gemm_common.h norm_fuse, computes the same bits), persistent like the kernel above: lane l of a row's wave holds
-// columns 256k + 4l .. 256k + 4l + 3 (k < NK = H / 256; 16-byte loads, 8-byte stores).  Per step: the lane's four
-// squares as a two-level tree, xor 1 / 2 complete the 16-column chunk, xor 4 / 8 / 16 / 32 the 256-column subtree --
-// every level pairs neighbours in column order, the perfect tree of norm_math.h -- and an in-lane tree over k the
-// row.  w (and the current item's 1 + scale, shift) stay in registers across rows; the next row is loaded under the
-// current one.
-template <bool F16, int NK>
-__global__ void __launch_bounds__(256) rmsnorm_mod_canon_kernel(const float* __restrict__ x, int M, int H,
-                                                                const float* __restrict__ w,
-                                                                const float* __restrict__ scale,
-                                                                const float* __restrict__ shift, int64_t mod_stride,
-                                                                int rows_per_item, float eps,
-                                                                uint16_t* __restrict__ out) {
-    const int nwaves = gridDim.x * 4;
-    int m = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (m >= M) return;
-    const int c0 = (threadIdx.x & 63) * 4;
-    float4 wv[NK], s1[NK], hv[NK], v[NK];
-#pragma unroll
-    for (int k = 0; k < NK; ++k) {
-        v[k] = *(const float4*)(x + (int64_t)m * H + 256 * k + c0);
-        wv[k] = *(const float4*)(w + 256 * k + c0);
-        s1[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-        hv[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    int item = -1;
-    for (;;) {
-        const int nxt = m + nwaves;
-        float4 vn[NK];
-        if (nxt < M) {  // wave-uniform
-#pragma unroll
-            for (int k = 0; k < NK; ++k) vn[k] = *(const float4*)(x + (int64_t)nxt * H + 256 * k + c0);
-        }
-        const int it = m / rows_per_item;
-        if (scale && it != item) {  // wave-uniform: a new batch item's modulation vectors
-            item = it;
-#pragma unroll
-            for (int k = 0; k < NK; ++k) {
-                const float4 a = *(const float4*)(scale + (int64_t)it * mod_stride + 256 * k + c0);
-                s1[k] = make_float4(rn_add(a.x, 1.0f), rn_add(a.y, 1.0f), rn_add(a.z, 1.0f), rn_add(a.w, 1.0f));
-                hv[k] = *(const float4*)(shift + (int64_t)it * mod_stride + 256 * k + c0);
-            }
-        }
-        float g[NK];
-#pragma unroll
-        for (int k = 0; k < NK; ++k) {
-            float q = rn_add(rn_add(rn_mul(v[k].x, v[k].x), rn_mul(v[k].y, v[k].y)),
-                             rn_add(rn_mul(v[k].z, v[k].z), rn_mul(v[k].w, v[k].w)));
-#pragma unroll
-            for (int sh = 1; sh < 64; sh *= 2) q = rn_add(q, __shfl_xor(q, sh));
-            g[k] = q;
-        }
-        const float sc = normc::rms_scale(normc::tree(g), H, eps);
-        const bool mod = scale != nullptr;
-        uint16_t* orow = out + (int64_t)m * H;
-#pragma unroll
-        for (int k = 0; k < NK; ++k) {
-            const uint16_t o0 = to_act(F16, normc::modulate(v[k].x, sc, wv[k].x, mod, s1[k].x, hv[k].x));
-            const uint16_t o1 = to_act(F16, normc::modulate(v[k].y, sc, wv[k].y, mod, s1[k].y, hv[k].y));
-            const uint16_t o2 = to_act(F16, normc::modulate(v[k].z, sc, wv[k].z, mod, s1[k].z, hv[k].z));
-            const uint16_t o3 = to_act(F16, normc::modulate(v[k].w, sc, wv[k].w, mod, s1[k].w, hv[k].w));
-            *(uint2*)(orow + 256 * k + c0) =
-                make_uint2((uint32_t)o0 | ((uint32_t)o1 << 16), (uint32_t)o2 | ((uint32_t)o3 << 16));
-        }
-        if (nxt >= M) break;
-        m = nxt;
-#pragma unroll
-        for (int k = 0; k < NK; ++k) v[k] = vn[k];
     }
 }
 
@@ -726,45 +653,6 @@ void launch_rmsnorm_mod(ActType t, const float* x, int M, int H, const float* w,
         const int v = e ? std::atoi(e) : 2;
         return v < 0 ? 0 : std::min(v, 16);
     }();
-    // The canonical summation order (rmsnorm_mod_canon_kernel) whenever the residual GEMMs may normalise rows
-    // themselves (launch_gemm_resid_norm on: both must give the same bits), or with ACE_MI_RMSNORM_CANON=1.  Otherwise
-    // the kernels below: 1 % faster at 60 s, equal at 240 s (profiles/r05/norm_fuse/rms_canon_ab.txt).
-    static const bool canon_env = [] {
-        const char* e = std::getenv("ACE_MI_RMSNORM_CANON");
-        return e && e[0] == '1';
-    }();
-    const bool canon = canon_env || gemm_norm_canonical();
-    const int nk = H % 256 == 0 ? H / 256 : 0;
-    const bool canon_nk = nk == 1 || nk == 2 || nk == 3 || nk == 4 || nk == 6 || nk == 8 || nk == 12 || nk == 16;
-    if (!x3 && canon && canon_nk) {
-        static int n_cu = 0;
-        if (n_cu == 0) {
-            int dev = 0;
-            ACEMI_HIP(hipGetDevice(&dev));
-            ACEMI_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
-        }
-        const dim3 g((unsigned)std::min<int64_t>((M + 3) / 4, (int64_t)n_cu * 2));
-#define ACEMI_RMSC(NK)                                                                                              \
-    if (f16)                                                                                                        \
-        hipLaunchKernelGGL((rmsnorm_mod_canon_kernel<true, NK>), g, dim3(256), 0, s, x, M, H, w, scale, shift,      \
-                           mod_stride, rows_per_item, eps, out);                                                   \
-    else                                                                                                            \
-        hipLaunchKernelGGL((rmsnorm_mod_canon_kernel<false, NK>), g, dim3(256), 0, s, x, M, H, w, scale, shift,     \
-                           mod_stride, rows_per_item, eps, out)
-        switch (nk) {
-            case 1: ACEMI_RMSC(1); break;
-            case 2: ACEMI_RMSC(2); break;
-            case 3: ACEMI_RMSC(3); break;
-            case 4: ACEMI_RMSC(4); break;
-            case 6: ACEMI_RMSC(6); break;
-            case 8: ACEMI_RMSC(8); break;
-            case 12: ACEMI_RMSC(12); break;
-            default: ACEMI_RMSC(16); break;
-        }
-#undef ACEMI_RMSC
-        ACEMI_HIP(hipGetLastError());
-        return;
-    }
     if (!x3 && persist > 0 && H % 512 == 0 && H <= 2048) {
         static int n_cu = 0;
         if (n_cu == 0) {

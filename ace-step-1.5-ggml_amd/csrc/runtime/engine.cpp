@@ -457,20 +457,6 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
         stage_layers_ = stage_per_call_ ? n_layers : 0;
     }
 
-    // The residual GEMMs (o, cross o, down) normalise the rows they produce for the next block in their epilogue
-    // when their tile allows (launch_gemm_resid_norm; same bits as the standalone kernel): `normed` says the next
-    // rmsnorm_mod has been done that way.  The output head's f32-weight form ([hi | hi | lo] rows) is not fused.
-    const int kout_head = m.proj_out_w.k_mult();
-    bool normed = false;
-    auto fuse_norm = [&](GemmEpilogue& e, const float* w, const float* sc, const float* sh, int64_t stride) {
-        e.norm.w = w;
-        e.norm.scale = sc;
-        e.norm.shift = sh;
-        e.norm.mod_stride = stride;
-        e.norm.rows_per_item = Np;
-        e.norm.eps = c.eps;
-        e.norm.out = act;
-    };
     for (int li = 0; li < n_layers; ++li) {  // :1466-1535
         const DevLayer& ly = m.layers[li];
         if (staged && restage) stage_layer(li, s);
@@ -485,12 +471,9 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
         const float* c_gate = lm + 5 * H;
 
         // self-attention block
-        if (!normed) {
-            tic(s);
-            launch_rmsnorm_mod(at, x, (int)M, H, ly.self_norm, scale_msa, shift_msa, mstride, Np, c.eps, act, s);
-            toc("rmsnorm_mod", s);
-        }
-        normed = false;
+        tic(s);
+        launch_rmsnorm_mod(at, x, (int)M, H, ly.self_norm, scale_msa, shift_msa, mstride, Np, c.eps, act, s);
+        toc("rmsnorm_mod", s);
         {
             // QKV projection with QK-RMSNorm, RoPE and the attention re-layout fused into its epilogue
             // (EPI_QKV_PREP; ACE_MI_UNFUSED_PREP=1 runs the f32 store + attn_prep pair instead)
@@ -558,23 +541,16 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
                 launch_gemm(attn, qd, lw.o, (int)M, H, qd, e, s);
                 launch_fault_tile(x, H, (int)M, fault_.row, fault_.col, fault_.amp, s);
             } else {
-                if (ly.cross && L > 0)
-                    fuse_norm(e, ly.cross_norm, nullptr, nullptr, 0);
-                else
-                    fuse_norm(e, ly.mlp_norm, c_scale, c_shift, mstride);
-                normed = launch_gemm_resid_norm(attn, qd, lw.o, (int)M, H, qd, e, s);
+                launch_gemm(attn, qd, lw.o, (int)M, H, qd, e, s);
             }
             toc("gemm_o", s);
         }
 
         // cross-attention block (:1502-1520): no AdaLN, no gate, no RoPE
         if (ly.cross && L > 0) {
-            if (!normed) {
-                tic(s);
-                launch_rmsnorm_mod(at, x, (int)M, H, ly.cross_norm, nullptr, nullptr, 0, Np, c.eps, act, s);
-                toc("rmsnorm_mod", s);
-            }
-            normed = false;
+            tic(s);
+            launch_rmsnorm_mod(at, x, (int)M, H, ly.cross_norm, nullptr, nullptr, 0, Np, c.eps, act, s);
+            toc("rmsnorm_mod", s);
             {
                 PrepArgs pa{};
                 pa.q_col = 0;
@@ -624,20 +600,16 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
                 e.kind = EPI_RESID;
                 e.c_f32 = x;
                 e.ldc = H;
-                fuse_norm(e, ly.mlp_norm, c_scale, c_shift, mstride);
                 tic(s);
-                normed = launch_gemm_resid_norm(attn, qd, lw.co, (int)M, H, qd, e, s);
+                launch_gemm(attn, qd, lw.co, (int)M, H, qd, e, s);
                 toc("gemm_cross_o", s);
             }
         }
 
         // MLP block (:1522-1534)
-        if (!normed) {
-            tic(s);
-            launch_rmsnorm_mod(at, x, (int)M, H, ly.mlp_norm, c_scale, c_shift, mstride, Np, c.eps, act, s);
-            toc("rmsnorm_mod", s);
-        }
-        normed = false;
+        tic(s);
+        launch_rmsnorm_mod(at, x, (int)M, H, ly.mlp_norm, c_scale, c_shift, mstride, Np, c.eps, act, s);
+        toc("rmsnorm_mod", s);
         {
             GemmEpilogue e;
             e.kind = EPI_SWIGLU;
@@ -655,18 +627,8 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
             e.gate = c_gate;
             e.gate_stride = mstride;
             e.rows_per_item = Np;
-            if (li + 1 < n_layers) {  // the next layer's self-attention norm
-                const float* nm = mods + (size_t)(li + 1) * B * 6 * H;
-                fuse_norm(e, m.layers[li + 1].self_norm, nm + 1 * H, nm + 0 * H, mstride);
-            } else if (kout_head != 3) {  // the output head's norm
-                const float* om = get<float>(outmod_);
-                fuse_norm(e, m.norm_out, om + H, om, 2LL * H);
-            }
             tic(s);
-            if (e.norm.w)
-                normed = launch_gemm_resid_norm(act2, I, lw.down, (int)M, H, I, e, s);
-            else
-                launch_gemm(act2, I, lw.down, (int)M, H, I, e, s);
+            launch_gemm(act2, I, lw.down, (int)M, H, I, e, s);
             toc("gemm_down", s);
         }
     }
@@ -676,12 +638,10 @@ void DitEngine::forward(const ForwardIO& io, hipStream_t s) {
         const float* om = get<float>(outmod_);
         const int kout = m.proj_out_w.k_mult();
         uint16_t* head_in = kout == 3 ? get<uint16_t>(act2_) : act;  // act2_ is sized for M x 3H too
-        if (!normed) {
-            tic(s);
-            launch_rmsnorm_mod(m.proj_out_w.act(), x, (int)M, H, m.norm_out, om + H, om, 2LL * H, Np, c.eps, head_in,
-                               s, kout == 3);
-            toc("rmsnorm_mod", s);
-        }
+        tic(s);
+        launch_rmsnorm_mod(m.proj_out_w.act(), x, (int)M, H, m.norm_out, om + H, om, 2LL * H, Np, c.eps, head_in,
+                           s, kout == 3);
+        toc("rmsnorm_mod", s);
         GemmEpilogue e;
         e.kind = EPI_PROJ_OUT;
         e.bias = m.proj_out_b;

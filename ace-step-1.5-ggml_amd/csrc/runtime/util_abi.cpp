@@ -14,16 +14,6 @@ ace_ggml_status ace_mi_gemm_variant(int32_t variant) {
     return ACE_GGML_OK;
 }
 
-// Fused row norm of the residual GEMMs (launch_gemm_resid_norm) for subsequent launches: -1 = ACE_MI_NORM_FUSE /
-// ACE_MI_NORM_SPIN_US, 0 = off (standalone norm kernel), 1 = on, 2 = on with no wait (every tile but a row block's
-// last hands its normalisation over: the hand-over path, for tests), 3 = off with the standalone kernel in the
-// fused epilogue's summation order (the tests' reference).
-ace_ggml_status ace_mi_norm_fuse(int32_t mode) {
-    if (mode < -1 || mode > 3) return ACE_GGML_ERR_INVALID_ARG;
-    acemi::gemm_norm_fuse_mode(mode);
-    return ACE_GGML_OK;
-}
-
 // ggml block quantization of rows (the loader's encoders): returns bytes written, or -1.
 int64_t ace_mi_quantize(int32_t qtype, const float* src, int64_t rows, int64_t cols, uint8_t* dst, size_t dst_size) {
     using namespace acemi;

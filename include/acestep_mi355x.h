@@ -104,11 +104,6 @@ ACE_GGML_API ace_ggml_status ace_mi_synchronize(ace_ggml_context* ctx);
  * 20..24, + 100 S for split-K over S blocks per tile; A/B measurements).  The kernel self-test and
  * micro-benchmark entries live in the separate test library (include/acestep_mi355x_selftest.h). */
 ACE_GGML_API ace_ggml_status ace_mi_gemm_variant(int32_t variant);
-// Fused row norm of the residual GEMMs (the o / cross-o / down projections normalise the rows they produce for the
-// next block in their epilogue): -1 = environment (ACE_MI_NORM_FUSE, ACE_MI_NORM_SPIN_US), 0 = off, 1 = on,
-// 2 = on without waiting (tests of the hand-over path), 3 = off with the standalone norm in the fused order.  A/B
-// and test hook (the fusion is off by default: slower on MI355X); no counterpart in the reference.
-ACE_GGML_API ace_ggml_status ace_mi_norm_fuse(int32_t mode);
 
 /* VAE decode on device pointers, stream-ordered: latents [n_frames][latent_channels] f32 ->
  * out [out_len][audio_channels] f32 (out_len from ace_mi_vae_out_len: n_frames*hop for even strides). */

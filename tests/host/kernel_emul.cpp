@@ -134,7 +134,6 @@ float weight_val(const WeightView& W, int K, int n, int k) {
 }  // namespace
 
 void gemm_force_variant(int) {}
-void gemm_norm_fuse_mode(int) {}
 
 void launch_dequant_bf16(const WeightView& W, int N, int K, uint16_t* out, hipStream_t) {
     ACEMI_CHECK(weight_quantized(W.fmt) && K % 32 == 0, "dequant: quantized [N][K] weight");
@@ -219,15 +218,6 @@ void launch_gemm(ActType t, const uint16_t* A, int lda, const uint16_t* W, int l
     w.q = W;
     w.ld = ldw;
     launch_gemm(A, lda, w, M, N, K, epi, s);
-}
-
-// the fused row norm is a GPU epilogue: here the plain GEMM, and the caller runs the norm (returns false)
-bool launch_gemm_resid_norm(const uint16_t* A, int lda, const WeightView& W, int M, int N, int K,
-                            const GemmEpilogue& epi, hipStream_t s) {
-    GemmEpilogue e = epi;
-    e.norm = NormFuse{};
-    launch_gemm(A, lda, W, M, N, K, e, s);
-    return false;
 }
 
 // Read the first and last element of the range the real kernel touches, so that an allocation smaller

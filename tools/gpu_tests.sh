@@ -5,7 +5,7 @@ cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 rocminfo 2>/dev/null | grep -m2 -E "gfx950|Marketing" > gpurun_out/dev.txt
 worst=0
-for spec in ${SUITES:-kernels:400 forward:900 parity_strict:900 configs:900 lyric_timbre:300 quant:900 qact:300 norm_fuse:300 sampler:300 text_encoder:300 vae:600}; do
+for spec in ${SUITES:-kernels:400 forward:900 parity_strict:900 configs:900 lyric_timbre:300 quant:900 qact:300 sampler:300 text_encoder:300 vae:600}; do
     name=${spec%%:*}
     lim=${spec##*:}
     timeout -k 10 "$lim" python -u -m pytest "tests/test_gpu_${name}.py" -v -s -m gpu --timeout 300 --timeout-method thread ${FWD_ARGS} \
