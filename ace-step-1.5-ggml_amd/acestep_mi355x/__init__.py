@@ -20,4 +20,24 @@ import os
 PACKAGE_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PACKAGE_DIR, "lib", "libacestep_mi355x.so")
 
-__all__ = ["PACKAGE_DIR", "LIB_PATH"]
+CSRC_DIR = os.path.join(os.path.dirname(PACKAGE_DIR), "csrc")
+
+
+def source_hash() -> str:
+    """sha256 (16 hex digits) over the library's sources (csrc/**, Makefile, include/*.h): the build stamp that
+    profiles/pmc_traffic.json carries, so bench.py uses counter data only when it came from the same kernels."""
+    import hashlib
+    h = hashlib.sha256()
+    inc = os.path.join(os.path.dirname(os.path.dirname(PACKAGE_DIR)), "include")
+    files = []
+    for root in (CSRC_DIR, inc):
+        for dp, _, fns in os.walk(root):
+            files += [os.path.join(dp, f) for f in fns if f.endswith((".hip", ".h", ".cpp", "Makefile"))]
+    for f in sorted(files, key=lambda x: os.path.relpath(x, os.path.dirname(CSRC_DIR))):
+        h.update(os.path.relpath(f, os.path.dirname(CSRC_DIR)).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+__all__ = ["PACKAGE_DIR", "LIB_PATH", "CSRC_DIR", "source_hash"]

@@ -49,6 +49,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "ace-step-1.5-ggml_amd"))
 sys.path.insert(0, ROOT)
+from acestep_mi355x import source_hash  # noqa: E402  (build stamp of the kernel sources)
 
 METRIC = "DiT denoising steps/sec (240s@5Hz latent, bs=1..8) + single-step ms; 1/2/4/8 GPU"
 # DiT attention operand precision of the headline (the engine's default; ACE_MI_BENCH_ATTN overrides for A/B runs):
@@ -273,6 +274,7 @@ def main():
     breakdown = {}
     roofline = None
     roofline_attn = None
+    roofline_gemm = None
     if not args.no_profile:
         br.profile_enable(True)
         br.profile_reset()
@@ -287,25 +289,33 @@ def main():
             breakdown[name] = {"ms_per_step": round(ms / nprof, 4), "launches_per_step": round(cnt / nprof, 3),
                                "avg_us": round(1000.0 * ms / max(cnt, 1), 2)}
         gu = [p for p in prof if p[0] == "gemm_gate_up"]
+        roofline_gu = None
         if gu:
             name, ms, cnt = gu[0]
             M = b_loc * ((T + 1) // 2)
             flops = 2.0 * M * (2 * info.intermediate_size) * info.hidden_size
             avg_s = ms / cnt / 1000.0
             ach = flops / avg_s / 1e12
-            roofline = {"kernel": f"gemm_gate_up (MLP gate|up, {wdesc} weights, bf16 MFMA, SwiGLU epilogue)",
-                        "bound": "mfma",
-                        "achieved": round(ach, 1), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                        "frac": round(ach / BF16_PEAK_TFLOPS, 4), "traffic": None,
-                        "flops_per_launch": flops, "avg_launch_us": round(avg_s * 1e6, 2),
-                        "shape_MNK": [M, 2 * info.intermediate_size, info.hidden_size]}
-            traffic = pmc_traffic(T, L, b_loc, args.qtype or "bf16")
-            if traffic is not None:
-                roofline["traffic"] = traffic
+            roofline_gu = {"kernel": f"gemm_gate_up (MLP gate|up, {wdesc} weights, bf16 MFMA, SwiGLU epilogue)",
+                           "bound": "mfma",
+                           "achieved": round(ach, 1), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                           "frac": round(ach / BF16_PEAK_TFLOPS, 4),
+                           "traffic": pmc_traffic(T, L, b_loc, args.qtype or "bf16", "gate_up"),
+                           "flops_per_launch": flops, "avg_launch_us": round(avg_s * 1e6, 2),
+                           "ms_per_step": round(ms / nprof, 4),
+                           "shape_MNK": [M, 2 * info.intermediate_size, info.hidden_size]}
         frac = block_linear_frac(prof, nprof, T, b_loc, info)
         if frac is not None:
             breakdown["_dit_block_linears"] = {"tflops": round(frac * BF16_PEAK_TFLOPS, 1), "frac_of_bf16_peak": frac}
         roofline_attn = attention_roofline(prof, nprof, T, L, b_loc, info)
+        if roofline_attn is not None:
+            roofline_attn["traffic"] = pmc_traffic(T, L, b_loc, args.qtype or "bf16", "attention")
+        # `roofline` names the dominant kernel of the step (the most GPU time per step: the f8c attention operator or
+        # the gate|up GEMM); the other one stays in its own field
+        cands = [r for r in (roofline_attn, roofline_gu) if r is not None]
+        if cands:
+            roofline = max(cands, key=lambda r: r["ms_per_step"])
+        roofline_gemm = roofline_gu
 
     extras = {}
     single = world == 1 and not args.emulate
@@ -513,6 +523,8 @@ def main():
                       "items_per_rank": [len(shard_indices(B, world, r)) for r in range(world)]},
             "roofline": roofline,
             "roofline_attention": roofline_attn,
+            "roofline_gemm": roofline_gemm,
+            "build": source_hash(),
             "bf16_line": bf16_line,
             **extras,
             "cpu_baseline": cpu,
@@ -681,10 +693,11 @@ def attention_roofline(prof, nprof, T, L, b_loc, info):
             "ms_per_step": round(tot_ms / nprof, 4), "classes": out}
 
 
-def pmc_traffic(T, L, b_loc, weights):
-    """HBM bytes per launch of the gate|up GEMM from the committed PMC summary of the same workload
-    (tools/gpu_pmc.sh -> tools/pmc_summary.py -> profiles/pmc_traffic.json, whose "config" names
-    T / enc_len / batch_per_gpu / weights); None when no matching summary exists."""
+def pmc_traffic(T, L, b_loc, weights, kernel):
+    """HBM bytes per launch of `kernel` ("gate_up" or "attention") from the committed PMC summary
+    (tools/gpu_pmc.sh -> tools/pmc_summary.py -> profiles/pmc_traffic.json) -- only when that summary was collected on
+    the same workload (its "config": T / enc_len / batch_per_gpu / weights) AND from the same kernel sources (its
+    "build" = acestep_mi355x.source_hash() of this tree); None otherwise."""
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_traffic.json")
     try:
         with open(path, "r", encoding="utf-8") as f:
@@ -692,7 +705,9 @@ def pmc_traffic(T, L, b_loc, weights):
         c = d["config"]
         if (c["latent_frames"], c["enc_len"], c["batch_per_gpu"], c["weights"]) != (T, L, b_loc, weights):
             return None
-        return float(d["gate_up"]["hbm_bytes"])
+        if d.get("build") != source_hash():
+            return None
+        return float(d[kernel]["hbm_bytes"])
     except (OSError, KeyError, ValueError, TypeError):
         return None
 

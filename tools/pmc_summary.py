@@ -3,7 +3,10 @@
 Usage: python tools/pmc_summary.py gpurun_out/pmc  > summary.json
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch; on gfx950 FETCH_SIZE counts half the bytes of a wide
 streaming read (MI355X_MICROARCH.md, HBM section), so fetch bytes = 2 x 1024 x FETCH_SIZE.  The
-"gate_up" entry is the MLP gate|up GEMM (the SwiGLU-epilogue GEMM, EPI 4) that bench.py's roofline names.
+"gate_up" entry is the MLP gate|up GEMM (the SwiGLU-epilogue GEMM, EPI 4); "attention" the f8c attention kernel
+(attn2_kernel<..., F8 = true> instances, every class: full / sliding / cross), launch-weighted.  "build" is
+acestep_mi355x.source_hash() of the tree the passes ran: bench.py uses the bytes only when its own tree has the same
+hash (and the same workload), so a changed kernel never reports stale traffic.
 """
 import csv
 import glob
@@ -40,6 +43,15 @@ def main(root, bench_json=None):
     gu = [k for k in out["kernels"] if pat.search(k)]
     if gu:
         out["gate_up"] = {"kernel": gu[0], **out["kernels"][gu[0]]}
+    att = [k for k in out["kernels"] if "attn2_kernel" in k and k.replace(" ", "").endswith("1,true>(acemi::AttnArgs)")]
+    if att:
+        n = sum(out["kernels"][k]["launches"] for k in att)
+        out["attention"] = {"kernels": att, "launches": n,
+                            "hbm_bytes": sum(out["kernels"][k]["hbm_bytes"] * out["kernels"][k]["launches"]
+                                             for k in att) / max(n, 1)}
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ace-step-1.5-ggml_amd"))
+    from acestep_mi355x import source_hash
+    out["build"] = source_hash()
     if bench_json:  # the workload these passes ran (bench.py matches it before using the bytes)
         with open(bench_json, "r", encoding="utf-8") as f:
             line = [ln for ln in f if ln.startswith("{")][-1]
