@@ -46,7 +46,8 @@ EXPORTED_SYMBOLS = (
 # Every symbol declared in include/acestep_mi355x_selftest.h: the TEST library (libacestep_mi355x_selftest.so = the
 # product objects + the kernel self-test / micro-benchmark entries); the product library does not export them.
 SELFTEST_SYMBOLS = ("ace_mi_kernel_gemm", "ace_mi_kernel_attention", "ace_mi_bench_attention", "ace_mi_bench_gemm",
-                    "ace_mi_kernel_gemm_q", "ace_mi_kernel_dequant", "ace_mi_bench_gemm_q", "ace_mi_kernel_gemm_a8")
+                    "ace_mi_kernel_gemm_q", "ace_mi_kernel_dequant", "ace_mi_bench_gemm_q", "ace_mi_kernel_gemm_a8",
+                    "ace_mi_kernel_gemm_a8_mode")
 
 # qtype codes of ace_mi_quantize & co. (names as parse_quant_type, acestep_dit_model.cpp:27-37)
 QTYPES = {"q8_0": 1, "q4_k": 2, "q6_k": 3}
@@ -228,6 +229,8 @@ def load_selftest_library() -> ctypes.CDLL:
     i8p = ctypes.POINTER(ctypes.c_int8)
     lib.ace_mi_kernel_gemm_a8.argtypes = [i32, i32, i32, i32, i32, fp, u8p, fp, fp, i8p, fp, fp]
     lib.ace_mi_kernel_gemm_a8.restype = ctypes.c_int
+    lib.ace_mi_kernel_gemm_a8_mode.argtypes = [i32]
+    lib.ace_mi_kernel_gemm_a8_mode.restype = ctypes.c_int
     _SELFTEST = lib
     return lib
 
@@ -749,3 +752,8 @@ def gemm_variant(variant: int) -> None:
     if lib.ace_mi_gemm_variant(int(variant)) != ACE_GGML_OK:
         raise ValueError(variant)
 
+
+def kernel_gemm_a8_mode(mode: int) -> None:
+    """Q8_0 GEMM form of the q8 mode in this process: -1 environment / default (bf16 MFMA), 0 i8 MFMA, 1 bf16 MFMA."""
+    if load_selftest_library().ace_mi_kernel_gemm_a8_mode(int(mode)) != ACE_GGML_OK:
+        raise ValueError(mode)

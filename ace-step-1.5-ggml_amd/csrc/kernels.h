@@ -117,19 +117,30 @@ enum QActKind : int { QACT_Q8_0 = 0, QACT_Q8_K = 1 };
 struct QAct {
     int kind = QACT_Q8_0;
     const int8_t* q = nullptr;
+    const uint16_t* q16 = nullptr;  // Q8_0: bf16(q) [M][K] (exact integers) for the bf16-MFMA form of the GEMM
     const float* s = nullptr;
     const float* bsum = nullptr;
     int64_t ld_s = 0;
 };
 inline int qact_kind_for(int weight_fmt) { return weight_fmt == WF_Q8_0 ? QACT_Q8_0 : QACT_Q8_K; }
 // x f32 [M][ldx] (silu first when silu_in) -> the blocks of `kind` in q / s / bsum (layout above)
+// (q16: Q8_0 only, bf16(q) rows as well / instead -- either output may be null, not both)
 void launch_quantize_act(int kind, const float* x, int64_t ldx, int M, int K, bool silu_in, int8_t* q, float* s,
-                         float* bsum, int64_t ld_s, hipStream_t st);
+                         float* bsum, int64_t ld_s, hipStream_t st, uint16_t* q16 = nullptr);
 // C = dequant(A blocks) . dequant(W)^T with ggml's per-block integer dot products (v_mfma_i32_16x16x32_i8) and an
 // f32 sum of d_w * d_a * isum over the blocks; W quantized (WF_Q8_0 with QACT_Q8_0, WF_Q4_K / WF_Q6_K with
 // QACT_Q8_K); the epilogues of launch_gemm plus EPI_SWIGLU_F32 (a bias on EPI_RESID adds to the product first).
 // N % 128 == 0, K % 32 (Q8_0) / % 256 (K-quants) == 0.
-void launch_gemm_a8(const QAct& a, const WeightView& W, int M, int N, int K, const GemmEpilogue& epi, hipStream_t s);
+// With a.q16 and w16 (the bf16(q) image of W's int8 plane, launch_q8_image) a Q8_0 GEMM runs on the bf16 MFMA
+// (gemm_a8s_kernel: each 32-value block's integer dot is exact there; same bits as the i8 kernel), K % 64 == 0.
+void launch_gemm_a8(const QAct& a, const WeightView& W, int M, int N, int K, const GemmEpilogue& epi, hipStream_t s,
+                    const uint16_t* w16 = nullptr);
+// int8 plane [n] -> bf16 image [n] (exact integers), n % 16 == 0
+void launch_q8_image(const int8_t* q, int64_t n, uint16_t* out, hipStream_t s);
+// whether the q8 mode runs a GEMM with this weight format / depth on the bf16 MFMA: ACE_MI_QACT_GEMM=0 (or
+// gemm_a8_mode(0)) keeps every one on the i8 kernel; gemm_a8_mode(-1) = the environment / default (on)
+bool gemm_a8_bf16_path(int fmt, int K);
+void gemm_a8_mode(int mode);
 // launch_rmsnorm_mod's operator with an f32 output [M][H]
 void launch_rmsnorm_mod_f32(const float* x, int M, int H, const float* w, const float* scale, const float* shift,
                             int64_t mod_stride, int rows_per_item, float eps, float* out, hipStream_t s);

@@ -36,8 +36,8 @@ struct A8Params {
 // Q8_0 (x86 quantize_row_q8_0): per 32 values amax = max|x|, d = amax / 127 stored as fp16, id = 127 / amax (0 for
 // an all-zero block), q = round-half-even(x * id).  One thread per block.
 __global__ void __launch_bounds__(256) quantize_q8_0_kernel(const float* __restrict__ x, int64_t ldx, int M, int K,
-                                                            bool silu_in, int8_t* __restrict__ q, float* __restrict__ s,
-                                                            int64_t ld_s) {
+                                                            bool silu_in, int8_t* __restrict__ q, uint16_t* __restrict__ q16,
+                                                            float* __restrict__ s, int64_t ld_s) {
     const int nb = K >> 5;
     const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (t >= (int64_t)M * nb) return;
@@ -68,9 +68,25 @@ __global__ void __launch_bounds__(256) quantize_q8_0_kernel(const float* __restr
         for (int j = 0; j < 4; ++j) p |= ((uint32_t)(int)__builtin_rintf(rn_mul(v[4 * i + j], id)) & 0xffu) << (8 * j);
         w[i] = p;
     }
-    int8_t* qr = q + (int64_t)m * K + b * 32;
-    *(uint4*)qr = make_uint4(w[0], w[1], w[2], w[3]);
-    *(uint4*)(qr + 16) = make_uint4(w[4], w[5], w[6], w[7]);
+    if (q) {
+        int8_t* qr = q + (int64_t)m * K + b * 32;
+        *(uint4*)qr = make_uint4(w[0], w[1], w[2], w[3]);
+        *(uint4*)(qr + 16) = make_uint4(w[4], w[5], w[6], w[7]);
+    }
+    if (q16) {  // bf16(q): the integers exactly (the bf16-MFMA Q8_0 GEMM's A operand)
+        uint16_t* hr = q16 + (int64_t)m * K + b * 32;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            uint32_t h[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t p = w[2 * i + (j >> 1)];
+                const int q0 = (int)(int8_t)((p >> (16 * (j & 1))) & 0xff), q1 = (int)(int8_t)((p >> (16 * (j & 1) + 8)) & 0xff);
+                h[j] = (__float_as_uint((float)q0) >> 16) | (__float_as_uint((float)q1) & 0xffff0000u);
+            }
+            *(uint4*)(hr + 8 * i) = make_uint4(h[0], h[1], h[2], h[3]);
+        }
+    }
     s[(int64_t)b * ld_s + m] = (float)(_Float16)d;
 }
 
@@ -228,6 +244,44 @@ __global__ void pack_input_f32_kernel(const float* __restrict__ hidden, const fl
     }
 }
 
+// The epilogues of both Q8 GEMMs, on a wave's 4 x 4 grid of 16 x 16 accumulators (the bf16 form's C/D map)
+template <int EPI, int SMEM>
+__device__ __forceinline__ void a8_epilogue(const GemmParams& p, f32x4 (&acc)[4][4], int m0, int n0, int wm0, int wn0,
+                                            int tid, char* smem) {
+    const int lane = tid & 63, g = lane >> 4, c = lane & 15;
+    const GemmEpilogue& e = p.e;
+    if constexpr (EPI == EPI_QKV_PREP) {
+        qkv_prep_tile<A8_BM, 4, 4, 4, SMEM>(p, acc, m0, n0, wm0, wn0, tid, smem);
+    } else if constexpr (EPI == EPI_SWIGLU_F32) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = m0 + wm0 + i * 16 + 4 * g + r;
+                if (m >= p.M) continue;
+#pragma unroll
+                for (int j = 0; j < 4; j += 2) {
+                    const int n = n0 + wn0 + j * 16;  // gate columns n .. n + 15, up columns n + 16 .. n + 31
+                    e.c_f32[(int64_t)m * e.ldc + (n >> 1) + c] = rn_mul(silu_f(acc[i][j][r]), acc[i][j + 1][r]);
+                }
+            }
+    } else {
+        if constexpr (EPI == EPI_RESID || EPI == EPI_RESID_GATED) {
+            if (e.bias) {  // x + (W x_a + b): the bias joins the product before the residual add
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float bj = e.bias[n0 + wn0 + j * 16 + c];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) acc[i][j][r] = rn_add(acc[i][j][r], bj);
+                }
+            }
+        }
+        gemm_epilogue<4, 4, false, EPI, 1024>(p, acc, m0 + wm0, n0 + wn0, lane);
+    }
+}
+
 // ---------------------------------------------------------------- the GEMM
 // 256 threads, a 128 x 128 tile as 2 x 2 waves of 64 x 64 (4 x 4 accumulators of 16 x 16).  i8 MFMA 16x16x32
 // operands: lane l holds A row l & 15 / B column l & 15, k = 8 (l >> 4) .. + 7; result row 4 (l >> 4) + r,
@@ -353,37 +407,217 @@ __global__ void __launch_bounds__(256) gemm_a8_kernel(A8Params p) {
         }
     }
 
-    const GemmEpilogue& e = p.g.e;
-    if constexpr (EPI == EPI_QKV_PREP) {
-        qkv_prep_tile<A8_BM, 4, 4, 4, A8_PREP_SMEM>(p.g, acc, m0, n0, wm0, wn0, tid, smem);
-    } else if constexpr (EPI == EPI_SWIGLU_F32) {
+    a8_epilogue<EPI, (EPI == EPI_QKV_PREP ? A8_PREP_SMEM : 16)>(p.g, acc, m0, n0, wm0, wn0, tid, smem);
+}
+
+// ---------------------------------------------------------------- Q8_0 on the bf16 MFMA (round 6)
+// ggml's Q8_0 block dot is exact in a bf16 MFMA: every q of an activation or weight block is an integer in [-127, 127]
+// (exact in bf16), each product is exact in f32 and so is the 32-term block sum (|sum| <= 32 * 127^2 < 2^24).  So
+// v_mfma_f32_16x16x32_bf16 over ONE 32-value block, accumulator zero, returns the block's integer dot already in f32 --
+// the value v_mfma_i32_16x16x32_i8 returns, with no convert -- and the per-block scaling is acc = fma(dot, d_w * d_a,
+// acc) in block order, exactly the kernel above (same bits).  The operands are the activation quantizer's bf16(q)
+// rows and a bf16(q) image of the weight plane (launch_q8_image; the q8 mode keeps one per matrix), so the dense
+// GEMM's machinery applies: 128 x 128 tiles of 2 x 2 waves (64 x 64 each), BK = 64 (two blocks), both operands staged
+// by LDS-DMA into a double-buffered, XOR-swizzled LDS image (released early: every fragment is read before the
+// barrier) and the two blocks' d_a [2][128] and d_w [128][2] into a three-slot ring read during the MFMAs, fragment
+// reads as inline asm with one counted vmcnt (block 1's fragments read under block 0's MFMAs), two workgroups per CU.
+// Per block and 16 x 16 tile: one MFMA
+// and, per output, one multiply (d_w * d_a) and one FMA.
+constexpr int A8S_STAGE = (A8_BM + A8_BN) * 128;  // A and W k-tiles, 128-byte rows (two buffers)
+constexpr int A8S_SC = 2 * A8_BM * 4 + A8_BN * 2 * 4;  // d_a [2][BM] + d_w [BN][2] of one k-tile (a three-slot ring)
+constexpr int A8S_DA = 0, A8S_DW = 2 * A8_BM * 4;
+constexpr int A8S_SMEM = 2 * A8S_STAGE + 3 * A8S_SC;  // 71 680 B: two workgroups per CU
+static_assert(A8S_SMEM >= A8_PREP_SMEM, "the prep epilogue reuses the stage buffers");
+
+struct A8SParams {
+    GemmParams g;        // M, N, K and the epilogue
+    const uint16_t* a;   // bf16(q) activation rows [M][K]
+    const uint16_t* w;   // bf16(q) weight image [N][K]
+    const float* as;     // d_a [K/32][ld_s]
+    int64_t ld_s;
+    const float* ws;     // d_w [N][K/32]
+};
+
+template <int OFF>
+__device__ __forceinline__ uint2 ds_read_b64_off(uint32_t addr) {
+    typedef __attribute__((ext_vector_type(2))) unsigned u32x2_t;
+    u32x2_t v;
+    asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
+    return make_uint2(v[0], v[1]);
+}
+
+template <int EPI>
+__global__ void __launch_bounds__(256, 2) gemm_a8s_kernel(A8SParams p) {
+    constexpr int TM = 4, TN = 4, BK = 64, ROWB = 128;
+    constexpr int G_AW = (A8_BM + A8_BN) / 8 / 4;  // 1 KiB A / W pieces per wave per k-tile
+    constexpr int G = G_AW + 2;                    // + one d_a and one d_w dword piece
+    __shared__ __attribute__((aligned(16))) char smem[A8S_SMEM];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int M = p.g.M, K = p.g.K;
+    const int nb = K >> 5, nk = K / BK;
+    int m0, n0;
+    block_tile<A8_BM, A8_BN>(p.g, m0, n0);
+    const int wm0 = (wid >> 1) * 64, wn0 = (wid & 1) * 64;
+    const int g = lane >> 4, c = lane & 15;
+
+    // LDS-DMA sources as 32-bit element offsets (pieces j < G_AW / 2 are A rows, the rest W rows): 64-bit pointers
+    // cost the registers that keep this kernel at two workgroups per CU without scratch
+    static_assert(G_AW % 2 == 0 && (G_AW / 2) * 4 * 8 == A8_BM, "A / W piece split");
+    int src[G_AW];
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int m = m0 + wm0 + i * 16 + 4 * g + r;
-                if (m >= M) continue;
-#pragma unroll
-                for (int j = 0; j < 4; j += 2) {
-                    const int n = n0 + wn0 + j * 16;  // gate columns n .. n + 15, up columns n + 16 .. n + 31
-                    e.c_f32[(int64_t)m * e.ldc + (n >> 1) + c] = rn_mul(silu_f(acc[i][j][r]), acc[i][j + 1][r]);
-                }
-            }
-    } else {
-        if constexpr (EPI == EPI_RESID || EPI == EPI_RESID_GATED) {
-            if (e.bias) {  // x + (W x_a + b): the bias joins the product before the residual add
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const float bj = e.bias[n0 + wn0 + j * 16 + c];
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) acc[i][j][r] = rn_add(acc[i][j][r], bj);
-                }
-            }
-        }
-        gemm_epilogue<4, 4, false, EPI, 1024>(p.g, acc, m0 + wm0, n0 + wn0, lane);
+    for (int j = 0; j < G_AW; ++j) {
+        const int row = (wid + 4 * j) * 8 + (lane >> 3);
+        const int ch = (lane & 7) ^ swz(row);
+        src[j] = j < G_AW / 2 ? min(m0 + row, M - 1) * K + ch * 8 : (n0 + row - A8_BM) * K + ch * 8;
     }
+    // scale pieces: element e = 64 wid + lane of d_a [2][BM] (block e / BM, row e % BM; rows past M read the zero-padded
+    // plane, ld_s >= M rounded up to 128) and of d_w [BN][2] (column e / 2, block e % 2)
+    const int e = 64 * wid + lane;
+    const float* sa = p.as + (int64_t)(e / A8_BM) * p.ld_s + m0 + e % A8_BM;
+    const float* sw = p.ws + (int64_t)(n0 + (e >> 1)) * nb + (e & 1);
+    auto stage = [&](int buf, int kt) {
+        char* base = smem + buf * A8S_STAGE;
+#pragma unroll
+        for (int j = 0; j < G_AW; ++j)
+            __builtin_amdgcn_global_load_lds((const void*)((j < G_AW / 2 ? p.a : p.w) + (src[j] + kt * BK)),
+                                             (lds_void*)(base + (wid + 4 * j) * 1024), 16, 0, 0);
+        char* sc = smem + 2 * A8S_STAGE + (kt % 3) * A8S_SC;
+        __builtin_amdgcn_global_load_lds((const void*)(sa + (int64_t)(2 * kt) * p.ld_s), (lds_void*)(sc + A8S_DA + wid * 256),
+                                         4, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)(sw + 2 * kt), (lds_void*)(sc + A8S_DW + wid * 256), 4, 0, 0);
+    };
+
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+    const int lrow = lane & 15, lchunk = lane >> 4;
+    uint4 a[2][TM], b[2][TN];  // the two blocks' fragments (block 1's are read under block 0's MFMAs)
+    uint4 da[2][TM];           // d_a of this lane's 4 rows of each 16-row tile, per block
+    uint2 dw[TN];        // d_w of this lane's column of each 16-column tile, both blocks
+    auto read_frags = [&](int buf, auto kk_c) {
+        constexpr int kk = decltype(kk_c)::value;
+        const uint32_t sbase = lds0 + buf * A8S_STAGE;
+        const int ch = (kk * 4 + lchunk) ^ ((lrow >> 1) & 7);
+        const uint32_t bb = sbase + A8_BM * ROWB + (wn0 + lrow) * ROWB + ch * 16;
+        const uint32_t ab = sbase + (wm0 + lrow) * ROWB + ch * 16;
+        static_for<0, TN>([&](auto j_c) {
+            constexpr int j = decltype(j_c)::value;
+            b[kk][j] = ds_read_b128_off<j * 16 * ROWB>(bb);
+        });
+        static_for<0, TM>([&](auto i_c) {
+            constexpr int i = decltype(i_c)::value;
+            a[kk][i] = ds_read_b128_off<i * 16 * ROWB>(ab);
+        });
+    };
+    auto read_dw = [&](int kt) {
+        const uint32_t dwb = lds0 + 2 * A8S_STAGE + (kt % 3) * A8S_SC + A8S_DW + (wn0 + c) * 8;
+        dw[0] = ds_read_b64_off<0 * 128>(dwb);
+        dw[1] = ds_read_b64_off<1 * 128>(dwb);
+        dw[2] = ds_read_b64_off<2 * 128>(dwb);
+        dw[3] = ds_read_b64_off<3 * 128>(dwb);
+    };
+    auto read_da = [&](int kt, auto kk_c) {
+        constexpr int kk = decltype(kk_c)::value;
+        const uint32_t dab = lds0 + 2 * A8S_STAGE + (kt % 3) * A8S_SC + A8S_DA + (kk * A8_BM + wm0 + 4 * g) * 4;
+        da[kk][0] = ds_read_b128_off<0 * 64>(dab);
+        da[kk][1] = ds_read_b128_off<1 * 64>(dab);
+        da[kk][2] = ds_read_b128_off<2 * 64>(dab);
+        da[kk][3] = ds_read_b128_off<3 * 64>(dab);
+    };
+    const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+    // One block (kk): row group i's four MFMAs are issued in step i and scaled into acc in step i + 1, under the next
+    // group's MFMAs.  Empty asm statements pin the order (hipcc otherwise hoists all sixteen MFMAs of both blocks and
+    // sinks the scaling behind them, holding 32 results at once: spills): step i's MFMAs read a[i] after an asm that
+    // "writes" it, and the FMAs of step i produce acc rows that an asm "reads" in the same step.
+    auto block = [&](auto kk_c) {
+        constexpr int kk = decltype(kk_c)::value;
+        f32x4 tp[TN], tc[TN];
+        static_for<0, TM + 1>([&](auto i_c) {
+            constexpr int i = decltype(i_c)::value;
+            if constexpr (i < TM) {
+                u32x4 ai = __builtin_bit_cast(u32x4, a[kk][i]);
+                asm volatile("" : "+v"(ai));
+                a[kk][i] = __builtin_bit_cast(uint4, ai);
+#pragma unroll
+                for (int j = 0; j < TN; ++j) tc[j] = mfma16<false>(a[kk][i], b[kk][j], zero);
+            }
+            if constexpr (i > 0) {
+                const uint4 dv = da[kk][i - 1];
+                const float d4[4] = {__uint_as_float(dv.x), __uint_as_float(dv.y), __uint_as_float(dv.z),
+                                     __uint_as_float(dv.w)};
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const float dwj = __uint_as_float(kk == 0 ? dw[j].x : dw[j].y);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        acc[i - 1][j][r] = __builtin_fmaf(tp[j][r], rn_mul(dwj, d4[r]), acc[i - 1][j][r]);
+                    asm volatile("" : "+v"(acc[i - 1][j]));
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j) tp[j] = tc[j];
+        });
+    };
+    auto wait_retire = [&](int younger) {
+        if (younger >= 1)
+            wait_vmcnt<G>();
+        else
+            wait_vmcnt<0>();
+    };
+
+    // Double buffer, one k-tile ahead: tile kt + 2 is staged into buffer kt & 1 once every wave has finished reading it
+    // (the barrier that ends iteration kt), so each tile has the whole next iteration to land; the fragments of each
+    // block are read right before its MFMAs (one block's operands live at a time).
+    using K0 = std::integral_constant<int, 0>;
+    using K1 = std::integral_constant<int, 1>;
+    stage(0, 0);
+    if (nk > 1) stage(1, 1);
+    for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        wait_retire(kt + 1 < nk ? 1 : 0);  // tile kt landed (tile kt + 1 may stay in flight)
+        __builtin_amdgcn_s_barrier();       // ... for every wave's pieces
+        read_frags(cur, K0{});
+        read_dw(kt);
+        read_da(kt, K0{});
+        lds_wait_all();
+        read_frags(cur, K1{});  // in flight under block 0
+        read_da(kt, K1{});
+        block(K0{});
+        mfma_war_retire(a[0], b[0]);
+        lds_wait_all();
+        block(K1{});
+        mfma_war_retire(a[1], b[1]);
+        __builtin_amdgcn_s_barrier();  // every wave is done with buffer `cur` and scale slot kt % 3
+        if (kt + 2 < nk) stage(cur, kt + 2);
+    }
+    a8_epilogue<EPI, A8S_SMEM>(p.g, acc, m0, n0, wm0, wn0, tid, smem);
+}
+
+template <int EPI>
+void launch_a8s_epi(const A8SParams& p, dim3 grid, hipStream_t s) {
+    hipLaunchKernelGGL((gemm_a8s_kernel<EPI>), grid, dim3(256), 0, s, p);
+}
+
+// int8 plane -> its bf16 image (exact integers), 16 values per thread
+__global__ void __launch_bounds__(256) q8_image_kernel(const int8_t* __restrict__ q, int64_t n16, uint16_t* __restrict__ out) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= n16) return;
+    const uint4 v = *(const uint4*)(q + t * 16);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t o[8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int x0 = (int)(int8_t)(w[i] & 0xff), x1 = (int)(int8_t)((w[i] >> 8) & 0xff);
+        const int x2 = (int)(int8_t)((w[i] >> 16) & 0xff), x3 = (int)(int8_t)(w[i] >> 24);
+        o[2 * i] = (__float_as_uint((float)x0) >> 16) | (__float_as_uint((float)x1) & 0xffff0000u);
+        o[2 * i + 1] = (__float_as_uint((float)x2) >> 16) | (__float_as_uint((float)x3) & 0xffff0000u);
+    }
+    *(uint4*)(out + t * 16) = make_uint4(o[0], o[1], o[2], o[3]);
+    *(uint4*)(out + t * 16 + 8) = make_uint4(o[4], o[5], o[6], o[7]);
 }
 
 template <int WQ>
@@ -406,13 +640,14 @@ dim3 grid_1d(int64_t n) { return dim3((unsigned)((n + 255) / 256)); }
 }  // namespace
 
 void launch_quantize_act(int kind, const float* x, int64_t ldx, int M, int K, bool silu_in, int8_t* q, float* s,
-                         float* bsum, int64_t ld_s, hipStream_t st) {
+                         float* bsum, int64_t ld_s, hipStream_t st, uint16_t* q16) {
     ACEMI_CHECK(M >= 1 && ld_s >= M && ldx >= K && ldx % 4 == 0, "quantize_act: bad shape");
     if (kind == QACT_Q8_0) {
-        ACEMI_CHECK(K % 32 == 0, "quantize_act: Q8_0 needs K % 32 == 0");
+        ACEMI_CHECK(K % 32 == 0 && (q || q16), "quantize_act: Q8_0 needs K % 32 == 0 and an output");
         hipLaunchKernelGGL(quantize_q8_0_kernel, grid_1d((int64_t)M * (K / 32)), dim3(256), 0, st, x, ldx, M, K, silu_in,
-                           q, s, ld_s);
+                           q, q16, s, ld_s);
     } else {
+        ACEMI_CHECK(q != nullptr && q16 == nullptr, "quantize_act: Q8_K has the int8 form only");
         ACEMI_CHECK(K % 256 == 0 && bsum != nullptr, "quantize_act: Q8_K needs K % 256 == 0 and a block-sum plane");
         hipLaunchKernelGGL(quantize_q8_k_kernel, grid_1d((int64_t)M * (K / 256) * 8), dim3(256), 0, st, x, ldx, M, K,
                            silu_in, q, s, bsum, ld_s);
@@ -420,8 +655,56 @@ void launch_quantize_act(int kind, const float* x, int64_t ldx, int M, int K, bo
     ACEMI_HIP(hipGetLastError());
 }
 
-void launch_gemm_a8(const QAct& a, const WeightView& W, int M, int N, int K, const GemmEpilogue& epi, hipStream_t s) {
+static int g_a8_mode = -1;
+void gemm_a8_mode(int mode) { g_a8_mode = mode; }
+bool gemm_a8_bf16_path(int fmt, int K) {
+    static const int env = [] {
+        const char* e = std::getenv("ACE_MI_QACT_GEMM");
+        return (e && e[0] == '0') ? 0 : 1;
+    }();
+    const int mode = g_a8_mode >= 0 ? g_a8_mode : env;
+    return mode == 1 && fmt == WF_Q8_0 && K % 64 == 0;
+}
+
+void launch_q8_image(const int8_t* q, int64_t n, uint16_t* out, hipStream_t s) {
+    ACEMI_CHECK(n % 16 == 0, "q8_image: n % 16 == 0");
+    hipLaunchKernelGGL(q8_image_kernel, grid_1d(n / 16), dim3(256), 0, s, q, n / 16, out);
+    ACEMI_HIP(hipGetLastError());
+}
+
+void launch_gemm_a8(const QAct& a, const WeightView& W, int M, int N, int K, const GemmEpilogue& epi, hipStream_t s,
+                    const uint16_t* w16) {
     ACEMI_CHECK(weight_quantized(W.fmt) && W.q && W.s, "gemm_a8: the weight must be in a ggml block format");
+    if (a.q16 && w16) {  // Q8_0 on the bf16 MFMA (gemm_a8s_kernel)
+        ACEMI_CHECK(W.fmt == WF_Q8_0 && a.kind == QACT_Q8_0 && K % 64 == 0 && K >= 64 && M >= 1 && N % A8_BN == 0,
+                    "gemm_a8: the bf16-MFMA form is Q8_0 with K % 64 == 0, N % 128 == 0");
+        ACEMI_CHECK(a.s && a.ld_s >= (int64_t)(M + A8_BM - 1) / A8_BM * A8_BM, "gemm_a8: activation scale plane too small");
+        A8SParams p{};
+        p.g.M = M;
+        p.g.N = N;
+        p.g.K = K;
+        p.g.e = epi;
+        p.a = a.q16;
+        p.w = w16;
+        p.as = a.s;
+        p.ld_s = a.ld_s;
+        p.ws = W.s;
+        const dim3 grid((unsigned)(((M + A8_BM - 1) / A8_BM) * (N / A8_BN)));
+        switch (epi.kind) {
+            case EPI_STORE_F32: launch_a8s_epi<EPI_STORE_F32>(p, grid, s); break;
+            case EPI_STORE_ACT: launch_a8s_epi<EPI_STORE_ACT>(p, grid, s); break;
+            case EPI_RESID_GATED: launch_a8s_epi<EPI_RESID_GATED>(p, grid, s); break;
+            case EPI_RESID: launch_a8s_epi<EPI_RESID>(p, grid, s); break;
+            case EPI_SWIGLU: launch_a8s_epi<EPI_SWIGLU>(p, grid, s); break;
+            case EPI_PROJ_OUT: launch_a8s_epi<EPI_PROJ_OUT>(p, grid, s); break;
+            case EPI_QKV_PREP: launch_a8s_epi<EPI_QKV_PREP>(p, grid, s); break;
+            case EPI_SWIGLU_F32: launch_a8s_epi<EPI_SWIGLU_F32>(p, grid, s); break;
+            default: throw std::runtime_error("gemm_a8: unknown epilogue");
+        }
+        ACEMI_HIP(hipGetLastError());
+        return;
+    }
+    ACEMI_CHECK(a.q != nullptr, "gemm_a8: the i8 kernel needs the int8 activation blocks");
     ACEMI_CHECK(a.kind == qact_kind_for(W.fmt), "gemm_a8: activation blocks do not match the weight's vec_dot_type");
     ACEMI_CHECK(M >= 1 && N % A8_BN == 0 && K % (W.fmt == WF_Q8_0 ? 32 : 256) == 0, "gemm_a8: bad shape");
     ACEMI_CHECK(a.q && a.s && a.ld_s >= (int64_t)(M + A8_BM - 1) / A8_BM * A8_BM && a.ld_s % 4 == 0,

@@ -50,6 +50,9 @@ DitEngine::~DitEngine() {
     if (wring_.p) (void)hipFree(wring_.p);
     for (auto& kv : img_)
         if (kv.second.p) (void)hipFree(kv.second.p);
+    for (auto& kv : q8img_)
+        if (kv.second.p) (void)hipFree(kv.second.p);
+    if (qa16_.p) (void)hipFree(qa16_.p);
 }
 
 namespace {

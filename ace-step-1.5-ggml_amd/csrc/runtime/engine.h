@@ -149,6 +149,9 @@ class DitEngine {
     // product path keeps bf16 activations.
     bool qact_ = false;
     Buf qf_, qa_, qs_, qb_, encf_;  // f32 activation rows, their int8 blocks, block scales / sums, f32 condition
+    Buf qa16_;                      // Q8_0 activation blocks as bf16(q) rows (the bf16-MFMA form, gemm_a8_bf16_path)
+    std::map<const void*, Buf> q8img_;  // bf16(q) image of each Q8_0 plane, made at its first q8-mode use
+    const uint16_t* q8_image(const WeightView& w, int N, int K, hipStream_t s);
     void forward_qact(const ForwardIO& io, hipStream_t s);
     void qlinear(const float* x, int64_t ldx, int M, const WeightView& w, int N, int K, const GemmEpilogue& e,
                  const char* name, hipStream_t s, bool silu_in = false);

@@ -16,7 +16,22 @@ namespace acemi {
 void DitEngine::qlinear(const float* x, int64_t ldx, int M, const WeightView& w, int N, int K, const GemmEpilogue& e,
                         const char* name, hipStream_t s, bool silu_in) {
     tic(s);
-    if (weight_quantized(w.fmt)) {
+    if (weight_quantized(w.fmt) && gemm_a8_bf16_path(w.fmt, K)) {
+        // Q8_0 on the bf16 MFMA: the activation blocks as bf16(q) rows, the weight as its bf16(q) image (same bits as
+        // the i8 kernel below, kernels/gemm_a8.hip gemm_a8s_kernel)
+        const int64_t ld_s = round_up(M, 128);
+        ensure(qa16_, (size_t)M * K * 2);
+        ensure(qs_, (size_t)(K / 32) * ld_s * 4);
+        const uint16_t* w16 = q8_image(w, N, K, s);
+        launch_quantize_act(QACT_Q8_0, x, ldx, M, K, silu_in, nullptr, get<float>(qs_), nullptr, ld_s, s,
+                            get<uint16_t>(qa16_));
+        QAct a;
+        a.kind = QACT_Q8_0;
+        a.q16 = get<uint16_t>(qa16_);
+        a.s = get<float>(qs_);
+        a.ld_s = ld_s;
+        launch_gemm_a8(a, w, M, N, K, e, s, w16);
+    } else if (weight_quantized(w.fmt)) {
         const int kind = qact_kind_for(w.fmt);
         const int64_t ld_s = round_up(M, 128);
         ensure(qa_, (size_t)M * K);
@@ -40,6 +55,17 @@ void DitEngine::qlinear(const float* x, int64_t ldx, int M, const WeightView& w,
         launch_gemm(xa, K, w, M, N, K, e, s);
     }
     toc(name, s);
+}
+
+// bf16(q) image of a Q8_0 weight's int8 plane, made once on the stream that first needs it and kept while the model is
+// loaded (the engine is rebuilt with every load, so a plane pointer names one weight for the cache's lifetime)
+const uint16_t* DitEngine::q8_image(const WeightView& w, int N, int K, hipStream_t s) {
+    Buf& b = q8img_[w.q];
+    if (!b.p) {
+        ensure(b, (size_t)N * K * 2);
+        launch_q8_image(static_cast<const int8_t*>(w.q), (int64_t)N * K, static_cast<uint16_t*>(b.p), s);
+    }
+    return static_cast<const uint16_t*>(b.p);
 }
 
 void DitEngine::timestep_embed_qact(const float* t, const float* r, int rows, float* proj, float* temb_t,

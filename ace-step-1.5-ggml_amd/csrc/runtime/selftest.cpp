@@ -434,8 +434,16 @@ ace_ggml_status ace_mi_kernel_gemm_a8(int32_t qtype, int32_t epi, int32_t M, int
         a.s = dAs.as<float>();
         a.bsum = dAb.as<float>();
         a.ld_s = ld_s;
+        // Q8_0 with K % 64 == 0 runs the bf16-MFMA form unless ace_mi_kernel_gemm_a8_mode(0) (or ACE_MI_QACT_GEMM=0)
+        // keeps it on the i8 kernel: the int8 blocks are returned either way
+        const bool bf16_path = gemm_a8_bf16_path(t == quant::Q8_0 ? WF_Q8_0 : WF_Q4_K, K);
+        DevMem dA16(bf16_path ? (size_t)M * K * 2 : 16), dW16(bf16_path ? (size_t)N * K * 2 : 16);
         launch_quantize_act(a.kind, dX.as<float>(), K, M, K, false, dAq.as<int8_t>(), dAs.as<float>(), dAb.as<float>(),
-                            ld_s, nullptr);
+                            ld_s, nullptr, bf16_path ? dA16.as<uint16_t>() : nullptr);
+        if (bf16_path) {
+            a.q16 = dA16.as<uint16_t>();
+            launch_q8_image(dQ.as<int8_t>(), (int64_t)N * K, dW16.as<uint16_t>(), nullptr);
+        }
         GemmEpilogue e;
         e.kind = epi;
         e.bias = bias ? dB.as<float>() : nullptr;
@@ -445,7 +453,7 @@ ace_ggml_status ace_mi_kernel_gemm_a8(int32_t qtype, int32_t epi, int32_t M, int
         w.fmt = t == quant::Q8_0 ? WF_Q8_0 : (t == quant::Q4_K ? WF_Q4_K : WF_Q6_K);
         w.q = dQ.p;
         w.s = dS.as<float>();
-        launch_gemm_a8(a, w, M, N, K, e, nullptr);
+        launch_gemm_a8(a, w, M, N, K, e, nullptr, bf16_path ? dW16.as<uint16_t>() : nullptr);
         ACEMI_HIP(hipDeviceSynchronize());
         ACEMI_HIP(hipMemcpy(out_f32, dC.p, (size_t)M * ncol * 4, hipMemcpyDeviceToHost));
         if (q_out) ACEMI_HIP(hipMemcpy(q_out, dAq.p, (size_t)M * K, hipMemcpyDeviceToHost));
@@ -461,6 +469,14 @@ ace_ggml_status ace_mi_kernel_gemm_a8(int32_t qtype, int32_t epi, int32_t M, int
         std::fprintf(stderr, "ace_mi_kernel_gemm_a8: %s\n", ex.what());
         return ACE_GGML_ERR;
     }
+    return ACE_GGML_OK;
+}
+
+// Which form ace_mi_kernel_gemm_a8 (and the q8 mode of this process) runs a Q8_0 GEMM in: -1 the environment / default
+// (the bf16 MFMA), 0 the i8 kernel, 1 the bf16 MFMA.
+ace_ggml_status ace_mi_kernel_gemm_a8_mode(int32_t mode) {
+    if (mode < -1 || mode > 1) return ACE_GGML_ERR_INVALID_ARG;
+    acemi::gemm_a8_mode(mode);
     return ACE_GGML_OK;
 }
 

@@ -396,7 +396,8 @@ def main():
         el_qa = timed(run)
         extras["qact_line"] = line(B * args.steps, el_qa,
                                    "the headline loop with ACE_MI_QUANT_ACT=q8: ggml's quantized arithmetic (Q8_0 "
-                                   "activation blocks, i8-MFMA block dots, f32 activations, f32-precision attention)")
+                                   "activation blocks, exact per-block integer dots on the bf16 MFMA from bf16(q) "
+                                   "operands, f32 activations, f32-precision attention)")
         if not args.no_profile:
             br.profile_enable(True)
             br.profile_reset()

@@ -57,6 +57,10 @@ ACE_GGML_API ace_ggml_status ace_mi_kernel_dequant(int32_t qtype, int32_t N, int
 ACE_GGML_API ace_ggml_status ace_mi_kernel_gemm_a8(int32_t qtype, int32_t epi, int32_t M, int32_t N, int32_t K,
                                                    const float* x, const uint8_t* W_blocks, const float* bias,
                                                    float* out_f32, int8_t* q_out, float* s_out, float* bsum_out);
+/* The form ace_mi_kernel_gemm_a8 and the q8 mode of this process run Q8_0 GEMMs in (K % 64 == 0): -1 = the
+ * environment (ACE_MI_QACT_GEMM=0: i8) / default (bf16 MFMA over exact integer bf16 operands), 0 = the i8-MFMA kernel,
+ * 1 = the bf16-MFMA kernel.  Both give the same bits. */
+ACE_GGML_API ace_ggml_status ace_mi_kernel_gemm_a8_mode(int32_t mode);
 /* Dequant-fused GEMM micro-benchmark: average ms per launch (HIP events). */
 ACE_GGML_API ace_ggml_status ace_mi_bench_gemm_q(int32_t qtype, int32_t epi, int32_t variant, int32_t M, int32_t N,
                                                  int32_t K, int32_t iters, float* avg_ms);

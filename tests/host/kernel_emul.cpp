@@ -294,9 +294,11 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t) {
 }
 
 // ---- quantized-activation mode (kernels/gemm_a8.hip), restated
-void launch_quantize_act(int kind, const float* x, int64_t ldx, int M, int K, bool sl, int8_t* q, float* s, float* bs,
-                         int64_t ld_s, hipStream_t) {
-    ACEMI_CHECK(M >= 1 && ld_s >= M && ldx >= K, "quantize_act: bad shape");
+void launch_quantize_act(int kind, const float* x, int64_t ldx, int M, int K, bool sl, int8_t* q_out, float* s,
+                         float* bs, int64_t ld_s, hipStream_t, uint16_t* q16) {
+    ACEMI_CHECK(M >= 1 && ld_s >= M && ldx >= K && (q_out || q16), "quantize_act: bad shape");
+    ACEMI_CHECK(kind == QACT_Q8_0 || (q_out && !q16), "quantize_act: Q8_K has the int8 form only");
+    std::vector<int8_t> qtmp((size_t)K);
     const int QK = kind == QACT_Q8_0 ? 32 : 256;
     ACEMI_CHECK(K % QK == 0, "quantize_act: K");
     for (int m = 0; m < M; ++m)
@@ -310,10 +312,12 @@ void launch_quantize_act(int kind, const float* x, int64_t ldx, int M, int K, bo
                     mx = v[i];
                 }
             }
-            int8_t* qr = q + (int64_t)m * K + b0;
+            int8_t* qr = q_out ? q_out + (int64_t)m * K + b0 : qtmp.data() + b0;
             if (kind == QACT_Q8_0) {
                 const float d = amax / 127.0f, id = amax != 0.f ? 127.0f / amax : 0.f;
                 for (int i = 0; i < 32; ++i) qr[i] = (int8_t)std::nearbyint(v[i] * id);
+                if (q16)  // bf16(q): the integer exactly
+                    for (int i = 0; i < 32; ++i) q16[(int64_t)m * K + b0 + i] = to_bf16((float)qr[i]);
                 s[(int64_t)(b0 / 32) * ld_s + m] = f16f(to_f16(d));
                 continue;
             }
@@ -330,8 +334,24 @@ void launch_quantize_act(int kind, const float* x, int64_t ldx, int M, int K, bo
         }
 }
 
-void launch_gemm_a8(const QAct& a, const WeightView& W, int M, int N, int K, const GemmEpilogue& e, hipStream_t st) {
+static int g_a8_mode = -1;
+void gemm_a8_mode(int mode) { g_a8_mode = mode; }
+bool gemm_a8_bf16_path(int fmt, int K) {
+    const char* e = std::getenv("ACE_MI_QACT_GEMM");
+    const int mode = g_a8_mode >= 0 ? g_a8_mode : ((e && e[0] == '0') ? 0 : 1);
+    return mode == 1 && fmt == WF_Q8_0 && K % 64 == 0;
+}
+void launch_q8_image(const int8_t* q, int64_t n, uint16_t* out, hipStream_t) {
+    ACEMI_CHECK(n % 16 == 0, "q8_image: n % 16 == 0");
+    for (int64_t i = 0; i < n; ++i) out[i] = to_bf16((float)q[i]);
+}
+
+void launch_gemm_a8(const QAct& a, const WeightView& W, int M, int N, int K, const GemmEpilogue& e, hipStream_t st,
+                    const uint16_t* w16) {
     ACEMI_CHECK(weight_quantized(W.fmt) && a.kind == qact_kind_for(W.fmt), "gemm_a8: format mismatch");
+    ACEMI_CHECK(a.q || (a.q16 && w16 && W.fmt == WF_Q8_0 && K % 64 == 0), "gemm_a8: operand forms");
+    if (a.q16 && w16) touch(w16, (int64_t)N * K);
+    auto aq = [&](int64_t i) { return a.q16 && w16 ? bf16f(a.q16[i]) : (float)a.q[i]; };
     ACEMI_CHECK(M >= 1 && N % 128 == 0 && a.ld_s >= (M + 127) / 128 * 128, "gemm_a8: bad shape");
     touch(a.s, (int64_t)(K / 32 - 1) * a.ld_s + (M + 127) / 128 * 128);
     std::vector<float> acc((size_t)M * N);
@@ -344,7 +364,8 @@ void launch_gemm_a8(const QAct& a, const WeightView& W, int M, int N, int K, con
                 for (int k = 32 * b; k < 32 * b + 32; ++k) {
                     float w;  // the dequantized weight element in f32 (not rounded to bf16)
                     if (W.fmt == WF_Q8_0) {
-                        w = (float)((const int8_t*)W.q)[(int64_t)n * K + k] * W.s[(int64_t)n * nb + b];
+                        const float qw = a.q16 && w16 ? bf16f(w16[(int64_t)n * K + k]) : (float)((const int8_t*)W.q)[(int64_t)n * K + k];
+                        w = qw * W.s[(int64_t)n * nb + b];
                     } else if (W.fmt == WF_Q6_K) {
                         w = (float)((const int8_t*)W.q)[(int64_t)n * K + k] * W.s[(int64_t)n * (K / 16) + k / 16];
                     } else {
@@ -354,7 +375,7 @@ void launch_gemm_a8(const QAct& a, const WeightView& W, int M, int N, int K, con
                         const float* sm = W.s + ((int64_t)n * nb + b) * 2;
                         w = (float)qv * sm[0] - sm[1];
                     }
-                    sum += (double)a.q[(int64_t)m * K + k] * da * w;
+                    sum += (double)aq((int64_t)m * K + k) * da * w;
                 }
             }
             acc[(size_t)m * N + n] = (float)sum;

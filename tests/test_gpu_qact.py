@@ -69,6 +69,31 @@ def test_gemm_a8_matches_block_integer_dot(qtype, M, N, K):
     assert np.all(err <= 5e-6 * mag + 1e-30), float(np.max(err / (mag + 1e-30)))
 
 
+@pytest.mark.parametrize("M,N,K", [(1, 128, 64), (77, 256, 128), (129, 384, 2048), (300, 128, 6144), (3000, 2048, 2048)])
+@pytest.mark.parametrize("epi", [0, 3, 7])
+def test_gemm_a8_bf16_mfma_form_is_bit_identical(M, N, K, epi):
+    """Q8_0 on the bf16 MFMA (gemm_a8s_kernel: each block's integer dot is exact in f32 from bf16(q) operands, the
+    default for K % 64 == 0) against the i8-MFMA kernel: the same integer dots, scales and f32 order -> the same bits,
+    with every epilogue the comparison covers."""
+    capi = _capi()
+    rng = np.random.default_rng(M + N + K + epi)
+    x = rng.standard_normal((M, K)).astype(np.float32)
+    x[:, :32] *= 40.0
+    w = (rng.standard_normal((N, K)) * 0.02).astype(np.float32)
+    blocks = capi.quantize(w, "q8_0")
+    b = rng.standard_normal(N).astype(np.float32)
+    x0 = rng.standard_normal((M, N)).astype(np.float32) if epi == 3 else None
+    outs = []
+    try:
+        for mode in (0, 1):
+            capi.kernel_gemm_a8_mode(mode)
+            outs.append(capi.kernel_gemm_a8(x, blocks, "q8_0", epi=epi, bias=None if epi == 7 else b, x0=x0))
+    finally:
+        capi.kernel_gemm_a8_mode(-1)
+    for i0, i1 in zip(outs[0], outs[1]):
+        np.testing.assert_array_equal(np.asarray(i0).view(np.uint8), np.asarray(i1).view(np.uint8))
+
+
 @pytest.mark.parametrize("qtype", ["q8_0", "q4_k"])
 def test_gemm_a8_epilogues(qtype):
     """bias store, residual with bias (x + (acc + b): ggml adds the bias to the mul_mat result), SwiGLU in f32"""
