@@ -245,13 +245,14 @@ __global__ void pack_input_f32_kernel(const float* __restrict__ hidden, const fl
 }
 
 // The epilogues of both Q8 GEMMs, on a wave's 4 x 4 grid of 16 x 16 accumulators (the bf16 form's C/D map)
-template <int EPI, int SMEM>
-__device__ __forceinline__ void a8_epilogue(const GemmParams& p, f32x4 (&acc)[4][4], int m0, int n0, int wm0, int wn0,
+template <int EPI, int SMEM, int TN = 4>
+__device__ __forceinline__ void a8_epilogue(const GemmParams& p, f32x4 (&acc)[4][TN], int m0, int n0, int wm0, int wn0,
                                             int tid, char* smem) {
+    static_assert(EPI != EPI_QKV_PREP || TN == 4, "the prep epilogue takes whole 128-column heads");
     const int lane = tid & 63, g = lane >> 4, c = lane & 15;
     const GemmEpilogue& e = p.e;
     if constexpr (EPI == EPI_QKV_PREP) {
-        qkv_prep_tile<A8_BM, 4, 4, 4, SMEM>(p, acc, m0, n0, wm0, wn0, tid, smem);
+        qkv_prep_tile<A8_BM, 4, 4, TN, SMEM>(p, acc, m0, n0, wm0, wn0, tid, smem);
     } else if constexpr (EPI == EPI_SWIGLU_F32) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -260,7 +261,7 @@ __device__ __forceinline__ void a8_epilogue(const GemmParams& p, f32x4 (&acc)[4]
                 const int m = m0 + wm0 + i * 16 + 4 * g + r;
                 if (m >= p.M) continue;
 #pragma unroll
-                for (int j = 0; j < 4; j += 2) {
+                for (int j = 0; j < TN; j += 2) {
                     const int n = n0 + wn0 + j * 16;  // gate columns n .. n + 15, up columns n + 16 .. n + 31
                     e.c_f32[(int64_t)m * e.ldc + (n >> 1) + c] = rn_mul(silu_f(acc[i][j][r]), acc[i][j + 1][r]);
                 }
@@ -269,7 +270,7 @@ __device__ __forceinline__ void a8_epilogue(const GemmParams& p, f32x4 (&acc)[4]
         if constexpr (EPI == EPI_RESID || EPI == EPI_RESID_GATED) {
             if (e.bias) {  // x + (W x_a + b): the bias joins the product before the residual add
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
+                for (int j = 0; j < TN; ++j) {
                     const float bj = e.bias[n0 + wn0 + j * 16 + c];
 #pragma unroll
                     for (int i = 0; i < 4; ++i)
@@ -278,7 +279,7 @@ __device__ __forceinline__ void a8_epilogue(const GemmParams& p, f32x4 (&acc)[4]
                 }
             }
         }
-        gemm_epilogue<4, 4, false, EPI, 1024>(p, acc, m0 + wm0, n0 + wn0, lane);
+        gemm_epilogue<4, TN, false, EPI, 1024>(p, acc, m0 + wm0, n0 + wn0, lane);
     }
 }
 
@@ -423,7 +424,7 @@ __global__ void __launch_bounds__(256) gemm_a8_kernel(A8Params p) {
 // reads as inline asm with one counted vmcnt (block 1's fragments read under block 0's MFMAs), two workgroups per CU.
 // Per block and 16 x 16 tile: one MFMA
 // and, per output, one multiply (d_w * d_a) and one FMA.
-constexpr int A8S_STAGE = (A8_BM + A8_BN) * 128;  // A and W k-tiles, 128-byte rows (two buffers)
+constexpr int A8S_STAGE = (A8_BM + A8_BN) * 128;  // A and W k-tiles, 128-byte rows (two buffers; BN = 64 uses less)
 constexpr int A8S_SC = 2 * A8_BM * 4 + A8_BN * 2 * 4;  // d_a [2][BM] + d_w [BN][2] of one k-tile (a three-slot ring)
 constexpr int A8S_DA = 0, A8S_DW = 2 * A8_BM * 4;
 constexpr int A8S_SMEM = 2 * A8S_STAGE + 3 * A8S_SC;  // 71 680 B: two workgroups per CU
@@ -446,42 +447,47 @@ __device__ __forceinline__ uint2 ds_read_b64_off(uint32_t addr) {
     return make_uint2(v[0], v[1]);
 }
 
-template <int EPI>
+// BN = 128 (2 x 2 waves of 64 x 64) or 64 (waves of 64 x 32: grids that a 128-wide tile leaves under one round of two
+// workgroups per CU, e.g. the N = 2048 projections at M = 3000: 384 tiles for 512 slots)
+template <int EPI, int BN = 128>
 __global__ void __launch_bounds__(256, 2) gemm_a8s_kernel(A8SParams p) {
-    constexpr int TM = 4, TN = 4, BK = 64, ROWB = 128;
-    constexpr int G_AW = (A8_BM + A8_BN) / 8 / 4;  // 1 KiB A / W pieces per wave per k-tile
+    constexpr int TM = 4, TN = BN / 32, BK = 64, ROWB = 128;
+    constexpr int GA = A8_BM / 32, GW = BN / 32;  // 1 KiB A / W pieces per wave per k-tile
+    constexpr int G_AW = GA + GW;
     constexpr int G = G_AW + 2;                    // + one d_a and one d_w dword piece
+    constexpr int STAGE = (A8_BM + BN) * ROWB;
     __shared__ __attribute__((aligned(16))) char smem[A8S_SMEM];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int M = p.g.M, K = p.g.K;
     const int nb = K >> 5, nk = K / BK;
     int m0, n0;
-    block_tile<A8_BM, A8_BN>(p.g, m0, n0);
-    const int wm0 = (wid >> 1) * 64, wn0 = (wid & 1) * 64;
+    block_tile<A8_BM, BN>(p.g, m0, n0);
+    const int wm0 = (wid >> 1) * 64, wn0 = (wid & 1) * (BN / 2);
     const int g = lane >> 4, c = lane & 15;
 
     // LDS-DMA sources as 32-bit element offsets (pieces j < G_AW / 2 are A rows, the rest W rows): 64-bit pointers
     // cost the registers that keep this kernel at two workgroups per CU without scratch
-    static_assert(G_AW % 2 == 0 && (G_AW / 2) * 4 * 8 == A8_BM, "A / W piece split");
     int src[G_AW];
 #pragma unroll
     for (int j = 0; j < G_AW; ++j) {
         const int row = (wid + 4 * j) * 8 + (lane >> 3);
         const int ch = (lane & 7) ^ swz(row);
-        src[j] = j < G_AW / 2 ? min(m0 + row, M - 1) * K + ch * 8 : (n0 + row - A8_BM) * K + ch * 8;
+        src[j] = j < GA ? min(m0 + row, M - 1) * K + ch * 8 : (n0 + row - A8_BM) * K + ch * 8;
     }
     // scale pieces: element e = 64 wid + lane of d_a [2][BM] (block e / BM, row e % BM; rows past M read the zero-padded
-    // plane, ld_s >= M rounded up to 128) and of d_w [BN][2] (column e / 2, block e % 2)
+    // plane, ld_s >= M rounded up to 128) and of d_w [BN][2] (column e / 2, block e % 2; BN = 64: waves 2, 3 re-read
+    // column BN - 1 into the unused half of the slot's d_w region)
     const int e = 64 * wid + lane;
     const float* sa = p.as + (int64_t)(e / A8_BM) * p.ld_s + m0 + e % A8_BM;
-    const float* sw = p.ws + (int64_t)(n0 + (e >> 1)) * nb + (e & 1);
+    const int ew = min(e, 2 * BN - 1);
+    const float* sw = p.ws + (int64_t)(n0 + (ew >> 1)) * nb + (ew & 1);
     auto stage = [&](int buf, int kt) {
-        char* base = smem + buf * A8S_STAGE;
+        char* base = smem + buf * STAGE;
 #pragma unroll
         for (int j = 0; j < G_AW; ++j)
-            __builtin_amdgcn_global_load_lds((const void*)((j < G_AW / 2 ? p.a : p.w) + (src[j] + kt * BK)),
+            __builtin_amdgcn_global_load_lds((const void*)((j < GA ? p.a : p.w) + (src[j] + kt * BK)),
                                              (lds_void*)(base + (wid + 4 * j) * 1024), 16, 0, 0);
-        char* sc = smem + 2 * A8S_STAGE + (kt % 3) * A8S_SC;
+        char* sc = smem + 2 * STAGE + (kt % 3) * A8S_SC;
         __builtin_amdgcn_global_load_lds((const void*)(sa + (int64_t)(2 * kt) * p.ld_s), (lds_void*)(sc + A8S_DA + wid * 256),
                                          4, 0, 0);
         __builtin_amdgcn_global_load_lds((const void*)(sw + 2 * kt), (lds_void*)(sc + A8S_DW + wid * 256), 4, 0, 0);
@@ -500,7 +506,7 @@ __global__ void __launch_bounds__(256, 2) gemm_a8s_kernel(A8SParams p) {
     uint2 dw[TN];        // d_w of this lane's column of each 16-column tile, both blocks
     auto read_frags = [&](int buf, auto kk_c) {
         constexpr int kk = decltype(kk_c)::value;
-        const uint32_t sbase = lds0 + buf * A8S_STAGE;
+        const uint32_t sbase = lds0 + buf * STAGE;
         const int ch = (kk * 4 + lchunk) ^ ((lrow >> 1) & 7);
         const uint32_t bb = sbase + A8_BM * ROWB + (wn0 + lrow) * ROWB + ch * 16;
         const uint32_t ab = sbase + (wm0 + lrow) * ROWB + ch * 16;
@@ -514,15 +520,15 @@ __global__ void __launch_bounds__(256, 2) gemm_a8s_kernel(A8SParams p) {
         });
     };
     auto read_dw = [&](int kt) {
-        const uint32_t dwb = lds0 + 2 * A8S_STAGE + (kt % 3) * A8S_SC + A8S_DW + (wn0 + c) * 8;
-        dw[0] = ds_read_b64_off<0 * 128>(dwb);
-        dw[1] = ds_read_b64_off<1 * 128>(dwb);
-        dw[2] = ds_read_b64_off<2 * 128>(dwb);
-        dw[3] = ds_read_b64_off<3 * 128>(dwb);
+        const uint32_t dwb = lds0 + 2 * STAGE + (kt % 3) * A8S_SC + A8S_DW + (wn0 + c) * 8;
+        static_for<0, TN>([&](auto j_c) {
+            constexpr int j = decltype(j_c)::value;
+            dw[j] = ds_read_b64_off<j * 128>(dwb);
+        });
     };
     auto read_da = [&](int kt, auto kk_c) {
         constexpr int kk = decltype(kk_c)::value;
-        const uint32_t dab = lds0 + 2 * A8S_STAGE + (kt % 3) * A8S_SC + A8S_DA + (kk * A8_BM + wm0 + 4 * g) * 4;
+        const uint32_t dab = lds0 + 2 * STAGE + (kt % 3) * A8S_SC + A8S_DA + (kk * A8_BM + wm0 + 4 * g) * 4;
         da[kk][0] = ds_read_b128_off<0 * 64>(dab);
         da[kk][1] = ds_read_b128_off<1 * 64>(dab);
         da[kk][2] = ds_read_b128_off<2 * 64>(dab);
@@ -594,12 +600,29 @@ __global__ void __launch_bounds__(256, 2) gemm_a8s_kernel(A8SParams p) {
         __builtin_amdgcn_s_barrier();  // every wave is done with buffer `cur` and scale slot kt % 3
         if (kt + 2 < nk) stage(cur, kt + 2);
     }
-    a8_epilogue<EPI, A8S_SMEM>(p.g, acc, m0, n0, wm0, wn0, tid, smem);
+    a8_epilogue<EPI, A8S_SMEM, TN>(p.g, acc, m0, n0, wm0, wn0, tid, smem);
 }
 
 template <int EPI>
-void launch_a8s_epi(const A8SParams& p, dim3 grid, hipStream_t s) {
-    hipLaunchKernelGGL((gemm_a8s_kernel<EPI>), grid, dim3(256), 0, s, p);
+void launch_a8s_epi(const A8SParams& p, hipStream_t s) {
+    const int nbm = (p.g.M + A8_BM - 1) / A8_BM;
+    // a 128-wide tile grid under half a round of two workgroups per CU takes the 64-wide tile (twice the tiles, each
+    // half the work); the prep epilogue needs whole 128-column heads.  Measured (tools/qact_bench.py, 240 s): the
+    // N = 2048 projections (384 tiles of 128 for 512 slots) are slower on 64-wide tiles (o 80 -> 86 us, down 214 ->
+    // 227), the small grids faster (proj_out 64 -> 48, condition 50 -> 38): hence half a round, not one.
+    static int n_cu = 0;
+    if (n_cu == 0) {
+        int dev = 0;
+        ACEMI_HIP(hipGetDevice(&dev));
+        ACEMI_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    if constexpr (EPI != EPI_QKV_PREP) {
+        if ((int64_t)nbm * (p.g.N / 128) < n_cu && p.g.N % 64 == 0) {
+            hipLaunchKernelGGL((gemm_a8s_kernel<EPI, 64>), dim3(nbm * (p.g.N / 64)), dim3(256), 0, s, p);
+            return;
+        }
+    }
+    hipLaunchKernelGGL((gemm_a8s_kernel<EPI, 128>), dim3(nbm * (p.g.N / 128)), dim3(256), 0, s, p);
 }
 
 // int8 plane -> its bf16 image (exact integers), 16 values per thread
@@ -689,16 +712,15 @@ void launch_gemm_a8(const QAct& a, const WeightView& W, int M, int N, int K, con
         p.as = a.s;
         p.ld_s = a.ld_s;
         p.ws = W.s;
-        const dim3 grid((unsigned)(((M + A8_BM - 1) / A8_BM) * (N / A8_BN)));
         switch (epi.kind) {
-            case EPI_STORE_F32: launch_a8s_epi<EPI_STORE_F32>(p, grid, s); break;
-            case EPI_STORE_ACT: launch_a8s_epi<EPI_STORE_ACT>(p, grid, s); break;
-            case EPI_RESID_GATED: launch_a8s_epi<EPI_RESID_GATED>(p, grid, s); break;
-            case EPI_RESID: launch_a8s_epi<EPI_RESID>(p, grid, s); break;
-            case EPI_SWIGLU: launch_a8s_epi<EPI_SWIGLU>(p, grid, s); break;
-            case EPI_PROJ_OUT: launch_a8s_epi<EPI_PROJ_OUT>(p, grid, s); break;
-            case EPI_QKV_PREP: launch_a8s_epi<EPI_QKV_PREP>(p, grid, s); break;
-            case EPI_SWIGLU_F32: launch_a8s_epi<EPI_SWIGLU_F32>(p, grid, s); break;
+            case EPI_STORE_F32: launch_a8s_epi<EPI_STORE_F32>(p, s); break;
+            case EPI_STORE_ACT: launch_a8s_epi<EPI_STORE_ACT>(p, s); break;
+            case EPI_RESID_GATED: launch_a8s_epi<EPI_RESID_GATED>(p, s); break;
+            case EPI_RESID: launch_a8s_epi<EPI_RESID>(p, s); break;
+            case EPI_SWIGLU: launch_a8s_epi<EPI_SWIGLU>(p, s); break;
+            case EPI_PROJ_OUT: launch_a8s_epi<EPI_PROJ_OUT>(p, s); break;
+            case EPI_QKV_PREP: launch_a8s_epi<EPI_QKV_PREP>(p, s); break;
+            case EPI_SWIGLU_F32: launch_a8s_epi<EPI_SWIGLU_F32>(p, s); break;
             default: throw std::runtime_error("gemm_a8: unknown epilogue");
         }
         ACEMI_HIP(hipGetLastError());

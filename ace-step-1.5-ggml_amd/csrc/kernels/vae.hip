@@ -242,85 +242,6 @@ __global__ void __launch_bounds__(256, 2) conv_gemm_kernel(ConvGemmArgs p) {
         }
     }
 
-    const float* bias_e = FUSE2 ? p.bias2 : p.bias;
-
-    // Epilogue through LDS: the bias-added tile goes to LDS as f32 [BM][BN] (64 KB = both stage buffers), then
-    // every wave sweeps two whole tile rows per instruction (lane = 4 consecutive columns), so the residual read,
-    // the f32 store and the fp16 Snake store are 16 / 16 / 8-byte accesses over 512 contiguous bytes of a row.
-    // (From the accumulator layout each wave instruction touched 4 rows x 64 B, with 4-byte accesses; at 128
-    // channels the read-modify-write of x cost as much as the MFMAs.)  Same arithmetic per element: acc + bias,
-    // then x + that, then the Snake of the sum.
-    static_assert(BM * BN * 4 <= 2 * STAGE, "epilogue tile must fit the stage buffers");
-    float* zt = reinterpret_cast<float*>(smem);
-    const int c4 = (lane & 31) * 4;
-    const int n = n0 + c4;
-    const int rr = p.up > 1 ? n / p.Cout : 0;
-    const int co = n - rr * p.Cout;
-    constexpr int RPI = NW * 2;  // tile rows per sweep iteration
-    constexpr int NIT = BM / RPI;
-    // output offset of sweep iteration `it` (this lane's 4 columns), or -1 outside the sequence / the crop
-    // (branch-free: the residual loads below are issued unconditionally from a clamped offset -- behind a branch,
-    // hipcc waited for every earlier load before the next one)
-    auto out_off = [&](int it) -> int64_t {
-        const int m = m0 + it * RPI + wid * 2 + (lane >> 5);
-        const int item = m / Mi, ml = m - item * Mi;
-        const int u = p.up > 1 ? ml * p.up + rr - p.crop : ml;
-        const bool ok = m < mlim && u >= 0 && u < p.T_out;
-        return ok ? ((int64_t)item * p.T_out + u) * p.Cout + co : (int64_t)-1;
-    };
-    // per-column bias and Snake parameters first: a wait for any load issued after the residual loads below would
-    // also wait for those (vmcnt retires in issue order)
-    const int ccol = lane & 15, crow = (lane >> 4) * 4;
-    float bz[TN];
-    float ea[4], reb[4];
-    float4 xo[NIT];
-    // the epilogue's loads: per-column bias / Snake parameters, then the residual's old values of the whole sweep.  The
-    // fused residual unit issues them before its k1 MFMAs, so they land under those and not after them (round 6); the
-    // plain convs issue them right before the tile goes through LDS.
-    // (the fused unit issues the first NE sweep iterations' residual loads early and the rest at the epilogue: all 16
-    // early need 64 more registers than its k1 phase has free)
-#ifndef ACEMI_VAE_EARLY_X
-#define ACEMI_VAE_EARLY_X 1  // (0: A/B builds only -- every residual load at the epilogue, the round-5 schedule)
-#endif
-    constexpr int NE = FUSE2 ? (ACEMI_VAE_EARLY_X ? NIT / 2 : 0) : NIT;
-    auto epi_loads_late = [&]() {
-        const float* xsrc = p.resid ? p.X : reinterpret_cast<const float*>(p.zero);
-#pragma unroll
-        for (int it = NE; it < NIT; ++it) {
-            const int64_t o = out_off(it);
-            xo[it] = *reinterpret_cast<const float4*>(xsrc + (p.resid && o >= 0 ? o : 0));
-        }
-    };
-    auto epi_loads = [&]() {
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            int cz = n0 + wn0 + j * 16 + ccol;
-            if (p.up > 1) cz -= (cz / p.Cout) * p.Cout;
-            bz[j] = bias_e ? bias_e[cz] : 0.f;
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            ea[e] = p.snake_ea ? p.snake_ea[co + e] : 0.f;
-            reb[e] = p.snake_eb ? __builtin_amdgcn_rcpf(p.snake_eb[co + e]) : 0.f;
-        }
-        // the residual's old values for the whole sweep are requested here, before the tile goes through LDS, so one
-        // HBM round trip (under the z writes and the barriers) replaces one per group of iterations
-        // (no resid: the loads read the zero buffer -- a branch around them made hipcc wait vmcnt(0) at the first use
-        // of the bias loads, i.e. for all of them)
-        // (the asm uses make hipcc retire the bias / Snake loads here: its wait at their first later use was vmcnt(0),
-        // i.e. for every residual load too)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(bz[j]));
-#pragma unroll
-        for (int e = 0; e < 4; ++e) asm volatile("" ::"v"(ea[e]), "v"(reb[e]));
-        __builtin_amdgcn_sched_barrier(0);
-        const float* xsrc = p.resid ? p.X : reinterpret_cast<const float*>(p.zero);
-#pragma unroll
-        for (int it = 0; it < NE; ++it) {
-            const int64_t o = out_off(it);
-            xo[it] = *reinterpret_cast<const float4*>(xsrc + (p.resid && o >= 0 ? o : 0));
-        }
-    };
     if constexpr (FUSE2) {
         // k1 conv of the residual unit on this tile (N = Cout = 128: the tile holds every channel).
         // W2 fragments straight from global memory (32 KB, L2-resident), issued before the LDS round trip.
@@ -353,7 +274,6 @@ __global__ void __launch_bounds__(256, 2) conv_gemm_kernel(ConvGemmArgs p) {
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __syncthreads();
-        epi_loads();  // (the k7 accumulators are dead here: room for the 64 residual registers without scratch)
         const uint32_t y0 = lds_addr(ytile);
 #pragma unroll
         for (int i = 0; i < TM; ++i)
@@ -378,8 +298,66 @@ __global__ void __launch_bounds__(256, 2) conv_gemm_kernel(ConvGemmArgs p) {
         }
         (void)y0;
     }
-    if constexpr (!FUSE2) epi_loads();
-    epi_loads_late();
+    const float* bias_e = FUSE2 ? p.bias2 : p.bias;
+
+    // Epilogue through LDS: the bias-added tile goes to LDS as f32 [BM][BN] (64 KB = both stage buffers), then
+    // every wave sweeps two whole tile rows per instruction (lane = 4 consecutive columns), so the residual read,
+    // the f32 store and the fp16 Snake store are 16 / 16 / 8-byte accesses over 512 contiguous bytes of a row.
+    // (From the accumulator layout each wave instruction touched 4 rows x 64 B, with 4-byte accesses; at 128
+    // channels the read-modify-write of x cost as much as the MFMAs.)  Same arithmetic per element: acc + bias,
+    // then x + that, then the Snake of the sum.
+    static_assert(BM * BN * 4 <= 2 * STAGE, "epilogue tile must fit the stage buffers");
+    float* zt = reinterpret_cast<float*>(smem);
+    const int c4 = (lane & 31) * 4;
+    const int n = n0 + c4;
+    const int rr = p.up > 1 ? n / p.Cout : 0;
+    const int co = n - rr * p.Cout;
+    constexpr int RPI = NW * 2;  // tile rows per sweep iteration
+    constexpr int NIT = BM / RPI;
+    // output offset of sweep iteration `it` (this lane's 4 columns), or -1 outside the sequence / the crop
+    // (branch-free: the residual loads below are issued unconditionally from a clamped offset -- behind a branch,
+    // hipcc waited for every earlier load before the next one)
+    auto out_off = [&](int it) -> int64_t {
+        const int m = m0 + it * RPI + wid * 2 + (lane >> 5);
+        const int item = m / Mi, ml = m - item * Mi;
+        const int u = p.up > 1 ? ml * p.up + rr - p.crop : ml;
+        const bool ok = m < mlim && u >= 0 && u < p.T_out;
+        return ok ? ((int64_t)item * p.T_out + u) * p.Cout + co : (int64_t)-1;
+    };
+    // per-column bias and Snake parameters first: a wait for any load issued after the residual loads below would
+    // also wait for those (vmcnt retires in issue order)
+    const int ccol = lane & 15, crow = (lane >> 4) * 4;
+    float bz[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        int cz = n0 + wn0 + j * 16 + ccol;
+        if (p.up > 1) cz -= (cz / p.Cout) * p.Cout;
+        bz[j] = bias_e ? bias_e[cz] : 0.f;
+    }
+    float ea[4], reb[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        ea[e] = p.snake_ea ? p.snake_ea[co + e] : 0.f;
+        reb[e] = p.snake_eb ? __builtin_amdgcn_rcpf(p.snake_eb[co + e]) : 0.f;
+    }
+    // the residual's old values for the whole sweep are requested here, before the tile goes through LDS, so one
+    // HBM round trip (under the z writes and the barriers) replaces one per group of iterations
+    // (no resid: the loads read the zero buffer -- a branch around them made hipcc wait vmcnt(0) at the first use
+    // of the bias loads, i.e. for all of them)
+    // (the asm uses make hipcc retire the bias / Snake loads here: its wait at their first later use was vmcnt(0),
+    // i.e. for every residual load too)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(bz[j]));
+#pragma unroll
+    for (int e = 0; e < 4; ++e) asm volatile("" ::"v"(ea[e]), "v"(reb[e]));
+    __builtin_amdgcn_sched_barrier(0);
+    const float* xsrc = p.resid ? p.X : reinterpret_cast<const float*>(p.zero);
+    float4 xo[NIT];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+        const int64_t o = out_off(it);
+        xo[it] = *reinterpret_cast<const float4*>(xsrc + (p.resid && o >= 0 ? o : 0));
+    }
     __builtin_amdgcn_sched_barrier(0);
     {
         __builtin_amdgcn_s_barrier();  // every wave is done with the stage buffers / the fused conv's y tile

@@ -69,12 +69,14 @@ def test_gemm_a8_matches_block_integer_dot(qtype, M, N, K):
     assert np.all(err <= 5e-6 * mag + 1e-30), float(np.max(err / (mag + 1e-30)))
 
 
-@pytest.mark.parametrize("M,N,K", [(1, 128, 64), (77, 256, 128), (129, 384, 2048), (300, 128, 6144), (3000, 2048, 2048)])
+@pytest.mark.parametrize("M,N,K", [(1, 128, 64), (77, 256, 128), (129, 384, 2048), (300, 128, 6144), (3000, 2048, 2048),
+                                   (2048, 8192, 128)])
 @pytest.mark.parametrize("epi", [0, 3, 7])
 def test_gemm_a8_bf16_mfma_form_is_bit_identical(M, N, K, epi):
     """Q8_0 on the bf16 MFMA (gemm_a8s_kernel: each block's integer dot is exact in f32 from bf16(q) operands, the
     default for K % 64 == 0) against the i8-MFMA kernel: the same integer dots, scales and f32 order -> the same bits,
-    with every epilogue the comparison covers."""
+    with every epilogue the comparison covers; both tile widths (128 for grids of >= one round of two workgroups per
+    CU, e.g. 2048 x 8192; 64 below that)."""
     capi = _capi()
     rng = np.random.default_rng(M + N + K + epi)
     x = rng.standard_normal((M, K)).astype(np.float32)
