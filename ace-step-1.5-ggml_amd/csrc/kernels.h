@@ -175,7 +175,7 @@ struct AttnArgs {
     int split_from = 0;  // set by launch_attention: > 0 = tail split (blocks [0, split_from) whole, the rest in two
                          // key-range parts; ksplit = 2 gives the partials' layout)
     // f32 output [B*nq][Hq*128] instead of `out` (the ggml-faithful quantized-activation mode, whose next linear
-    // quantizes the f32 rows): every block runs as two key-range parts (needs `part`), merged into f32
+    // quantizes the f32 rows), under the same key-split policy: whole blocks and the merges write f32 rows
     float* out_f32 = nullptr;
     bool f8 = false;  // f8c mode (needs split + pv_split): the lo planes hold fp8 hi / lo operands (prep_math.h), the
                       // correction products Kl.Qh + Kh.Ql and Vl.Ph + Vh.Pl run as block-scaled fp8 MFMAs

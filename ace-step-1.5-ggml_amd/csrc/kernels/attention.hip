@@ -757,6 +757,19 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
         return;
     }
     const float inv = 1.0f / l;
+    if (a.out_f32) {  // f32 rows (the quantized-activation mode: the next linear quantizes them)
+        if (qrow < a.nq) {
+            float* of = a.out_f32 + ((int64_t)b * a.nq + qrow) * (a.Hq * D) + head * D;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int g4 = 0; g4 < 4; ++g4)
+                    *(float4*)(of + 32 * dt + 8 * g4 + 4 * h) =
+                        make_float4(o[dt][4 * g4 + 0] * inv, o[dt][4 * g4 + 1] * inv, o[dt][4 * g4 + 2] * inv,
+                                    o[dt][4 * g4 + 3] * inv);
+        }
+        return;
+    }
     if (qrow < a.nq) {
         uint16_t* op = a.out + ((int64_t)b * a.nq + qrow) * (a.Hq * D) + head * D;
 #pragma unroll
@@ -932,11 +945,9 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s) {
         // trip and a ticket, no merge launch: neutral at 60 s, 4 % slower lines at 240 s, profiles/r05/attn_fused_merge.txt;
         // removed from the product library in round 6)
     }
-    if (a.out_f32) {  // f32 output: every block in two key-range parts, merged into f32 rows
-        ACEMI_CHECK(a.part != nullptr, "attention: f32 output needs the partials workspace");
-        b.ksplit = 2;
-        b.split_from = 0;
-    }
+    // (f32 output, AttnArgs::out_f32: the same split policy -- whole blocks write f32 rows themselves, the merges
+    // below write f32 rows; until round 6 every block ran in two key-range parts with a full merge, 0.84 ms per 240 s
+    // step of the quantized-activation mode)
     const int64_t n_blk = (int64_t)a.B * a.Hkv * n_qt;
     // XCD-aware order (attn_block): whole multiples of 8 launch indices per range
     const dim3 grid(b.split_from > 0 ? (unsigned)(b.split_from + 8 * ((2 * (n_blk - b.split_from) + 7) / 8))
@@ -963,7 +974,13 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s) {
         ACEMI_CHECK(b.ksplit == 2 || b.ksplit == 4, "attention: the merge handles 2 or 4 key-split parts");
         const dim3 mgrid((unsigned)((rows + 7) / 8));
         if (a.out_f32) {
-            hipLaunchKernelGGL((attn_merge_kernel<false, 2, false, true>), mgrid, dim3(256), 0, s, b);
+            if (b.split_from > 0)
+                hipLaunchKernelGGL((attn_merge_kernel<false, 2, true, true>), dim3((unsigned)((n_blk - b.split_from) * 16)),
+                                   dim3(256), 0, s, b);
+            else if (b.ksplit == 2)
+                hipLaunchKernelGGL((attn_merge_kernel<false, 2, false, true>), mgrid, dim3(256), 0, s, b);
+            else
+                hipLaunchKernelGGL((attn_merge_kernel<false, 4, false, true>), mgrid, dim3(256), 0, s, b);
         } else if (b.split_from > 0) {
             const dim3 tgrid((unsigned)((n_blk - b.split_from) * 16));  // 128 rows per split block, 8 per workgroup
             if (out_t == ActType::F16)
