@@ -788,6 +788,536 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// attn_kh_kernel (round 6): the f8c mode at two waves per SIMD.  attn2 holds a whole 64-key tile's scores and P
+// operands, both ring stages and the Q planes in one wave (312 registers, so one wave per SIMD; its per-tile stream is
+// dependency-bound at ~2.2x its MFMA time).  Here a workgroup of 8 waves runs the same block (item, kv
+// head, 128 query rows) over the same LDS rings: wave w = 4 kh + wq takes query group wq's 32 rows against key half kh
+// (keys [32 kh, 32 kh + 32)) of every tile -- exactly attn2's half t = kh -- with its own online softmax, and the two
+// halves of a row meet once after the key loop, through LDS (the key-split merge's combination).  Per wave and tile:
+//   S^T half   8 fp16 hi MFMAs + 4 block-scaled e4m3 corrections (Kl.Qh, Kh.Ql over D = 128), one accumulator;
+//   O^T        8 fp16 hi MFMAs + 4 e4m3 MFMAs, each carrying BOTH P.V corrections of one d-tile in one K = 64 product:
+//              lanes 0-31 (K block 0) hold Vl x Ph with E8M0 scale 2^-11, lanes 32-63 (K block 1) Vh x Pl with scale 1
+//              -- the MFMA's block scale is per lane, i.e. per 32-element K block -- after one permlane32_swap per P
+//              word regroups [Ph | Pl] of the lane halves into [Ph (all 32 keys) ; Pl (all 32 keys)].
+// The same MFMA cycles per key as attn2, at <= 256 registers: the partner wave on the SIMD runs while one waits.
+// Pipeline, DMA ring and masks as attn2 (phase B: S(i+1) || softmax finish of i; phase C: O += V(i) P(i) || softmax
+// start of i+1), with 4 K + 4 V^T LDS-DMA pieces per wave and tile.
+template <bool F16OUT, bool KBIAS>
+__global__ void __launch_bounds__(512) attn_kh_kernel(AttnArgs a) {
+    using RG = Ring<true, true>;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int kh = wid >> 2, wq = wid & 3;
+    const int h = lane >> 5;
+    const int lq = lane & 31;
+
+    const int rep = a.Hq / a.Hkv;
+    const int qpb = 128 / rep;
+    const int n_qt = (a.nq + qpb - 1) / qpb;
+    int bid, split, ks;
+    if (!attn_block(a, a.B * a.Hkv * n_qt, bid, split, ks)) return;
+    const int qt = bid % n_qt;
+    bid /= n_qt;
+    const int kvh = bid % a.Hkv;
+    const int b = bid / a.Hkv;
+    const int waves_per_head = 4 / rep;
+    const int head = kvh * rep + wq / waves_per_head;
+    const int q0 = qt * qpb;
+    const int qrow = q0 + (wq % waves_per_head) * 32 + lq;
+
+    int klo = 0, khi = a.nk;
+    if (a.window > 0) {
+        klo = max(0, q0 - a.window);
+        khi = min(a.nk, q0 + qpb - 1 + a.window + 1);
+    }
+    if (a.causal) khi = min(khi, q0 + qpb);
+    const int n_all = max(0, (khi + KT - 1) / KT - klo / KT);
+    const int chunk = (n_all + ks - 1) / ks;
+    const int kt_begin = klo / KT + split * chunk;
+    const int n = max(0, min(chunk, n_all - split * chunk));
+
+    int lo_abs = 0, hi_abs = a.nk;
+    if (a.window > 0) {
+        lo_abs = max(lo_abs, qrow - a.window);
+        hi_abs = min(hi_abs, qrow + a.window + 1);
+    }
+    if (a.causal) hi_abs = min(hi_abs, qrow + 1);
+    lo_abs -= 4 * h;
+    hi_abs -= 4 * h;
+
+    const uint16_t* qptr = a.q + (((int64_t)b * a.Hq + head) * a.nq_pad + qrow) * D + 8 * h;
+    frag qf[8];
+    v8i q8[4];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) qf[j] = *(const frag*)(qptr + 16 * j);
+    {
+        const char* q8row = reinterpret_cast<const char*>(qptr - 8 * h + a.q_plane) + 32 * h;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) q8[c] = cat8(*(const frag*)(q8row + 64 * c), *(const frag*)(q8row + 64 * c + 16));
+    }
+
+    const uint16_t* kbase = a.k + ((int64_t)b * a.Hkv + kvh) * a.nk_pad * D;
+    const uint16_t* vbase = a.vt + ((int64_t)b * a.Hkv + kvh) * D * a.nk_pad;
+    const float* kb = KBIAS ? a.kbias + (int64_t)b * a.nk_pad : nullptr;
+
+    // LDS-DMA pieces (1 KiB per wave instruction): K piece p = hi / lo plane (p >= 2) rows 4 (wid + 8 (p & 1)) +
+    // lane / 16; V^T piece p = hi / lo plane (p >= 2) d-rows 8 (wid + 8 (p & 1)) + lane / 8; the key bias: wave 0
+    constexpr int NPK = 4, NPV = 4;
+    const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc((void*)kbase, 0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc((void*)vbase, 0, 0x7fffffff, 0x00020000);
+    const int krow = 4 * wid + (lane >> 4);
+    const int kvoff = krow * 256 + (((lane & 15) ^ (krow & 15)) << 4);
+    const int vrow = 8 * wid + (lane >> 3);
+    const int vvoff = vrow * a.nk_pad * 2 + (((lane & 7) ^ ((vrow >> 1) & 7)) << 4);
+    const int kplane_b = (int)(a.k_plane * 2), vplane_b = (int)(a.v_plane * 2);
+    auto k_piece = [&](int slot, int kt, int p) {
+        const int so = kt * (KT * D * 2) + (p & 1) * 8192 + (p >= 2 ? kplane_b : 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            krs, (lds_void*)(smem + slot * RG::KS + (p >= 2 ? RG::K_LO : RG::K_HI) + (wid + 8 * (p & 1)) * 1024), 16, kvoff,
+            so, 0, 0);
+    };
+    auto v_piece = [&](int slot, int kt, int p) {
+        const int so = kt * (KT * 2) + (p & 1) * (128 * a.nk_pad) + (p >= 2 ? vplane_b : 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            vrs, (lds_void*)(smem + RG::V0 + slot * RG::VS + (p >= 2 ? RG::V_LO : 0) + (wid + 8 * (p & 1)) * 1024), 16,
+            vvoff, so, 0, 0);
+    };
+    auto bias_piece = [&](int slot, int kt) {
+        if constexpr (KBIAS) {
+            if (wid == 0)
+                __builtin_amdgcn_global_load_lds((const void*)(kb + kt * KT + lane), (lds_void*)(smem + slot * RG::KS + RG::KB),
+                                                 4, 0, 0);
+        }
+    };
+
+    // fragment addresses (slot 0; the slot is an immediate offset): K hi row 32 kh + lq, k-slice j; its fp8 row
+    // [Kl8 | Kh8] chunks 4 c + 2 h + e; V^T hi d-row lq of d-tile 0, 16-key group 2 kh + g; the fp8 V^T row's
+    // correction chunks 4 h + 2 e + kh (lane half 0: Vl of the half's keys, lane half 1: Vh)
+    const uint32_t smem_l = lds_addr(smem);
+    const int cK = h ^ (lq & 15);
+    const int cV = h ^ ((lq >> 1) & 7);
+    uint32_t kaddr[8], k8a[4][2], vaddr[2], v8a[2];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) kaddr[j] = smem_l + RG::K_HI + (32 * kh + lq) * 256 + (((2 * j) ^ cK) << 4);
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+            k8a[c][e] = smem_l + RG::K_LO + (32 * kh + lq) * 256 + (((4 * c + 2 * h + e) ^ (lq & 15)) << 4);
+#pragma unroll
+    for (int g = 0; g < 2; ++g) vaddr[g] = smem_l + RG::V0 + lq * 128 + (((2 * (2 * kh + g)) ^ cV) << 4);
+#pragma unroll
+    for (int e = 0; e < 2; ++e) v8a[e] = smem_l + RG::V0 + RG::V_LO + lq * 128 + (((4 * h + 2 * e + kh) ^ ((lq >> 1) & 7)) << 4);
+    const uint32_t kbaddr = smem_l + RG::KB + 16 * h + 128 * kh;
+
+    const float c_log2 = a.scale * 1.4426950408889634f;
+    const float one_rt = a.scale / a.scale;  // exactly 1, opaque to the compiler (attn2's plo)
+
+    // Two waves per SIMD: no VALU or LDS read may write an A / B register of an MFMA that may still be waiting for the
+    // matrix pipe (tools/audit_mfma_war.py, --loads).  The first fragment of every step comes from a
+    // ring of RA + 3 slots, the second one of the correction steps (every third step) from a ring of 2; every step's
+    // fragments stay allocated to the end of the second step after it (the ring slots are only names: liveness is what
+    // keeps hipcc from giving a just-read operand register to a new value), a correction's concatenated operand to
+    // the next correction, and each phase ends with 16 wait states.
+    constexpr int RX = RA + 3;
+    auto keep = [](const frag& x) { asm volatile("" ::"v"(x)); };
+    auto keep8 = [](const v8i& x) { asm volatile("" ::"v"(x)); };
+
+    // phase B positions: p % 3 == 2 the correction c = p / 3 (two 16-byte reads), else the hi k-slice p - p / 3
+    constexpr int NB = 12;
+    auto k_read = [&](auto slot_c, auto p_c, frag& x, frag& y) {
+        constexpr int SLOT = decltype(slot_c)::value;
+        constexpr int p = decltype(p_c)::value;
+        if constexpr (p % 3 != 2) {
+            x = lds_frag<SLOT * RG::KS>(kaddr[p - p / 3]);
+        } else {
+            x = lds_frag<SLOT * RG::KS>(k8a[p / 3][0]);
+            y = lds_frag<SLOT * RG::KS>(k8a[p / 3][1]);
+        }
+    };
+    auto rk = [](int p) constexpr { return p % 3 == 2 ? 2 : 1; };
+    auto qk_phase = [&](auto slot_c, f32x16& sn, auto&& fin, auto&& dma) {
+        frag kx[RX], ky[2];
+        v8i kc;  // the last correction step's concatenated A operand (hipcc may copy the two fragments into it)
+        static_for<0, RA>([&](auto r_c) {
+            constexpr int r = decltype(r_c)::value;
+            k_read(slot_c, r_c, kx[r], ky[0]);
+        });
+        static_for<0, NB>([&](auto p_c) {
+            constexpr int p = decltype(p_c)::value;
+            if constexpr (p + RA < NB)
+                k_read(slot_c, std::integral_constant<int, p + RA>{}, kx[(p + RA) % RX], ky[((p + RA) / 3) % 2]);
+            constexpr int after = reads_after(p, NB, rk);
+            asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(after) : "memory");
+            asm volatile("" : "+v"(kx[p % RX]));
+            if constexpr (rk(p) == 2) asm volatile("" : "+v"(ky[(p / 3) % 2]));
+            if constexpr (p % 3 == 2) {
+                constexpr int c = p / 3;  // Kl.Qh (c = 0, 1: 2^-11 on A) + Kh.Ql (c = 2, 3: on B)
+                kc = cat8(kx[p % RX], ky[(p / 3) % 2]);
+                sn = mfma_f8(kc, q8[c], sn, c < 2 ? F8_SCALE_LO : F8_SCALE_1, c < 2 ? F8_SCALE_1 : F8_SCALE_LO);
+            } else {
+                constexpr int j = p - p / 3;
+                sn = j == 0 ? mfma32(kx[p % RX], qf[0], f32x16{}) : mfma32(kx[p % RX], qf[j], sn);
+            }
+            dma(p_c);
+            fin(p_c);
+            static_for<1, 3>([&](auto d_c) {  // the fragments of the two steps before stay allocated
+                constexpr int pd = p - decltype(d_c)::value;
+                if constexpr (pd >= 0) {
+                    keep(kx[pd % RX]);
+                    if constexpr (rk(pd) == 2) keep(ky[(pd / 3) % 2]);
+                }
+            });
+            if constexpr (p > 2) keep8(kc);
+            __builtin_amdgcn_sched_barrier(0);
+        });
+        asm volatile("" : "+v"(sn));  // (the phase's MFMAs stay above the wait states: IR passes sink the last ones)
+        asm volatile("s_nop 7\n\ts_nop 7");
+        keep(kx[(NB - 1) % RX]);
+        keep(kx[(NB - 2) % RX]);
+        keep(ky[((NB - 1) / 3) % 2]);
+        keep8(kc);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) keep(qf[j]);  // (the last iteration's phase B is their last use)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) keep8(q8[c]);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    float m_run = -INFINITY;
+    float l_run = 0.f;
+    f32x16 o[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
+
+    auto mask_tile = [&](f32x16& sn, int i) {
+        const int k0 = (kt_begin + i) * KT;
+        const int lo = lo_abs - k0, hi = hi_abs - k0;
+        if (__builtin_amdgcn_ballot_w64(lo > 32 * kh || hi < 32 * kh + 28) != 0) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int kr = 32 * kh + key_of(0, r);
+                sn[r] = (kr >= lo && kr < hi) ? sn[r] : -INFINITY;
+            }
+        }
+    };
+    auto bias_tile = [&](auto slot_c, f32x16& sn) {
+        if constexpr (KBIAS) {
+            constexpr int SLOT = decltype(slot_c)::value;
+            frag kbv[4];
+            static_for<0, 4>([&](auto j_c) {
+                constexpr int j = decltype(j_c)::value;
+                kbv[j] = lds_frag<SLOT * RG::KS + 32 * j>(kbaddr);
+            });
+            lds_wait_tie(kbv);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sn[r] = __builtin_fmaf(sn[r], c_log2, __uint_as_float(kbv[r >> 2][r & 3]));
+        }
+    };
+    auto finish_max = [&](float mraw) -> float {
+        const float mx = KBIAS ? mraw : (mraw == -INFINITY ? -INFINITY : mraw * c_log2);
+        return fmaxf(mx, __shfl_xor(mx, 32));
+    };
+    float alpha = 1.f;
+    bool rescale = false;
+    auto update_max = [&](float mloc) {
+        const bool move = mloc > m_run + RESCALE_LOG2;
+        alpha = move ? __builtin_amdgcn_exp2f(m_run - mloc) : 1.f;
+        m_run = move ? mloc : m_run;
+        rescale = __builtin_amdgcn_ballot_w64(move) != 0;
+    };
+    auto apply_rescale = [&]() {
+        if (rescale) {
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+            l_run *= alpha;
+        }
+    };
+
+    f32x16 sA, sB;
+    auto no_fin = [](auto) {};
+    auto no_dma = [](auto) {};
+    if (n > 0) {
+#pragma unroll
+        for (int p = 0; p < NPK; ++p) k_piece(0, kt_begin, p);
+        bias_piece(0, kt_begin);
+#pragma unroll
+        for (int p = 0; p < NPV; ++p) v_piece(0, kt_begin, p);
+        if (n > 1) {
+#pragma unroll
+            for (int p = 0; p < NPK; ++p) k_piece(1, kt_begin + 1, p);
+            bias_piece(1, kt_begin + 1);
+        }
+        wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        qk_phase(std::integral_constant<int, 0>{}, sA, no_fin, no_dma);
+        bias_tile(std::integral_constant<int, 0>{}, sA);
+        mask_tile(sA, 0);
+        float mr = -INFINITY;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mr = fmaxf(mr, sA[r]);
+        update_max(finish_max(mr));
+        apply_rescale();
+        __builtin_amdgcn_s_barrier();  // every wave has read K slot 0: iteration 0 restages it
+    }
+
+    auto iter = [&](auto slot_c, f32x16& sc, f32x16& sn, int i) {
+        constexpr int SLOT = decltype(slot_c)::value;
+        constexpr int NXT = SLOT ^ 1;
+        const bool more = i + 1 < n;
+        const int ktk = kt_begin + min(i + 2, n - 1), ktv = kt_begin + min(i + 1, n - 1);
+        const float m_use = ((m_run == -INFINITY) ? 0.f : m_run) - PSCALE_F8_LOG2;
+        const float nm = -m_use;
+        float lsum = 0.f;
+        frag pf[2];
+        uint32_t ph8[4] = {}, pl8[4] = {};  // fp8 P and P - f16(P): byte r = the lane's score r of the half
+        auto plo = [&](auto j_c) {
+            constexpr int j = decltype(j_c)::value;
+            constexpr int r = 2 * j;
+            constexpr int fi = r >> 3, fj = (r & 7) >> 1;
+            int w8 = (int)pl8[j >> 1];
+            typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+            const h2v hv = __builtin_bit_cast(h2v, (uint32_t)pf[fi][fj]);
+            const float l0 = __builtin_fmaf(-(float)hv[0], one_rt, sc[r]);
+            const float l1 = __builtin_fmaf(-(float)hv[1], one_rt, sc[r + 1]);
+            w8 = __builtin_amdgcn_cvt_pk_fp8_f32(l0 * 2048.f, l1 * 2048.f, w8, (j & 1) != 0);  // 2^11 (P - f16(P))
+            asm volatile("" : "+v"(w8));
+            pl8[j >> 1] = (uint32_t)w8;
+        };
+        // softmax finish of tile i: hi step j forms P pair j (scores 2j, 2j + 1); correction step c forms the lo
+        // parts of pairs 2c, 2c + 1 (formed by the two hi steps before it)
+        auto fin = [&](auto p_c) {
+            constexpr int p = decltype(p_c)::value;
+            if constexpr (p % 3 == 2) {
+                plo(std::integral_constant<int, 2 * (p / 3)>{});
+                plo(std::integral_constant<int, 2 * (p / 3) + 1>{});
+            } else {
+                constexpr int j = p - p / 3;
+                constexpr int r = 2 * j;
+                float p0, p1;
+                if constexpr (KBIAS) {
+                    p0 = __builtin_amdgcn_exp2f(sc[r] + nm);
+                    p1 = __builtin_amdgcn_exp2f(sc[r + 1] + nm);
+                } else {
+                    p0 = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[r], c_log2, nm));
+                    p1 = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[r + 1], c_log2, nm));
+                }
+                lsum += p0;
+                lsum += p1;
+                constexpr int fi = r >> 3, fj = (r & 7) >> 1;
+                typedef float f2 __attribute__((ext_vector_type(2)));
+                typedef _Float16 h2t __attribute__((ext_vector_type(2)));
+                const h2t hv = __builtin_convertvector((f2){p0, p1}, h2t);
+                uint32_t w = __builtin_bit_cast(uint32_t, hv);
+                int w8 = (int)ph8[j >> 1];
+                w8 = __builtin_amdgcn_cvt_pk_fp8_f32(p0, p1, w8, (j & 1) != 0);
+                asm volatile("" : "+v"(w), "+v"(w8), "+v"(lsum), "+v"(p0), "+v"(p1));
+                pf[fi][fj] = w;
+                ph8[j >> 1] = (uint32_t)w8;
+                sc[r] = p0;
+                sc[r + 1] = p1;
+            }
+        };
+        // K(i + 2) behind phase B's correction MFMAs (the bias with the first)
+        auto dma = [&](auto p_c) {
+            constexpr int p = decltype(p_c)::value;
+            if constexpr (p % 3 == 2) {
+                k_piece(SLOT, ktk, p / 3);
+                if constexpr (p == 2) bias_piece(SLOT, ktk);
+            }
+        };
+        qk_phase(std::integral_constant<int, NXT>{}, sn, [&](auto j_c) { fin(j_c); }, [&](auto j_c) { dma(j_c); });
+        l_run += lsum;
+
+        // V(i), requested in the previous iteration's phase C, landed for every wave
+        if (KBIAS && wid == 0)
+            wait_vmcnt<NPK + 1>();
+        else
+            wait_vmcnt<NPK>();
+        __builtin_amdgcn_s_barrier();
+        bias_tile(std::integral_constant<int, NXT>{}, sn);
+        mask_tile(sn, i + 1);
+        float mr = -INFINITY;
+        {
+            // phase C positions: q % 3 == 2 the correction of d-tile q / 3, else the hi step s = q - q / 3 (d-tile
+            // s & 3, 16-key group s >> 2 of the half)
+            constexpr int NC = 12;
+            uint32_t pb[8];  // [Ph ; Pl] of the half's 32 keys: lane half 0 the Ph bytes, lane half 1 the Pl bytes
+            frag vx[RX], vy[2];
+            v8i vc;
+            auto v_read = [&](auto q_c, frag& x, frag& y) {
+                constexpr int q = decltype(q_c)::value;
+                if constexpr (q % 3 != 2) {
+                    constexpr int s = q - q / 3;
+                    x = lds_frag<SLOT * RG::VS + (s & 3) * 32 * 128>(vaddr[s >> 2]);
+                } else {
+                    x = lds_frag<SLOT * RG::VS + (q / 3) * 32 * 128>(v8a[0]);
+                    y = lds_frag<SLOT * RG::VS + (q / 3) * 32 * 128>(v8a[1]);
+                }
+            };
+            auto rv = [](int q) constexpr { return q % 3 == 2 ? 2 : 1; };
+            static_for<0, RA>([&](auto r_c) {
+                constexpr int r = decltype(r_c)::value;
+                v_read(r_c, vx[r], vy[0]);
+            });
+            static_for<0, NC>([&](auto q_c) {
+                constexpr int q = decltype(q_c)::value;
+                if constexpr (q + RA < NC)
+                    v_read(std::integral_constant<int, q + RA>{}, vx[(q + RA) % RX], vy[((q + RA) / 3) % 2]);
+                if constexpr (q == 0) {
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) {
+                        const auto sw = __builtin_amdgcn_permlane32_swap(ph8[w], pl8[w], false, false);
+                        pb[w] = sw[0];
+                        pb[4 + w] = sw[1];
+                    }
+                }
+                constexpr int after = reads_after(q, NC, rv);
+                asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(after) : "memory");
+                asm volatile("" : "+v"(vx[q % RX]));
+                if constexpr (rv(q) == 2) asm volatile("" : "+v"(vy[(q / 3) % 2]));
+                if constexpr (q % 3 != 2) {
+                    constexpr int s = q - q / 3;
+                    o[s & 3] = mfma32(vx[q % RX], pf[s >> 2], o[s & 3]);
+                } else {
+                    constexpr int dt = q / 3;
+                    vc = cat8(vx[q % RX], vy[(q / 3) % 2]);
+                    o[dt] = mfma_f8(vc, cat8(pb), o[dt], F8_SCALE_LO, F8_SCALE_1);
+                }
+                if constexpr (q % 3 != 2) {
+                    constexpr int s = q - q / 3;
+                    mr = fmaxf(mr, fmaxf(sn[2 * s], sn[2 * s + 1]));
+                    asm volatile("" : "+v"(mr));
+                } else {
+                    v_piece(NXT, ktv, q / 3);  // V(i + 1) behind the correction MFMAs
+                }
+                static_for<1, 3>([&](auto d_c) {
+                    constexpr int qd = q - decltype(d_c)::value;
+                    if constexpr (qd >= 0) {
+                        keep(vx[qd % RX]);
+                        if constexpr (rv(qd) == 2) keep(vy[(qd / 3) % 2]);
+                    }
+                });
+                if constexpr (q > 2) keep8(vc);  // (phase C's hi steps are short: held until the next correction)
+                __builtin_amdgcn_sched_barrier(0);
+            });
+            // the P operands and the last fragments stay allocated through the retire (phase B rewrites pf / ph8 / pl8)
+            asm volatile("" : "+v"(o[0]), "+v"(o[1]), "+v"(o[2]), "+v"(o[3]));
+            asm volatile("s_nop 7\n\ts_nop 7");
+            keep(vx[(NC - 1) % RX]);
+            keep(vx[(NC - 2) % RX]);
+            keep(vy[((NC - 1) / 3) % 2]);
+            keep8(vc);
+            keep(pf[0]);
+            keep(pf[1]);
+#pragma unroll
+            for (int w = 0; w < 8; ++w) asm volatile("" ::"v"(pb[w]));
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        const float mnx = finish_max(mr);
+        if (more) {
+            update_max(mnx);
+            apply_rescale();
+            wait_vmcnt<NPV>();  // K(i + 2) landed (V(i + 1), issued after it, may stay in flight)
+            __builtin_amdgcn_s_barrier();
+        }
+    };
+
+    int i = 0;
+    for (; i + 1 < n; i += 2) {
+        iter(std::integral_constant<int, 0>{}, sA, sB, i);
+        iter(std::integral_constant<int, 1>{}, sB, sA, i + 1);
+    }
+    if (i < n) iter(std::integral_constant<int, 0>{}, sA, sB, i);
+    wait_vmcnt<0>();
+
+    // the two key halves of each row: half 1 hands (O, m, l) to half 0 through LDS (the rings are free after the
+    // barrier), half 0 combines them as the key-split merge does (weight 2^(m_k - M), 0 for a half with no key)
+    float l = l_run + __shfl_xor(l_run, 32);
+    __builtin_amdgcn_s_barrier();
+    float4* xch = reinterpret_cast<float4*>(smem) + wq * 17 * 64 + lane;
+    if (kh == 1) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+            xch[j * 64] = make_float4(o[j >> 2][4 * (j & 3)], o[j >> 2][4 * (j & 3) + 1], o[j >> 2][4 * (j & 3) + 2],
+                                      o[j >> 2][4 * (j & 3) + 3]);
+        xch[16 * 64] = make_float4(m_run, l, 0.f, 0.f);
+    }
+    __syncthreads();
+    if (kh == 1) return;
+    {
+        const float4 ml = xch[16 * 64];
+        const float M = fmaxf(m_run, ml.x);
+        const float w0 = m_run == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m_run - M);
+        const float w1 = ml.x == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(ml.x - M);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const float4 x = xch[j * 64];
+            f32x16& od = o[j >> 2];
+            const int r = 4 * (j & 3);
+            od[r] = od[r] * w0 + x.x * w1;
+            od[r + 1] = od[r + 1] * w0 + x.y * w1;
+            od[r + 2] = od[r + 2] * w0 + x.z * w1;
+            od[r + 3] = od[r + 3] * w0 + x.w * w1;
+        }
+        l = l * w0 + ml.y * w1;
+        m_run = M;
+    }
+    if (ks > 1) {
+        if (qrow < a.nq) {
+            const int64_t row = ((int64_t)split * a.B + b) * a.nq + qrow;
+            float* po = a.part + row * (a.Hq * D) + head * D;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int g4 = 0; g4 < 4; ++g4)
+                    *(float4*)(po + 32 * dt + 8 * g4 + 4 * h) =
+                        make_float4(o[dt][4 * g4 + 0], o[dt][4 * g4 + 1], o[dt][4 * g4 + 2], o[dt][4 * g4 + 3]);
+            if (h == 0)
+                *(float2*)(a.part + (int64_t)a.ksplit * a.B * a.nq * a.Hq * D + (row * a.Hq + head) * 2) =
+                    make_float2(m_run, l);
+        }
+        return;
+    }
+    const float inv = 1.0f / l;
+    if (a.out_f32) {
+        if (qrow < a.nq) {
+            float* of = a.out_f32 + ((int64_t)b * a.nq + qrow) * (a.Hq * D) + head * D;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int g4 = 0; g4 < 4; ++g4)
+                    *(float4*)(of + 32 * dt + 8 * g4 + 4 * h) =
+                        make_float4(o[dt][4 * g4 + 0] * inv, o[dt][4 * g4 + 1] * inv, o[dt][4 * g4 + 2] * inv,
+                                    o[dt][4 * g4 + 3] * inv);
+        }
+        return;
+    }
+    if (qrow < a.nq) {
+        uint16_t* op = a.out + ((int64_t)b * a.nq + qrow) * (a.Hq * D) + head * D;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+                const int d = 32 * dt + 8 * g4 + 4 * h;
+                uint2 w;
+                w.x = (uint32_t)to_act<F16OUT>(o[dt][4 * g4 + 0] * inv) |
+                      ((uint32_t)to_act<F16OUT>(o[dt][4 * g4 + 1] * inv) << 16);
+                w.y = (uint32_t)to_act<F16OUT>(o[dt][4 * g4 + 2] * inv) |
+                      ((uint32_t)to_act<F16OUT>(o[dt][4 * g4 + 3] * inv) << 16);
+                *(uint2*)(op + d) = w;
+            }
+        }
+    }
+}
+
 // Combine the S key-range parts of one (item, query, head) row: M = max m_k, weights 2^(m_k - M) (0 for a
 // part whose keys were all masked), out = sum w_k O_k / sum w_k l_k; a row with no unmasked key at all stays
 // 0/0 = NaN as in ggml.  Half a wave per row, 16-byte partial reads, every load issued before the first use.
@@ -848,6 +1378,21 @@ void launch_t(const AttnArgs& a, dim3 grid, hipStream_t s) {
     // classifies those pairs as single-wave).  Round 3's kernel (attn_kernel, ACE_MI_ATTN_V1) and the
     // two-per-CU fp16 instance are gone: the fp16 mode is a diagnostic precision, not a product one.
     if constexpr (PVS) {
+        if constexpr (SPLIT) {
+            // f8c: the two-waves-per-SIMD kernel (ACE_MI_ATTN_KH=0: attn2, one wave per SIMD)
+            static int kh = -1;
+            if (kh < 0) {
+                const char* e = std::getenv("ACE_MI_ATTN_KH");
+                kh = (e && e[0] == '0') ? 0 : 1;
+            }
+            if (a.f8 && kh) {
+                if (a.kbias)
+                    hipLaunchKernelGGL((attn_kh_kernel<F16OUT, true>), grid, dim3(512), lds, s, a);
+                else
+                    hipLaunchKernelGGL((attn_kh_kernel<F16OUT, false>), grid, dim3(512), lds, s, a);
+                return;
+            }
+        }
         if (a.f8) {  // f8c (SPLIT) or pv8 (fp16 Q.K)
             if (a.kbias)
                 hipLaunchKernelGGL((attn2_kernel<F16OUT, SPLIT, true, true, 1, true>), grid, dim3(256), lds, s, a);

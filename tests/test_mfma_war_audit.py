@@ -4,8 +4,9 @@ Round 5 root-caused wrong 16-column groups in the register-dequant GEMM to a VAL
 of the MFMA issued just before it, at two waves per SIMD.  These tests read the .s that the build keeps
 (-save-temps) and fail when any kernel that can run two waves per SIMD has a VALU write to an in-flight MFMA's A / B /
 scale register within 8 issue slots on some control-flow path.  Kernels whose registers allow one wave per SIMD only
-(hipcc's `; Occupancy: 1`) are reported, not failed: the product attention kernel is one of them, and that it stays
-so is asserted below."""
+(hipcc's `; Occupancy: 1`) are reported, not failed: round 5's attention kernel (attn2, now the ACE_MI_ATTN_KH=0 /
+non-f8c path) is one of them, and that it stays so is asserted below.  Round 6's f8c kernel (attn_kh_kernel) runs two
+waves per SIMD by design: it must be clean of VALU AND LDS-read overwrites (--loads)."""
 import os
 import sys
 
@@ -35,14 +36,27 @@ def test_no_exposed_mfma_operand_overwrite(name):
     assert not exposed, f"unguarded MFMA operand overwrites in two-wave kernels:\n{msg}"
 
 
-def test_product_attention_instances_are_single_wave():
-    """the f8c (DiT default) and f32 (condition / text encoders, q8 mode) instances must keep one wave per SIMD: the
-    hand-laid stream reuses P-pack and address registers right after the MFMAs that read them"""
+def test_attn2_instances_are_single_wave():
+    """attn2 (f32 for the condition / text encoders and the q8 mode; f8c with ACE_MI_ATTN_KH=0) must keep one wave per
+    SIMD: its hand-laid stream reuses P-pack and address registers right after the MFMAs that read them"""
     funcs = aw.parse(_s("attention"))
     attn2 = {k: f for k, f in funcs.items() if "attn2_kernel" in k}
     assert attn2, "no attn2_kernel instance in attention.s"
     for k, f in attn2.items():
         assert f.occupancy == 1, f"{k}: occupancy {f.occupancy}"
+
+
+def test_two_wave_attention_kernel_is_clean_of_operand_overwrites():
+    """attn_kh_kernel (the f8c default, 8 waves = two per SIMD): no VALU and no LDS / memory load may write an A / B /
+    scale register within 8 issue slots of the MFMA that reads it (fragment liveness + phase-end wait states)"""
+    s = _s("attention")
+    funcs = aw.parse(s)
+    kh = {k: f for k, f in funcs.items() if "attn_kh_kernel" in k}
+    assert len(kh) == 4, sorted(kh)  # bf16 / fp16 output x key bias
+    for k, f in kh.items():
+        assert f.occupancy == 2, f"{k}: occupancy {f.occupancy}"
+    res = aw.audit(s, window=8, ksub="attn_kh_kernel", valu_only=False)
+    assert res == {}, {k[:80]: (occ, h[:3]) for k, (occ, h) in res.items()}
 
 
 def _fake(tmp_path, body, occupancy):

@@ -21,6 +21,7 @@ CASES = [  # name, B, hq, hkv, nq, nk, window, masked
 def main():
     only = os.environ.get("ATTN_CASE")  # e.g. "self_full 240s" (one mode, ATTN_MODE or split) for a PMC pass
     only_mode = os.environ.get("ATTN_MODE", "split")
+    modes_env = os.environ.get("ATTN_MODES")  # e.g. "f8c" or "f8c,fp16": these modes for every case
     for name, B, hq, hkv, nq, nk, win, masked in CASES:
         if only and name != only:
             continue
@@ -29,11 +30,13 @@ def main():
         for mode, (split, pvs, f8) in modes.items():
             if only and mode != only_mode:
                 continue
+            if modes_env and mode not in modes_env.split(","):
+                continue
             ms = capi.bench_attention(B, hq, hkv, nq, nk, win, split=split, masked=masked, iters=10, pv_split=pvs,
                                       f8=f8)
             nk_eff = min(nk, 2 * win + 1) if win else nk
             flop = 4.0 * B * nq * nk_eff * 128 * hq
-            print(json.dumps({"case": name, "mode": mode, "ms": round(ms, 4),
+            print(json.dumps({"case": name, "mode": mode, "kh": os.environ.get("ACE_MI_ATTN_KH", "1"), "ms": round(ms, 4),
                               "tflops_alg": round(flop / (ms * 1e-3) / 1e12, 1)}), flush=True)
 
 
