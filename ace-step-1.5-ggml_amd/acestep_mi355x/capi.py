@@ -47,7 +47,7 @@ EXPORTED_SYMBOLS = (
 # product objects + the kernel self-test / micro-benchmark entries); the product library does not export them.
 SELFTEST_SYMBOLS = ("ace_mi_kernel_gemm", "ace_mi_kernel_attention", "ace_mi_bench_attention", "ace_mi_bench_gemm",
                     "ace_mi_kernel_gemm_q", "ace_mi_kernel_dequant", "ace_mi_bench_gemm_q", "ace_mi_kernel_gemm_a8",
-                    "ace_mi_kernel_gemm_a8_mode")
+                    "ace_mi_kernel_gemm_a8_mode", "ace_mi_kernel_attn_kh")
 
 # qtype codes of ace_mi_quantize & co. (names as parse_quant_type, acestep_dit_model.cpp:27-37)
 QTYPES = {"q8_0": 1, "q4_k": 2, "q6_k": 3}
@@ -231,6 +231,8 @@ def load_selftest_library() -> ctypes.CDLL:
     lib.ace_mi_kernel_gemm_a8.restype = ctypes.c_int
     lib.ace_mi_kernel_gemm_a8_mode.argtypes = [i32]
     lib.ace_mi_kernel_gemm_a8_mode.restype = ctypes.c_int
+    lib.ace_mi_kernel_attn_kh.argtypes = [i32]
+    lib.ace_mi_kernel_attn_kh.restype = ctypes.c_int
     _SELFTEST = lib
     return lib
 
@@ -751,6 +753,12 @@ def gemm_variant(variant: int) -> None:
     lib = load_library()
     if lib.ace_mi_gemm_variant(int(variant)) != ACE_GGML_OK:
         raise ValueError(variant)
+
+
+def kernel_attn_kh(mode: int) -> None:
+    """f8c attention kernel of this process: -1 environment / default policy, 0 attn2 (one wave per SIMD), 1 attn_kh."""
+    if load_selftest_library().ace_mi_kernel_attn_kh(int(mode)) != ACE_GGML_OK:
+        raise ValueError(mode)
 
 
 def kernel_gemm_a8_mode(mode: int) -> None:

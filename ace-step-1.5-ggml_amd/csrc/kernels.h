@@ -181,6 +181,9 @@ struct AttnArgs {
                       // correction products Kl.Qh + Kh.Ql and Vl.Ph + Vh.Pl run as block-scaled fp8 MFMAs
 };
 size_t attn_part_floats(int B, int nq, int Hq);
+// Which kernel runs the f8c mode: -1 = ACE_MI_ATTN_KH (0 never, 1 always) / default (attn_kh_kernel, two waves per
+// SIMD, for blocks of >= 16 key tiles; attn2 below that), 0 = attn2 always, 1 = attn_kh_kernel always
+void attn_kh_mode(int mode);
 // Operand precision of the attention MFMAs: FP16 = single fp16 operands (two workgroups per CU),
 // SPLIT = hi/lo fp16 Q.K (three MFMAs per product) with fp16 P.V, F32 = hi/lo fp16 for both products
 // (~22-bit operands, the f32-faithful mode), F8C = hi/lo for both products with the two correction products as

@@ -178,11 +178,6 @@ __device__ __forceinline__ void lds_wait_tie(frag (&r)[N]) {
     for (int j = 0; j < N; ++j) asm volatile("" : "+v"(r[j]));
 }
 
-__device__ __forceinline__ uint32_t pack_f16x2(float a, float b) {
-    _Float16 ha = (_Float16)a, hb = (_Float16)b;
-    return (uint32_t)__builtin_bit_cast(uint16_t, ha) | ((uint32_t)__builtin_bit_cast(uint16_t, hb) << 16);
-}
-
 __device__ __forceinline__ uint16_t f32_to_bf16_rne(float f) {
     uint32_t u = __float_as_uint(f);
     if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 64u);
@@ -1370,8 +1365,10 @@ __global__ void __launch_bounds__(256) attn_merge_kernel(AttnArgs a) {
                    (uint32_t)to_act<F16OUT>(v[2] * inv) | ((uint32_t)to_act<F16OUT>(v[3] * inv) << 16));
 }
 
+int g_kh_mode = -1;
+
 template <bool F16OUT, bool SPLIT, bool PVS>
-void launch_t(const AttnArgs& a, dim3 grid, hipStream_t s) {
+void launch_t(const AttnArgs& a, dim3 grid, hipStream_t s, bool kh) {
     const size_t lds = Ring<SPLIT, PVS>::BYTES;
     // One workgroup per CU in every mode (round 6): each instance then runs one wave per SIMD, the only occupancy at
     // which attn2's hand-laid stream may reuse an MFMA's A / B register right after issuing it (tools/audit_mfma_war.py
@@ -1379,13 +1376,7 @@ void launch_t(const AttnArgs& a, dim3 grid, hipStream_t s) {
     // two-per-CU fp16 instance are gone: the fp16 mode is a diagnostic precision, not a product one.
     if constexpr (PVS) {
         if constexpr (SPLIT) {
-            // f8c: the two-waves-per-SIMD kernel (ACE_MI_ATTN_KH=0: attn2, one wave per SIMD)
-            static int kh = -1;
-            if (kh < 0) {
-                const char* e = std::getenv("ACE_MI_ATTN_KH");
-                kh = (e && e[0] == '0') ? 0 : 1;
-            }
-            if (a.f8 && kh) {
+            if (a.f8 && kh) {  // f8c at two waves per SIMD (launch_attention's policy)
                 if (a.kbias)
                     hipLaunchKernelGGL((attn_kh_kernel<F16OUT, true>), grid, dim3(512), lds, s, a);
                 else
@@ -1499,19 +1490,33 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s) {
                                      : (unsigned)(8 * ((n_blk * b.ksplit + 7) / 8)));
     const bool f16 = out_t == ActType::F16;
     ACEMI_CHECK(!a.f8 || a.pv_split, "attention: the fp8 correction modes need pv_split");
+    // f8c kernel: attn_kh_kernel (two waves per SIMD) where a block streams >= 16 key tiles (full self-attention
+    // layers; measured 240 s: full 173.3 vs 175.2 us, bs 8 1.340 vs 1.355 ms), attn2 on short ranges (cross 50.8 vs
+    // 48.1 us, sliding 42.4 vs 41.4: the 8-wave prologue and the pair merge outweigh the gain), profiles/r06/attn_kh/
+    bool kh;
+    {
+        static int env = -2;
+        if (env == -2) {
+            const char* e = std::getenv("ACE_MI_ATTN_KH");
+            env = (e && (e[0] == '0' || e[0] == '1')) ? e[0] - '0' : -1;
+        }
+        const int mode = g_kh_mode >= 0 ? g_kh_mode : env;
+        const int span = a.window > 0 ? std::min(a.nk, qpb + 2 * a.window) : a.nk;
+        kh = mode == 1 || (mode < 0 && (span + KT - 1) / KT >= 16);
+    }
     if (a.split) {
         ACEMI_CHECK(a.q_plane > 0 && a.k_plane > 0, "attention: split mode needs lo planes");
         if (a.pv_split) {
             ACEMI_CHECK(a.v_plane > 0, "attention: hi/lo P.V needs the V lo plane");
-            f16 ? launch_t<true, true, true>(b, grid, s) : launch_t<false, true, true>(b, grid, s);
+            f16 ? launch_t<true, true, true>(b, grid, s, kh) : launch_t<false, true, true>(b, grid, s, kh);
         } else {
-            f16 ? launch_t<true, true, false>(b, grid, s) : launch_t<false, true, false>(b, grid, s);
+            f16 ? launch_t<true, true, false>(b, grid, s, kh) : launch_t<false, true, false>(b, grid, s, kh);
         }
     } else if (a.pv_split) {
         ACEMI_CHECK(a.f8 && a.v_plane > 0, "attention: pv8 mode needs the fp8 V lo plane");
-        f16 ? launch_t<true, false, true>(b, grid, s) : launch_t<false, false, true>(b, grid, s);
+        f16 ? launch_t<true, false, true>(b, grid, s, kh) : launch_t<false, false, true>(b, grid, s, kh);
     } else {
-        f16 ? launch_t<true, false, false>(b, grid, s) : launch_t<false, false, false>(b, grid, s);
+        f16 ? launch_t<true, false, false>(b, grid, s, kh) : launch_t<false, false, false>(b, grid, s, kh);
     }
     ACEMI_HIP(hipGetLastError());
     if (b.ksplit > 1) {
@@ -1546,6 +1551,8 @@ void launch_attention(ActType out_t, const AttnArgs& a, hipStream_t s) {
         ACEMI_HIP(hipGetLastError());
     }
 }
+
+void attn_kh_mode(int mode) { g_kh_mode = mode; }
 
 size_t attn_part_floats(int B, int nq, int Hq) {
     const size_t rows = (size_t)B * nq * Hq;

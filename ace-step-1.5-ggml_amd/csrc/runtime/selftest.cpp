@@ -480,6 +480,13 @@ ace_ggml_status ace_mi_kernel_gemm_a8_mode(int32_t mode) {
     return ACE_GGML_OK;
 }
 
+// Which kernel runs f8c attention in this process: -1 the environment / default policy, 0 attn2, 1 attn_kh_kernel.
+ace_ggml_status ace_mi_kernel_attn_kh(int32_t mode) {
+    if (mode < -1 || mode > 1) return ACE_GGML_ERR_INVALID_ARG;
+    acemi::attn_kh_mode(mode);
+    return ACE_GGML_OK;
+}
+
 // Dequant-fused GEMM micro-benchmark (random N(0, 0.02) weights quantized with the loader's encoder).
 ace_ggml_status ace_mi_bench_gemm_q(int32_t qtype, int32_t epi, int32_t variant, int32_t M, int32_t N, int32_t K,
                                     int32_t iters, float* avg_ms) {

@@ -61,6 +61,10 @@ ACE_GGML_API ace_ggml_status ace_mi_kernel_gemm_a8(int32_t qtype, int32_t epi, i
  * environment (ACE_MI_QACT_GEMM=0: i8) / default (bf16 MFMA over exact integer bf16 operands), 0 = the i8-MFMA kernel,
  * 1 = the bf16-MFMA kernel.  Both give the same bits. */
 ACE_GGML_API ace_ggml_status ace_mi_kernel_gemm_a8_mode(int32_t mode);
+/* The kernel that runs f8c attention in this process: -1 = the environment (ACE_MI_ATTN_KH=0 / 1) / default policy
+ * (the two-waves-per-SIMD kernel for blocks of >= 16 key tiles), 0 = the one-wave-per-SIMD kernel, 1 = the two-wave
+ * kernel everywhere.  Same results within the f8c bound. */
+ACE_GGML_API ace_ggml_status ace_mi_kernel_attn_kh(int32_t mode);
 /* Dequant-fused GEMM micro-benchmark: average ms per launch (HIP events). */
 ACE_GGML_API ace_ggml_status ace_mi_bench_gemm_q(int32_t qtype, int32_t epi, int32_t variant, int32_t M, int32_t N,
                                                  int32_t K, int32_t iters, float* avg_ms);

@@ -149,6 +149,34 @@ def test_attention_vs_fp64(B, hq, hkv, nq, nk, window, masked, mode):
     _check_attn(got, q, kv, hq, hkv, window, kmask, scale, mode)
 
 
+ATTN_CASES = [(1, 2, 1, 64, 64, 0, False), (2, 16, 8, 300, 77, 0, True), (1, 2, 2, 130, 130, 128, True),
+              (1, 4, 1, 97, 500, 0, False), (1, 2, 1, 150, 1500, 0, True), (1, 16, 8, 3000, 1100, 0, True),
+              (1, 16, 8, 3000, 3000, 128, False)]
+
+
+@pytest.mark.parametrize("B,hq,hkv,nq,nk,window,masked", ATTN_CASES)
+@pytest.mark.parametrize("kh", [0, 1])
+def test_attention_f8c_both_kernels(B, hq, hkv, nq, nk, window, masked, kh):
+    """f8c through each of its kernels on every range length (the default policy picks attn_kh_kernel -- two waves
+    per SIMD, query group x key half, pair merge through LDS -- only for >= 16 key tiles): same fp64 bound, and the
+    two kernels within the f8c bound of each other."""
+    capi = _capi()
+    rng = np.random.default_rng(B * 1000 + nq + nk + window)
+    q = rng.standard_normal((B, nq, hq * 128)).astype(np.float32) * 2.0
+    kv = rng.standard_normal((B, nk, 2 * hkv * 128)).astype(np.float32) * 0.3
+    kmask = None
+    if masked:
+        kmask = (rng.random((B, nk)) > 0.3).astype(np.int32)
+        kmask[:, 0] = 1
+    scale = 1.0 / np.sqrt(128.0)
+    capi.kernel_attn_kh(kh)
+    try:
+        got = capi.kernel_attention(q, kv, hq, hkv, window=window, kmask=kmask, scale=scale, **MODES["f8c"])
+    finally:
+        capi.kernel_attn_kh(-1)
+    _check_attn(got, q, kv, hq, hkv, window, kmask, scale, "f8c")
+
+
 @pytest.mark.parametrize("mode", list(MODES))
 def test_attention_fully_masked_row_is_nan(mode):
     """ggml soft_max of an all -inf row gives NaN (acestep_dit_model.cpp:1245); so does the kernel."""
@@ -356,13 +384,20 @@ def test_product_gemm_picks_run_to_run_identical(name, N, K, epi):
                               outs[0].view(np.uint32) if outs[0].dtype == np.float32 else outs[0]), (name, i)
 
 
+@pytest.mark.parametrize("kh", [-1, 0, 1])
 @pytest.mark.parametrize("window", [0, 128])
-def test_product_attention_run_to_run_identical(window):
-    """f8c (the DiT default) at the 240 s self-attention shape: full layers (tail split + merge) and sliding ones."""
+def test_product_attention_run_to_run_identical(window, kh):
+    """f8c (the DiT default) at the 240 s self-attention shape: full layers (tail split + merge) and sliding ones, through
+    the default policy and each kernel forced (attn_kh_kernel runs two waves per SIMD: the operand-overwrite hazard's
+    condition, audited statically by tests/test_mfma_war_audit.py)."""
     rng = np.random.default_rng(5 + window)
     q = rng.standard_normal((1, 3000, 16 * 128)).astype(np.float32)
     kv = rng.standard_normal((1, 3000, 2 * 8 * 128)).astype(np.float32) * 0.5
-    outs = [_capi().kernel_attention(q, kv, 16, 8, window=window, scale=1 / np.sqrt(128.0), **MODES["f8c"])
-            for _ in range(5)]
+    _capi().kernel_attn_kh(kh)
+    try:
+        outs = [_capi().kernel_attention(q, kv, 16, 8, window=window, scale=1 / np.sqrt(128.0), **MODES["f8c"])
+                for _ in range(5)]
+    finally:
+        _capi().kernel_attn_kh(-1)
     for i, o in enumerate(outs[1:], 1):
         assert np.array_equal(o.view(np.uint32), outs[0].view(np.uint32)), (window, i)
