@@ -3,8 +3,8 @@
 Usage: python tools/pmc_summary.py gpurun_out/pmc  > summary.json
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch; on gfx950 FETCH_SIZE counts half the bytes of a wide
 streaming read (MI355X_MICROARCH.md, HBM section), so fetch bytes = 2 x 1024 x FETCH_SIZE.  The
-"gate_up" entry is the MLP gate|up GEMM (the SwiGLU-epilogue GEMM, EPI 4); "attention" the f8c attention kernel
-(attn2_kernel<..., F8 = true> instances, every class: full / sliding / cross), launch-weighted.  "build" is
+"gate_up" entry is the MLP gate|up GEMM (the SwiGLU-epilogue GEMM, EPI 4); "attention" the f8c attention kernels
+(attn_kh_kernel instances -- full layers -- and attn2_kernel<..., F8 = true> ones -- sliding / cross), launch-weighted.  "build" is
 acestep_mi355x.source_hash() of the tree the passes ran: bench.py uses the bytes only when its own tree has the same
 hash (and the same workload), so a changed kernel never reports stale traffic.
 """
@@ -43,7 +43,8 @@ def main(root, bench_json=None):
     gu = [k for k in out["kernels"] if pat.search(k)]
     if gu:
         out["gate_up"] = {"kernel": gu[0], **out["kernels"][gu[0]]}
-    att = [k for k in out["kernels"] if "attn2_kernel" in k and k.replace(" ", "").endswith("1,true>(acemi::AttnArgs)")]
+    att = [k for k in out["kernels"] if "attn_kh_kernel" in k
+           or ("attn2_kernel" in k and k.replace(" ", "").endswith("1,true>(acemi::AttnArgs)"))]
     if att:
         n = sum(out["kernels"][k]["launches"] for k in att)
         out["attention"] = {"kernels": att, "launches": n,
