@@ -50,6 +50,33 @@ def test_causal_attention_kernel(B, hq, hkv, n, masked, mode):
     assert np.all(err <= 2.0 ** -8 * np.abs(ref) + (1e-5 if f32 else 2e-3)), float(err.max())
 
 
+@pytest.mark.parametrize("kh", [0, 1])
+@pytest.mark.parametrize("n,masked", [(300, True), (1100, False)])
+def test_causal_attention_kernel_f8c(n, masked, kh):
+    """The f8c mode under the causal mask through each of its kernels (the one-wave attn2 and the two-wave attn_kh,
+    whose blocks see different key ranges per query tile): the f8c bound of tests/test_gpu_kernels.py."""
+    from acestep_mi355x import capi
+    rng = np.random.default_rng(n + kh)
+    B, hq, hkv = 1, 4, 2
+    q = rng.standard_normal((B, n, hq * 128)).astype(np.float32) * 2.0
+    kv = rng.standard_normal((B, n, 2 * hkv * 128)).astype(np.float32) * 0.3
+    kmask = None
+    if masked:
+        kmask = (rng.random((B, n)) > 0.3).astype(np.int32)
+        kmask[:, 0] = 1
+    scale = 1.0 / np.sqrt(128.0)
+    capi.kernel_attn_kh(kh)
+    try:
+        got = capi.kernel_attention(q, kv, hq, hkv, kmask=kmask, scale=scale, split=True, pv_split=True, f8=True,
+                                    causal=True)
+    finally:
+        capi.kernel_attn_kh(-1)
+    ref = _causal_ref(q, kv, hq, hkv, kmask, scale)
+    vmax = float(np.abs(kv[:, :, hkv * 128:]).max())
+    err = np.abs(got - ref)
+    assert np.all(err <= 2.0 ** -8 * np.abs(ref) + 2.0 ** -13 * vmax), float(err.max())
+
+
 @pytest.fixture(scope="module")
 def text_ckpt():
     from acestep_mi355x.synthetic import TEXT_TINY_CONFIG, text_tensor_specs, write_checkpoint
