@@ -785,17 +785,20 @@ __global__ void __launch_bounds__(256, OCC) attn2_kernel(AttnArgs a) {
 
 // ---------------------------------------------------------------------------------------------------------------
 // attn_kh_kernel (round 6): the f8c mode at two waves per SIMD.  attn2 holds a whole 64-key tile's scores and P
-// operands, both ring stages and the Q planes in one wave (312 registers, so one wave per SIMD; its per-tile stream is
-// dependency-bound at ~2.2x its MFMA time).  Here a workgroup of 8 waves runs the same block (item, kv
+// operands, both ring stages and the Q planes in one wave (312 registers, so one wave per SIMD; its per-tile stream
+// takes ~2.2x its MFMA time).  Here a workgroup of 8 waves runs the same block (item, kv
 // head, 128 query rows) over the same LDS rings: wave w = 4 kh + wq takes query group wq's 32 rows against key half kh
 // (keys [32 kh, 32 kh + 32)) of every tile -- exactly attn2's half t = kh -- with its own online softmax, and the two
 // halves of a row meet once after the key loop, through LDS (the key-split merge's combination).  Per wave and tile:
 //   S^T half   8 fp16 hi MFMAs + 4 block-scaled e4m3 corrections (Kl.Qh, Kh.Ql over D = 128), one accumulator;
 //   O^T        8 fp16 hi MFMAs + 4 e4m3 MFMAs, each carrying BOTH P.V corrections of one d-tile in one K = 64 product:
-//              lanes 0-31 (K block 0) hold Vl x Ph with E8M0 scale 2^-11, lanes 32-63 (K block 1) Vh x Pl with scale 1
-//              -- the MFMA's block scale is per lane, i.e. per 32-element K block -- after one permlane32_swap per P
-//              word regroups [Ph | Pl] of the lane halves into [Ph (all 32 keys) ; Pl (all 32 keys)].
-// The same MFMA cycles per key as attn2, at <= 256 registers: the partner wave on the SIMD runs while one waits.
+//              K 0-31 (lanes 0-31) Vl x Ph, K 32-63 (lanes 32-63) Vh x Pl, after one permlane32_swap per P word has
+//              regrouped [Ph | Pl] of the lane halves into [Ph (all 32 keys) ; Pl (all 32 keys)].  Both halves carry
+//              2^11 (Vl is stored as fp8(2^11 lo) by the prep, Pl is formed as fp8(2^11 (P - f16(P))), which also keeps
+//              it clear of e4m3's subnormals) and share one uniform E8M0 scale 2^-11: a VGPR scale that differs between
+//              the lane halves is not applied per K block (measured, profiles/r06/attn_kh/diag_per_lane_scale_attempt.jsonl).
+// The same MFMA cycles per key as attn2 at <= 256 registers, so a partner wave shares each SIMD -- measured equal in
+// speed to attn2 (the issue per tile and SIMD is the same); launch_attention runs it on >= 16-tile blocks.
 // Pipeline, DMA ring and masks as attn2 (phase B: S(i+1) || softmax finish of i; phase C: O += V(i) P(i) || softmax
 // start of i+1), with 4 K + 4 V^T LDS-DMA pieces per wave and tile.
 template <bool F16OUT, bool KBIAS>

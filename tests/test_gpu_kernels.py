@@ -151,7 +151,7 @@ def test_attention_vs_fp64(B, hq, hkv, nq, nk, window, masked, mode):
 
 ATTN_CASES = [(1, 2, 1, 64, 64, 0, False), (2, 16, 8, 300, 77, 0, True), (1, 2, 2, 130, 130, 128, True),
               (1, 4, 1, 97, 500, 0, False), (1, 2, 1, 150, 1500, 0, True), (1, 16, 8, 3000, 1100, 0, True),
-              (1, 16, 8, 3000, 3000, 128, False)]
+              (1, 16, 8, 3000, 3000, 128, False), (2, 16, 8, 1500, 1500, 0, True)]
 
 
 @pytest.mark.parametrize("B,hq,hkv,nq,nk,window,masked", ATTN_CASES)
