@@ -107,6 +107,11 @@ constexpr float PSCALE_F8_LOG2 = 5.0f;  // f8c: P <= 2^(5 + RESCALE_LOG2) = 256,
 #define ACEMI_ATTN_RA 2
 #endif
 constexpr int RA = ACEMI_ATTN_RA;
+// attn_kh_kernel (round 6): 1 = each phase's wait-and-barrier after its 7th step, the next phase's first RA fragments read
+// right behind it (0 = the barriers between the phases, A/B builds only)
+#ifndef ACEMI_KH_EARLY
+#define ACEMI_KH_EARLY 1
+#endif
 // Diagnostic ablation (A/B builds only, tools/build_ab.sh; results wrong by design): 1 = no next-tile LDS-DMA inside
 // the attn2 pipeline (every tile computes on the prologue's K / V), 2 = no exp2 in the softmax finish (P = the raw
 // score), 4 = no P lo formation in phase C (f8c / pv8), 8 = no workgroup barrier inside the tile loop, 16 = no wait
@@ -937,18 +942,31 @@ __global__ void __launch_bounds__(512) attn_kh_kernel(AttnArgs a) {
         }
     };
     auto rk = [](int p) constexpr { return p % 3 == 2 ? 2 : 1; };
-    auto qk_phase = [&](auto slot_c, f32x16& sn, auto&& fin, auto&& dma) {
+    // EARLY: each phase waits for the next tile's DMA and meets the other waves after its step MID (the MFMAs issued
+    // before it keep the pipe busy through the barrier), and right behind that barrier reads the first RA fragments of
+    // the phase that follows (V in phase B, the next iteration's K in phase C), so no phase opens on an LDS latency.
+    // Those RA reads sit between the step reads: the two steps after MID count them in their lgkmcnt.  The K ones cross
+    // the loop's back-edge only after they have landed and been tied (end of phase C), so no register copy of an asm-load
+    // destination can run before its wait.
+    constexpr bool EARLY = ACEMI_KH_EARLY;
+    constexpr int MID = 6;
+    auto extra = [](int p) constexpr { return (EARLY && (p == MID + 1 || p == MID + 2)) ? RA : 0; };
+    frag kpre[RA], vpre[RA];
+    auto qk_phase = [&](auto slot_c, f32x16& sn, auto&& fin, auto&& dma, auto&& mid, auto pre_c) {
         frag kx[RX], ky[2];
         v8i kc;  // the last correction step's concatenated A operand (hipcc may copy the two fragments into it)
         static_for<0, RA>([&](auto r_c) {
             constexpr int r = decltype(r_c)::value;
-            k_read(slot_c, r_c, kx[r], ky[0]);
+            if constexpr (decltype(pre_c)::value)
+                kx[r] = kpre[r];
+            else
+                k_read(slot_c, r_c, kx[r], ky[0]);
         });
         static_for<0, NB>([&](auto p_c) {
             constexpr int p = decltype(p_c)::value;
             if constexpr (p + RA < NB)
                 k_read(slot_c, std::integral_constant<int, p + RA>{}, kx[(p + RA) % RX], ky[((p + RA) / 3) % 2]);
-            constexpr int after = reads_after(p, NB, rk);
+            constexpr int after = reads_after(p, NB, rk) + (decltype(pre_c)::value ? extra(p) : 0);
             asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(after) : "memory");
             asm volatile("" : "+v"(kx[p % RX]));
             if constexpr (rk(p) == 2) asm volatile("" : "+v"(ky[(p / 3) % 2]));
@@ -970,6 +988,7 @@ __global__ void __launch_bounds__(512) attn_kh_kernel(AttnArgs a) {
                 }
             });
             if constexpr (p > 2) keep8(kc);
+            mid(p_c);
             __builtin_amdgcn_sched_barrier(0);
         });
         asm volatile("" : "+v"(sn));  // (the phase's MFMAs stay above the wait states: IR passes sink the last ones)
@@ -1042,6 +1061,12 @@ __global__ void __launch_bounds__(512) attn_kh_kernel(AttnArgs a) {
     f32x16 sA, sB;
     auto no_fin = [](auto) {};
     auto no_dma = [](auto) {};
+    auto pre_k = [&](auto slot_c) {  // the first RA fragments of a phase B that reads K slot SLOT (hi steps: no second read)
+        static_for<0, RA>([&](auto r_c) {
+            frag unused;
+            k_read(slot_c, r_c, kpre[decltype(r_c)::value], unused);
+        });
+    };
     if (n > 0) {
 #pragma unroll
         for (int p = 0; p < NPK; ++p) k_piece(0, kt_begin, p);
@@ -1055,7 +1080,7 @@ __global__ void __launch_bounds__(512) attn_kh_kernel(AttnArgs a) {
         }
         wait_vmcnt<0>();
         __builtin_amdgcn_s_barrier();
-        qk_phase(std::integral_constant<int, 0>{}, sA, no_fin, no_dma);
+        qk_phase(std::integral_constant<int, 0>{}, sA, no_fin, no_dma, no_fin, std::false_type{});
         bias_tile(std::integral_constant<int, 0>{}, sA);
         mask_tile(sA, 0);
         float mr = -INFINITY;
@@ -1064,6 +1089,10 @@ __global__ void __launch_bounds__(512) attn_kh_kernel(AttnArgs a) {
         update_max(finish_max(mr));
         apply_rescale();
         __builtin_amdgcn_s_barrier();  // every wave has read K slot 0: iteration 0 restages it
+        if constexpr (EARLY) {
+            pre_k(std::integral_constant<int, 1>{});
+            lds_wait_tie(kpre);
+        }
     }
 
     auto iter = [&](auto slot_c, f32x16& sc, f32x16& sn, int i) {
@@ -1131,15 +1160,46 @@ __global__ void __launch_bounds__(512) attn_kh_kernel(AttnArgs a) {
                 if constexpr (p == 2) bias_piece(SLOT, ktk);
             }
         };
-        qk_phase(std::integral_constant<int, NXT>{}, sn, [&](auto j_c) { fin(j_c); }, [&](auto j_c) { dma(j_c); });
+        // phase C's V reads (defined below) and, EARLY, the mid-phase-B point: V(i), requested in the previous iteration's
+        // phase C, landed for every wave (K(i + 2)'s first two pieces + the bias are the only later requests), then
+        // phase C's first RA fragments
+        auto v_read = [&](auto q_c, frag& x, frag& y) {
+            constexpr int q = decltype(q_c)::value;
+            if constexpr (q % 3 != 2) {
+                constexpr int s = q - q / 3;
+                x = lds_frag<SLOT * RG::VS + (s & 3) * 32 * 128>(vaddr[s >> 2]);
+            } else {
+                x = lds_frag<SLOT * RG::VS + (q / 3) * 32 * 128>(v8a[0]);
+                y = lds_frag<SLOT * RG::VS + (q / 3) * 32 * 128>(v8a[1]);
+            }
+        };
+        auto midB = [&](auto p_c) {
+            if constexpr (EARLY && decltype(p_c)::value == MID) {
+                if (KBIAS && wid == 0)
+                    wait_vmcnt<3>();
+                else
+                    wait_vmcnt<2>();
+                __builtin_amdgcn_s_barrier();
+                static_for<0, RA>([&](auto r_c) {
+                    frag unused;
+                    v_read(r_c, vpre[decltype(r_c)::value], unused);
+                });
+            }
+        };
+        qk_phase(std::integral_constant<int, NXT>{}, sn, [&](auto j_c) { fin(j_c); }, [&](auto j_c) { dma(j_c); },
+                 [&](auto j_c) { midB(j_c); }, std::integral_constant<bool, EARLY>{});
         l_run += lsum;
 
-        // V(i), requested in the previous iteration's phase C, landed for every wave
-        if (KBIAS && wid == 0)
-            wait_vmcnt<NPK + 1>();
-        else
-            wait_vmcnt<NPK>();
-        __builtin_amdgcn_s_barrier();
+        if constexpr (EARLY) {
+            asm volatile("" : "+v"(vpre[0]), "+v"(vpre[1]));  // landed: phase B's last steps waited for every read
+        } else {
+            // V(i), requested in the previous iteration's phase C, landed for every wave
+            if (KBIAS && wid == 0)
+                wait_vmcnt<NPK + 1>();
+            else
+                wait_vmcnt<NPK>();
+            __builtin_amdgcn_s_barrier();
+        }
         bias_tile(std::integral_constant<int, NXT>{}, sn);
         mask_tile(sn, i + 1);
         float mr = -INFINITY;
@@ -1150,20 +1210,13 @@ __global__ void __launch_bounds__(512) attn_kh_kernel(AttnArgs a) {
             uint32_t pb[8];  // [Ph ; Pl] of the half's 32 keys: lane half 0 the Ph bytes, lane half 1 the Pl bytes
             frag vx[RX], vy[2];
             v8i vc;
-            auto v_read = [&](auto q_c, frag& x, frag& y) {
-                constexpr int q = decltype(q_c)::value;
-                if constexpr (q % 3 != 2) {
-                    constexpr int s = q - q / 3;
-                    x = lds_frag<SLOT * RG::VS + (s & 3) * 32 * 128>(vaddr[s >> 2]);
-                } else {
-                    x = lds_frag<SLOT * RG::VS + (q / 3) * 32 * 128>(v8a[0]);
-                    y = lds_frag<SLOT * RG::VS + (q / 3) * 32 * 128>(v8a[1]);
-                }
-            };
             auto rv = [](int q) constexpr { return q % 3 == 2 ? 2 : 1; };
             static_for<0, RA>([&](auto r_c) {
                 constexpr int r = decltype(r_c)::value;
-                v_read(r_c, vx[r], vy[0]);
+                if constexpr (EARLY)
+                    vx[r] = vpre[r];
+                else
+                    v_read(r_c, vx[r], vy[0]);
             });
             static_for<0, NC>([&](auto q_c) {
                 constexpr int q = decltype(q_c)::value;
@@ -1177,7 +1230,7 @@ __global__ void __launch_bounds__(512) attn_kh_kernel(AttnArgs a) {
                         pb[4 + w] = sw[1];
                     }
                 }
-                constexpr int after = reads_after(q, NC, rv);
+                constexpr int after = reads_after(q, NC, rv) + extra(q);
                 asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(after) : "memory");
                 asm volatile("" : "+v"(vx[q % RX]));
                 if constexpr (rv(q) == 2) asm volatile("" : "+v"(vy[(q / 3) % 2]));
@@ -1204,6 +1257,14 @@ __global__ void __launch_bounds__(512) attn_kh_kernel(AttnArgs a) {
                     }
                 });
                 if constexpr (q > 2) keep8(vc);  // (phase C's hi steps are short: held until the next correction)
+                if constexpr (EARLY && q == MID) {
+                    // K(i + 2) landed for every wave (V(i + 1)'s first two pieces are the later requests), then the next
+                    // phase B's first fragments (K(i + 2) sits in this iteration's slot)
+                    wait_vmcnt<2>();
+                    __builtin_amdgcn_s_barrier();
+                    pre_k(slot_c);
+                }
+                if constexpr (EARLY && q == NC - 1) asm volatile("" : "+v"(kpre[0]), "+v"(kpre[1]));  // landed (lgkmcnt(0))
                 __builtin_amdgcn_sched_barrier(0);
             });
             // the P operands and the last fragments stay allocated through the retire (phase B rewrites pf / ph8 / pl8)
@@ -1223,8 +1284,10 @@ __global__ void __launch_bounds__(512) attn_kh_kernel(AttnArgs a) {
         if (more) {
             update_max(mnx);
             apply_rescale();
-            wait_vmcnt<NPV>();  // K(i + 2) landed (V(i + 1), issued after it, may stay in flight)
-            __builtin_amdgcn_s_barrier();
+            if constexpr (!EARLY) {
+                wait_vmcnt<NPV>();  // K(i + 2) landed (V(i + 1), issued after it, may stay in flight)
+                __builtin_amdgcn_s_barrier();
+            }
         }
     };
 
